@@ -1,0 +1,200 @@
+/*
+ * pbgpu.h -- C ABI of the MI355X-native jf_aligner hot path.
+ *
+ * This is the drop-in boundary for the reference's C++ class API on the
+ * L4 -> L3 line: the CLIs (jf_aligner, create_mega_reads)
+ * call it instead of
+ *   superread_parse(first, last, min, max)        superread_parser.hpp:219-224
+ *   coarse_aligner(psa, k, factor, constant, cap,  coarse_aligner.hpp:55-72
+ *                  window, forward, max_match, max_count, M, B)
+ *   coarse_aligner::unitigs_lengths(ul, k)         coarse_aligner.hpp:76-81
+ *   coarse_aligner::thread::align_sequence_max()   coarse_aligner.cc:68-72
+ *   coarse_aligner::thread::coords()               coarse_aligner.hpp:146
+ *   print_coords_header / print_coords             jf_aligner.cc:32-70
+ * Differences by design: reads are aligned in batches (one call per batch,
+ * not per read); records carry an SR index instead of frag_info pointers;
+ * records of a read come back already sorted by (rs, re, ql) with the
+ * deterministic tie-break (sr_index, emission order).
+ *
+ * Plain pointers and sizes only; no exceptions cross this boundary.  Every
+ * function returns a pbgpu_status; pbgpu_last_error() returns a thread-local
+ * message for the last failure on the calling thread.
+ * Thread-safety: distinct aligners may be used concurrently; one aligner is
+ * single-threaded (like coarse_aligner::thread).  The index is read-only
+ * after build and may be shared by aligners on the same device.
+ */
+#ifndef PBGPU_H
+#define PBGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PBGPU_ABI_VERSION 1
+
+typedef enum pbgpu_status {
+  PBGPU_OK = 0,
+  PBGPU_ERR_INVALID = 1,      /* bad argument (std::logic_error / yaggo error() upstream) */
+  PBGPU_ERR_IO = 2,           /* cannot open / parse input (std::runtime_error upstream) */
+  PBGPU_ERR_NOMEM = 3,        /* device or host allocation failed */
+  PBGPU_ERR_DEVICE = 4,       /* HIP runtime error, or no usable GPU */
+  PBGPU_ERR_UNSUPPORTED = 5,  /* configuration outside the implemented envelope */
+  PBGPU_ERR_INTERNAL = 6
+} pbgpu_status;
+
+typedef struct pbgpu_index pbgpu_index;
+typedef struct pbgpu_aligner pbgpu_aligner;
+typedef struct pbgpu_reads pbgpu_reads;
+
+int         pbgpu_abi_version(void);
+const char* pbgpu_last_error(void);
+/* number of visible GPUs (0 if none); never fails */
+int         pbgpu_device_count(void);
+
+/* ------------------------------------------------------------------ index
+ * Replaces superread_parse() + sequence_psa (superread_parser.hpp:53-224):
+ * the super-read text is 2-bit packed with the reference's compact_dna line
+ * rules, and a canonical k-mer hash index (counts incl. SR-boundary-crossing
+ * occurrences, non-crossing occurrence lists in descending text position) is
+ * built on and kept resident in device memory. */
+typedef struct {
+  uint32_t k;        /* -m, mer size: 2 <= k <= 31 */
+  uint32_t psa_min;  /* --psa-min; must be < k (k <= psa_min gives a
+                        thread-order-dependent hit order upstream) */
+  int32_t  device;   /* HIP device ordinal */
+  int32_t  threads;  /* host threads for FASTA parsing (0 = all cores) */
+} pbgpu_index_params;
+
+/* superread_parser.cc:12-46: multi-line FASTA, full header line kept as the
+ * name, empty records dropped.  PBGPU_ERR_IO for a missing file or a file
+ * that does not start with '>' ("Not in fasta format"). */
+pbgpu_status pbgpu_index_build_fasta(const char* const* paths, size_t n_paths,
+                                     const pbgpu_index_params* params, pbgpu_index** out);
+/* In-memory super-reads, each sequence treated as one FASTA line. */
+pbgpu_status pbgpu_index_build(const char* const* names, const char* const* seqs,
+                               const uint64_t* lens, size_t n,
+                               const pbgpu_index_params* params, pbgpu_index** out);
+pbgpu_status pbgpu_index_free(pbgpu_index* ix);
+
+typedef struct {
+  uint64_t n_sr;            /* super-reads kept */
+  uint64_t text_len;        /* concatenated bases */
+  uint64_t n_kmers;         /* canonical k-mers (distinct) */
+  uint64_t n_occurrences;   /* non-crossing occurrences stored */
+  uint64_t table_buckets;   /* 64-byte hash buckets */
+  uint64_t device_bytes;    /* resident index footprint */
+  double   build_seconds;
+} pbgpu_index_info;
+pbgpu_status pbgpu_index_get_info(const pbgpu_index* ix, pbgpu_index_info* info);
+/* frag_info.hpp:18-35: fwd name = header line, bwd name = reversed unitigs */
+const char*  pbgpu_index_sr_name(const pbgpu_index* ix, uint32_t sr, int bwd);
+uint32_t     pbgpu_index_sr_len(const pbgpu_index* ix, uint32_t sr);
+
+/* ---------------------------------------------------------------- aligner
+ * coarse_aligner ctor (coarse_aligner.hpp:55-72) + unitigs_lengths(). */
+typedef struct {
+  uint32_t k;                 /* must equal the index k */
+  double   stretch_factor;    /* --stretch-factor (1.3) */
+  double   stretch_constant;  /* --stretch-constant (10) */
+  double   stretch_cap;       /* --stretch-cap (10000) */
+  uint32_t window_size;       /* --window-size (1) */
+  int32_t  forward;           /* -f */
+  int32_t  max_match;         /* --max-match */
+  int32_t  max_count;         /* --max-count (5000); 0 is rejected: INT_MAX semantics are UB upstream */
+  double   mers_matching;     /* -M percent (0) */
+  double   bases_matching;    /* -B percent (17) */
+  uint32_t unitigs_k;         /* -k; 0 = no k-unitig accounting */
+  const int32_t* unitig_lengths; /* -l table, index = line number (misc.cc:11-19); copied */
+  uint64_t n_unitigs;
+  uint32_t fine_k;            /* -F; 0 = off (non-zero: PBGPU_ERR_UNSUPPORTED for now) */
+} pbgpu_align_params;
+
+void         pbgpu_align_params_default(pbgpu_align_params* p);
+/* unitig lengths with forward == 0 -> PBGPU_ERR_INVALID (coarse_aligner.hpp:77) */
+pbgpu_status pbgpu_aligner_create(const pbgpu_index* ix, const pbgpu_align_params* params,
+                                  pbgpu_aligner** out);
+pbgpu_status pbgpu_aligner_free(pbgpu_aligner* al);
+
+/* ------------------------------------------------------------------ reads */
+typedef struct {
+  uint64_t    n_reads;
+  const char* seq;            /* concatenated ASCII bases (any bytes; non-ACGT reset k-mers) */
+  const uint64_t* offsets;    /* n_reads + 1 offsets into seq */
+} pbgpu_read_batch;
+
+/* ---------------------------------------------------------------- records
+ * coords_info (pb_aligner.hpp:103-175) without pointers. */
+typedef struct {
+  int32_t  rs, re, qs, qe;
+  int32_t  nb_mers;
+  uint32_t pb_cons, sr_cons, pb_cover, sr_cover;
+  uint32_t ql;                /* super-read length */
+  uint32_t sr_index;          /* index into the index's super-reads */
+  uint32_t read;              /* read index within the batch */
+  uint32_t emit;              /* emission order within (read, super-read) (--max-match) */
+  uint32_t flags;             /* bit0 rn, bit1 use the bwd (reversed) name */
+  uint32_t n_info;            /* kmers_info / bases_info length */
+  uint32_t reserved;
+  uint64_t info_offset;       /* into kmers_info / bases_info */
+  double   stretch, offset, avg_err;
+} pbgpu_record;
+
+typedef struct {
+  uint64_t n_reads;
+  uint64_t n_records;
+  const uint64_t* read_offsets;  /* n_reads + 1 into records */
+  const pbgpu_record* records;    /* per read sorted by (rs, re, ql, sr_index, emit) */
+  uint64_t n_info;
+  const int32_t* kmers_info;
+  const int32_t* bases_info;
+} pbgpu_coords_batch;
+
+/* Host batch in, host records out (synchronous). */
+pbgpu_status pbgpu_align_batch(pbgpu_aligner* al, const pbgpu_read_batch* batch,
+                               pbgpu_coords_batch** out);
+pbgpu_status pbgpu_coords_free(pbgpu_coords_batch* c);
+
+/* Device-resident path (used by bench.py: inputs resident in HBM). */
+pbgpu_status pbgpu_reads_upload(pbgpu_aligner* al, const pbgpu_read_batch* batch, pbgpu_reads** out);
+pbgpu_status pbgpu_reads_free(pbgpu_reads* r);
+/* Runs the whole GPU path on a resident batch; records stay on the device
+ * until pbgpu_download().  Synchronous. */
+pbgpu_status pbgpu_align_resident(pbgpu_aligner* al, const pbgpu_reads* reads);
+pbgpu_status pbgpu_download(pbgpu_aligner* al, pbgpu_coords_batch** out);
+
+/* Per-stage device time (HIP events on the aligner's stream, summed over
+ * launches since the last reset) and algorithmic counters. */
+typedef struct {
+  uint64_t n_batches;
+  uint64_t n_reads, n_bases;
+  uint64_t n_kmers;        /* valid PB k-mers */
+  uint64_t n_probes;       /* hash-bucket probes (64 B each) */
+  uint64_t n_kept;         /* k-mers kept after SSR/toggle/max-count */
+  uint64_t n_hits;         /* (pb_off, sr_off) hits grouped */
+  uint64_t n_chains;       /* (read, super-read) chains */
+  uint64_t n_lis_tests;    /* LIS predecessor tests */
+  uint64_t n_records;
+  double   ms_seed, ms_group, ms_lis, ms_records, ms_other;
+  uint64_t launches_seed, launches_group, launches_lis, launches_records;
+} pbgpu_stats;
+pbgpu_status pbgpu_aligner_get_stats(const pbgpu_aligner* al, pbgpu_stats* s);
+pbgpu_status pbgpu_aligner_reset_stats(pbgpu_aligner* al);
+
+/* --------------------------------------------------------------- output
+ * print_coords_header + print_coords (jf_aligner.cc:32-70): headers are the
+ * full FASTA header lines of the reads (name = up to the first whitespace),
+ * read_lens the read lengths (Rlen).  Text is malloc'd; free with
+ * pbgpu_free_text. */
+pbgpu_status pbgpu_format_coords(const pbgpu_index* ix, const pbgpu_coords_batch* c,
+                                 const char* const* read_headers, const uint64_t* read_lens,
+                                 int compact, int header, int zero_match, int threads,
+                                 char** text, uint64_t* len);
+void         pbgpu_free_text(char* text);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PBGPU_H */

@@ -1,0 +1,843 @@
+// pbgpu_api.hip -- host side of the C ABI (include/pbgpu.h): FASTA loading
+// with the reference's compact_dna rules, device index build, the per-batch
+// pipeline on one HIP stream, result download and coords formatting.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/pbgpu.h"
+#include "pbgpu_internal.h"
+
+namespace pbgpu {
+// kernels (pbgpu_kernels.hip)
+void launch_build_keys(IndexView ix, uint64_t N, uint64_t* keys, uint64_t* vals, hipStream_t st);
+void launch_runs(const uint64_t* keys, const uint64_t* uidx, uint64_t N, uint64_t* run_start, hipStream_t st);
+void launch_occ_fill(const uint64_t* vals, const uint64_t* uidx, const uint64_t* kpos, uint64_t N, uint64_t* occ,
+                     hipStream_t st);
+void launch_headers(const uint64_t* keys, const uint64_t* kpos, const uint64_t* run_start, uint64_t U, uint64_t* occ,
+                    ulonglong2* table, uint64_t bucket_mask, uint32_t k, hipStream_t st);
+void launch_seed(IndexView ix, const uint8_t* seq, const uint64_t* roff, uint32_t n_reads, AlignParamsDev P,
+                 KRec* krec, uint32_t* n_kept, uint32_t* thr, uint64_t* nhits, unsigned long long* stats, hipStream_t st);
+void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const uint32_t* n_kept, const uint32_t* thr,
+                  const uint64_t* hit_off, const uint32_t* read_list, uint32_t n_list, uint32_t hcap_log2,
+                  uint32_t* gtable, GroupOut O, unsigned long long* stats, hipStream_t st);
+int chain_cap_small();
+int chain_cap_large();
+void launch_chain_small(IndexView, AlignParamsDev, LisParams, const ChainDesc*, uint32_t, const int2*, const uint64_t*,
+                        ChainOut, hipStream_t);
+void launch_chain_large(IndexView, AlignParamsDev, LisParams, const ChainDesc*, uint32_t, const int2*, const uint64_t*,
+                        ChainOut, hipStream_t);
+void launch_chain_huge(IndexView, AlignParamsDev, LisParams, const ChainDesc*, uint32_t, const int2*, const uint64_t*,
+                       uint8_t*, ChainOut, hipStream_t);
+void launch_rec_hist(const Rec* recs, uint32_t n, uint32_t* per_read, hipStream_t st);
+void launch_rec_scatter(const Rec* recs, uint32_t n, const uint64_t* rec_off, uint32_t* cursor, uint32_t* order,
+                        hipStream_t st);
+int rec_sort_lcap();
+void launch_rec_sort(const Rec* recs, const uint64_t* rec_off, const uint32_t* order, uint32_t* gscratch,
+                     uint32_t n_reads, Rec* out, hipStream_t st);
+}  // namespace pbgpu
+
+using namespace pbgpu;
+
+// ------------------------------------------------------------ error state
+static thread_local std::string g_err;
+static pbgpu_status fail(pbgpu_status s, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return s;
+}
+struct hip_error : std::runtime_error {
+  hipError_t e;
+  hip_error(hipError_t e_, const char* what) : std::runtime_error(what), e(e_) {}
+};
+#define HIPCHK(x)                                                                                      \
+  do {                                                                                                 \
+    hipError_t _e = (x);                                                                               \
+    if (_e != hipSuccess) {                                                                            \
+      char _b[512];                                                                                    \
+      snprintf(_b, sizeof _b, "%s failed at %s:%d: %s", #x, __FILE__, __LINE__, hipGetErrorString(_e)); \
+      throw hip_error(_e, _b);                                                                         \
+    }                                                                                                  \
+  } while (0)
+struct bad_input : std::runtime_error { using std::runtime_error::runtime_error; };
+struct unsupported : std::runtime_error { using std::runtime_error::runtime_error; };
+
+#define API_TRY try {
+#define API_CATCH                                                                 \
+  }                                                                               \
+  catch (const hip_error& e) {                                                    \
+    return fail(e.e == hipErrorOutOfMemory ? PBGPU_ERR_NOMEM : PBGPU_ERR_DEVICE, "%s", e.what()); \
+  }                                                                               \
+  catch (const bad_input& e) { return fail(PBGPU_ERR_IO, "%s", e.what()); }       \
+  catch (const unsupported& e) { return fail(PBGPU_ERR_UNSUPPORTED, "%s", e.what()); } \
+  catch (const std::bad_alloc&) { return fail(PBGPU_ERR_NOMEM, "host allocation failed"); } \
+  catch (const std::exception& e) { return fail(PBGPU_ERR_INTERNAL, "%s", e.what()); }
+
+// --------------------------------------------------------- device buffer
+template <typename T>
+struct dbuf {
+  T* p = nullptr;
+  size_t n = 0;
+  dbuf() = default;
+  dbuf(const dbuf&) = delete;
+  dbuf& operator=(const dbuf&) = delete;
+  ~dbuf() { release(); }
+  void release() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
+  void alloc(size_t cnt) { release(); if (cnt) { HIPCHK(hipMalloc((void**)&p, cnt * sizeof(T))); n = cnt; } }
+  void ensure(size_t cnt) { if (cnt > n) alloc(std::max(cnt, n + n / 4)); }
+  size_t bytes() const { return n * sizeof(T); }
+};
+
+static void* temp_storage(dbuf<uint8_t>& t, size_t bytes) {
+  t.ensure(bytes ? bytes : 1);
+  return t.p;
+}
+
+// ------------------------------------------------------------------ names
+// super_read_name::parse (super_read_name.cc:74-90) -> unitig ids + oris
+static void parse_unitigs(const std::string& name, std::vector<uint32_t>& id, std::vector<uint8_t>& ori) {
+  id.clear(); ori.clear();
+  if (name.empty()) return;
+  size_t pn = 0;
+  for (;;) {
+    size_t us = name.find('_', pn);
+    const char* s = name.c_str() + pn;
+    char* end;
+    errno = 0;
+    unsigned long v = strtoul(s, &end, 10);
+    if (end == s || errno == ERANGE) { id.clear(); ori.clear(); return; }
+    const char oc = us != std::string::npos ? name[us - 1] : name[name.size() - 1];
+    id.push_back((uint32_t)v & 0x7fffffffu);
+    ori.push_back(oc == 'R');
+    if (us == std::string::npos) break;
+    pn = us + 1;
+  }
+}
+
+// ------------------------------------------------------------------ index
+struct pbgpu_index {
+  int device = 0;
+  uint32_t k = 0, psa_min = 0;
+  uint64_t n = 0, n_sr = 0, n_kmers = 0, n_occ = 0, buckets = 0;
+  double build_seconds = 0;
+  std::vector<std::string> name_fwd, name_bwd;
+  std::vector<uint64_t> sr_start;            // host copy
+  dbuf<uint64_t> text, d_sr_start, occ;
+  dbuf<ulonglong2> table;
+  dbuf<uint32_t> sr_uoff, sr_uids;
+  IndexView view() const {
+    IndexView v;
+    v.text = text.p; v.n = n; v.sr_start = d_sr_start.p; v.n_sr = (uint32_t)n_sr; v.k = k;
+    v.table = table.p; v.bucket_mask = buckets - 1; v.occ = occ.p; v.sr_uoff = sr_uoff.p; v.sr_uids = sr_uids.p;
+    return v;
+  }
+  uint64_t device_bytes() const {
+    return text.bytes() + d_sr_start.bytes() + occ.bytes() + table.bytes() + sr_uoff.bytes() + sr_uids.bytes();
+  }
+};
+
+// host-side text accumulation with compact_dna line encoding
+struct text_builder {
+  std::vector<uint64_t> words;  // MSB-first
+  uint64_t n = 0;
+  std::vector<uint64_t> starts{0};
+  std::vector<std::string> names;
+  void reserve(uint64_t bases) { words.reserve(bases / 32 + 2); }
+  inline void put(uint64_t code) {
+    const uint64_t w = n >> 5;
+    if (w >= words.size()) words.resize(std::max<size_t>(w + 1, words.size() * 2), 0);
+    words[w] |= code << (62 - 2 * (n & 31));
+    ++n;
+  }
+  // compact_dna::copy_from_str (compact_dna.hpp:89-136) on an 8-aligned line
+  void add_line(const char* s, size_t len) {
+    const size_t fast = len & ~(size_t)7;
+    for (size_t i = 0; i < fast; ++i) {
+      const unsigned b = (unsigned char)s[i];
+      put(((b >> 1) ^ (b >> 2)) & 3);
+    }
+    uint64_t c = 0;
+    for (size_t i = fast; i < len; ++i) {
+      switch (s[i]) {
+      case 'a': case 'A': c = 0; break;
+      case 'c': case 'C': c = 1; break;
+      case 'g': case 'G': c = 2; break;
+      case 't': case 'T': c = 3; break;
+      default: break;
+      }
+      put(c);
+    }
+  }
+  void end_record(const std::string& header, uint64_t start) {
+    if (n > start) { names.push_back(header); starts.push_back(n); }
+  }
+};
+
+static void load_fasta(const char* path, text_builder& tb) {
+  std::ifstream is(path);
+  if (!is.good()) throw bad_input(std::string("Can't open file ") + path);
+  int c = is.peek();
+  if (c != '>') throw bad_input(std::string("Not in fasta format: ") + path);
+  std::string line, header;
+  for (; c != EOF; c = is.peek()) {
+    std::getline(is, header);
+    const uint64_t start = tb.n;
+    for (c = is.peek(); c != '>' && c != EOF; c = is.peek()) {
+      std::getline(is, line);
+      tb.add_line(line.data(), line.size());
+    }
+    tb.end_record(header.substr(1), start);
+  }
+}
+
+static void build_device_index(pbgpu_index* ix, text_builder& tb) {
+  auto t0 = std::chrono::steady_clock::now();
+  HIPCHK(hipSetDevice(ix->device));
+  hipStream_t st;
+  HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  struct stream_guard { hipStream_t s; ~stream_guard() { (void)hipStreamDestroy(s); } } sg{st};
+  const uint32_t k = ix->k;
+  ix->n = tb.n;
+  ix->n_sr = tb.names.size();
+  ix->sr_start = tb.starts;
+  // names, bwd names (frag_info.hpp:22-35), unitig ids
+  ix->name_fwd = std::move(tb.names);
+  ix->name_bwd.resize(ix->n_sr);
+  std::vector<uint32_t> uoff(ix->n_sr + 1, 0), uids, id;
+  std::vector<uint8_t> ori;
+  for (uint64_t i = 0; i < ix->n_sr; ++i) {
+    parse_unitigs(ix->name_fwd[i], id, ori);
+    uoff[i] = (uint32_t)uids.size();
+    uids.insert(uids.end(), id.begin(), id.end());
+    if (!id.empty()) {
+      std::string b;
+      for (size_t t = 0; t < id.size(); ++t) {
+        const size_t s = id.size() - 1 - t;
+        b += (t ? "_" : "") + std::to_string(id[s]) + (ori[s] ? 'F' : 'R');
+      }
+      ix->name_bwd[i] = b;
+    } else {
+      ix->name_bwd[i] = ix->name_fwd[i];
+    }
+  }
+  uoff[ix->n_sr] = (uint32_t)uids.size();
+  tb.words.resize(tb.n / 32 + 2, 0);
+  ix->text.alloc(tb.words.size());
+  HIPCHK(hipMemcpy(ix->text.p, tb.words.data(), tb.words.size() * 8, hipMemcpyHostToDevice));
+  std::vector<uint64_t>().swap(tb.words);
+  ix->d_sr_start.alloc(ix->sr_start.size());
+  HIPCHK(hipMemcpy(ix->d_sr_start.p, ix->sr_start.data(), ix->sr_start.size() * 8, hipMemcpyHostToDevice));
+  ix->sr_uoff.alloc(uoff.size());
+  HIPCHK(hipMemcpy(ix->sr_uoff.p, uoff.data(), uoff.size() * 4, hipMemcpyHostToDevice));
+  ix->sr_uids.alloc(std::max<size_t>(uids.size(), 1));
+  if (!uids.empty()) HIPCHK(hipMemcpy(ix->sr_uids.p, uids.data(), uids.size() * 4, hipMemcpyHostToDevice));
+
+  const uint64_t N = ix->n >= k ? ix->n - k + 1 : 0;
+  IndexView v = ix->view();
+  if (N == 0) {
+    ix->buckets = 1;
+    ix->table.alloc(4);
+    HIPCHK(hipMemset(ix->table.p, 0xFF, ix->table.bytes()));
+    ix->occ.alloc(2);
+    ix->build_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return;
+  }
+  dbuf<uint64_t> k0, k1, v0, v1;
+  k0.alloc(N); k1.alloc(N); v0.alloc(N); v1.alloc(N);
+  launch_build_keys(v, N, k0.p, v0.p, st);
+  HIPCHK(hipGetLastError());
+  dbuf<uint8_t> tmp;
+  size_t tbytes = 0;
+  hipcub::DoubleBuffer<uint64_t> dk(k0.p, k1.p), dv(v0.p, v1.p);
+  HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tbytes, dk, dv, N, 0, (int)(2 * k + 1), st));
+  HIPCHK(hipcub::DeviceRadixSort::SortPairs(temp_storage(tmp, tbytes), tbytes, dk, dv, N, 0, (int)(2 * k + 1), st));
+  uint64_t* keys = dk.Current();
+  uint64_t* vals = dv.Current();
+  uint64_t* spare_k = dk.Alternate();
+  uint64_t* spare_v = dv.Alternate();
+  // uidx = inclusive scan of run heads (into spare_k), kpos = exclusive scan of keep (N+1, into a new buffer)
+  struct HeadOp {
+    const uint64_t* keys;
+    __host__ __device__ uint64_t operator()(const uint64_t& i) const {
+      return (i == 0 || (keys[i] >> 1) != (keys[i - 1] >> 1)) ? 1ull : 0ull;
+    }
+  };
+  struct KeepOp {
+    const uint64_t* vals; uint64_t N;
+    __host__ __device__ uint64_t operator()(const uint64_t& i) const { return (i < N && vals[i] != ~0ull) ? 1ull : 0ull; }
+  };
+  hipcub::CountingInputIterator<uint64_t> cnt(0);
+  hipcub::TransformInputIterator<uint64_t, HeadOp, hipcub::CountingInputIterator<uint64_t>> heads(cnt, HeadOp{keys});
+  uint64_t* uidx = spare_k;
+  tbytes = 0;
+  HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tbytes, heads, uidx, N, st));
+  HIPCHK(hipcub::DeviceScan::InclusiveSum(temp_storage(tmp, tbytes), tbytes, heads, uidx, N, st));
+  dbuf<uint64_t> kpos;
+  kpos.alloc(N + 1);
+  hipcub::TransformInputIterator<uint64_t, KeepOp, hipcub::CountingInputIterator<uint64_t>> keeps(cnt, KeepOp{vals, N});
+  tbytes = 0;
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tbytes, keeps, kpos.p, N + 1, st));
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(temp_storage(tmp, tbytes), tbytes, keeps, kpos.p, N + 1, st));
+  uint64_t U = 0, kept = 0;
+  HIPCHK(hipMemcpyAsync(&U, uidx + N - 1, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&kept, kpos.p + N, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  uint64_t* run_start = spare_v;  // U + 1 <= N + 1 ... spare_v has N entries; U < N unless all distinct
+  dbuf<uint64_t> rs_extra;
+  if (U + 1 > N) { rs_extra.alloc(U + 1); run_start = rs_extra.p; }
+  launch_runs(keys, uidx, N, run_start, st);
+  HIPCHK(hipMemcpyAsync(run_start + U, &N, 8, hipMemcpyHostToDevice, st));
+  ix->n_kmers = U;
+  ix->n_occ = kept;
+  ix->occ.alloc(2 * U + kept);
+  uint64_t buckets = 1;
+  while (buckets * 2 < U) buckets <<= 1;  // slots = 4*buckets >= 2U: load <= 0.5
+  ix->buckets = buckets;
+  ix->table.alloc(4 * buckets);
+  HIPCHK(hipMemsetAsync(ix->table.p, 0xFF, ix->table.bytes(), st));
+  launch_occ_fill(vals, uidx, kpos.p, N, ix->occ.p, st);
+  launch_headers(keys, kpos.p, run_start, U, ix->occ.p, ix->table.p, buckets - 1, k, st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(st));
+  ix->build_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+static pbgpu_status index_common(const pbgpu_index_params* p) {
+  if (!p) return fail(PBGPU_ERR_INVALID, "null params");
+  if (p->k < 2 || p->k > 31) return fail(PBGPU_ERR_UNSUPPORTED, "k=%u outside [2,31]", p->k);
+  if (p->psa_min >= p->k)
+    return fail(PBGPU_ERR_UNSUPPORTED,
+                "psa_min (%u) >= k (%u): the reference's hit order then depends on thread timing (mer_sa_imp.hpp:247)",
+                p->psa_min, p->k);
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(PBGPU_ERR_DEVICE, "no HIP device available");
+  if (p->device < 0 || p->device >= ndev) return fail(PBGPU_ERR_INVALID, "device %d out of range", p->device);
+  return PBGPU_OK;
+}
+
+extern "C" {
+
+int pbgpu_abi_version(void) { return PBGPU_ABI_VERSION; }
+const char* pbgpu_last_error(void) { return g_err.c_str(); }
+int pbgpu_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+pbgpu_status pbgpu_index_build_fasta(const char* const* paths, size_t n_paths, const pbgpu_index_params* params,
+                                     pbgpu_index** out) {
+  if (!out || (!paths && n_paths)) return fail(PBGPU_ERR_INVALID, "null argument");
+  pbgpu_status s = index_common(params);
+  if (s != PBGPU_OK) return s;
+  API_TRY
+  text_builder tb;
+  for (size_t i = 0; i < n_paths; ++i) load_fasta(paths[i], tb);
+  std::unique_ptr<pbgpu_index> ix(new pbgpu_index);
+  ix->device = params->device; ix->k = params->k; ix->psa_min = params->psa_min;
+  build_device_index(ix.get(), tb);
+  *out = ix.release();
+  return PBGPU_OK;
+  API_CATCH
+}
+
+pbgpu_status pbgpu_index_build(const char* const* names, const char* const* seqs, const uint64_t* lens, size_t n,
+                               const pbgpu_index_params* params, pbgpu_index** out) {
+  if (!out || (n && (!names || !seqs || !lens))) return fail(PBGPU_ERR_INVALID, "null argument");
+  pbgpu_status s = index_common(params);
+  if (s != PBGPU_OK) return s;
+  API_TRY
+  text_builder tb;
+  uint64_t total = 0;
+  for (size_t i = 0; i < n; ++i) total += lens[i];
+  tb.reserve(total);
+  tb.words.assign(total / 32 + 2, 0);
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t start = tb.n;
+    tb.add_line(seqs[i], lens[i]);
+    tb.end_record(names[i], start);
+  }
+  std::unique_ptr<pbgpu_index> ix(new pbgpu_index);
+  ix->device = params->device; ix->k = params->k; ix->psa_min = params->psa_min;
+  build_device_index(ix.get(), tb);
+  *out = ix.release();
+  return PBGPU_OK;
+  API_CATCH
+}
+
+pbgpu_status pbgpu_index_free(pbgpu_index* ix) {
+  if (!ix) return PBGPU_OK;
+  (void)hipSetDevice(ix->device);
+  delete ix;
+  return PBGPU_OK;
+}
+
+pbgpu_status pbgpu_index_get_info(const pbgpu_index* ix, pbgpu_index_info* info) {
+  if (!ix || !info) return fail(PBGPU_ERR_INVALID, "null argument");
+  info->n_sr = ix->n_sr; info->text_len = ix->n; info->n_kmers = ix->n_kmers; info->n_occurrences = ix->n_occ;
+  info->table_buckets = ix->buckets; info->device_bytes = ix->device_bytes(); info->build_seconds = ix->build_seconds;
+  return PBGPU_OK;
+}
+const char* pbgpu_index_sr_name(const pbgpu_index* ix, uint32_t sr, int bwd) {
+  if (!ix || sr >= ix->n_sr) return nullptr;
+  return bwd ? ix->name_bwd[sr].c_str() : ix->name_fwd[sr].c_str();
+}
+uint32_t pbgpu_index_sr_len(const pbgpu_index* ix, uint32_t sr) {
+  if (!ix || sr >= ix->n_sr) return 0;
+  return (uint32_t)(ix->sr_start[sr + 1] - ix->sr_start[sr]);
+}
+
+void pbgpu_align_params_default(pbgpu_align_params* p) {
+  memset(p, 0, sizeof(*p));
+  p->k = 17; p->stretch_factor = 1.3; p->stretch_constant = 10; p->stretch_cap = 10000; p->window_size = 1;
+  p->max_count = 5000; p->mers_matching = 0; p->bases_matching = 17;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- aligner
+struct pbgpu_reads {
+  pbgpu_aligner* owner = nullptr;
+  uint64_t n_reads = 0, n_bases = 0;
+  std::vector<uint64_t> h_off;
+  dbuf<uint8_t> seq;
+  dbuf<uint64_t> off;
+};
+
+struct pbgpu_aligner {
+  const pbgpu_index* ix = nullptr;
+  pbgpu_align_params prm{};
+  AlignParamsDev P{};
+  LisParams lp{};
+  hipStream_t st = nullptr;
+  dbuf<int32_t> ul;
+  // per-batch buffers
+  dbuf<KRec> krec;
+  dbuf<uint32_t> n_kept, thr, rec_per_read, rec_cursor, order, sort_scratch, ovf_reads, counters;
+  dbuf<uint64_t> nhits, hit_off, rec_off, huge_elems;
+  dbuf<int2> hits;
+  dbuf<ChainDesc> chains[3];
+  dbuf<Rec> recs, recs_sorted;
+  dbuf<int32_t> info_m, info_b;
+  dbuf<uint8_t> tmp, huge_scratch;
+  dbuf<uint32_t> gtable;
+  dbuf<unsigned long long> stats, info_count;
+  // last result
+  uint64_t last_reads = 0, last_records = 0, last_info = 0;
+  bool have_result = false;
+  // stats
+  pbgpu_stats acc{};
+  hipEvent_t ev[8]{};
+};
+
+static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd);
+
+extern "C" {
+
+pbgpu_status pbgpu_aligner_create(const pbgpu_index* ix, const pbgpu_align_params* params, pbgpu_aligner** out) {
+  if (!ix || !params || !out) return fail(PBGPU_ERR_INVALID, "null argument");
+  if (params->k != ix->k) return fail(PBGPU_ERR_INVALID, "aligner k (%u) != index k (%u)", params->k, ix->k);
+  if (params->max_count <= 0)
+    return fail(PBGPU_ERR_INVALID, "max_count must be > 0 (0 means INT_MAX upstream, which is undefined behaviour)");
+  if (params->n_unitigs && !params->forward)
+    return fail(PBGPU_ERR_INVALID, "Forward flag must be used if passing unitigs lengths");
+  if (params->fine_k) return fail(PBGPU_ERR_UNSUPPORTED, "fine aligner (-F) is not implemented yet");
+  if (params->unitigs_k && !params->unitig_lengths)
+    return fail(PBGPU_ERR_INVALID, "unitigs_k given without unitig lengths");
+  API_TRY
+  HIPCHK(hipSetDevice(ix->device));
+  std::unique_ptr<pbgpu_aligner> al(new pbgpu_aligner);
+  al->ix = ix;
+  al->prm = *params;
+  al->prm.unitig_lengths = nullptr;
+  if (params->unitigs_k && params->n_unitigs) {
+    al->ul.alloc(params->n_unitigs);
+    HIPCHK(hipMemcpy(al->ul.p, params->unitig_lengths, params->n_unitigs * 4, hipMemcpyHostToDevice));
+  }
+  AlignParamsDev& P = al->P;
+  P.k = params->k; P.window = params->window_size;
+  P.a = params->stretch_factor; P.b = params->stretch_constant; P.C = params->stretch_cap;
+  P.forward = params->forward; P.max_match = params->max_match; P.max_count = params->max_count;
+  P.mers_factor = params->mers_matching / 100.0; P.bases_factor = params->bases_matching / 100.0;
+  P.unitigs_k = params->unitigs_k && params->n_unitigs ? params->unitigs_k : 0;
+  P.ul = al->ul.p; P.n_ul = params->unitigs_k ? params->n_unitigs : 0;
+  al->lp.W = params->window_size; al->lp.a = params->stretch_factor; al->lp.b = params->stretch_constant;
+  al->lp.C = params->stretch_cap; al->lp.mer_all = 0; al->lp.seq_all = 0;
+  HIPCHK(hipStreamCreateWithFlags(&al->st, hipStreamNonBlocking));
+  for (auto& e : al->ev) HIPCHK(hipEventCreate(&e));
+  al->stats.alloc(ST_N);
+  al->info_count.alloc(1);
+  al->counters.alloc(16);
+  *out = al.release();
+  return PBGPU_OK;
+  API_CATCH
+}
+
+pbgpu_status pbgpu_aligner_free(pbgpu_aligner* al) {
+  if (!al) return PBGPU_OK;
+  (void)hipSetDevice(al->ix->device);
+  for (auto& e : al->ev) if (e) (void)hipEventDestroy(e);
+  if (al->st) (void)hipStreamDestroy(al->st);
+  delete al;
+  return PBGPU_OK;
+}
+
+pbgpu_status pbgpu_reads_upload(pbgpu_aligner* al, const pbgpu_read_batch* b, pbgpu_reads** out) {
+  if (!al || !b || !out || (b->n_reads && (!b->offsets || !b->seq))) return fail(PBGPU_ERR_INVALID, "null argument");
+  API_TRY
+  HIPCHK(hipSetDevice(al->ix->device));
+  std::unique_ptr<pbgpu_reads> r(new pbgpu_reads);
+  r->owner = al;
+  r->n_reads = b->n_reads;
+  r->h_off.resize(b->n_reads + 1);
+  const uint64_t o0 = b->n_reads ? b->offsets[0] : 0;
+  for (uint64_t i = 0; i <= b->n_reads; ++i) {
+    r->h_off[i] = b->n_reads ? b->offsets[i] - o0 : 0;
+    if (i && r->h_off[i] < r->h_off[i - 1]) throw std::invalid_argument("offsets must be non-decreasing");
+  }
+  r->n_bases = r->h_off[b->n_reads];
+  if (r->n_bases > 0xFFFFFFFFull * 8) throw unsupported("batch too large");
+  r->seq.alloc(r->n_bases + 1);
+  if (r->n_bases) HIPCHK(hipMemcpy(r->seq.p, b->seq + o0, r->n_bases, hipMemcpyHostToDevice));
+  r->off.alloc(b->n_reads + 1);
+  HIPCHK(hipMemcpy(r->off.p, r->h_off.data(), (b->n_reads + 1) * 8, hipMemcpyHostToDevice));
+  *out = r.release();
+  return PBGPU_OK;
+  API_CATCH
+}
+
+pbgpu_status pbgpu_reads_free(pbgpu_reads* r) {
+  if (!r) return PBGPU_OK;
+  (void)hipSetDevice(r->owner->ix->device);
+  delete r;
+  return PBGPU_OK;
+}
+
+pbgpu_status pbgpu_align_resident(pbgpu_aligner* al, const pbgpu_reads* rd) {
+  if (!al || !rd) return fail(PBGPU_ERR_INVALID, "null argument");
+  if (rd->owner != al) return fail(PBGPU_ERR_INVALID, "reads were uploaded for another aligner");
+  API_TRY
+  HIPCHK(hipSetDevice(al->ix->device));
+  aligner_pipeline(al, rd);
+  return PBGPU_OK;
+  API_CATCH
+}
+
+}  // extern "C"
+
+static float ev_ms(hipEvent_t a, hipEvent_t b) {
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, a, b));
+  return ms;
+}
+
+static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
+  const pbgpu_index* ix = al->ix;
+  const IndexView v = ix->view();
+  hipStream_t st = al->st;
+  const uint32_t n = (uint32_t)rd->n_reads;
+  al->have_result = false;
+  al->last_reads = n;
+  al->acc.n_batches++;
+  al->acc.n_reads += n;
+  al->acc.n_bases += rd->n_bases;
+  al->rec_off.ensure(n + 1);
+  if (n == 0) {
+    HIPCHK(hipMemsetAsync(al->rec_off.p, 0, 8, st));
+    HIPCHK(hipStreamSynchronize(st));
+    al->last_records = 0; al->last_info = 0; al->have_result = true;
+    return;
+  }
+  HIPCHK(hipMemsetAsync(al->stats.p, 0, ST_N * 8, st));
+  // ---------------------------------------------------------------- seed
+  al->krec.ensure(rd->n_bases + 1);
+  al->n_kept.ensure(n); al->thr.ensure(n); al->nhits.ensure(n); al->hit_off.ensure(n + 1);
+  HIPCHK(hipEventRecord(al->ev[0], st));
+  launch_seed(v, rd->seq.p, rd->off.p, n, al->P, al->krec.p, al->n_kept.p, al->thr.p, al->nhits.p, al->stats.p, st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(al->ev[1], st));
+  {
+    struct HitOp {
+      const uint64_t* h; uint64_t n;
+      __host__ __device__ uint64_t operator()(const uint64_t& i) const { return i < n ? h[i] : 0ull; }
+    };
+    hipcub::CountingInputIterator<uint64_t> cnt(0);
+    hipcub::TransformInputIterator<uint64_t, HitOp, hipcub::CountingInputIterator<uint64_t>> in(cnt, HitOp{al->nhits.p, n});
+    size_t tb = 0;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, al->hit_off.p, (uint64_t)n + 1, st));
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(temp_storage(al->tmp, tb), tb, in, al->hit_off.p, (uint64_t)n + 1, st));
+  }
+  uint64_t H = 0;
+  HIPCHK(hipMemcpyAsync(&H, al->hit_off.p + n, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  // --------------------------------------------------------------- group
+  al->hits.ensure(H + 1);
+  const uint32_t hcap_log2 = 11;
+  const uint64_t chain_bound = std::min<uint64_t>(H, (uint64_t)n << hcap_log2) + 1;
+  const uint32_t cap_small = (uint32_t)chain_cap_small(), cap_large = (uint32_t)chain_cap_large();
+  al->chains[0].ensure(chain_bound);
+  const uint64_t lg_bound = std::min<uint64_t>(chain_bound, H / (cap_small + 1) + 1);
+  al->chains[1].ensure(lg_bound);
+  al->chains[2].ensure(std::min<uint64_t>(chain_bound, H / (cap_large + 1) + 1));
+  al->ovf_reads.ensure(n);
+  al->huge_elems.ensure(1);
+  GroupOut O;
+  O.hits = al->hits.p;
+  for (int c = 0; c < 3; ++c) { O.chains[c] = al->chains[c].p; O.chain_cap[c] = (uint32_t)std::min<uint64_t>(al->chains[c].n, 0xFFFFFFFFu); }
+  O.chain_count = al->counters.p;       // [0..2]
+  O.n_overflow = al->counters.p + 3;
+  O.huge_elems = al->huge_elems.p;
+  O.cap_small = cap_small; O.cap_large = cap_large;
+  O.overflow_reads = al->ovf_reads.p;
+  HIPCHK(hipMemsetAsync(al->counters.p, 0, 16 * 4, st));
+  HIPCHK(hipMemsetAsync(al->huge_elems.p, 0, 8, st));
+  launch_group(v, al->krec.p, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, nullptr, n, hcap_log2, nullptr, O,
+               al->stats.p, st);
+  HIPCHK(hipGetLastError());
+  uint32_t cnt[4];
+  HIPCHK(hipMemcpyAsync(cnt, al->counters.p, 16, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (cnt[3]) {  // reads with more super-reads than the LDS table holds
+    std::vector<uint32_t> ovf(cnt[3]);
+    HIPCHK(hipMemcpy(ovf.data(), al->ovf_reads.p, cnt[3] * 4, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> hh(n);
+    HIPCHK(hipMemcpy(hh.data(), al->nhits.p, n * 8, hipMemcpyDeviceToHost));
+    uint64_t mx = 0;
+    for (uint32_t r : ovf) mx = std::max(mx, hh[r]);
+    uint32_t lg = hcap_log2 + 1;
+    while ((1ull << lg) < 2 * mx) ++lg;
+    // process overflowed reads in groups bounded by scratch size (<= 1 GiB of table)
+    const uint64_t per = 16ull << lg;
+    const uint32_t group = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(cnt[3], (1ull << 30) / per));
+    al->gtable.ensure((uint64_t)group * 4 << lg);
+    for (uint32_t s = 0; s < cnt[3]; s += group) {
+      const uint32_t m = std::min(group, cnt[3] - s);
+      launch_group(v, al->krec.p, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, al->ovf_reads.p + s, m, lg,
+                   al->gtable.p, O, al->stats.p, st);
+      HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipMemcpyAsync(cnt, al->counters.p, 16, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  for (int c = 0; c < 3; ++c)
+    if (cnt[c] > O.chain_cap[c]) throw std::runtime_error("chain descriptor capacity exceeded");
+  HIPCHK(hipEventRecord(al->ev[2], st));
+  // --------------------------------------------------------------- chains
+  uint64_t huge_units = 0;
+  HIPCHK(hipMemcpy(&huge_units, al->huge_elems.p, 8, hipMemcpyDeviceToHost));
+  al->huge_scratch.ensure(huge_units * 48 + 64);
+  const uint64_t n_chains = (uint64_t)cnt[0] + cnt[1] + cnt[2];
+  uint64_t rec_cap = al->P.max_match ? n_chains * 2 + 1024 : n_chains + 1;
+  uint64_t info_cap = al->P.unitigs_k ? std::max<uint64_t>(1024, rec_cap * 16) : 1;
+  for (int attempt = 0;; ++attempt) {
+    al->recs.ensure(rec_cap);
+    al->info_m.ensure(info_cap); al->info_b.ensure(info_cap);
+    HIPCHK(hipMemsetAsync(al->counters.p + 4, 0, 4, st));
+    HIPCHK(hipMemsetAsync(al->info_count.p, 0, 8, st));
+    HIPCHK(hipMemsetAsync(al->stats.p + ST_REC_OVERFLOW, 0, 8, st));
+    HIPCHK(hipMemsetAsync(al->stats.p + ST_LIS_TESTS, 0, 8, st));
+    ChainOut CO;
+    CO.recs = al->recs.p; CO.rec_count = al->counters.p + 4; CO.rec_cap = (uint32_t)std::min<uint64_t>(al->recs.n, 0xFFFFFFFFu);
+    CO.info_m = al->info_m.p; CO.info_b = al->info_b.p; CO.info_count = al->info_count.p; CO.info_cap = al->info_m.n;
+    CO.stats = al->stats.p;
+    launch_chain_small(v, al->P, al->lp, al->chains[0].p, cnt[0], al->hits.p, rd->off.p, CO, st);
+    launch_chain_large(v, al->P, al->lp, al->chains[1].p, cnt[1], al->hits.p, rd->off.p, CO, st);
+    launch_chain_huge(v, al->P, al->lp, al->chains[2].p, cnt[2], al->hits.p, rd->off.p, al->huge_scratch.p, CO, st);
+    HIPCHK(hipGetLastError());
+    uint32_t nrec = 0;
+    unsigned long long ninfo = 0, ovf = 0;
+    HIPCHK(hipMemcpyAsync(&nrec, al->counters.p + 4, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&ninfo, al->info_count.p, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&ovf, al->stats.p + ST_REC_OVERFLOW, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (ovf == 0 && nrec <= al->recs.n) { al->last_records = nrec; al->last_info = ninfo; break; }
+    if (attempt > 8) throw std::runtime_error("record buffer growth did not converge");
+    rec_cap = std::max<uint64_t>(rec_cap * 2, (uint64_t)nrec + 1024);
+    info_cap = std::max<uint64_t>(info_cap * 2, ninfo + 1024);
+  }
+  HIPCHK(hipEventRecord(al->ev[3], st));
+  // ------------------------------------------------------------- records
+  const uint32_t nrec = (uint32_t)al->last_records;
+  al->rec_per_read.ensure(n); al->rec_cursor.ensure(n);
+  HIPCHK(hipMemsetAsync(al->rec_per_read.p, 0, n * 4, st));
+  HIPCHK(hipMemsetAsync(al->rec_cursor.p, 0, n * 4, st));
+  launch_rec_hist(al->recs.p, nrec, al->rec_per_read.p, st);
+  {
+    struct RecOp {
+      const uint32_t* c; uint64_t n;
+      __host__ __device__ uint64_t operator()(const uint64_t& i) const { return i < n ? (uint64_t)c[i] : 0ull; }
+    };
+    hipcub::CountingInputIterator<uint64_t> cnt0(0);
+    hipcub::TransformInputIterator<uint64_t, RecOp, hipcub::CountingInputIterator<uint64_t>> in(cnt0, RecOp{al->rec_per_read.p, n});
+    size_t tb = 0;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, al->rec_off.p, (uint64_t)n + 1, st));
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(temp_storage(al->tmp, tb), tb, in, al->rec_off.p, (uint64_t)n + 1, st));
+  }
+  al->order.ensure(nrec + 1);
+  al->sort_scratch.ensure(2ull * nrec + 2);
+  al->recs_sorted.ensure(nrec + 1);
+  launch_rec_scatter(al->recs.p, nrec, al->rec_off.p, al->rec_cursor.p, al->order.p, st);
+  launch_rec_sort(al->recs.p, al->rec_off.p, al->order.p, al->sort_scratch.p, n, al->recs_sorted.p, st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(al->ev[4], st));
+  unsigned long long sv[ST_N];
+  HIPCHK(hipMemcpyAsync(sv, al->stats.p, sizeof sv, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  al->acc.n_kmers += sv[ST_KMERS]; al->acc.n_probes += sv[ST_PROBES]; al->acc.n_kept += sv[ST_KEPT];
+  al->acc.n_hits += sv[ST_HITS]; al->acc.n_chains += sv[ST_CHAINS]; al->acc.n_lis_tests += sv[ST_LIS_TESTS];
+  al->acc.n_records += nrec;
+  al->acc.ms_seed += ev_ms(al->ev[0], al->ev[1]);
+  al->acc.ms_group += ev_ms(al->ev[1], al->ev[2]);
+  al->acc.ms_lis += ev_ms(al->ev[2], al->ev[3]);
+  al->acc.ms_records += ev_ms(al->ev[3], al->ev[4]);
+  al->acc.launches_seed += 1; al->acc.launches_group += 1; al->acc.launches_lis += 1; al->acc.launches_records += 1;
+  al->have_result = true;
+}
+
+// ---------------------------------------------------------------- download
+struct coords_holder {
+  pbgpu_coords_batch c{};
+  std::vector<uint64_t> off;
+  std::vector<pbgpu_record> recs;
+  std::vector<int32_t> km, kb;
+};
+
+extern "C" {
+
+pbgpu_status pbgpu_download(pbgpu_aligner* al, pbgpu_coords_batch** out) {
+  if (!al || !out) return fail(PBGPU_ERR_INVALID, "null argument");
+  if (!al->have_result) return fail(PBGPU_ERR_INVALID, "no result to download");
+  API_TRY
+  HIPCHK(hipSetDevice(al->ix->device));
+  std::unique_ptr<coords_holder> h(new coords_holder);
+  const uint64_t n = al->last_reads, nr = al->last_records;
+  h->off.resize(n + 1);
+  HIPCHK(hipMemcpy(h->off.data(), al->rec_off.p, (n + 1) * 8, hipMemcpyDeviceToHost));
+  h->recs.resize(nr);
+  static_assert(sizeof(pbgpu_record) == sizeof(Rec), "record layout");
+  if (nr) HIPCHK(hipMemcpy(h->recs.data(), al->recs_sorted.p, nr * sizeof(Rec), hipMemcpyDeviceToHost));
+  if (al->last_info) {
+    h->km.resize(al->last_info); h->kb.resize(al->last_info);
+    HIPCHK(hipMemcpy(h->km.data(), al->info_m.p, al->last_info * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(h->kb.data(), al->info_b.p, al->last_info * 4, hipMemcpyDeviceToHost));
+  }
+  h->c.n_reads = n; h->c.n_records = nr; h->c.read_offsets = h->off.data(); h->c.records = h->recs.data();
+  h->c.n_info = al->last_info; h->c.kmers_info = h->km.data(); h->c.bases_info = h->kb.data();
+  *out = &h.release()->c;
+  return PBGPU_OK;
+  API_CATCH
+}
+
+pbgpu_status pbgpu_coords_free(pbgpu_coords_batch* c) {
+  if (!c) return PBGPU_OK;
+  delete reinterpret_cast<coords_holder*>(c);  // c is the first member
+  return PBGPU_OK;
+}
+
+pbgpu_status pbgpu_align_batch(pbgpu_aligner* al, const pbgpu_read_batch* b, pbgpu_coords_batch** out) {
+  pbgpu_reads* r = nullptr;
+  pbgpu_status s = pbgpu_reads_upload(al, b, &r);
+  if (s != PBGPU_OK) return s;
+  s = pbgpu_align_resident(al, r);
+  if (s == PBGPU_OK) s = pbgpu_download(al, out);
+  pbgpu_reads_free(r);
+  return s;
+}
+
+pbgpu_status pbgpu_aligner_get_stats(const pbgpu_aligner* al, pbgpu_stats* s) {
+  if (!al || !s) return fail(PBGPU_ERR_INVALID, "null argument");
+  *s = al->acc;
+  return PBGPU_OK;
+}
+pbgpu_status pbgpu_aligner_reset_stats(pbgpu_aligner* al) {
+  if (!al) return fail(PBGPU_ERR_INVALID, "null argument");
+  memset(&al->acc, 0, sizeof al->acc);
+  return PBGPU_OK;
+}
+
+// print_coords (jf_aligner.cc:41-70).  std::ostream << double with default
+// flags is libstdc++'s "%.*g" at precision 6.
+pbgpu_status pbgpu_format_coords(const pbgpu_index* ix, const pbgpu_coords_batch* c, const char* const* hdrs,
+                                 const uint64_t* lens, int compact, int header, int zero_match, int threads,
+                                 char** text, uint64_t* len) {
+  if (!ix || !c || !text || !len || (c->n_reads && (!hdrs || !lens))) return fail(PBGPU_ERR_INVALID, "null argument");
+  API_TRY
+  const uint64_t n = c->n_reads;
+  if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
+  std::vector<std::string> parts(std::max<uint64_t>(1, (uint64_t)threads * 4));
+  const uint64_t np = parts.size();
+  std::atomic<uint64_t> next(0);
+  auto work = [&]() {
+    char buf[512];
+    for (;;) {
+      const uint64_t pi = next.fetch_add(1);
+      if (pi >= np) break;
+      const uint64_t r0 = n * pi / np, r1 = n * (pi + 1) / np;
+      std::string& o = parts[pi];
+      for (uint64_t r = r0; r < r1; ++r) {
+        const uint64_t a = c->read_offsets[r], b = c->read_offsets[r + 1];
+        if (a == b && !zero_match) continue;
+        const char* h = hdrs[r];
+        const size_t nl = strcspn(h, " \t\n\v\f\r");
+        if (compact) {
+          o += '>'; o += std::to_string(b - a); o += ' '; o.append(h, nl); o += '\n';
+        }
+        for (uint64_t i = a; i < b; ++i) {
+          const pbgpu_record& R = c->records[i];
+          if (!compact) { o.append(h, nl); o += ' '; }
+          int w = snprintf(buf, sizeof buf, "%d %d %d %d %d %u %u %u %u %llu %u %.6g %.6g %.6g ", R.rs, R.re, R.qs, R.qe,
+                           R.nb_mers, R.pb_cons, R.sr_cons, R.pb_cover, R.sr_cover, (unsigned long long)lens[r], R.ql,
+                           R.stretch, R.offset, R.avg_err);
+          o.append(buf, (size_t)w);
+          o += (R.flags & 2u) ? ix->name_bwd[R.sr_index] : ix->name_fwd[R.sr_index];
+          for (uint32_t t = 0; t < R.n_info; ++t) {
+            w = snprintf(buf, sizeof buf, " %d:%d", c->kmers_info[R.info_offset + t], c->bases_info[R.info_offset + t]);
+            o.append(buf, (size_t)w);
+          }
+          o += '\n';
+        }
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < threads; ++t) th.emplace_back(work);
+  work();
+  for (auto& t : th) t.join();
+  std::string hdr;
+  if (header)
+    hdr = std::string("Rstart Rend Qstart Qend Nmers Rcons Qcons Rcover Qcover Rlen Qlen Stretch Offset Err") +
+          (compact ? "" : " Rname") + " Qname\n";
+  uint64_t total = hdr.size();
+  for (auto& p : parts) total += p.size();
+  char* t = (char*)malloc(total + 1);
+  if (!t) return fail(PBGPU_ERR_NOMEM, "host allocation failed");
+  uint64_t o = 0;
+  memcpy(t, hdr.data(), hdr.size()); o += hdr.size();
+  for (auto& p : parts) { memcpy(t + o, p.data(), p.size()); o += p.size(); }
+  t[o] = 0;
+  *text = t; *len = o;
+  return PBGPU_OK;
+  API_CATCH
+}
+
+void pbgpu_free_text(char* text) { free(text); }
+
+}  // extern "C"

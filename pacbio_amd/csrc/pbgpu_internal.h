@@ -1,0 +1,107 @@
+// pbgpu_internal.h -- shared device/host layouts of the MI355X jf_aligner path.
+//
+// HBM layout (resident index, built once per device):
+//   text     : uint64[ceil(n/32)+2]  2-bit bases, MSB-first within a word
+//              (word w holds bases 32w..32w+31, base 32w in bits 63..62)
+//   sr_start : uint64[n_sr+1]        global text offset of every super-read
+//   table    : ulonglong2[4*buckets] 64-byte buckets of 4 {key, payload} slots,
+//              key = canonical k-mer code (EMPTY = ~0), payload =
+//              occ_ptr << 24 | min(count_total, 2^24-1)
+//   occ      : uint64[]              per canonical k-mer: 2 header words
+//              {count_total | pal<<32, nA | nB<<32} then nA occurrences of the
+//              canonical k-mer and nB of its reverse complement, each
+//              (sr_id << 32 | 1-based offset), descending text position
+//              (the SA tie-break of mer_sa_imp.hpp:363).
+#pragma once
+#include <stdint.h>
+#include <hip/hip_runtime.h>
+
+namespace pbgpu {
+
+constexpr uint64_t EMPTY_KEY = ~0ull;
+constexpr uint32_t SAT_COUNT = 0xFFFFFFu;
+constexpr uint32_t INVALID_UNITIG = 0x7fffffffu;
+
+struct IndexView {
+  const uint64_t* text;
+  uint64_t n;
+  const uint64_t* sr_start;   // n_sr + 1
+  uint32_t n_sr;
+  uint32_t k;
+  const ulonglong2* table;    // 4 slots per bucket
+  uint64_t bucket_mask;
+  const uint64_t* occ;
+  const uint32_t* sr_uoff;    // n_sr + 1 offsets into sr_uids
+  const uint32_t* sr_uids;    // unitig ids of the fwd name (super_read_name::unitig_id)
+};
+
+struct AlignParamsDev {
+  uint32_t k;
+  uint32_t window;
+  double a, b, C;          // affine_capped(stretch_factor, stretch_constant, stretch_cap)
+  int32_t forward, max_match;
+  int32_t max_count;       // never 0 here
+  double mers_factor;      // M / 100
+  double bases_factor;     // B / 100
+  uint32_t unitigs_k;
+  const int32_t* ul;
+  uint64_t n_ul;
+};
+
+// kept k-mer record, one per kept PB k-mer, in read order
+struct KRec {
+  int32_t pb_off;       // 1-based start of the k-mer in the read
+  uint32_t count;       // total occurrences of m and rm (incl. crossing)
+  uint64_t occ_ptr;     // header index in occ; bit 63 = is_canonical (m < rm)
+};
+
+struct ChainDesc {
+  uint32_t read, sr;
+  uint32_t nf, nb;
+  uint64_t hit_base;     // first fwd hit; bwd hits follow at hit_base + nf
+  uint64_t scratch;      // element offset into the large-path scratch
+};
+
+struct Rec {
+  int32_t rs, re, qs, qe, nb_mers;
+  uint32_t pb_cons, sr_cons, pb_cover, sr_cover;
+  uint32_t ql, sr, read, emit, flags, n_info, reserved;
+  uint64_t info_off;
+  double stretch, offset, avg_err;
+};
+static_assert(sizeof(Rec) == 96, "Rec layout must match pbgpu_record");
+
+enum StatSlot {
+  ST_KMERS = 0, ST_PROBES, ST_KEPT, ST_HITS, ST_CHAINS, ST_LIS_TESTS, ST_RECORDS,
+  ST_REC_OVERFLOW, ST_INFO_USED, ST_GROUP_OVERFLOW, ST_N
+};
+
+struct GroupOut {
+  int2* hits;
+  ChainDesc* chains[3];       // small / large / huge
+  uint32_t* chain_count;      // [3]
+  uint32_t chain_cap[3];
+  uint64_t* huge_elems;       // scratch elements reserved by huge chains
+  uint32_t cap_small, cap_large;
+  uint32_t* overflow_reads;
+  uint32_t* n_overflow;
+};
+
+struct LisParams {
+  uint32_t W;
+  double a, b, C;   // affine_capped; seq uses linear(a)
+  int mer_all, seq_all;
+};
+
+struct ChainOut {
+  Rec* recs;
+  uint32_t* rec_count;
+  uint32_t rec_cap;
+  int32_t* info_m;
+  int32_t* info_b;
+  unsigned long long* info_count;
+  uint64_t info_cap;
+  unsigned long long* stats;
+};
+
+}  // namespace pbgpu

@@ -1,0 +1,320 @@
+"""ctypes binding of the pbgpu C ABI (include/pbgpu.h).
+
+Plumbing for tests and bench.py only: the product is libpbgpu.so (HIP kernels
++ C ABI) and the C++ CLI pacbio_amd/bin/jf_aligner.  The classes mirror the
+reference objects they replace:
+
+  Index    <- superread_parse() / sequence_psa   (superread_parser.hpp:53-224)
+  Aligner  <- coarse_aligner + ::thread          (coarse_aligner.hpp:38-150)
+  Coords   <- coords_info_type of a whole batch  (pb_aligner.hpp:103-177)
+
+There is no CPU fallback: if libpbgpu.so is missing or no GPU is usable the
+calls raise.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpbgpu.so")
+
+PBGPU_OK = 0
+STATUS = {0: "OK", 1: "INVALID", 2: "IO", 3: "NOMEM", 4: "DEVICE", 5: "UNSUPPORTED", 6: "INTERNAL"}
+
+# every symbol include/pbgpu.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "pbgpu_abi_version", "pbgpu_last_error", "pbgpu_device_count",
+    "pbgpu_index_build_fasta", "pbgpu_index_build", "pbgpu_index_free", "pbgpu_index_get_info",
+    "pbgpu_index_sr_name", "pbgpu_index_sr_len",
+    "pbgpu_align_params_default", "pbgpu_aligner_create", "pbgpu_aligner_free",
+    "pbgpu_align_batch", "pbgpu_coords_free",
+    "pbgpu_reads_upload", "pbgpu_reads_free", "pbgpu_align_resident", "pbgpu_download",
+    "pbgpu_aligner_get_stats", "pbgpu_aligner_reset_stats",
+    "pbgpu_format_coords", "pbgpu_free_text",
+]
+
+
+class PbgpuError(RuntimeError):
+    def __init__(self, status, msg):
+        super().__init__(f"pbgpu {STATUS.get(status, status)}: {msg}")
+        self.status = status
+
+
+class IndexParams(C.Structure):
+    _fields_ = [("k", C.c_uint32), ("psa_min", C.c_uint32), ("device", C.c_int32), ("threads", C.c_int32)]
+
+
+class IndexInfo(C.Structure):
+    _fields_ = [("n_sr", C.c_uint64), ("text_len", C.c_uint64), ("n_kmers", C.c_uint64),
+                ("n_occurrences", C.c_uint64), ("table_buckets", C.c_uint64), ("device_bytes", C.c_uint64),
+                ("build_seconds", C.c_double)]
+
+
+class AlignParams(C.Structure):
+    _fields_ = [("k", C.c_uint32), ("stretch_factor", C.c_double), ("stretch_constant", C.c_double),
+                ("stretch_cap", C.c_double), ("window_size", C.c_uint32), ("forward", C.c_int32),
+                ("max_match", C.c_int32), ("max_count", C.c_int32), ("mers_matching", C.c_double),
+                ("bases_matching", C.c_double), ("unitigs_k", C.c_uint32),
+                ("unitig_lengths", C.POINTER(C.c_int32)), ("n_unitigs", C.c_uint64), ("fine_k", C.c_uint32)]
+
+
+class ReadBatch(C.Structure):
+    _fields_ = [("n_reads", C.c_uint64), ("seq", C.c_char_p), ("offsets", C.POINTER(C.c_uint64))]
+
+
+RECORD_DTYPE = np.dtype([
+    ("rs", "<i4"), ("re", "<i4"), ("qs", "<i4"), ("qe", "<i4"), ("nb_mers", "<i4"),
+    ("pb_cons", "<u4"), ("sr_cons", "<u4"), ("pb_cover", "<u4"), ("sr_cover", "<u4"),
+    ("ql", "<u4"), ("sr_index", "<u4"), ("read", "<u4"), ("emit", "<u4"), ("flags", "<u4"),
+    ("n_info", "<u4"), ("reserved", "<u4"), ("info_offset", "<u8"),
+    ("stretch", "<f8"), ("offset", "<f8"), ("avg_err", "<f8")])
+assert RECORD_DTYPE.itemsize == 96
+
+
+class CoordsBatch(C.Structure):
+    _fields_ = [("n_reads", C.c_uint64), ("n_records", C.c_uint64), ("read_offsets", C.POINTER(C.c_uint64)),
+                ("records", C.c_void_p), ("n_info", C.c_uint64), ("kmers_info", C.POINTER(C.c_int32)),
+                ("bases_info", C.POINTER(C.c_int32))]
+
+
+class Stats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("n_batches", "n_reads", "n_bases", "n_kmers", "n_probes", "n_kept",
+                                          "n_hits", "n_chains", "n_lis_tests", "n_records")] + \
+               [(n, C.c_double) for n in ("ms_seed", "ms_group", "ms_lis", "ms_records", "ms_other")] + \
+               [(n, C.c_uint64) for n in ("launches_seed", "launches_group", "launches_lis", "launches_records")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -m pacbio_amd.build`")
+        L = C.CDLL(LIB_PATH)
+        vp = C.c_void_p
+        L.pbgpu_abi_version.restype = C.c_int
+        L.pbgpu_last_error.restype = C.c_char_p
+        L.pbgpu_device_count.restype = C.c_int
+        L.pbgpu_index_build_fasta.argtypes = [C.POINTER(C.c_char_p), C.c_size_t, C.POINTER(IndexParams), C.POINTER(vp)]
+        L.pbgpu_index_build.argtypes = [C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.POINTER(C.c_uint64),
+                                        C.c_size_t, C.POINTER(IndexParams), C.POINTER(vp)]
+        L.pbgpu_index_free.argtypes = [vp]
+        L.pbgpu_index_get_info.argtypes = [vp, C.POINTER(IndexInfo)]
+        L.pbgpu_index_sr_name.argtypes = [vp, C.c_uint32, C.c_int]
+        L.pbgpu_index_sr_name.restype = C.c_char_p
+        L.pbgpu_index_sr_len.argtypes = [vp, C.c_uint32]
+        L.pbgpu_index_sr_len.restype = C.c_uint32
+        L.pbgpu_align_params_default.argtypes = [C.POINTER(AlignParams)]
+        L.pbgpu_align_params_default.restype = None
+        L.pbgpu_aligner_create.argtypes = [vp, C.POINTER(AlignParams), C.POINTER(vp)]
+        L.pbgpu_aligner_free.argtypes = [vp]
+        L.pbgpu_align_batch.argtypes = [vp, C.POINTER(ReadBatch), C.POINTER(C.POINTER(CoordsBatch))]
+        L.pbgpu_coords_free.argtypes = [C.POINTER(CoordsBatch)]
+        L.pbgpu_reads_upload.argtypes = [vp, C.POINTER(ReadBatch), C.POINTER(vp)]
+        L.pbgpu_reads_free.argtypes = [vp]
+        L.pbgpu_align_resident.argtypes = [vp, vp]
+        L.pbgpu_download.argtypes = [vp, C.POINTER(C.POINTER(CoordsBatch))]
+        L.pbgpu_aligner_get_stats.argtypes = [vp, C.POINTER(Stats)]
+        L.pbgpu_aligner_reset_stats.argtypes = [vp]
+        L.pbgpu_format_coords.argtypes = [vp, C.POINTER(CoordsBatch), C.POINTER(C.c_char_p), C.POINTER(C.c_uint64),
+                                          C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p),
+                                          C.POINTER(C.c_uint64)]
+        L.pbgpu_free_text.argtypes = [C.c_void_p]
+        L.pbgpu_free_text.restype = None
+        _lib = L
+    return _lib
+
+
+def _check(st):
+    if st != PBGPU_OK:
+        raise PbgpuError(st, lib().pbgpu_last_error().decode(errors="replace"))
+
+
+def _cstrs(items):
+    arr = (C.c_char_p * max(1, len(items)))()
+    for i, s in enumerate(items):
+        arr[i] = s if isinstance(s, bytes) else s.encode()
+    return arr
+
+
+def _pack_reads(seqs):
+    """list of str/bytes -> (blob bytes, offsets uint64)"""
+    bs = [s if isinstance(s, bytes) else s.encode() for s in seqs]
+    off = np.zeros(len(bs) + 1, dtype=np.uint64)
+    np.cumsum([len(b) for b in bs], out=off[1:])
+    return b"".join(bs), off
+
+
+class Index:
+    def __init__(self, handle):
+        self.h = handle
+
+    @classmethod
+    def from_fasta(cls, paths, k, psa_min=13, device=0, threads=0):
+        p = IndexParams(k, psa_min, device, threads)
+        h = C.c_void_p()
+        _check(lib().pbgpu_index_build_fasta(_cstrs(paths), len(paths), C.byref(p), C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def from_records(cls, names, seqs, k, psa_min=13, device=0, threads=0):
+        p = IndexParams(k, psa_min, device, threads)
+        bs = [s if isinstance(s, bytes) else s.encode() for s in seqs]
+        lens = (C.c_uint64 * max(1, len(bs)))(*[len(b) for b in bs])
+        h = C.c_void_p()
+        _check(lib().pbgpu_index_build(_cstrs(names), _cstrs(bs), lens, len(bs), C.byref(p), C.byref(h)))
+        return cls(h)
+
+    def info(self):
+        i = IndexInfo()
+        _check(lib().pbgpu_index_get_info(self.h, C.byref(i)))
+        return {n: getattr(i, n) for n, _ in i._fields_}
+
+    def sr_name(self, i, bwd=False):
+        r = lib().pbgpu_index_sr_name(self.h, i, 1 if bwd else 0)
+        return None if r is None else r.decode()
+
+    def close(self):
+        if self.h:
+            lib().pbgpu_index_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def align_params(k=17, stretch_factor=1.3, stretch_constant=10, stretch_cap=10000.0, window_size=1,
+                 forward=False, max_match=False, max_count=5000, mers_matching=0.0, bases_matching=17.0,
+                 unitigs_k=0, unitig_lengths=None, fine_k=0):
+    p = AlignParams()
+    lib().pbgpu_align_params_default(C.byref(p))
+    p.k = k; p.stretch_factor = stretch_factor; p.stretch_constant = stretch_constant
+    p.stretch_cap = stretch_cap; p.window_size = window_size; p.forward = int(bool(forward))
+    p.max_match = int(bool(max_match)); p.max_count = max_count; p.mers_matching = mers_matching
+    p.bases_matching = bases_matching; p.unitigs_k = unitigs_k; p.fine_k = fine_k
+    keep = None
+    if unitig_lengths is not None:
+        keep = np.ascontiguousarray(unitig_lengths, dtype=np.int32)
+        p.unitig_lengths = keep.ctypes.data_as(C.POINTER(C.c_int32))
+        p.n_unitigs = len(keep)
+    return p, keep
+
+
+class Coords:
+    """Host copy of one batch of records (owns the C allocation)."""
+
+    def __init__(self, ptr):
+        self.ptr = ptr
+        c = ptr.contents
+        n, nr = c.n_reads, c.n_records
+        self.read_offsets = np.ctypeslib.as_array(c.read_offsets, shape=(n + 1,)).copy() if n + 1 else np.zeros(1, np.uint64)
+        if nr:
+            buf = (C.c_char * (nr * RECORD_DTYPE.itemsize)).from_address(c.records)
+            self.records = np.frombuffer(buf, dtype=RECORD_DTYPE).copy()
+        else:
+            self.records = np.zeros(0, dtype=RECORD_DTYPE)
+        if c.n_info:
+            self.kmers_info = np.ctypeslib.as_array(c.kmers_info, shape=(c.n_info,)).copy()
+            self.bases_info = np.ctypeslib.as_array(c.bases_info, shape=(c.n_info,)).copy()
+        else:
+            self.kmers_info = np.zeros(0, np.int32)
+            self.bases_info = np.zeros(0, np.int32)
+
+    def format(self, index, headers, lens, compact=True, header=False, zero_match=False, threads=0):
+        t = C.c_void_p()
+        tl = C.c_uint64()
+        lens_a = (C.c_uint64 * max(1, len(lens)))(*[int(x) for x in lens])
+        _check(lib().pbgpu_format_coords(index.h, self.ptr, _cstrs(headers), lens_a, int(compact), int(header),
+                                         int(zero_match), threads, C.byref(t), C.byref(tl)))
+        try:
+            return C.string_at(t, tl.value).decode()
+        finally:
+            lib().pbgpu_free_text(t)
+
+    def close(self):
+        if self.ptr:
+            lib().pbgpu_coords_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Aligner:
+    def __init__(self, index, **kw):
+        self.index = index
+        self.params, self._ul = align_params(**kw)
+        h = C.c_void_p()
+        _check(lib().pbgpu_aligner_create(index.h, C.byref(self.params), C.byref(h)))
+        self.h = h
+
+    def align(self, seqs):
+        blob, off = _pack_reads(seqs)
+        b = ReadBatch(len(seqs), blob, off.ctypes.data_as(C.POINTER(C.c_uint64)))
+        out = C.POINTER(CoordsBatch)()
+        _check(lib().pbgpu_align_batch(self.h, C.byref(b), C.byref(out)))
+        return Coords(out)
+
+    def upload(self, seqs=None, blob=None, offsets=None):
+        if seqs is not None:
+            blob, offsets = _pack_reads(seqs)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        b = ReadBatch(len(offsets) - 1, blob, offsets.ctypes.data_as(C.POINTER(C.c_uint64)))
+        r = C.c_void_p()
+        _check(lib().pbgpu_reads_upload(self.h, C.byref(b), C.byref(r)))
+        return ResidentReads(r)
+
+    def align_resident(self, reads):
+        _check(lib().pbgpu_align_resident(self.h, reads.h))
+
+    def download(self):
+        out = C.POINTER(CoordsBatch)()
+        _check(lib().pbgpu_download(self.h, C.byref(out)))
+        return Coords(out)
+
+    def stats(self):
+        s = Stats()
+        _check(lib().pbgpu_aligner_get_stats(self.h, C.byref(s)))
+        return s.as_dict()
+
+    def reset_stats(self):
+        _check(lib().pbgpu_aligner_reset_stats(self.h))
+
+    def close(self):
+        if self.h:
+            lib().pbgpu_aligner_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class ResidentReads:
+    def __init__(self, h):
+        self.h = h
+
+    def close(self):
+        if self.h:
+            lib().pbgpu_reads_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
