@@ -1,0 +1,213 @@
+#!/usr/bin/env python3
+"""bench.py -- PacBio bases aligned/s of the MI355X jf_aligner path.
+
+Workload (BASELINE.json configs[1], the largest single-GPU config): E. coli
+scale, 50k synthetic PacBio CLR reads (lognormal, mean 12 kb, 13% errors) per
+GPU against 200k synthetic super-reads (~250 Mbp), k=17, with the production
+flags `-m 17 --psa-min 13 -l ul.txt -k 31 -f -B 15 --max-count 5000
+--stretch-cap 10000`.  One step = the whole GPU hot path over
+the rank's 50k resident reads: k-mer seeding + hash lookups + 99% threshold ->
+per-(read, super-read) grouping -> order-exact LIS + least squares + filters
+-> coords records sorted per read, left in HBM.  Index build is outside the
+timed region (reported separately).
+
+Multi-GPU: one process per GPU (torchrun); every rank builds its own replica
+of the index and aligns its own 50k-read shard (weak scaling, no collective on
+the data path).  Timing: barrier + device sync on both sides of exactly
+`--steps` steps, max over ranks.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def _dist():
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return rank, world, local
+
+
+class Comm:
+    """Barrier + max-reduction over ranks.  gloo on the host: the path itself
+    has no exchange step (read sharding), so no RCCL traffic is needed."""
+
+    def __init__(self, world):
+        self.world = world
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            self.dist = dist
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def max(self, x):
+        if self.world == 1:
+            return x
+        import torch
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x):
+        if self.world == 1:
+            return x
+        import torch
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+
+def _kernel_bytes(st, steps):
+    """Algorithmic HBM bytes per launch of each stage:
+    every byte the algorithm must move at least once, from the kernels' own
+    counters (not from the layout's actual traffic)."""
+    per = lambda v: v / steps
+    bases, probes, kept = per(st["n_bases"]), per(st["n_probes"]), per(st["n_kept"])
+    hits, chains, recs = per(st["n_hits"]), per(st["n_chains"]), per(st["n_records"])
+    return {
+        # read ASCII once, one 64-B bucket per probe, 16-B k-mer record written, 16-B header read
+        "seed": bases * 1 + probes * 64 + kept * 32,
+        # k-mer records + headers read, every occurrence (8 B) read, hits (8 B) + chain descriptors written
+        "group": kept * 32 + hits * 8 + hits * 8 + chains * 32,
+        # hits read once, chain descriptors read, records written
+        "chain": hits * 8 + chains * 32 + recs * 96,
+        # records read + written, per-read offsets
+        "records": recs * 96 * 2,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="C2", choices=["C1", "C2", "C3"])
+    ap.add_argument("--reads", type=int, default=0, help="override reads per GPU")
+    ap.add_argument("--cpu-sample-reads", type=int, default=0, help="CPU baseline sample (0 = auto)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    args = ap.parse_args()
+
+    rank, world, local = _dist()
+    comm = Comm(world)
+    from pacbio_amd import pbgpu
+    from tools.synth import Dataset, PRESETS
+
+    k = 21 if args.workload == "C3" else 17
+    n_pb = args.reads or PRESETS[args.workload]["n_pb"]
+    threads = min(16, os.cpu_count() or 1)
+    t0 = time.time()
+    ds = Dataset(args.workload, seed=42, threads=threads, n_pb=n_pb, pb_index_base=rank * n_pb)
+    t_gen = time.time() - t0
+    names, seqs = ds.sr_names(), ds.sr_seqs()
+    t0 = time.time()
+    index = pbgpu.Index.from_records(names, seqs, k, psa_min=13, device=local)
+    t_index = time.time() - t0
+    info = index.info()
+    al = pbgpu.Aligner(index, k=k, forward=True, unitigs_k=31, unitig_lengths=ds.unitig_lengths,
+                       bases_matching=15.0, max_count=5000, stretch_cap=10000.0)
+    blob, off = ds.pb_blob()
+    reads = al.upload(blob=blob, offsets=off)
+    bases_rank = int(off[-1])
+
+    for _ in range(args.warmup):
+        al.align_resident(reads)
+    al.reset_stats()
+    pbgpu.device_synchronize(local)
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        al.align_resident(reads)
+    pbgpu.device_synchronize(local)
+    comm.barrier()
+    elapsed = comm.max(time.perf_counter() - t0)
+    st = al.stats()
+
+    total_bases = comm.sum(bases_rank) * args.steps
+    value = total_bases / elapsed
+    stage_ms = {"seed": st["ms_seed"], "group": st["ms_group"], "chain": st["ms_lis"], "records": st["ms_records"]}
+    stage_launches = {"seed": st["launches_seed"], "group": st["launches_group"], "chain": st["launches_lis"],
+                      "records": st["launches_records"]}
+    kb = _kernel_bytes(st, args.steps)
+    dom = max(stage_ms, key=lambda s: stage_ms[s])
+    avg_ms = stage_ms[dom] / max(1, stage_launches[dom])
+    achieved = kb[dom] / (avg_ms * 1e-3) / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{dom}.json")
+    if os.path.exists(pmc_path):
+        try:
+            with open(pmc_path) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle.oracle import OracleIndex, params
+        cthreads = args.cpu_threads or threads
+        oix = OracleIndex.from_records(names, seqs, k, threads=cthreads)
+        p = params(k=k, forward=True, unitigs_k=31, unitig_lengths=ds.unitig_lengths, bases_matching=15.0,
+                   max_count=5000, stretch_cap=10000.0)
+        nsamp = args.cpu_sample_reads or max(1, min(len(off) - 1, 8 * cthreads))
+        pseqs = ds.pb_seqs()[:nsamp]
+        sec, nrec = oix.align_timed(p, pseqs, threads=cthreads)
+        sbases = sum(len(s) for s in pseqs)
+        cpu = {"value": sbases / sec, "unit": "bases/s", "cores": cthreads, "kind": "port",
+               "sample": f"first {nsamp} reads of the rank-0 shard ({sbases} bases) against the full "
+                         f"{args.workload} index, oracle/ C restatement, {cthreads} threads, {sec:.2f} s"}
+        oix.close()
+
+    if rank == 0:
+        out = {
+            "metric": "PacBio bases aligned/sec (coords out)",
+            "value": value,
+            "unit": "bases/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic (tools/pbsynth.cc, seed 42; SURVEY.md §8d generator)",
+            "config": {
+                "workload": {"C1": "C1: 100 PB x 10 kb vs 1k SRs, k=17",
+                             "C2": "C2 E. coli-scale: 50k PB (lognormal mean 12 kb, CLR 13%) per GPU vs 200k SRs, k=17",
+                             "C3": "C3 yeast-scale: PB (mean 12 kb) vs 1M SRs, k=21"}[args.workload],
+                "flags": f"-m {k} --psa-min 13 -l ul.txt -k 31 -f -B 15 --max-count 5000 --stretch-cap 10000",
+                "reads_per_gpu": len(off) - 1,
+                "bases_per_gpu": bases_rank,
+                "parallelism": f"read-sharded x{world}, index replicated per GPU",
+                "index": {"n_sr": info["n_sr"], "text_len": info["text_len"], "n_kmers": info["n_kmers"],
+                          "device_bytes": info["device_bytes"], "build_s": round(t_index, 3),
+                          "generate_s": round(t_gen, 3)},
+                "stage_ms_per_step": {s: round(v / args.steps, 3) for s, v in stage_ms.items()},
+                "counters_per_step": {n: st[n] // args.steps for n in
+                                      ("n_kmers", "n_probes", "n_kept", "n_hits", "n_chains", "n_lis_tests",
+                                       "n_records")},
+                "fit_dtype": "f64",
+            },
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "alg_bytes_per_launch": kb[dom], "avg_launch_ms": avg_ms},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    reads.close()
+    al.close()
+    index.close()
+
+
+if __name__ == "__main__":
+    main()

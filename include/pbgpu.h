@@ -53,6 +53,8 @@ int         pbgpu_abi_version(void);
 const char* pbgpu_last_error(void);
 /* number of visible GPUs (0 if none); never fails */
 int         pbgpu_device_count(void);
+/* hipDeviceSynchronize on `device` (bench brackets its timed region with it) */
+pbgpu_status pbgpu_device_synchronize(int device);
 
 /* ------------------------------------------------------------------ index
  * Replaces superread_parse() + sequence_psa (superread_parser.hpp:53-224):

@@ -33,16 +33,13 @@ void launch_headers(const uint64_t* keys, const uint64_t* kpos, const uint64_t* 
 void launch_seed(IndexView ix, const uint8_t* seq, const uint64_t* roff, uint32_t n_reads, AlignParamsDev P,
                  KRec* krec, uint32_t* n_kept, uint32_t* thr, uint64_t* nhits, unsigned long long* stats, hipStream_t st);
 void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const uint32_t* n_kept, const uint32_t* thr,
-                  const uint64_t* hit_off, const uint32_t* read_list, uint32_t n_list, uint32_t hcap_log2,
-                  uint32_t* gtable, GroupOut O, unsigned long long* stats, hipStream_t st);
-int chain_cap_small();
-int chain_cap_large();
-void launch_chain_small(IndexView, AlignParamsDev, LisParams, const ChainDesc*, uint32_t, const int2*, const uint64_t*,
-                        ChainOut, hipStream_t);
-void launch_chain_large(IndexView, AlignParamsDev, LisParams, const ChainDesc*, uint32_t, const int2*, const uint64_t*,
-                        ChainOut, hipStream_t);
-void launch_chain_huge(IndexView, AlignParamsDev, LisParams, const ChainDesc*, uint32_t, const int2*, const uint64_t*,
-                       uint8_t*, ChainOut, hipStream_t);
+                  const uint64_t* hit_off, uint64_t node_base, uint32_t r0, const uint32_t* read_list, uint32_t n_list,
+                  uint32_t hcap_log2, uint32_t* gtable, GroupOut O, unsigned long long* stats, hipStream_t st);
+uint64_t group_table_words(uint32_t hcap_log2);
+void launch_chain_hist(const ChainDesc* chains, uint32_t n, uint32_t* hist, hipStream_t st);
+void launch_chain_perm(const ChainDesc* chains, uint32_t n, uint32_t* cursor, uint32_t* perm, hipStream_t st);
+void launch_chain(IndexView ix, AlignParamsDev P, LisParams lp, const ChainDesc* chains, const uint32_t* perm,
+                  uint32_t n, Node* nodes, const uint64_t* roff, ChainOut O, hipStream_t st);
 void launch_rec_hist(const Rec* recs, uint32_t n, uint32_t* per_read, hipStream_t st);
 void launch_rec_scatter(const Rec* recs, uint32_t n, const uint64_t* rec_off, uint32_t* cursor, uint32_t* order,
                         hipStream_t st);
@@ -103,6 +100,17 @@ struct dbuf {
   void release() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
   void alloc(size_t cnt) { release(); if (cnt) { HIPCHK(hipMalloc((void**)&p, cnt * sizeof(T))); n = cnt; } }
   void ensure(size_t cnt) { if (cnt > n) alloc(std::max(cnt, n + n / 4)); }
+  // grow keeping the first `keep` elements (stream-ordered copy)
+  void grow_keep(size_t cnt, size_t keep, hipStream_t st) {
+    if (cnt <= n) return;
+    T* q = nullptr;
+    const size_t nn = std::max(cnt, n + n / 2);
+    HIPCHK(hipMalloc((void**)&q, nn * sizeof(T)));
+    if (p && keep) HIPCHK(hipMemcpyAsync(q, p, keep * sizeof(T), hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
+    release();
+    p = q; n = nn;
+  }
   size_t bytes() const { return n * sizeof(T); }
 };
 
@@ -343,6 +351,14 @@ int pbgpu_device_count(void) {
   return n;
 }
 
+pbgpu_status pbgpu_device_synchronize(int device) {
+  API_TRY
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(hipDeviceSynchronize());
+  return PBGPU_OK;
+  API_CATCH
+}
+
 pbgpu_status pbgpu_index_build_fasta(const char* const* paths, size_t n_paths, const pbgpu_index_params* params,
                                      pbgpu_index** out) {
   if (!out || (!paths && n_paths)) return fail(PBGPU_ERR_INVALID, "null argument");
@@ -434,10 +450,12 @@ struct pbgpu_aligner {
   dbuf<uint32_t> n_kept, thr, rec_per_read, rec_cursor, order, sort_scratch, ovf_reads, counters;
   dbuf<uint64_t> nhits, hit_off, rec_off, huge_elems;
   dbuf<int2> hits;
-  dbuf<ChainDesc> chains[3];
+  dbuf<ChainDesc> chains;
+  dbuf<uint32_t> perm;
+  dbuf<Node> nodes;
   dbuf<Rec> recs, recs_sorted;
   dbuf<int32_t> info_m, info_b;
-  dbuf<uint8_t> tmp, huge_scratch;
+  dbuf<uint8_t> tmp;
   dbuf<uint32_t> gtable;
   dbuf<unsigned long long> stats, info_count;
   // last result
@@ -446,6 +464,8 @@ struct pbgpu_aligner {
   // stats
   pbgpu_stats acc{};
   hipEvent_t ev[8]{};
+  uint64_t hit_budget = 1200000000ull, rec_hint = 0, info_per_chain = 32;
+  dbuf<uint32_t> ovf_list;
 };
 
 static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd);
@@ -485,7 +505,7 @@ pbgpu_status pbgpu_aligner_create(const pbgpu_index* ix, const pbgpu_align_param
   for (auto& e : al->ev) HIPCHK(hipEventCreate(&e));
   al->stats.alloc(ST_N);
   al->info_count.alloc(1);
-  al->counters.alloc(16);
+  al->counters.alloc(128);
   *out = al.release();
   return PBGPU_OK;
   API_CATCH
@@ -585,94 +605,122 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, al->hit_off.p, (uint64_t)n + 1, st));
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(temp_storage(al->tmp, tb), tb, in, al->hit_off.p, (uint64_t)n + 1, st));
   }
-  uint64_t H = 0;
-  HIPCHK(hipMemcpyAsync(&H, al->hit_off.p + n, 8, hipMemcpyDeviceToHost, st));
+  std::vector<uint64_t> hoff(n + 1);
+  HIPCHK(hipMemcpyAsync(hoff.data(), al->hit_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  // --------------------------------------------------------------- group
-  al->hits.ensure(H + 1);
+  // ------------------------------------- sub-batches: group -> chains (retry)
+  const uint64_t budget = al->hit_budget;
   const uint32_t hcap_log2 = 11;
-  const uint64_t chain_bound = std::min<uint64_t>(H, (uint64_t)n << hcap_log2) + 1;
-  const uint32_t cap_small = (uint32_t)chain_cap_small(), cap_large = (uint32_t)chain_cap_large();
-  al->chains[0].ensure(chain_bound);
-  const uint64_t lg_bound = std::min<uint64_t>(chain_bound, H / (cap_small + 1) + 1);
-  al->chains[1].ensure(lg_bound);
-  al->chains[2].ensure(std::min<uint64_t>(chain_bound, H / (cap_large + 1) + 1));
   al->ovf_reads.ensure(n);
-  al->huge_elems.ensure(1);
-  GroupOut O;
-  O.hits = al->hits.p;
-  for (int c = 0; c < 3; ++c) { O.chains[c] = al->chains[c].p; O.chain_cap[c] = (uint32_t)std::min<uint64_t>(al->chains[c].n, 0xFFFFFFFFu); }
-  O.chain_count = al->counters.p;       // [0..2]
-  O.n_overflow = al->counters.p + 3;
-  O.huge_elems = al->huge_elems.p;
-  O.cap_small = cap_small; O.cap_large = cap_large;
-  O.overflow_reads = al->ovf_reads.p;
-  HIPCHK(hipMemsetAsync(al->counters.p, 0, 16 * 4, st));
-  HIPCHK(hipMemsetAsync(al->huge_elems.p, 0, 8, st));
-  launch_group(v, al->krec.p, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, nullptr, n, hcap_log2, nullptr, O,
-               al->stats.p, st);
-  HIPCHK(hipGetLastError());
-  uint32_t cnt[4];
-  HIPCHK(hipMemcpyAsync(cnt, al->counters.p, 16, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  if (cnt[3]) {  // reads with more super-reads than the LDS table holds
-    std::vector<uint32_t> ovf(cnt[3]);
-    HIPCHK(hipMemcpy(ovf.data(), al->ovf_reads.p, cnt[3] * 4, hipMemcpyDeviceToHost));
-    std::vector<uint64_t> hh(n);
-    HIPCHK(hipMemcpy(hh.data(), al->nhits.p, n * 8, hipMemcpyDeviceToHost));
-    uint64_t mx = 0;
-    for (uint32_t r : ovf) mx = std::max(mx, hh[r]);
-    uint32_t lg = hcap_log2 + 1;
-    while ((1ull << lg) < 2 * mx) ++lg;
-    // process overflowed reads in groups bounded by scratch size (<= 1 GiB of table)
-    const uint64_t per = 16ull << lg;
-    const uint32_t group = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(cnt[3], (1ull << 30) / per));
-    al->gtable.ensure((uint64_t)group * 4 << lg);
-    for (uint32_t s = 0; s < cnt[3]; s += group) {
-      const uint32_t m = std::min(group, cnt[3] - s);
-      launch_group(v, al->krec.p, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, al->ovf_reads.p + s, m, lg,
-                   al->gtable.p, O, al->stats.p, st);
+  uint64_t rec_done = 0, info_done = 0;
+  double ms_group = 0, ms_chain = 0;
+  for (uint32_t r0 = 0; r0 < n;) {
+    uint32_t r1 = r0 + 1;
+    while (r1 < n && hoff[r1 + 1] - hoff[r0] <= budget) ++r1;
+    const uint64_t Hs = hoff[r1] - hoff[r0];
+    const uint32_t nr = r1 - r0;
+    al->nodes.ensure(Hs + 1);
+    const uint64_t chain_bound = std::min<uint64_t>(Hs, (uint64_t)nr << hcap_log2) + 1;
+    al->chains.ensure(chain_bound);
+    GroupOut O;
+    O.nodes = al->nodes.p; O.chains = al->chains.p;
+    O.chain_count = al->counters.p;
+    O.chain_cap = (uint32_t)std::min<uint64_t>(al->chains.n, 0xFFFFFFFFu);
+    O.n_overflow = al->counters.p + 3;
+    O.overflow_reads = al->ovf_reads.p;
+    for (int attempt = 0;; ++attempt) {
+      HIPCHK(hipEventRecord(al->ev[5], st));
+      HIPCHK(hipMemsetAsync(al->counters.p, 0, 16 * 4, st));
+      launch_group(v, al->krec.p, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], r0, nullptr, nr,
+                   hcap_log2, nullptr, O, al->stats.p, st);
       HIPCHK(hipGetLastError());
+      uint32_t cnt[4];
+      HIPCHK(hipMemcpyAsync(cnt, al->counters.p, 16, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      // reads touching more super-reads than the LDS table holds: global tables, growing until they fit
+      uint32_t lg = hcap_log2;
+      uint32_t n_ovf = cnt[3];
+      while (n_ovf) {
+        std::vector<uint32_t> ovf(n_ovf);
+        HIPCHK(hipMemcpy(ovf.data(), al->ovf_reads.p, n_ovf * 4, hipMemcpyDeviceToHost));
+        uint64_t mx = 0;
+        for (uint32_t r : ovf) mx = std::max(mx, hoff[r + 1] - hoff[r]);
+        lg += 2;
+        while ((1ull << lg) < 64) ++lg;
+        if ((1ull << (lg - 1)) > 2 * mx + 64) throw std::runtime_error("group table growth did not converge");
+        const uint64_t words = group_table_words(lg);
+        const uint32_t grp = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_ovf, (1ull << 28) / words));
+        al->gtable.ensure((uint64_t)grp * words);
+        al->ovf_list.ensure(n_ovf);
+        HIPCHK(hipMemcpyAsync(al->ovf_list.p, ovf.data(), n_ovf * 4, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemsetAsync(al->counters.p + 3, 0, 4, st));
+        for (uint32_t s0 = 0; s0 < n_ovf; s0 += grp) {
+          const uint32_t m = std::min(grp, n_ovf - s0);
+          HIPCHK(hipMemsetAsync(al->gtable.p, 0, (size_t)m * words * 4, st));
+          launch_group(v, al->krec.p, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0,
+                       al->ovf_list.p + s0, m, lg, al->gtable.p, O, al->stats.p, st);
+          HIPCHK(hipGetLastError());
+        }
+        HIPCHK(hipMemcpyAsync(cnt, al->counters.p, 16, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        n_ovf = cnt[3];
+      }
+      const uint32_t nch = cnt[0];
+      if (nch > O.chain_cap) throw std::runtime_error("chain descriptor capacity exceeded");
+      HIPCHK(hipEventRecord(al->ev[6], st));
+      // length-bucketed order (longest first), record/info capacity
+      uint32_t* hist = al->counters.p + 16;  // 32 buckets + 32 cursors
+      HIPCHK(hipMemsetAsync(hist, 0, 64 * 4, st));
+      launch_chain_hist(al->chains.p, nch, hist, st);
+      uint32_t h[32];
+      HIPCHK(hipMemcpyAsync(h, hist, 128, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      uint32_t cur[32], acc = 0;
+      for (int b = 31; b >= 0; --b) { cur[b] = acc; acc += h[b]; }
+      HIPCHK(hipMemcpyAsync(hist + 32, cur, 128, hipMemcpyHostToDevice, st));
+      al->perm.ensure(nch + 1);
+      launch_chain_perm(al->chains.p, nch, hist + 32, al->perm.p, st);
+      const uint64_t rec_need = rec_done + (uint64_t)nch * (al->P.max_match ? 2 : 1) + 1024 * (attempt + 1);
+      al->recs.grow_keep(std::max<uint64_t>(rec_need, al->rec_hint), rec_done, st);
+      if (al->P.unitigs_k) {
+        const uint64_t info_need = info_done + (uint64_t)nch * al->info_per_chain + 4096;
+        al->info_m.grow_keep(info_need, info_done, st);
+        al->info_b.grow_keep(info_need, info_done, st);
+      } else {
+        al->info_m.ensure(1); al->info_b.ensure(1);
+      }
+      uint32_t rc32 = (uint32_t)rec_done;
+      HIPCHK(hipMemcpyAsync(al->counters.p + 4, &rc32, 4, hipMemcpyHostToDevice, st));
+      unsigned long long ic = info_done;
+      HIPCHK(hipMemcpyAsync(al->info_count.p, &ic, 8, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemsetAsync(al->stats.p + ST_REC_OVERFLOW, 0, 8, st));
+      ChainOut CO;
+      CO.recs = al->recs.p; CO.rec_count = al->counters.p + 4;
+      CO.rec_cap = (uint32_t)std::min<uint64_t>(al->recs.n, 0xFFFFFFFFu);
+      CO.info_m = al->info_m.p; CO.info_b = al->info_b.p; CO.info_count = al->info_count.p; CO.info_cap = al->info_m.n;
+      CO.stats = al->stats.p;
+      launch_chain(v, al->P, al->lp, al->chains.p, al->perm.p, nch, al->nodes.p, rd->off.p, CO, st);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipEventRecord(al->ev[7], st));
+      uint32_t nrec = 0;
+      unsigned long long ninfo = 0, ovf = 0;
+      HIPCHK(hipMemcpyAsync(&nrec, al->counters.p + 4, 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(&ninfo, al->info_count.p, 8, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(&ovf, al->stats.p + ST_REC_OVERFLOW, 8, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      ms_group += ev_ms(al->ev[5], al->ev[6]);
+      ms_chain += ev_ms(al->ev[6], al->ev[7]);
+      if (ovf == 0 && nrec <= al->recs.n) { rec_done = nrec; info_done = ninfo; break; }
+      if (attempt > 8) throw std::runtime_error("record buffer growth did not converge");
+      // grow (keeping the records of earlier sub-batches) and redo this sub-batch from the group pass
+      al->rec_hint = std::max<uint64_t>(al->rec_hint, (uint64_t)nrec + 4096);
+      al->info_per_chain = al->info_per_chain * 2 + 16;
+      HIPCHK(hipMemsetAsync(al->stats.p + ST_CHAINS, 0, 8, st));
     }
-    HIPCHK(hipMemcpyAsync(cnt, al->counters.p, 16, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    r0 = r1;
   }
-  for (int c = 0; c < 3; ++c)
-    if (cnt[c] > O.chain_cap[c]) throw std::runtime_error("chain descriptor capacity exceeded");
-  HIPCHK(hipEventRecord(al->ev[2], st));
-  // --------------------------------------------------------------- chains
-  uint64_t huge_units = 0;
-  HIPCHK(hipMemcpy(&huge_units, al->huge_elems.p, 8, hipMemcpyDeviceToHost));
-  al->huge_scratch.ensure(huge_units * 48 + 64);
-  const uint64_t n_chains = (uint64_t)cnt[0] + cnt[1] + cnt[2];
-  uint64_t rec_cap = al->P.max_match ? n_chains * 2 + 1024 : n_chains + 1;
-  uint64_t info_cap = al->P.unitigs_k ? std::max<uint64_t>(1024, rec_cap * 16) : 1;
-  for (int attempt = 0;; ++attempt) {
-    al->recs.ensure(rec_cap);
-    al->info_m.ensure(info_cap); al->info_b.ensure(info_cap);
-    HIPCHK(hipMemsetAsync(al->counters.p + 4, 0, 4, st));
-    HIPCHK(hipMemsetAsync(al->info_count.p, 0, 8, st));
-    HIPCHK(hipMemsetAsync(al->stats.p + ST_REC_OVERFLOW, 0, 8, st));
-    HIPCHK(hipMemsetAsync(al->stats.p + ST_LIS_TESTS, 0, 8, st));
-    ChainOut CO;
-    CO.recs = al->recs.p; CO.rec_count = al->counters.p + 4; CO.rec_cap = (uint32_t)std::min<uint64_t>(al->recs.n, 0xFFFFFFFFu);
-    CO.info_m = al->info_m.p; CO.info_b = al->info_b.p; CO.info_count = al->info_count.p; CO.info_cap = al->info_m.n;
-    CO.stats = al->stats.p;
-    launch_chain_small(v, al->P, al->lp, al->chains[0].p, cnt[0], al->hits.p, rd->off.p, CO, st);
-    launch_chain_large(v, al->P, al->lp, al->chains[1].p, cnt[1], al->hits.p, rd->off.p, CO, st);
-    launch_chain_huge(v, al->P, al->lp, al->chains[2].p, cnt[2], al->hits.p, rd->off.p, al->huge_scratch.p, CO, st);
-    HIPCHK(hipGetLastError());
-    uint32_t nrec = 0;
-    unsigned long long ninfo = 0, ovf = 0;
-    HIPCHK(hipMemcpyAsync(&nrec, al->counters.p + 4, 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(&ninfo, al->info_count.p, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(&ovf, al->stats.p + ST_REC_OVERFLOW, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    if (ovf == 0 && nrec <= al->recs.n) { al->last_records = nrec; al->last_info = ninfo; break; }
-    if (attempt > 8) throw std::runtime_error("record buffer growth did not converge");
-    rec_cap = std::max<uint64_t>(rec_cap * 2, (uint64_t)nrec + 1024);
-    info_cap = std::max<uint64_t>(info_cap * 2, ninfo + 1024);
-  }
+  al->last_records = rec_done;
+  al->last_info = info_done;
   HIPCHK(hipEventRecord(al->ev[3], st));
   // ------------------------------------------------------------- records
   const uint32_t nrec = (uint32_t)al->last_records;
@@ -705,8 +753,8 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
   al->acc.n_hits += sv[ST_HITS]; al->acc.n_chains += sv[ST_CHAINS]; al->acc.n_lis_tests += sv[ST_LIS_TESTS];
   al->acc.n_records += nrec;
   al->acc.ms_seed += ev_ms(al->ev[0], al->ev[1]);
-  al->acc.ms_group += ev_ms(al->ev[1], al->ev[2]);
-  al->acc.ms_lis += ev_ms(al->ev[2], al->ev[3]);
+  al->acc.ms_group += ms_group;
+  al->acc.ms_lis += ms_chain;
   al->acc.ms_records += ev_ms(al->ev[3], al->ev[4]);
   al->acc.launches_seed += 1; al->acc.launches_group += 1; al->acc.launches_lis += 1; al->acc.launches_records += 1;
   al->have_result = true;

@@ -58,9 +58,18 @@ struct KRec {
 struct ChainDesc {
   uint32_t read, sr;
   uint32_t nf, nb;
-  uint64_t hit_base;     // first fwd hit; bwd hits follow at hit_base + nf
-  uint64_t scratch;      // element offset into the large-path scratch
+  uint64_t hit_base;     // first fwd node; bwd nodes follow at hit_base + nf
 };
+
+// One hit = one LIS node (32 B).  The group kernel writes (pb, sr); the chain
+// kernel fills the list fields.  rpb/rsr cache the coordinates of the node's
+// chain root (span_full == X - root, lis_align.hpp:167), aux holds the lis.
+struct __align__(16) Node {
+  int32_t pb, sr;
+  int32_t rpb, rsr;
+  uint32_t nxt, len, P, aux;
+};
+static_assert(sizeof(Node) == 32, "Node is one 32-byte record");
 
 struct Rec {
   int32_t rs, re, qs, qe, nb_mers;
@@ -77,12 +86,10 @@ enum StatSlot {
 };
 
 struct GroupOut {
-  int2* hits;
-  ChainDesc* chains[3];       // small / large / huge
-  uint32_t* chain_count;      // [3]
-  uint32_t chain_cap[3];
-  uint64_t* huge_elems;       // scratch elements reserved by huge chains
-  uint32_t cap_small, cap_large;
+  Node* nodes;
+  ChainDesc* chains;
+  uint32_t* chain_count;
+  uint32_t chain_cap;
   uint32_t* overflow_reads;
   uint32_t* n_overflow;
 };

@@ -360,41 +360,51 @@ __global__ __launch_bounds__(BLOCK) void k_seed(IndexView ix, const uint8_t* __r
 }
 
 // ================================================================= group
-// One workgroup per read: enumerate hits (pos_iterator order), group them by
-// super-read in an open-addressing table (LDS, or a global region for reads
-// with too many super-reads), emit one ChainDesc per (read, SR).
+// One wave per read: enumerate the read's hits exactly in the reference's
+// append order (kept k-mers in read order; per k-mer occ(m) then occ(rm),
+// each in descending text position == pos_iterator, superread_parser.hpp:
+// 110-140), group them by super-read in an open-addressing table (LDS, or a
+// global region for reads touching more super-reads than the LDS table
+// holds), and scatter every hit to its (read, SR, strand) list with an
+// order-preserving wave multisplit.  Each list comes out in exactly the
+// reference's frags_pos order (coarse_aligner.cc:128-140) -- no sort needed.
+constexpr uint32_t GROUP_PROBE_LIMIT = 64;
 
-template <int BLOCK, bool GLOBAL_TABLE>
-__global__ __launch_bounds__(BLOCK) void k_group(IndexView ix, const KRec* __restrict__ krec,
-                                                 const uint64_t* __restrict__ roff, const uint32_t* __restrict__ n_kept,
-                                                 const uint32_t* __restrict__ thr_in, const uint64_t* __restrict__ hit_off,
-                                                 const uint32_t* __restrict__ read_list, uint32_t n_list,
-                                                 uint32_t hcap_log2, uint32_t* gtable, GroupOut O,
-                                                 unsigned long long* stats) {
+template <bool GLOBAL_TABLE>
+__global__ __launch_bounds__(64) void k_group(IndexView ix, const KRec* __restrict__ krec,
+                                              const uint64_t* __restrict__ roff, const uint32_t* __restrict__ n_kept,
+                                              const uint32_t* __restrict__ thr_in, const uint64_t* __restrict__ hit_off,
+                                              uint64_t node_base, uint32_t r0, const uint32_t* __restrict__ read_list,
+                                              uint32_t n_list, uint32_t hcap_log2, uint32_t* gtable, GroupOut O,
+                                              unsigned long long* stats) {
   extern __shared__ uint32_t s_dyn[];
-  __shared__ uint32_t s_nf[BLOCK], s_nb[BLOCK], s_off[BLOCK + 1];
-  __shared__ int32_t s_pb[BLOCK];
-  __shared__ uint64_t s_pf[BLOCK], s_pbk[BLOCK];
-  __shared__ uint32_t s_tmp[BLOCK / 64];
-  __shared__ uint32_t s_flag[8];
+  __shared__ uint32_t s_nf[64], s_nb[64], s_off[65];
+  __shared__ int32_t s_pb[64];
+  __shared__ uint64_t s_pf[64], s_pbk[64];
+  __shared__ uint32_t s_flag, s_used;
   if (blockIdx.x >= n_list) return;
-  const uint32_t r = read_list ? read_list[blockIdx.x] : blockIdx.x;
-  const int tid = threadIdx.x;
+  const int lane = threadIdx.x;
+  const uint32_t r = read_list ? read_list[blockIdx.x] : r0 + blockIdx.x;
   const uint32_t hcap = 1u << hcap_log2;
-  uint32_t* tkey = GLOBAL_TABLE ? gtable + (uint64_t)blockIdx.x * 4 * hcap : s_dyn;
+  // table: key (sr + 1, 0 = empty), fwd count/cursor, bwd count/cursor, 2*hcap byte tags
+  uint32_t* tkey = GLOBAL_TABLE ? gtable + (uint64_t)blockIdx.x * (7u * hcap / 2) : s_dyn;
   uint32_t* tcf = tkey + hcap;
   uint32_t* tcb = tcf + hcap;
-  uint32_t* tbase = tcb + hcap;
-  for (uint32_t i = tid; i < hcap; i += BLOCK) { tkey[i] = 0; tcf[i] = 0; tcb[i] = 0; }
-  if (tid < 8) s_flag[tid] = 0;
+  uint8_t* tag = (uint8_t*)(tcb + hcap);
+  if (!GLOBAL_TABLE)  // the global variant is zeroed by hipMemsetAsync
+    for (uint32_t i = lane; i < hcap; i += 64) { tkey[i] = 0; tcf[i] = 0; tcb[i] = 0; }
+  if (lane == 0) { s_flag = 0; s_used = 0; }
   __syncthreads();
   const uint64_t kbase = roff[r];
   const uint32_t nk = n_kept[r], thr = thr_in[r];
-  const uint64_t hbase = hit_off[r];
+  const uint64_t hbase = hit_off[r] - node_base;
+  const uint32_t used_limit = hcap - hcap / 4;
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
 
   for (int pass = 0; pass < 2; ++pass) {
-    for (uint32_t c0 = 0; c0 < nk; c0 += BLOCK) {
-      const uint32_t i = c0 + tid;
+    for (uint32_t g0 = 0; g0 < nk; g0 += 64) {
+      if (s_flag) break;  // uniform (written before the last barrier)
+      const uint32_t i = g0 + lane;
       uint32_t nf = 0, nb = 0;
       if (i < nk) {
         const KRec kr = krec[kbase + i];
@@ -404,92 +414,119 @@ __global__ __launch_bounds__(BLOCK) void k_group(IndexView ix, const KRec* __res
           const uint64_t h0 = ix.occ[ptr], h1 = ix.occ[ptr + 1];
           const uint32_t nA = (uint32_t)(h1 & 0xFFFFFFFFull), nB = (uint32_t)(h1 >> 32);
           const uint64_t A = ptr + 2, B = ptr + 2 + nA;
-          // occ(m) -> fwd list (+off), occ(rm) -> bwd list (-off)   (A.3)
-          if ((h0 >> 32) & 1) { nf = nb = nA; s_pf[tid] = A; s_pbk[tid] = A; }
-          else if (canon) { nf = nA; s_pf[tid] = A; nb = nB; s_pbk[tid] = B; }
-          else { nf = nB; s_pf[tid] = B; nb = nA; s_pbk[tid] = A; }
-          s_pb[tid] = kr.pb_off;
+          // occ(m) -> fwd list (+off), occ(rm) -> bwd list (-off)    
+          if ((h0 >> 32) & 1) { nf = nb = nA; s_pf[lane] = A; s_pbk[lane] = A; }
+          else if (canon) { nf = nA; s_pf[lane] = A; nb = nB; s_pbk[lane] = B; }
+          else { nf = nB; s_pf[lane] = B; nb = nA; s_pbk[lane] = A; }
+          s_pb[lane] = kr.pb_off;
         }
       }
-      s_nf[tid] = nf; s_nb[tid] = nb;
-      uint32_t total;
-      const uint32_t off = block_excl_scan<BLOCK>(nf + nb, s_tmp, total);
-      s_off[tid] = off;
-      if (tid == 0) s_off[BLOCK] = total;
+      s_nf[lane] = nf; s_nb[lane] = nb;
+      uint32_t incl = nf + nb;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+      }
+      s_off[lane] = incl - (nf + nb);
+      const uint32_t total = __shfl(incl, 63, 64);
+      if (lane == 0) s_off[64] = total;
       __syncthreads();
-      for (uint32_t h = tid; h < total; h += BLOCK) {
-        uint32_t lo = 0, hi = BLOCK;  // last ri with s_off[ri] <= h
-        while (hi - lo > 1) { uint32_t md = (lo + hi) >> 1; if (s_off[md] <= h) lo = md; else hi = md; }
-        const uint32_t ri = lo;
-        const uint32_t local = h - s_off[ri];
-        const bool fwd = local < s_nf[ri];
-        const uint64_t e = ix.occ[fwd ? s_pf[ri] + local : s_pbk[ri] + (local - s_nf[ri])];
-        const uint32_t sr = (uint32_t)(e >> 32);
-        const int32_t so = (int32_t)(uint32_t)(e & 0xFFFFFFFFull);
-        uint32_t slot = (sr * 0x9E3779B1u) >> (32 - hcap_log2);
+      for (uint32_t h0 = 0; h0 < total; h0 += 64) {
+        const uint32_t h = h0 + lane;
+        const bool valid = h < total;
+        uint32_t sr = 0, slot = 0;
+        int32_t so = 0, pb = 0;
+        bool fwd = true;
+        if (valid) {
+          uint32_t lo = 0, hi = 64;  // last record with s_off <= h
+          while (hi - lo > 1) { const uint32_t md = (lo + hi) >> 1; if (s_off[md] <= h) lo = md; else hi = md; }
+          const uint32_t local = h - s_off[lo];
+          fwd = local < s_nf[lo];
+          const uint64_t e = ix.occ[fwd ? s_pf[lo] + local : s_pbk[lo] + (local - s_nf[lo])];
+          sr = (uint32_t)(e >> 32);
+          so = (int32_t)(uint32_t)(e & 0xFFFFFFFFull);
+          pb = s_pb[lo];
+          slot = (sr * 0x9E3779B1u) >> (32 - hcap_log2);
+        }
         if (pass == 0) {
-          uint32_t probe = 0;
-          for (;;) {
-            const uint32_t old = atomicCAS(&tkey[slot], 0u, sr + 1);
-            if (old == 0 || old == sr + 1) break;
-            slot = (slot + 1) & (hcap - 1);
-            if (++probe >= hcap) { s_flag[0] = 1; slot = ~0u; break; }
+          if (valid) {
+            uint32_t probe = 0;
+            for (;;) {
+              const uint32_t old = atomicCAS(&tkey[slot], 0u, sr + 1);
+              if (old == 0) { if (atomicAdd(&s_used, 1u) >= used_limit) s_flag = 1; break; }
+              if (old == sr + 1) break;
+              slot = (slot + 1) & (hcap - 1);
+              if (++probe >= GROUP_PROBE_LIMIT) { s_flag = 1; slot = ~0u; break; }
+            }
+            if (slot != ~0u) atomicAdd(fwd ? &tcf[slot] : &tcb[slot], 1u);
           }
-          if (slot != ~0u) atomicAdd(fwd ? &tcf[slot] : &tcb[slot], 1u);
         } else {
-          while (tkey[slot] != sr + 1) slot = (slot + 1) & (hcap - 1);
-          const uint32_t pos = atomicAdd(fwd ? &tcf[slot] : &tcb[slot], 1u);
-          O.hits[hbase + pos] = make_int2(s_pb[ri], fwd ? so : -so);
+          if (valid) while (tkey[slot] != sr + 1) slot = (slot + 1) & (hcap - 1);
+          // order-preserving multisplit over (slot, strand): rank among earlier lanes with the same key
+          const uint32_t key = (slot << 1) | (fwd ? 0u : 1u);
+          if (valid) tag[key] = (uint8_t)lane;
+          __syncthreads();
+          const bool dup = valid && tag[key] != (uint8_t)lane;
+          uint32_t pos = 0;
+          if (!__ballot(dup)) {  // common case: all keys of the chunk distinct
+            if (valid) { uint32_t* cur = fwd ? &tcf[slot] : &tcb[slot]; pos = *cur; *cur = pos + 1; }
+          } else {
+            const uint32_t k2 = valid ? key : 0xFFFFFFFFu;
+            uint64_t active = __ballot(valid);
+            while (active) {
+              const int leader = __ffsll((unsigned long long)active) - 1;
+              const uint32_t lk = __builtin_amdgcn_readlane(k2, leader);
+              const uint64_t peers = __ballot(k2 == lk);
+              uint32_t* cur = (lk & 1) ? &tcb[lk >> 1] : &tcf[lk >> 1];
+              if (k2 == lk) {
+                const uint32_t b = *cur;
+                pos = b + (uint32_t)__popcll(peers & lt_mask);
+                if (lane == leader) *cur = b + (uint32_t)__popcll(peers);
+              }
+              active &= ~peers;
+            }
+          }
+          if (valid) *(int2*)&O.nodes[hbase + pos] = make_int2(pb, fwd ? so : -so);
+          __syncthreads();
         }
       }
       __syncthreads();
     }
     if (pass == 0) {
-      if (s_flag[0]) {  // too many super-reads for the table: retry this read with a global table
-        if (tid == 0) { uint32_t o = atomicAdd(O.n_overflow, 1u); O.overflow_reads[o] = r; }
+      if (s_flag) {  // table too full: this read is redone with a larger global table
+        if (lane == 0) { const uint32_t o = atomicAdd(O.n_overflow, 1u); O.overflow_reads[o] = r; }
         return;
       }
-      // chain bases: scan (cf+cb) over the slots; classify; reserve descriptors
-      const uint32_t per = hcap / BLOCK;  // hcap >= BLOCK
-      uint32_t sum = 0, nsm = 0, nlg = 0, nhg = 0;
-      uint64_t hg_elems = 0;
+      const uint32_t per = hcap / 64;
+      uint32_t sum = 0, nn = 0;
       for (uint32_t j = 0; j < per; ++j) {
-        const uint32_t sl = tid * per + j;
-        if (tkey[sl]) {
-          const uint32_t cf = tcf[sl], cb = tcb[sl], mx = cf > cb ? cf : cb;
-          sum += cf + cb;
-          if (mx <= O.cap_small) ++nsm; else if (mx <= O.cap_large) ++nlg; else { ++nhg; hg_elems += cf + cb; }
-        }
+        const uint32_t sl = lane * per + j;
+        if (tkey[sl]) { sum += tcf[sl] + tcb[sl]; ++nn; }
       }
-      uint32_t tsum, tsm, tlg, thg;
-      uint32_t b0 = block_excl_scan<BLOCK>(sum, s_tmp, tsum);
-      uint32_t i_sm = block_excl_scan<BLOCK>(nsm, s_tmp, tsm);
-      uint32_t i_lg = block_excl_scan<BLOCK>(nlg, s_tmp, tlg);
-      uint32_t i_hg = block_excl_scan<BLOCK>(nhg, s_tmp, thg);
-      uint32_t hg_e32 = (uint32_t)hg_elems, thg_e;
-      uint32_t e_hg = block_excl_scan<BLOCK>(hg_e32, s_tmp, thg_e);
-      if (tid == 0) {
-        s_flag[1] = tsm ? atomicAdd(&O.chain_count[0], tsm) : 0;
-        s_flag[2] = tlg ? atomicAdd(&O.chain_count[1], tlg) : 0;
-        s_flag[3] = thg ? atomicAdd(&O.chain_count[2], thg) : 0;
-        unsigned long long hb = thg_e ? atomicAdd((unsigned long long*)O.huge_elems, (unsigned long long)thg_e) : 0ull;
-        s_flag[4] = (uint32_t)hb; s_flag[5] = (uint32_t)(hb >> 32);
-        atomicAdd(&stats[ST_CHAINS], (unsigned long long)(tsm + tlg + thg));
+      uint32_t isum = sum, inn = nn;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t a1 = __shfl_up(isum, o, 64), a2 = __shfl_up(inn, o, 64);
+        if (lane >= o) { isum += a1; inn += a2; }
       }
-      __syncthreads();
-      const uint64_t hgb = (uint64_t)s_flag[4] | ((uint64_t)s_flag[5] << 32);
-      i_sm += s_flag[1]; i_lg += s_flag[2]; i_hg += s_flag[3];
-      uint64_t e_cur = hgb + e_hg;
+      const uint32_t tn = __shfl(inn, 63, 64);
+      uint32_t bn = 0;
+      if (lane == 0) {
+        bn = atomicAdd(O.chain_count, tn);
+        atomicAdd(&stats[ST_CHAINS], (unsigned long long)tn);
+      }
+      bn = __shfl(bn, 0, 64);
+      uint32_t b0 = isum - sum, ci = bn + inn - nn;
       for (uint32_t j = 0; j < per; ++j) {
-        const uint32_t sl = tid * per + j;
+        const uint32_t sl = lane * per + j;
         if (!tkey[sl]) continue;
-        const uint32_t cf = tcf[sl], cb = tcb[sl], mx = cf > cb ? cf : cb;
-        ChainDesc d;
-        d.read = r; d.sr = tkey[sl] - 1; d.nf = cf; d.nb = cb; d.hit_base = hbase + b0; d.scratch = 0;
-        if (mx <= O.cap_small) { if (i_sm < O.chain_cap[0]) O.chains[0][i_sm] = d; ++i_sm; }
-        else if (mx <= O.cap_large) { if (i_lg < O.chain_cap[1]) O.chains[1][i_lg] = d; ++i_lg; }
-        else { d.scratch = e_cur; e_cur += cf + cb; if (i_hg < O.chain_cap[2]) O.chains[2][i_hg] = d; ++i_hg; }
-        tcf[sl] = b0;        // fwd cursor
+        const uint32_t cf = tcf[sl], cb = tcb[sl];
+        if (ci < O.chain_cap) {
+          ChainDesc d;
+          d.read = r; d.sr = tkey[sl] - 1; d.nf = cf; d.nb = cb; d.hit_base = hbase + b0;
+          O.chains[ci] = d;
+        }
+        ++ci;
+        tcf[sl] = b0;        // fwd cursor (read-local)
         tcb[sl] = b0 + cf;   // bwd cursor
         b0 += cf + cb;
       }
@@ -498,18 +535,31 @@ __global__ __launch_bounds__(BLOCK) void k_group(IndexView ix, const KRec* __res
   }
 }
 
+// chains by descending length class (ceil log2 of nf + nb): long chains start
+// first and lanes of a wave get chains of similar length
+DEV uint32_t chain_bucket(const ChainDesc& d) {
+  const uint32_t t = d.nf + d.nb;
+  return t ? 31u - (uint32_t)__clz(t) : 0u;  // floor(log2)
+}
+__global__ void k_chain_hist(const ChainDesc* __restrict__ chains, uint32_t n, uint32_t* hist) {
+  __shared__ uint32_t h[32];
+  if (threadIdx.x < 32) h[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x)
+    atomicAdd(&h[chain_bucket(chains[c])], 1u);
+  __syncthreads();
+  if (threadIdx.x < 32 && h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+}
+__global__ void k_chain_perm(const ChainDesc* __restrict__ chains, uint32_t n, uint32_t* cursor, uint32_t* perm) {
+  for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x)
+    perm[atomicAdd(&cursor[chain_bucket(chains[c])], 1u)] = c;
+}
+
 // ================================================================= chain
-// lis_align::compute_L_P (lis_align.hpp:139-182) for one wave.
-// The forward_list L is kept as an array in REVERSED list order (head at
-// the end) so that the common "extend the head" insertion is an append.
-// Node fields (SoA): j (element index), len, root (first element of its
-// chain: span_full == X[i] - X[root] exactly, all values are small ints).
-
-template <typename IDX>
-struct ListStore {
-  IDX* j; IDX* len; IDX* root; IDX* P;
-};
-
+// One LANE per chain (read, super-read): both strands' LIS, the fit, the
+// filters and --max-match, i.e. coarse_aligner::align_sequence_max's loop body
+// (coarse_aligner.cc:42-60) for one frags_pos entry.  A wave runs 64 chains;
+// the typical LIS scan stops at the list head, which stays in registers.
 DEV bool affine_ok(double a, double b, double C, double df, double ds) {
   // (s.first <= b + a*s.second) && (s.second <= b + a*s.first) && s.first <= C && s.second <= C
   return (df <= __dadd_rn(b, __dmul_rn(a, ds))) && (ds <= __dadd_rn(b, __dmul_rn(a, df))) && df <= C && ds <= C;
@@ -518,139 +568,74 @@ DEV bool linear_ok(double a, double df, double ds) {
   return (df <= __dmul_rn(a, ds)) && (ds <= __dmul_rn(a, df));
 }
 
-// returns LIS length; writes ascending indices to out[0..len)
-template <typename IDX>
-DEV uint32_t wave_lis(const int2* X, uint32_t n, ListStore<IDX> S, IDX* out, const LisParams& lp,
-                      uint64_t& tests) {
-  const int lane = lane_id();
-  uint32_t L = 0, longest = 0, longest_ind = 0;
+// lis_align::compute_L_P (lis_align.hpp:139-182) + indices (:190-204),
+// restated literally: singly linked list L, first acceptable predecessor in
+// list order, insertion after the first node of minimal length seen before
+// it.  The window test uses X[i] - X[anc_{W-1}(j)], which equals
+// sum_buffer::test_sum exactly (all values are small integers).
+// Returns the LIS length; the ascending lis is left in A[0..len).aux.
+DEV uint32_t lane_lis(Node* __restrict__ A, uint32_t n, const LisParams& lp, uint64_t& tests) {
+  constexpr uint32_t NONE = 0xFFFFFFFFu;
+  uint32_t head = NONE, longest = 0, longest_ind = 0;
+  int32_t hpb = 0, hsr = 0, hrpb = 0, hrsr = 0;  // head node cached in registers
+  uint32_t hnxt = NONE, hlen = 0;
   for (uint32_t i = 0; i < n; ++i) {
-    const int2 xi = X[i];
-    int found = -1;
-    uint32_t best_len = 0xFFFFFFFFu;
-    int best_t = -1;
-    for (uint32_t t0 = 0; t0 < L; t0 += 64) {
-      const uint32_t t = t0 + lane;
-      const bool valid = t < L;
-      uint32_t nl = 0xFFFFFFFFu;
-      bool cond = false;
-      if (valid) {
-        const uint32_t idx = L - 1 - t;
-        nl = S.len[idx];
-        const uint32_t j = S.j[idx];
-        const int2 xj = X[j];
-        if (xi.y > xj.y) {
-          if (lp.mer_all) cond = true;
-          else if (lp.W == 1) cond = affine_ok(lp.a, lp.b, lp.C, (double)(xi.x - xj.x), (double)(xi.y - xj.y));
-          else if (lp.W == 0 || nl < lp.W) cond = true;  // !will_be_filled()
+    const int2 xi = *(const int2*)&A[i];
+    uint32_t prev = NONE, prev_len = 0, prev_nxt = NONE, found = NONE;
+    uint32_t f_len = 0;
+    int32_t f_rpb = 0, f_rsr = 0;
+    if (head != NONE) {
+      uint32_t it = head, lj = hlen, nx = hnxt;
+      int32_t jpb = hpb, jsr = hsr, jrpb = hrpb, jrsr = hrsr;
+      for (;;) {
+        ++tests;
+        if (xi.y > jsr) {
+          bool ok;
+          if (lp.mer_all) ok = true;
+          else if (lp.W == 1) ok = affine_ok(lp.a, lp.b, lp.C, (double)(xi.x - jpb), (double)(xi.y - jsr));
+          else if (lp.W == 0 || lj < lp.W) ok = true;  // !will_be_filled()
           else {
-            uint32_t anc = j;  // test_sum == X[i] - X[anc_{W-1}(j)]
-            for (uint32_t w = 1; w < lp.W; ++w) anc = S.P[anc];
-            const int2 xa = X[anc];
-            cond = affine_ok(lp.a, lp.b, lp.C, (double)(xi.x - xa.x), (double)(xi.y - xa.y));
+            uint32_t anc = it;
+            for (uint32_t w = 1; w < lp.W; ++w) anc = A[anc].P;
+            const int2 xa = *(const int2*)&A[anc];
+            ok = affine_ok(lp.a, lp.b, lp.C, (double)(xi.x - xa.x), (double)(xi.y - xa.y));
           }
+          if (ok) { found = it; f_len = lj; f_rpb = jrpb; f_rsr = jrsr; break; }
         }
+        if (prev == NONE || lj < prev_len) { prev = it; prev_len = lj; prev_nxt = nx; }
+        it = nx;
+        if (it == NONE) break;
+        const Node nd = A[it];
+        jpb = nd.pb; jsr = nd.sr; jrpb = nd.rpb; jrsr = nd.rsr; lj = nd.len; nx = nd.nxt;
       }
-      const uint64_t mk = __ballot(cond);
-      const uint32_t lim = mk ? (uint32_t)(__ffsll((unsigned long long)mk) - 1) : 64u;
-      tests += (uint64_t)(lim < 64 ? lim + 1 : (L - t0 < 64 ? L - t0 : 64));
-      const uint64_t key = (valid && (uint32_t)lane < lim) ? (((uint64_t)nl << 32) | t) : ~0ull;
-      const uint64_t mn = wave_min_u64(key);
-      if (mn != ~0ull && (uint32_t)(mn >> 32) < best_len) { best_len = (uint32_t)(mn >> 32); best_t = (int)(uint32_t)mn; }
-      if (mk) { found = (int)(t0 + lim); break; }
     }
-    uint32_t e_len, e_root, Pi;
-    if (found >= 0) {
-      const uint32_t idx = L - 1 - (uint32_t)found;
-      e_len = (uint32_t)S.len[idx] + 1; Pi = S.j[idx]; e_root = S.root[idx];
+    Node e;
+    e.pb = xi.x; e.sr = xi.y; e.aux = 0;
+    if (found != NONE) { e.len = f_len + 1; e.rpb = f_rpb; e.rsr = f_rsr; e.P = found; }
+    else { e.len = 1; e.rpb = xi.x; e.rsr = xi.y; e.P = NONE; }
+    if (prev == NONE) {  // insert at the head
+      e.nxt = head;
+      head = i; hpb = e.pb; hsr = e.sr; hrpb = e.rpb; hrsr = e.rsr; hnxt = e.nxt; hlen = e.len;
     } else {
-      e_len = 1; Pi = n; e_root = i;
+      e.nxt = prev_nxt;
+      A[prev].nxt = i;
+      if (prev == head) hnxt = i;
     }
-    uint32_t dst;
-    if (best_t < 0) {
-      dst = L;  // insert at the list head
-    } else {
-      // insert after list position q: move R[L-1-q .. L-1] up by one
-      const int64_t lo = (int64_t)L - 1 - best_t;
-      for (int64_t top = (int64_t)L - 1; top >= lo; top -= 64) {
-        const int64_t sidx = top - lane;
-        IDX vj = 0, vl = 0, vr = 0;
-        const bool act = sidx >= lo;
-        if (act) { vj = S.j[sidx]; vl = S.len[sidx]; vr = S.root[sidx]; }
-        wave_sync();
-        if (act) { S.j[sidx + 1] = vj; S.len[sidx + 1] = vl; S.root[sidx + 1] = vr; }
-        wave_sync();
-      }
-      dst = (uint32_t)lo;
-    }
-    if (lane == 0) {
-      S.j[dst] = (IDX)i; S.len[dst] = (IDX)e_len; S.root[dst] = (IDX)e_root; S.P[i] = (IDX)Pi;
-    }
-    wave_sync();
-    ++L;
-    if (longest < e_len) {
-      const int2 xr = X[e_root];
-      if (lp.seq_all || linear_ok(lp.a, (double)(xi.x - xr.x), (double)(xi.y - xr.y))) { longest = e_len; longest_ind = i; }
+    A[i] = e;
+    if (longest < e.len &&
+        (lp.seq_all || linear_ok(lp.a, (double)(xi.x - e.rpb), (double)(xi.y - e.rsr)))) {
+      longest = e.len; longest_ind = i;
     }
   }
-  if (lane == 0) {
-    uint32_t s = longest_ind;
-    for (uint32_t t = 0; t < longest; ++t) { out[longest - 1 - t] = (IDX)s; s = S.P[s]; }
-  }
-  wave_sync();
+  uint32_t s = longest_ind;
+  for (uint32_t t = 0; t < longest; ++t) { A[longest - 1 - t].aux = s; s = A[s].P; }
   return longest;
 }
 
-// wave-level bitonic sort of np2 (power of two) u64 keys, ascending
-DEV void wave_bitonic(uint64_t* a, uint32_t np2) {
-  const int lane = lane_id();
-  for (uint32_t kk = 2; kk <= np2; kk <<= 1) {
-    for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
-      for (uint32_t i = lane; i < np2; i += 64) {
-        const uint32_t l = i ^ j;
-        if (l > i) {
-          const uint64_t x = a[i], y = a[l];
-          const bool up = (i & kk) == 0;
-          if ((x > y) == up) { a[i] = y; a[l] = x; }
-        }
-      }
-      wave_sync();
-    }
-  }
-}
-
-// per-chain list: (pb_off asc, |sr_off| desc) == append order of
-// fetch_super_reads (PB k-mer order, then pos_iterator's descending SA order)
-DEV void load_sort_strand(const int2* src, uint32_t n, bool bwd, uint64_t* keys) {
-  const int lane = lane_id();
-  uint32_t np2 = 1;
-  while (np2 < n) np2 <<= 1;
-  for (uint32_t i = lane; i < np2; i += 64) {
-    uint64_t kk = ~0ull;
-    if (i < n) {
-      const int2 h = src[i];
-      const uint32_t a = (uint32_t)(h.y < 0 ? -h.y : h.y);
-      kk = ((uint64_t)(uint32_t)h.x << 32) | (uint64_t)(0xFFFFFFFFu - a);
-    }
-    keys[i] = kk;
-  }
-  wave_sync();
-  if (n > 1) wave_bitonic(keys, np2);
-  int2* X = (int2*)keys;
-  for (uint32_t i = lane; i < n; i += 64) {
-    const uint64_t kk = keys[i];
-    const int32_t a = (int32_t)(0xFFFFFFFFu - (uint32_t)kk);
-    X[i] = make_int2((int32_t)(kk >> 32), bwd ? -a : a);
-  }
-  wave_sync();
-}
-
-
-// compute_kmers_info (pb_aligner.cc:84-143) for one lis, on lane 0.
+// compute_kmers_info (pb_aligner.cc:84-143) along one lis.
 // ids: unitig ids of the fwd name; rev => bwd name (reversed list).
-DEV uint32_t kmers_info_run(const uint32_t* ids, uint32_t nsz, bool rev, const AlignParamsDev& P,
-                            const int2* X, const uint32_t* lisv, uint32_t nlis, bool fwd_align, uint32_t ql,
-                            int32_t* mers, int32_t* bases) {
+DEV uint32_t kmers_info_run(const uint32_t* ids, uint32_t nsz, bool rev, const AlignParamsDev& P, const Node* A,
+                            uint32_t nlis, bool fwd_align, uint32_t ql, int32_t* mers, int32_t* bases) {
   const int32_t k = (int32_t)P.k, uk = (int32_t)P.unitigs_k;
   auto uid = [&](uint32_t i) -> uint32_t { return i >= nsz ? INVALID_UNITIG : (rev ? ids[nsz - 1 - i] : ids[i]); };
   const uint32_t id0 = uid(0);
@@ -661,7 +646,7 @@ DEV uint32_t kmers_info_run(const uint32_t* ids, uint32_t nsz, bool rev, const A
   int32_t cend = P.ul[id0];
   int32_t prev_pos = (int32_t)(0u - P.k);
   for (uint32_t t = 0; t < nlis; ++t) {
-    const int32_t so = X[lisv[t]].y;
+    const int32_t so = A[A[t].aux].sr;
     const int32_t pos = fwd_align ? so : (int32_t)(ql + (uint32_t)so - P.k + 2u);
     const int32_t sr_pos = pos < 0 ? -pos : pos;
     const int32_t new_bases = k < sr_pos - prev_pos ? k : sr_pos - prev_pos;
@@ -694,23 +679,24 @@ DEV uint32_t kmers_info_run(const uint32_t* ids, uint32_t nsz, bool rev, const A
   return size;
 }
 
-// compute_coords_info (pb_aligner.cc:11-82) + filters of align_sequence_max
-// (coarse_aligner.cc:46-54), lane 0. Returns true if the record is kept.
+// compute_coords_info (pb_aligner.cc:11-82) + the filters of
+// align_sequence_max (coarse_aligner.cc:46-54). Returns true if kept.
 DEV bool coords_record(const IndexView& ix, const AlignParamsDev& P, const ChainDesc& d, uint32_t rl,
-                       const int2* X, const uint32_t* lisv, uint32_t nlis, bool fwd_align, Rec& R) {
+                       const Node* A, uint32_t nlis, bool fwd_align, Rec& R) {
   const uint32_t k = P.k;
   const uint32_t ql = (uint32_t)(ix.sr_start[d.sr + 1] - ix.sr_start[d.sr]);
   R.nb_mers = (int32_t)nlis; R.pb_cons = 0; R.sr_cons = 0; R.pb_cover = k; R.sr_cover = k;
   R.ql = ql; R.sr = d.sr; R.read = d.read; R.flags = (P.forward && !fwd_align) ? 2u : 0u;
-  R.n_info = 0; R.reserved = 0; R.info_off = 0;
+  R.n_info = 0; R.reserved = 0; R.info_off = 0; R.emit = 0;
   R.stretch = 0; R.offset = 0; R.avg_err = 0;
   if (nlis == 0) return false;
-  // least_square_2d (least_square_2d.hpp:47-67)
+  // least_square_2d::add (least_square_2d.hpp:47-67), x = sr offset, y = pb offset
   double EX = 0, EY = 0, EXX = 0, EXY = 0, VX = 0, CXY = 0, NB = 0;
   long n = 0;
-  int2 prev = X[lisv[0]];
+  int2 prev = *(const int2*)&A[A[0].aux];
+  const int2 first = prev;
   for (uint32_t t = 0; t < nlis; ++t) {
-    const int2 c = X[lisv[t]];
+    const int2 c = *(const int2*)&A[A[t].aux];
     if (t) {
       const uint32_t pb_diff = (uint32_t)(c.x - prev.x);
       R.pb_cons += pb_diff == 1u;
@@ -737,6 +723,7 @@ DEV bool coords_record(const IndexView& ix, const AlignParamsDev& P, const Chain
     NB = __dadd_rn(NB, __dadd_rn(__dmul_rn(deltaXY, ndeltaX), -__dmul_rn(deltaXX, ndeltaY)));
     prev = c;
   }
+  const int2 last = prev;
   if (n == 1) {
     R.stretch = 1.0; R.offset = __dadd_rn(EY, -EX); R.avg_err = 0;
   } else {
@@ -744,16 +731,15 @@ DEV bool coords_record(const IndexView& ix, const AlignParamsDev& P, const Chain
     R.stretch = a; R.offset = b;
     double e = 0;
     for (uint32_t t = 0; t < nlis; ++t) {
-      const int2 c = X[lisv[t]];
+      const int2 c = *(const int2*)&A[A[t].aux];
       e = __dadd_rn(e, fabs(__dadd_rn(__dadd_rn(__dmul_rn(a, (double)c.y), b), -(double)c.x)));
     }
     R.avg_err = __ddiv_rn(e, (double)n);
   }
-  const int2 first = X[lisv[0]], last = X[lisv[nlis - 1]];
   R.rs = first.x;
   R.re = (int32_t)((uint32_t)last.x + k - 1u);
   R.qs = first.y; R.qe = last.y;
-  // canonicalize (pb_aligner.hpp:151-167)
+  // coords_info::canonicalize (pb_aligner.hpp:151-167)
   if (R.qs < 0) {
     if (P.forward) {
       R.qs = (int32_t)(uint32_t)((uint64_t)ql + (uint64_t)(int64_t)R.qs - (uint64_t)k + 2ull);
@@ -769,7 +755,7 @@ DEV bool coords_record(const IndexView& ix, const AlignParamsDev& P, const Chain
   } else {
     R.qe = (int32_t)((uint32_t)R.qe + k - 1u);
   }
-  // filters
+  // filters: fabs(stretch)==0, min_mers (-M), min_bases (-B)  (pb_aligner.hpp:169-174)
   if (fabs(R.stretch) == 0.0) return false;
   const double drl = (double)rl;
   double vs = __dadd_rn(R.stretch, R.offset);
@@ -785,146 +771,59 @@ DEV bool coords_record(const IndexView& ix, const AlignParamsDev& P, const Chain
   return true;
 }
 
-// off_lis::discard_LIS (pb_aligner.hpp:47-61): in-place ordered compaction
-// of X without the lis elements. `mark` is scratch (>= n entries).
-template <typename IDX>
-DEV uint32_t wave_discard(int2* X, uint32_t n, const IDX* lisv, uint32_t nlis, IDX* mark) {
-  const int lane = lane_id();
-  for (uint32_t i = lane; i < n; i += 64) mark[i] = 0;
-  wave_sync();
-  for (uint32_t t = lane; t < nlis; t += 64) mark[lisv[t]] = 1;
-  wave_sync();
-  uint32_t w = 0;
-  for (uint32_t c0 = 0; c0 < n; c0 += 64) {
-    const uint32_t i = c0 + lane;
-    const bool keep = i < n && !mark[i];
-    const uint64_t bm = __ballot(keep);
-    const uint32_t rank = __popcll(bm & ((1ull << lane) - 1ull));
-    int2 v = make_int2(0, 0);
-    if (keep) v = X[i];
-    wave_sync();
-    if (keep) X[w + rank] = v;
-    wave_sync();
-    w += (uint32_t)__popcll(bm);
-  }
-  return w;
-}
-
-template <typename IDX>
-struct ChainMem {
-  int2* Xf; int2* Xb;          // sorted strands (sort keys live here first)
-  IDX* lisf; IDX* lisb;
-  ListStore<IDX> S;            // list arrays + P (capacity >= max(nf, nb))
-  uint32_t* lis32;             // lane-0 view of the chosen lis as u32 (capacity >= max)
-};
-
-template <typename IDX>
-DEV void process_chain(const IndexView& ix, const AlignParamsDev& P, const LisParams& lp, const ChainDesc& d,
-                       const int2* hits, const uint64_t* roff, ChainMem<IDX> M, const ChainOut& O,
-                       uint64_t& tests) {
-  const int lane = lane_id();
-  load_sort_strand(hits + d.hit_base, d.nf, false, (uint64_t*)M.Xf);
-  load_sort_strand(hits + d.hit_base + d.nf, d.nb, true, (uint64_t*)M.Xb);
-  uint32_t nf = d.nf, nb = d.nb;
-  uint32_t lf = wave_lis<IDX>(M.Xf, nf, M.S, M.lisf, lp, tests);
-  uint32_t lb = wave_lis<IDX>(M.Xb, nb, M.S, M.lisb, lp, tests);
-  const uint32_t rl = (uint32_t)(roff[d.read + 1] - roff[d.read]);
-  uint32_t emit = 0;
-  for (;;) {
-    const bool fwd_align = lf >= lb;
-    const uint32_t nl = fwd_align ? lf : lb;
-    if (nl == 0) break;
-    const int2* X = fwd_align ? M.Xf : M.Xb;
-    const IDX* lis = fwd_align ? M.lisf : M.lisb;
-    for (uint32_t t = lane; t < nl; t += 64) M.lis32[t] = (uint32_t)lis[t];
-    wave_sync();
-    int keep = 0;
-    if (lane == 0) {
+__global__ __launch_bounds__(256) void k_chain(IndexView ix, AlignParamsDev P, LisParams lp,
+                                               const ChainDesc* __restrict__ chains, const uint32_t* __restrict__ perm,
+                                               uint32_t n_chains, Node* __restrict__ nodes,
+                                               const uint64_t* __restrict__ roff, ChainOut O) {
+  uint64_t tests = 0;
+  for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < n_chains; w += gridDim.x * blockDim.x) {
+    const ChainDesc d = chains[perm ? perm[w] : w];
+    Node* F = nodes + d.hit_base;
+    Node* B = F + d.nf;
+    uint32_t nf = d.nf, nb = d.nb;
+    uint32_t lf = lane_lis(F, nf, lp, tests);
+    uint32_t lb = lane_lis(B, nb, lp, tests);
+    const uint32_t rl = (uint32_t)(roff[d.read + 1] - roff[d.read]);
+    for (uint32_t emit = 0;; ++emit) {
+      const bool fwd_align = lf >= lb;
+      const uint32_t nl = fwd_align ? lf : lb;
+      if (nl == 0) break;
+      const Node* A = fwd_align ? F : B;
       Rec R;
-      keep = coords_record(ix, P, d, rl, X, M.lis32, nl, fwd_align, R);
-      if (keep) {
-        R.emit = emit;
-        if (P.unitigs_k) {
-          const uint32_t u0 = ix.sr_uoff[d.sr], nsz = ix.sr_uoff[d.sr + 1] - u0;
-          const uint32_t need = nsz ? 2 * nsz - 1 : 0;
-          if (need) {
-            const unsigned long long io = atomicAdd(O.info_count, (unsigned long long)need);
-            if (io + need <= O.info_cap) {
-              const uint32_t got = kmers_info_run(ix.sr_uids + u0, nsz, (R.flags & 2u) != 0, P, X, M.lis32, nl,
-                                                  fwd_align, R.ql, O.info_m + io, O.info_b + io);
-              R.n_info = got; R.info_off = io;
-            } else {
-              atomicAdd(&O.stats[ST_REC_OVERFLOW], 1ull);
-            }
+      if (!coords_record(ix, P, d, rl, A, nl, fwd_align, R)) break;
+      R.emit = emit;
+      bool ok = true;
+      if (P.unitigs_k) {
+        const uint32_t u0 = ix.sr_uoff[d.sr], nsz = ix.sr_uoff[d.sr + 1] - u0;
+        const uint32_t need = nsz ? 2 * nsz - 1 : 0;
+        if (need) {
+          const unsigned long long io = atomicAdd(O.info_count, (unsigned long long)need);
+          if (io + need <= O.info_cap) {
+            R.n_info = kmers_info_run(ix.sr_uids + u0, nsz, (R.flags & 2u) != 0, P, A, nl, fwd_align, R.ql,
+                                      O.info_m + io, O.info_b + io);
+            R.info_off = io;
+          } else {
+            ok = false;
           }
         }
-        const uint32_t ri = atomicAdd(O.rec_count, 1u);
-        if (ri < O.rec_cap) O.recs[ri] = R;
-        else atomicAdd(&O.stats[ST_REC_OVERFLOW], 1ull);
       }
+      const uint32_t ri = atomicAdd(O.rec_count, 1u);
+      if (ri < O.rec_cap && ok) O.recs[ri] = R;
+      else atomicAdd(&O.stats[ST_REC_OVERFLOW], 1ull);
+      if (!P.max_match) break;
+      // mer_lists::discard_update_LIS (pb_aligner.hpp:86-92): the longer lis, bwd on ties;
+      // off_lis::discard_LIS (pb_aligner.hpp:47-61) keeps the remaining offsets in order
+      Node* D = lf > lb ? F : B;
+      uint32_t& nD = lf > lb ? nf : nb;
+      uint32_t& lD = lf > lb ? lf : lb;
+      uint32_t wpos = 0, li = 0;
+      for (uint32_t rpos = 0; rpos < nD; ++rpos) {
+        if (li < lD && rpos == D[li].aux) { ++li; continue; }
+        *(int2*)&D[wpos++] = *(const int2*)&D[rpos];
+      }
+      nD -= lD;
+      lD = lane_lis(D, nD, lp, tests);
     }
-    keep = __shfl(keep, 0, 64);
-    if (!keep) break;
-    ++emit;
-    if (!P.max_match) break;
-    // mer_lists::discard_update_LIS (pb_aligner.hpp:86-92): larger lis, bwd on ties
-    if (lf > lb) {
-      nf = wave_discard<IDX>(M.Xf, nf, M.lisf, lf, M.S.P);
-      lf = wave_lis<IDX>(M.Xf, nf, M.S, M.lisf, lp, tests);
-    } else {
-      nb = wave_discard<IDX>(M.Xb, nb, M.lisb, lb, M.S.P);
-      lb = wave_lis<IDX>(M.Xb, nb, M.S, M.lisb, lp, tests);
-    }
-  }
-}
-
-// LDS path: WAVES waves per block, each with its own CAP-element slice.
-template <int WAVES, int CAP>
-__global__ __launch_bounds__(WAVES * 64) void k_chain_lds(IndexView ix, AlignParamsDev P, LisParams lp,
-                                                          const ChainDesc* __restrict__ chains, uint32_t n_chains,
-                                                          const int2* __restrict__ hits, const uint64_t* __restrict__ roff,
-                                                          ChainOut O) {
-  // per wave: Xf, Xb (8B), lisf, lisb, j, len, root, P (2B) , lis32 (4B)
-  constexpr int BYTES = CAP * (8 + 8 + 2 * 6 + 4);
-  extern __shared__ __align__(16) uint8_t s_mem[];
-  const int w = threadIdx.x >> 6;
-  uint8_t* base = s_mem + (size_t)w * BYTES;
-  ChainMem<uint16_t> M;
-  M.Xf = (int2*)base; M.Xb = (int2*)(base + 8 * CAP);
-  uint16_t* p16 = (uint16_t*)(base + 16 * CAP);
-  M.lisf = p16; M.lisb = p16 + CAP; M.S.j = p16 + 2 * CAP; M.S.len = p16 + 3 * CAP; M.S.root = p16 + 4 * CAP;
-  M.S.P = p16 + 5 * CAP;
-  M.lis32 = (uint32_t*)(base + 28 * CAP);
-  uint64_t tests = 0;
-  for (uint32_t c = blockIdx.x * WAVES + w; c < n_chains; c += gridDim.x * WAVES) {
-    const ChainDesc d = chains[c];
-    process_chain<uint16_t>(ix, P, lp, d, hits, roff, M, O, tests);
-  }
-  tests = wave_sum_u64(tests);
-  if (lane_id() == 0 && tests) atomicAdd(&O.stats[ST_LIS_TESTS], (unsigned long long)tests);
-}
-
-// Global-memory path for chains longer than the LDS capacities.  Scratch
-// per chain at d.scratch (elements): Xf/Xb sort keys (8B x np2), lis (4B),
-// list arrays (4 x 4B) -- all sized by the chain's element counts.
-__global__ __launch_bounds__(64) void k_chain_global(IndexView ix, AlignParamsDev P, LisParams lp,
-                                                     const ChainDesc* __restrict__ chains, uint32_t n_chains,
-                                                     const int2* __restrict__ hits, const uint64_t* __restrict__ roff,
-                                                     uint8_t* scratch, ChainOut O) {
-  uint64_t tests = 0;
-  for (uint32_t c = blockIdx.x; c < n_chains; c += gridDim.x) {
-    const ChainDesc d = chains[c];
-    const uint32_t mx = d.nf > d.nb ? d.nf : d.nb;
-    uint32_t np2 = 1;
-    while (np2 < mx) np2 <<= 1;
-    // region size: 2*8*np2 + 8*4*np2 bytes, reserved as 48*np2 per chain by the host
-    uint8_t* base = scratch + d.scratch * 48;  // d.scratch counts elements of np2 granularity
-    ChainMem<uint32_t> M;
-    M.Xf = (int2*)base; M.Xb = (int2*)(base + 8ull * np2);
-    uint32_t* p32 = (uint32_t*)(base + 16ull * np2);
-    M.lisf = p32; M.lisb = p32 + np2; M.S.j = p32 + 2 * np2; M.S.len = p32 + 3 * np2; M.S.root = p32 + 4 * np2;
-    M.S.P = p32 + 5 * np2; M.lis32 = p32 + 6 * np2;
-    process_chain<uint32_t>(ix, P, lp, d, hits, roff, M, O, tests);
   }
   tests = wave_sum_u64(tests);
   if (lane_id() == 0 && tests) atomicAdd(&O.stats[ST_LIS_TESTS], (unsigned long long)tests);
@@ -1015,53 +914,37 @@ void launch_seed(IndexView ix, const uint8_t* seq, const uint64_t* roff, uint32_
                      krec, n_kept, thr, nhits, stats);
 }
 
-constexpr int GROUP_BLOCK = 256;
 void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const uint32_t* n_kept, const uint32_t* thr,
-                  const uint64_t* hit_off, const uint32_t* read_list, uint32_t n_list, uint32_t hcap_log2,
-                  uint32_t* gtable, GroupOut O, unsigned long long* stats, hipStream_t st) {
+                  const uint64_t* hit_off, uint64_t node_base, uint32_t r0, const uint32_t* read_list, uint32_t n_list,
+                  uint32_t hcap_log2, uint32_t* gtable, GroupOut O, unsigned long long* stats, hipStream_t st) {
+  if (!n_list) return;
   if (!gtable) {
-    const size_t lds = (size_t)4 * sizeof(uint32_t) << hcap_log2;
-    hipLaunchKernelGGL((k_group<GROUP_BLOCK, false>), dim3(n_list), dim3(GROUP_BLOCK), lds, st, ix, krec, roff, n_kept,
-                       thr, hit_off, read_list, n_list, hcap_log2, gtable, O, stats);
+    const size_t lds = ((size_t)7 << hcap_log2) / 2 * sizeof(uint32_t);
+    hipLaunchKernelGGL((k_group<false>), dim3(n_list), dim3(64), lds, st, ix, krec, roff, n_kept, thr, hit_off,
+                       node_base, r0, read_list, n_list, hcap_log2, gtable, O, stats);
   } else {
-    hipLaunchKernelGGL((k_group<GROUP_BLOCK, true>), dim3(n_list), dim3(GROUP_BLOCK), 0, st, ix, krec, roff, n_kept,
-                       thr, hit_off, read_list, n_list, hcap_log2, gtable, O, stats);
+    hipLaunchKernelGGL((k_group<true>), dim3(n_list), dim3(64), 0, st, ix, krec, roff, n_kept, thr, hit_off,
+                       node_base, r0, read_list, n_list, hcap_log2, gtable, O, stats);
   }
 }
+uint64_t group_table_words(uint32_t hcap_log2) { return ((uint64_t)7 << hcap_log2) / 2; }
 
-constexpr int CH_SMALL_WAVES = 4, CH_SMALL_CAP = 512;
-constexpr int CH_LARGE_WAVES = 1, CH_LARGE_CAP = 4096;
-int chain_cap_small() { return CH_SMALL_CAP; }
-int chain_cap_large() { return CH_LARGE_CAP; }
-
-void launch_chain_small(IndexView ix, AlignParamsDev P, LisParams lp, const ChainDesc* chains, uint32_t n,
-                        const int2* hits, const uint64_t* roff, ChainOut O, hipStream_t st) {
-  if (!n) return;
-  constexpr size_t lds = (size_t)CH_SMALL_WAVES * CH_SMALL_CAP * (8 + 8 + 2 * 6 + 4);
-  uint32_t grid = (n + CH_SMALL_WAVES - 1) / CH_SMALL_WAVES;
-  if (grid > 16384) grid = 16384;
-  hipLaunchKernelGGL((k_chain_lds<CH_SMALL_WAVES, CH_SMALL_CAP>), dim3(grid), dim3(CH_SMALL_WAVES * 64), lds, st, ix, P,
-                     lp, chains, n, hits, roff, O);
+static uint32_t grid_for(uint32_t n, uint32_t block, uint32_t cap = 65536) {
+  uint64_t g = ((uint64_t)n + block - 1) / block;
+  return (uint32_t)(g < 1 ? 1 : (g > cap ? cap : g));
 }
-void launch_chain_large(IndexView ix, AlignParamsDev P, LisParams lp, const ChainDesc* chains, uint32_t n,
-                        const int2* hits, const uint64_t* roff, ChainOut O, hipStream_t st) {
+void launch_chain_hist(const ChainDesc* chains, uint32_t n, uint32_t* hist, hipStream_t st) {
   if (!n) return;
-  constexpr size_t lds = (size_t)CH_LARGE_WAVES * CH_LARGE_CAP * (8 + 8 + 2 * 6 + 4);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_chain_lds<CH_LARGE_WAVES, CH_LARGE_CAP>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr = true;
-  }
-  uint32_t grid = n < 4096 ? n : 4096;
-  hipLaunchKernelGGL((k_chain_lds<CH_LARGE_WAVES, CH_LARGE_CAP>), dim3(grid), dim3(CH_LARGE_WAVES * 64), lds, st, ix, P,
-                     lp, chains, n, hits, roff, O);
+  hipLaunchKernelGGL(k_chain_hist, dim3(grid_for(n, 256, 2048)), dim3(256), 0, st, chains, n, hist);
 }
-void launch_chain_huge(IndexView ix, AlignParamsDev P, LisParams lp, const ChainDesc* chains, uint32_t n,
-                       const int2* hits, const uint64_t* roff, uint8_t* scratch, ChainOut O, hipStream_t st) {
+void launch_chain_perm(const ChainDesc* chains, uint32_t n, uint32_t* cursor, uint32_t* perm, hipStream_t st) {
   if (!n) return;
-  uint32_t grid = n < 1024 ? n : 1024;
-  hipLaunchKernelGGL(k_chain_global, dim3(grid), dim3(64), 0, st, ix, P, lp, chains, n, hits, roff, scratch, O);
+  hipLaunchKernelGGL(k_chain_perm, dim3(grid_for(n, 256)), dim3(256), 0, st, chains, n, cursor, perm);
+}
+void launch_chain(IndexView ix, AlignParamsDev P, LisParams lp, const ChainDesc* chains, const uint32_t* perm,
+                  uint32_t n, Node* nodes, const uint64_t* roff, ChainOut O, hipStream_t st) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_chain, dim3(grid_for(n, 256)), dim3(256), 0, st, ix, P, lp, chains, perm, n, nodes, roff, O);
 }
 
 void launch_rec_hist(const Rec* recs, uint32_t n, uint32_t* per_read, hipStream_t st) {

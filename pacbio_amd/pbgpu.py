@@ -24,7 +24,7 @@ STATUS = {0: "OK", 1: "INVALID", 2: "IO", 3: "NOMEM", 4: "DEVICE", 5: "UNSUPPORT
 
 # every symbol include/pbgpu.h declares (checked by tests/test_abi.py)
 EXPORTS = [
-    "pbgpu_abi_version", "pbgpu_last_error", "pbgpu_device_count",
+    "pbgpu_abi_version", "pbgpu_last_error", "pbgpu_device_count", "pbgpu_device_synchronize",
     "pbgpu_index_build_fasta", "pbgpu_index_build", "pbgpu_index_free", "pbgpu_index_get_info",
     "pbgpu_index_sr_name", "pbgpu_index_sr_len",
     "pbgpu_align_params_default", "pbgpu_aligner_create", "pbgpu_aligner_free",
@@ -60,7 +60,7 @@ class AlignParams(C.Structure):
 
 
 class ReadBatch(C.Structure):
-    _fields_ = [("n_reads", C.c_uint64), ("seq", C.c_char_p), ("offsets", C.POINTER(C.c_uint64))]
+    _fields_ = [("n_reads", C.c_uint64), ("seq", C.c_void_p), ("offsets", C.POINTER(C.c_uint64))]
 
 
 RECORD_DTYPE = np.dtype([
@@ -101,6 +101,7 @@ def lib():
         L.pbgpu_abi_version.restype = C.c_int
         L.pbgpu_last_error.restype = C.c_char_p
         L.pbgpu_device_count.restype = C.c_int
+        L.pbgpu_device_synchronize.argtypes = [C.c_int]
         L.pbgpu_index_build_fasta.argtypes = [C.POINTER(C.c_char_p), C.c_size_t, C.POINTER(IndexParams), C.POINTER(vp)]
         L.pbgpu_index_build.argtypes = [C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.POINTER(C.c_uint64),
                                         C.c_size_t, C.POINTER(IndexParams), C.POINTER(vp)]
@@ -136,11 +137,23 @@ def _check(st):
         raise PbgpuError(st, lib().pbgpu_last_error().decode(errors="replace"))
 
 
+def device_synchronize(device=0):
+    _check(lib().pbgpu_device_synchronize(device))
+
+
 def _cstrs(items):
     arr = (C.c_char_p * max(1, len(items)))()
     for i, s in enumerate(items):
         arr[i] = s if isinstance(s, bytes) else s.encode()
     return arr
+
+
+def _addr(blob):
+    """address of a bytes object or a ctypes buffer (kept alive by the caller)"""
+    if isinstance(blob, (bytes, bytearray)):
+        return C.cast(C.c_char_p(bytes(blob)), C.c_void_p).value if isinstance(blob, bytearray) else \
+            C.cast(C.c_char_p(blob), C.c_void_p).value
+    return C.addressof(blob)
 
 
 def _pack_reads(seqs):
@@ -262,7 +275,7 @@ class Aligner:
 
     def align(self, seqs):
         blob, off = _pack_reads(seqs)
-        b = ReadBatch(len(seqs), blob, off.ctypes.data_as(C.POINTER(C.c_uint64)))
+        b = ReadBatch(len(seqs), _addr(blob), off.ctypes.data_as(C.POINTER(C.c_uint64)))
         out = C.POINTER(CoordsBatch)()
         _check(lib().pbgpu_align_batch(self.h, C.byref(b), C.byref(out)))
         return Coords(out)
@@ -271,7 +284,7 @@ class Aligner:
         if seqs is not None:
             blob, offsets = _pack_reads(seqs)
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
-        b = ReadBatch(len(offsets) - 1, blob, offsets.ctypes.data_as(C.POINTER(C.c_uint64)))
+        b = ReadBatch(len(offsets) - 1, _addr(blob), offsets.ctypes.data_as(C.POINTER(C.c_uint64)))
         r = C.c_void_p()
         _check(lib().pbgpu_reads_upload(self.h, C.byref(b), C.byref(r)))
         return ResidentReads(r)

@@ -42,6 +42,7 @@ struct pbsynth_config {
   uint32_t unitig_min;
   uint32_t sr_max_unitigs; // random walk length in [1, sr_max_unitigs]
   double   repeat_frac;    // fraction of the genome covered by repeat copies (0 = none)
+  uint64_t pb_index_base;  // PB read i is drawn as global read pb_index_base + i (rank shards)
 };
 
 struct pbsynth_seqs {
@@ -211,7 +212,7 @@ int pbsynth_make(const pbsynth_config* cfg, int threads, pbsynth_seqs* sr, pbsyn
     std::vector<std::string> seqs(c.n_pb), names(c.n_pb);
     const double psig = c.pb_len_sigma, pmu = std::log(c.pb_len_mean) - psig * psig / 2;
     parallel_for(c.n_pb, threads, [&](uint64_t i) {
-      std::mt19937_64 r(stream_seed(c.seed, 5, i));
+      std::mt19937_64 r(stream_seed(c.seed, 5, c.pb_index_base + i));
       uint64_t len = (uint64_t)c.pb_len_mean;
       if (psig > 0) {
         std::lognormal_distribution<double> ln(pmu, psig);
@@ -235,7 +236,7 @@ int pbsynth_make(const pbsynth_config* cfg, int threads, pbsynth_seqs* sr, pbsyn
         if (c.n_run_rate > 0 && U(r) < c.n_run_rate) { uint64_t nl = 1 + r() % 20; out.append(nl, 'N'); }
       }
       seqs[i].swap(out);
-      names[i] = std::to_string(i);
+      names[i] = std::to_string(c.pb_index_base + i);
     });
     pack(seqs, names, pb);
   }

@@ -15,7 +15,7 @@ class SynthConfig(C.Structure):
                 ("pb_len_max", C.c_uint32), ("err_ins", C.c_double), ("err_del", C.c_double),
                 ("err_sub", C.c_double), ("n_run_rate", C.c_double), ("unitig_k", C.c_uint32),
                 ("unitig_mean", C.c_double), ("unitig_min", C.c_uint32), ("sr_max_unitigs", C.c_uint32),
-                ("repeat_frac", C.c_double)]
+                ("repeat_frac", C.c_double), ("pb_index_base", C.c_uint64)]
 
 
 class SynthSeqs(C.Structure):
