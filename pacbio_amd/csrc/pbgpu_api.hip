@@ -36,6 +36,7 @@ void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const ui
                   const uint64_t* hit_off, uint64_t node_base, uint32_t r0, const uint32_t* read_list, uint32_t n_list,
                   uint32_t hcap_log2, uint32_t* gtable, GroupOut O, unsigned long long* stats, hipStream_t st);
 uint64_t group_table_words(uint32_t hcap_log2);
+constexpr uint32_t kGroupLdsMaxLog2 = 13;  // 8192-slot table, 112 KiB of LDS
 void launch_chain_hist(const ChainDesc* chains, uint32_t n, uint32_t* hist, hipStream_t st);
 void launch_chain_perm(const ChainDesc* chains, uint32_t n, uint32_t* cursor, uint32_t* perm, hipStream_t st);
 void launch_chain(IndexView ix, AlignParamsDev P, LisParams lp, const ChainDesc* chains, const uint32_t* perm,
@@ -465,7 +466,7 @@ struct pbgpu_aligner {
   pbgpu_stats acc{};
   hipEvent_t ev[8]{};
   uint64_t hit_budget = 1200000000ull, rec_hint = 0, info_per_chain = 32;
-  dbuf<uint32_t> ovf_list;
+  dbuf<uint32_t> ovf_list, read_list;
 };
 
 static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd);
@@ -614,30 +615,43 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
   al->ovf_reads.ensure(n);
   uint64_t rec_done = 0, info_done = 0;
   double ms_group = 0, ms_chain = 0;
+  uint64_t n_chains = 0, n_tests = 0;
   for (uint32_t r0 = 0; r0 < n;) {
     uint32_t r1 = r0 + 1;
     while (r1 < n && hoff[r1 + 1] - hoff[r0] <= budget) ++r1;
     const uint64_t Hs = hoff[r1] - hoff[r0];
     const uint32_t nr = r1 - r0;
     al->nodes.ensure(Hs + 1);
-    const uint64_t chain_bound = std::min<uint64_t>(Hs, (uint64_t)nr << hcap_log2) + 1;
-    al->chains.ensure(chain_bound);
+    al->chains.ensure(std::min<uint64_t>(Hs, (uint64_t)nr << 10) + 1);  // grown below if a batch needs more
     GroupOut O;
     O.nodes = al->nodes.p; O.chains = al->chains.p;
     O.chain_count = al->counters.p;
     O.chain_cap = (uint32_t)std::min<uint64_t>(al->chains.n, 0xFFFFFFFFu);
     O.n_overflow = al->counters.p + 3;
     O.overflow_reads = al->ovf_reads.p;
+    // reads longest first (hits), so the long-read tail starts early
+    {
+      std::vector<uint32_t> rl(nr);
+      for (uint32_t i = 0; i < nr; ++i) rl[i] = r0 + i;
+      std::stable_sort(rl.begin(), rl.end(), [&](uint32_t a, uint32_t b) {
+        return hoff[a + 1] - hoff[a] > hoff[b + 1] - hoff[b];
+      });
+      al->read_list.ensure(nr);
+      HIPCHK(hipMemcpyAsync(al->read_list.p, rl.data(), (size_t)nr * 4, hipMemcpyHostToDevice, st));
+    }
     for (int attempt = 0;; ++attempt) {
       HIPCHK(hipEventRecord(al->ev[5], st));
       HIPCHK(hipMemsetAsync(al->counters.p, 0, 16 * 4, st));
-      launch_group(v, al->krec.p, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], r0, nullptr, nr,
+      static_assert(ST_LIS_TESTS == ST_CHAINS + 1, "per-attempt stat slots are adjacent");
+      HIPCHK(hipMemsetAsync(al->stats.p + ST_CHAINS, 0, 16, st));  // redone on a retry: counted per attempt
+      launch_group(v, al->krec.p, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0, al->read_list.p, nr,
                    hcap_log2, nullptr, O, al->stats.p, st);
       HIPCHK(hipGetLastError());
       uint32_t cnt[4];
       HIPCHK(hipMemcpyAsync(cnt, al->counters.p, 16, hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
-      // reads touching more super-reads than the LDS table holds: global tables, growing until they fit
+      // reads touching more super-reads than the table holds: a 4x LDS table, then
+      // global tables growing until they fit
       uint32_t lg = hcap_log2;
       uint32_t n_ovf = cnt[3];
       while (n_ovf) {
@@ -645,28 +659,39 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
         HIPCHK(hipMemcpy(ovf.data(), al->ovf_reads.p, n_ovf * 4, hipMemcpyDeviceToHost));
         uint64_t mx = 0;
         for (uint32_t r : ovf) mx = std::max(mx, hoff[r + 1] - hoff[r]);
+        if ((1ull << lg) > 2 * mx + 256) throw std::runtime_error("group table growth did not converge");
         lg += 2;
-        while ((1ull << lg) < 64) ++lg;
-        if ((1ull << (lg - 1)) > 2 * mx + 64) throw std::runtime_error("group table growth did not converge");
-        const uint64_t words = group_table_words(lg);
-        const uint32_t grp = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_ovf, (1ull << 28) / words));
-        al->gtable.ensure((uint64_t)grp * words);
         al->ovf_list.ensure(n_ovf);
         HIPCHK(hipMemcpyAsync(al->ovf_list.p, ovf.data(), n_ovf * 4, hipMemcpyHostToDevice, st));
         HIPCHK(hipMemsetAsync(al->counters.p + 3, 0, 4, st));
-        for (uint32_t s0 = 0; s0 < n_ovf; s0 += grp) {
-          const uint32_t m = std::min(grp, n_ovf - s0);
-          HIPCHK(hipMemsetAsync(al->gtable.p, 0, (size_t)m * words * 4, st));
+        if (lg <= kGroupLdsMaxLog2) {
           launch_group(v, al->krec.p, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0,
-                       al->ovf_list.p + s0, m, lg, al->gtable.p, O, al->stats.p, st);
+                       al->ovf_list.p, n_ovf, lg, nullptr, O, al->stats.p, st);
           HIPCHK(hipGetLastError());
+        } else {
+          const uint64_t words = group_table_words(lg);
+          const uint32_t grp = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_ovf, (1ull << 28) / words));
+          al->gtable.ensure((uint64_t)grp * words);
+          for (uint32_t s0 = 0; s0 < n_ovf; s0 += grp) {
+            const uint32_t m = std::min(grp, n_ovf - s0);
+            HIPCHK(hipMemsetAsync(al->gtable.p, 0, (size_t)m * words * 4, st));
+            launch_group(v, al->krec.p, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0,
+                         al->ovf_list.p + s0, m, lg, al->gtable.p, O, al->stats.p, st);
+            HIPCHK(hipGetLastError());
+          }
         }
         HIPCHK(hipMemcpyAsync(cnt, al->counters.p, 16, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         n_ovf = cnt[3];
       }
       const uint32_t nch = cnt[0];
-      if (nch > O.chain_cap) throw std::runtime_error("chain descriptor capacity exceeded");
+      if (nch > O.chain_cap) {  // descriptor buffer too small: grow, redo this sub-batch's grouping
+        if (attempt > 8) throw std::runtime_error("chain descriptor capacity did not converge");
+        al->chains.ensure((uint64_t)nch + nch / 8 + 1);
+        O.chains = al->chains.p;
+        O.chain_cap = (uint32_t)std::min<uint64_t>(al->chains.n, 0xFFFFFFFFu);
+        continue;
+      }
       HIPCHK(hipEventRecord(al->ev[6], st));
       // length-bucketed order (longest first), record/info capacity
       uint32_t* hist = al->counters.p + 16;  // 32 buckets + 32 cursors
@@ -707,15 +732,20 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
       HIPCHK(hipMemcpyAsync(&nrec, al->counters.p + 4, 4, hipMemcpyDeviceToHost, st));
       HIPCHK(hipMemcpyAsync(&ninfo, al->info_count.p, 8, hipMemcpyDeviceToHost, st));
       HIPCHK(hipMemcpyAsync(&ovf, al->stats.p + ST_REC_OVERFLOW, 8, hipMemcpyDeviceToHost, st));
+      unsigned long long sub[2];
+      HIPCHK(hipMemcpyAsync(sub, al->stats.p + ST_CHAINS, 16, hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
       ms_group += ev_ms(al->ev[5], al->ev[6]);
       ms_chain += ev_ms(al->ev[6], al->ev[7]);
-      if (ovf == 0 && nrec <= al->recs.n) { rec_done = nrec; info_done = ninfo; break; }
+      if (ovf == 0 && nrec <= al->recs.n) {
+        rec_done = nrec; info_done = ninfo;
+        n_chains += sub[0]; n_tests += sub[1];
+        break;
+      }
       if (attempt > 8) throw std::runtime_error("record buffer growth did not converge");
       // grow (keeping the records of earlier sub-batches) and redo this sub-batch from the group pass
       al->rec_hint = std::max<uint64_t>(al->rec_hint, (uint64_t)nrec + 4096);
       al->info_per_chain = al->info_per_chain * 2 + 16;
-      HIPCHK(hipMemsetAsync(al->stats.p + ST_CHAINS, 0, 8, st));
     }
     r0 = r1;
   }
@@ -750,7 +780,7 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
   HIPCHK(hipMemcpyAsync(sv, al->stats.p, sizeof sv, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   al->acc.n_kmers += sv[ST_KMERS]; al->acc.n_probes += sv[ST_PROBES]; al->acc.n_kept += sv[ST_KEPT];
-  al->acc.n_hits += sv[ST_HITS]; al->acc.n_chains += sv[ST_CHAINS]; al->acc.n_lis_tests += sv[ST_LIS_TESTS];
+  al->acc.n_hits += sv[ST_HITS]; al->acc.n_chains += n_chains; al->acc.n_lis_tests += n_tests;
   al->acc.n_records += nrec;
   al->acc.ms_seed += ev_ms(al->ev[0], al->ev[1]);
   al->acc.ms_group += ms_group;

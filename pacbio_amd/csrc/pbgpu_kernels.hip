@@ -360,30 +360,33 @@ __global__ __launch_bounds__(BLOCK) void k_seed(IndexView ix, const uint8_t* __r
 }
 
 // ================================================================= group
-// One wave per read: enumerate the read's hits exactly in the reference's
+// One workgroup (4 waves) per read: enumerate the read's hits exactly in the reference's
 // append order (kept k-mers in read order; per k-mer occ(m) then occ(rm),
 // each in descending text position == pos_iterator, superread_parser.hpp:
 // 110-140), group them by super-read in an open-addressing table (LDS, or a
 // global region for reads touching more super-reads than the LDS table
 // holds), and scatter every hit to its (read, SR, strand) list with an
-// order-preserving wave multisplit.  Each list comes out in exactly the
+// order-preserving multisplit.  Each list comes out in exactly the
 // reference's frags_pos order (coarse_aligner.cc:128-140) -- no sort needed.
-constexpr uint32_t GROUP_PROBE_LIMIT = 64;
+constexpr uint32_t GROUP_BLOCK = 256;  // 4 waves share one read's table
 
 template <bool GLOBAL_TABLE>
-__global__ __launch_bounds__(64) void k_group(IndexView ix, const KRec* __restrict__ krec,
-                                              const uint64_t* __restrict__ roff, const uint32_t* __restrict__ n_kept,
-                                              const uint32_t* __restrict__ thr_in, const uint64_t* __restrict__ hit_off,
-                                              uint64_t node_base, uint32_t r0, const uint32_t* __restrict__ read_list,
-                                              uint32_t n_list, uint32_t hcap_log2, uint32_t* gtable, GroupOut O,
-                                              unsigned long long* stats) {
+__global__ __launch_bounds__(GROUP_BLOCK) void k_group(IndexView ix, const KRec* __restrict__ krec,
+                                                       const uint64_t* __restrict__ roff, const uint32_t* __restrict__ n_kept,
+                                                       const uint32_t* __restrict__ thr_in, const uint64_t* __restrict__ hit_off,
+                                                       uint64_t node_base, uint32_t r0, const uint32_t* __restrict__ read_list,
+                                                       uint32_t n_list, uint32_t hcap_log2, uint32_t* gtable, GroupOut O,
+                                                       unsigned long long* stats) {
+  constexpr uint32_t B = GROUP_BLOCK;
   extern __shared__ uint32_t s_dyn[];
-  __shared__ uint32_t s_nf[64], s_nb[64], s_off[65];
-  __shared__ int32_t s_pb[64];
-  __shared__ uint64_t s_pf[64], s_pbk[64];
-  __shared__ uint32_t s_flag, s_used;
+  __shared__ uint32_t s_nf[B], s_nb[B], s_off[B + 1], s_scan[8];
+  __shared__ int32_t s_pb[B];
+  __shared__ uint64_t s_pf[B], s_pbk[B];
+  __shared__ uint32_t s_flag, s_used, s_cbase;
   if (blockIdx.x >= n_list) return;
-  const int lane = threadIdx.x;
+  const uint32_t tid = threadIdx.x;
+  const int lane = lane_id();
+  const uint32_t wave = tid >> 6;
   const uint32_t r = read_list ? read_list[blockIdx.x] : r0 + blockIdx.x;
   const uint32_t hcap = 1u << hcap_log2;
   // table: key (sr + 1, 0 = empty), fwd count/cursor, bwd count/cursor, 2*hcap byte tags
@@ -392,8 +395,8 @@ __global__ __launch_bounds__(64) void k_group(IndexView ix, const KRec* __restri
   uint32_t* tcb = tcf + hcap;
   uint8_t* tag = (uint8_t*)(tcb + hcap);
   if (!GLOBAL_TABLE)  // the global variant is zeroed by hipMemsetAsync
-    for (uint32_t i = lane; i < hcap; i += 64) { tkey[i] = 0; tcf[i] = 0; tcb[i] = 0; }
-  if (lane == 0) { s_flag = 0; s_used = 0; }
+    for (uint32_t i = tid; i < hcap; i += B) { tkey[i] = 0; tcf[i] = 0; tcb[i] = 0; }
+  if (tid == 0) { s_flag = 0; s_used = 0; }
   __syncthreads();
   const uint64_t kbase = roff[r];
   const uint32_t nk = n_kept[r], thr = thr_in[r];
@@ -402,9 +405,9 @@ __global__ __launch_bounds__(64) void k_group(IndexView ix, const KRec* __restri
   const uint64_t lt_mask = (1ull << lane) - 1ull;
 
   for (int pass = 0; pass < 2; ++pass) {
-    for (uint32_t g0 = 0; g0 < nk; g0 += 64) {
+    for (uint32_t g0 = 0; g0 < nk; g0 += B) {
       if (s_flag) break;  // uniform (written before the last barrier)
-      const uint32_t i = g0 + lane;
+      const uint32_t i = g0 + tid;
       uint32_t nf = 0, nb = 0;
       if (i < nk) {
         const KRec kr = krec[kbase + i];
@@ -413,33 +416,29 @@ __global__ __launch_bounds__(64) void k_group(IndexView ix, const KRec* __restri
           const bool canon = kr.occ_ptr >> 63;
           const uint64_t h0 = ix.occ[ptr], h1 = ix.occ[ptr + 1];
           const uint32_t nA = (uint32_t)(h1 & 0xFFFFFFFFull), nB = (uint32_t)(h1 >> 32);
-          const uint64_t A = ptr + 2, B = ptr + 2 + nA;
+          const uint64_t A = ptr + 2, Bp = ptr + 2 + nA;
           // occ(m) -> fwd list (+off), occ(rm) -> bwd list (-off)    
-          if ((h0 >> 32) & 1) { nf = nb = nA; s_pf[lane] = A; s_pbk[lane] = A; }
-          else if (canon) { nf = nA; s_pf[lane] = A; nb = nB; s_pbk[lane] = B; }
-          else { nf = nB; s_pf[lane] = B; nb = nA; s_pbk[lane] = A; }
-          s_pb[lane] = kr.pb_off;
+          if ((h0 >> 32) & 1) { nf = nb = nA; s_pf[tid] = A; s_pbk[tid] = A; }
+          else if (canon) { nf = nA; s_pf[tid] = A; nb = nB; s_pbk[tid] = Bp; }
+          else { nf = nB; s_pf[tid] = Bp; nb = nA; s_pbk[tid] = A; }
+          s_pb[tid] = kr.pb_off;
         }
       }
-      s_nf[lane] = nf; s_nb[lane] = nb;
-      uint32_t incl = nf + nb;
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += y;
-      }
-      s_off[lane] = incl - (nf + nb);
-      const uint32_t total = __shfl(incl, 63, 64);
-      if (lane == 0) s_off[64] = total;
+      s_nf[tid] = nf; s_nb[tid] = nb;
+      uint32_t total;
+      s_off[tid] = block_excl_scan<B>(nf + nb, s_scan, total);
+      if (tid == 0) s_off[B] = total;
       __syncthreads();
-      for (uint32_t h0 = 0; h0 < total; h0 += 64) {
-        const uint32_t h = h0 + lane;
+      for (uint32_t h0 = 0; h0 < total; h0 += B) {
+        const uint32_t h = h0 + tid;
         const bool valid = h < total;
-        uint32_t sr = 0, slot = 0;
+        uint32_t sr = 0, slot = 0, rec = 0xFFFFFFFFu;
         int32_t so = 0, pb = 0;
         bool fwd = true;
         if (valid) {
-          uint32_t lo = 0, hi = 64;  // last record with s_off <= h
+          uint32_t lo = 0, hi = B;  // last record with s_off <= h
           while (hi - lo > 1) { const uint32_t md = (lo + hi) >> 1; if (s_off[md] <= h) lo = md; else hi = md; }
+          rec = lo;
           const uint32_t local = h - s_off[lo];
           fwd = local < s_nf[lo];
           const uint64_t e = ix.occ[fwd ? s_pf[lo] + local : s_pbk[lo] + (local - s_nf[lo])];
@@ -449,75 +448,94 @@ __global__ __launch_bounds__(64) void k_group(IndexView ix, const KRec* __restri
           slot = (sr * 0x9E3779B1u) >> (32 - hcap_log2);
         }
         if (pass == 0) {
+          // order-free: distinct super-reads and per-strand list lengths
           if (valid) {
-            uint32_t probe = 0;
+            bool ok = true;
             for (;;) {
               const uint32_t old = atomicCAS(&tkey[slot], 0u, sr + 1);
-              if (old == 0) { if (atomicAdd(&s_used, 1u) >= used_limit) s_flag = 1; break; }
+              if (old == 0) { if (atomicAdd(&s_used, 1u) >= used_limit) { s_flag = 1; ok = false; } break; }
               if (old == sr + 1) break;
               slot = (slot + 1) & (hcap - 1);
-              if (++probe >= GROUP_PROBE_LIMIT) { s_flag = 1; slot = ~0u; break; }
             }
-            if (slot != ~0u) atomicAdd(fwd ? &tcf[slot] : &tcb[slot], 1u);
+            if (ok) atomicAdd(fwd ? &tcf[slot] : &tcb[slot], 1u);
           }
         } else {
           if (valid) while (tkey[slot] != sr + 1) slot = (slot + 1) & (hcap - 1);
-          // order-preserving multisplit over (slot, strand): rank among earlier lanes with the same key
+          // Order-preserving multisplit over (slot, strand) keys.  The four waves hold
+          // consecutive 64-hit runs; they take the list cursors in wave order (LDS only,
+          // after all loads are in flight).  Within a wave, hits of one k-mer record hit
+          // distinct super-reads (except SRs holding the k-mer twice), so the run is
+          // processed record segment by record segment (usually 1-2), each segment in
+          // one conflict-free step; a tag check catches in-record repeats.
           const uint32_t key = (slot << 1) | (fwd ? 0u : 1u);
-          if (valid) tag[key] = (uint8_t)lane;
-          __syncthreads();
-          const bool dup = valid && tag[key] != (uint8_t)lane;
           uint32_t pos = 0;
-          if (!__ballot(dup)) {  // common case: all keys of the chunk distinct
-            if (valid) { uint32_t* cur = fwd ? &tcf[slot] : &tcb[slot]; pos = *cur; *cur = pos + 1; }
-          } else {
-            const uint32_t k2 = valid ? key : 0xFFFFFFFFu;
-            uint64_t active = __ballot(valid);
-            while (active) {
-              const int leader = __ffsll((unsigned long long)active) - 1;
-              const uint32_t lk = __builtin_amdgcn_readlane(k2, leader);
-              const uint64_t peers = __ballot(k2 == lk);
-              uint32_t* cur = (lk & 1) ? &tcb[lk >> 1] : &tcf[lk >> 1];
-              if (k2 == lk) {
-                const uint32_t b = *cur;
-                pos = b + (uint32_t)__popcll(peers & lt_mask);
-                if (lane == leader) *cur = b + (uint32_t)__popcll(peers);
+          for (uint32_t w = 0; w < B / 64; ++w) {
+            if (wave == w) {
+              uint64_t active = __ballot(valid);
+              while (active) {
+                const int leader = __ffsll((unsigned long long)active) - 1;
+                const uint32_t lrec = __builtin_amdgcn_readlane(rec, leader);
+                const bool in_seg = rec == lrec;
+                const uint64_t seg = __ballot(in_seg);
+                if (in_seg) tag[key] = (uint8_t)lane;
+                if (GLOBAL_TABLE) __threadfence_block();
+                __builtin_amdgcn_s_waitcnt(0);
+                __builtin_amdgcn_wave_barrier();
+                const bool dup = in_seg && tag[key] != (uint8_t)lane;
+                if (!__ballot(dup)) {
+                  if (in_seg) { uint32_t* cur = fwd ? &tcf[slot] : &tcb[slot]; pos = *cur; *cur = pos + 1; }
+                } else {
+                  const uint32_t k2 = in_seg ? key : 0xFFFFFFFFu;
+                  uint64_t act2 = seg;
+                  while (act2) {
+                    const int l2 = __ffsll((unsigned long long)act2) - 1;
+                    const uint32_t lk = __builtin_amdgcn_readlane(k2, l2);
+                    const uint64_t peers = __ballot(k2 == lk);
+                    uint32_t* cur = (lk & 1) ? &tcb[lk >> 1] : &tcf[lk >> 1];
+                    if (k2 == lk) {
+                      const uint32_t b = *cur;
+                      pos = b + (uint32_t)__popcll(peers & lt_mask);
+                      if (lane == l2) *cur = b + (uint32_t)__popcll(peers);
+                    }
+                    act2 &= ~peers;
+                  }
+                }
+                if (GLOBAL_TABLE) __threadfence_block();
+                __builtin_amdgcn_s_waitcnt(0);
+                __builtin_amdgcn_wave_barrier();
+                active &= ~seg;
               }
-              active &= ~peers;
             }
+            __syncthreads();
           }
           if (valid) *(int2*)&O.nodes[hbase + pos] = make_int2(pb, fwd ? so : -so);
-          __syncthreads();
         }
       }
       __syncthreads();
     }
     if (pass == 0) {
-      if (s_flag) {  // table too full: this read is redone with a larger global table
-        if (lane == 0) { const uint32_t o = atomicAdd(O.n_overflow, 1u); O.overflow_reads[o] = r; }
+      if (s_flag) {  // table too full: this read is redone with a larger table
+        if (tid == 0) { const uint32_t o = atomicAdd(O.n_overflow, 1u); O.overflow_reads[o] = r; }
         return;
       }
-      const uint32_t per = hcap / 64;
+      // chain descriptors, slot order; cursors become read-local list starts
+      const uint32_t per = hcap / B;
       uint32_t sum = 0, nn = 0;
       for (uint32_t j = 0; j < per; ++j) {
-        const uint32_t sl = lane * per + j;
+        const uint32_t sl = tid * per + j;
         if (tkey[sl]) { sum += tcf[sl] + tcb[sl]; ++nn; }
       }
-      uint32_t isum = sum, inn = nn;
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t a1 = __shfl_up(isum, o, 64), a2 = __shfl_up(inn, o, 64);
-        if (lane >= o) { isum += a1; inn += a2; }
-      }
-      const uint32_t tn = __shfl(inn, 63, 64);
-      uint32_t bn = 0;
-      if (lane == 0) {
-        bn = atomicAdd(O.chain_count, tn);
+      uint32_t tsum, tn;
+      const uint32_t esum = block_excl_scan<B>(sum, s_scan, tsum);
+      const uint32_t enn = block_excl_scan<B>(nn, s_scan, tn);
+      if (tid == 0) {
+        s_cbase = atomicAdd(O.chain_count, tn);
         atomicAdd(&stats[ST_CHAINS], (unsigned long long)tn);
       }
-      bn = __shfl(bn, 0, 64);
-      uint32_t b0 = isum - sum, ci = bn + inn - nn;
+      __syncthreads();
+      uint32_t b0 = esum, ci = s_cbase + enn;
       for (uint32_t j = 0; j < per; ++j) {
-        const uint32_t sl = lane * per + j;
+        const uint32_t sl = tid * per + j;
         if (!tkey[sl]) continue;
         const uint32_t cf = tcf[sl], cb = tcb[sl];
         if (ci < O.chain_cap) {
@@ -530,6 +548,7 @@ __global__ __launch_bounds__(64) void k_group(IndexView ix, const KRec* __restri
         tcb[sl] = b0 + cf;   // bwd cursor
         b0 += cf + cb;
       }
+      if (GLOBAL_TABLE) __threadfence_block();
       __syncthreads();
     }
   }
@@ -551,8 +570,17 @@ __global__ void k_chain_hist(const ChainDesc* __restrict__ chains, uint32_t n, u
   if (threadIdx.x < 32 && h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
 }
 __global__ void k_chain_perm(const ChainDesc* __restrict__ chains, uint32_t n, uint32_t* cursor, uint32_t* perm) {
-  for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x)
-    perm[atomicAdd(&cursor[chain_bucket(chains[c])], 1u)] = c;
+  // block-aggregated: one global atomic per (block, bucket)
+  __shared__ uint32_t cnt[32], base[32];
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (threadIdx.x < 32) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t b = 0, loc = 0;
+  if (c < n) { b = chain_bucket(chains[c]); loc = atomicAdd(&cnt[b], 1u); }
+  __syncthreads();
+  if (threadIdx.x < 32 && cnt[threadIdx.x]) base[threadIdx.x] = atomicAdd(&cursor[threadIdx.x], cnt[threadIdx.x]);
+  __syncthreads();
+  if (c < n) perm[base[b] + loc] = c;
 }
 
 // ================================================================= chain
@@ -918,12 +946,17 @@ void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const ui
                   const uint64_t* hit_off, uint64_t node_base, uint32_t r0, const uint32_t* read_list, uint32_t n_list,
                   uint32_t hcap_log2, uint32_t* gtable, GroupOut O, unsigned long long* stats, hipStream_t st) {
   if (!n_list) return;
-  if (!gtable) {
+  if (!gtable) {  // LDS table: hcap_log2 <= 13
     const size_t lds = ((size_t)7 << hcap_log2) / 2 * sizeof(uint32_t);
-    hipLaunchKernelGGL((k_group<false>), dim3(n_list), dim3(64), lds, st, ix, krec, roff, n_kept, thr, hit_off,
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)k_group<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 16 * 1024);
+      attr = true;
+    }
+    hipLaunchKernelGGL((k_group<false>), dim3(n_list), dim3(GROUP_BLOCK), lds, st, ix, krec, roff, n_kept, thr, hit_off,
                        node_base, r0, read_list, n_list, hcap_log2, gtable, O, stats);
   } else {
-    hipLaunchKernelGGL((k_group<true>), dim3(n_list), dim3(64), 0, st, ix, krec, roff, n_kept, thr, hit_off,
+    hipLaunchKernelGGL((k_group<true>), dim3(n_list), dim3(GROUP_BLOCK), 0, st, ix, krec, roff, n_kept, thr, hit_off,
                        node_base, r0, read_list, n_list, hcap_log2, gtable, O, stats);
   }
 }
@@ -939,7 +972,7 @@ void launch_chain_hist(const ChainDesc* chains, uint32_t n, uint32_t* hist, hipS
 }
 void launch_chain_perm(const ChainDesc* chains, uint32_t n, uint32_t* cursor, uint32_t* perm, hipStream_t st) {
   if (!n) return;
-  hipLaunchKernelGGL(k_chain_perm, dim3(grid_for(n, 256)), dim3(256), 0, st, chains, n, cursor, perm);
+  hipLaunchKernelGGL(k_chain_perm, dim3((n + 255) / 256), dim3(256), 0, st, chains, n, cursor, perm);
 }
 void launch_chain(IndexView ix, AlignParamsDev P, LisParams lp, const ChainDesc* chains, const uint32_t* perm,
                   uint32_t n, Node* nodes, const uint64_t* roff, ChainOut O, hipStream_t st) {
