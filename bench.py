@@ -67,22 +67,24 @@ class Comm:
         return float(t.item())
 
 
-def _kernel_bytes(st, steps):
-    """Algorithmic HBM bytes per launch of each stage:
-    every byte the algorithm must move at least once, from the kernels' own
-    counters (not from the layout's actual traffic)."""
-    per = lambda v: v / steps
-    bases, probes, kept = per(st["n_bases"]), per(st["n_probes"]), per(st["n_kept"])
-    hits, chains, recs = per(st["n_hits"]), per(st["n_chains"]), per(st["n_records"])
+def _kernel_bytes(st):
+    """Algorithmic HBM bytes per launch of each individually timed kernel
+    (DESIGN.md "Roofline"): every byte the algorithm must move at least once,
+    from the kernels' own counters, divided by that kernel's launch count."""
+    kn = st["kernel_launches"]
+    per = lambda v, k: v / max(1, kn[k])
     return {
-        # read ASCII once, one 64-B bucket per probe, 16-B k-mer record written, 16-B header read
-        "seed": bases * 1 + probes * 64 + kept * 32,
-        # k-mer records + headers read, every occurrence (8 B) read, hits (8 B) + chain descriptors written
-        "group": kept * 32 + hits * 8 + hits * 8 + chains * 32,
-        # hits read once, chain descriptors read, records written
-        "chain": hits * 8 + chains * 32 + recs * 96,
-        # records read + written, per-read offsets
-        "records": recs * 96 * 2,
+        # read bases (1 B), one 64-B bucket per probe, kept k-mer records (16 B) written
+        "k_seed": per(st["n_bases"] + st["n_probes"] * 64 + st["n_kept"] * 16, "k_seed"),
+        # k-mer records (16 B) + occurrence headers (16 B) read, every occurrence (8 B) read,
+        # every hit (8 B) written, chain descriptors (24 B) written
+        "k_group": per(st["n_kept"] * 32 + st["n_hits"] * 16 + st["n_chains"] * 24, "k_group"),
+        # every hit read (8 B), a node written per hit (8 B), lis points written (<= 8 B/hit)
+        "k_lis": per(st["n_hits"] * 24 + st["n_chains"] * 24, "k_lis"),
+        # chain descriptors + lis lengths read, lis points read, records written
+        "k_coords": per(st["n_chains"] * 32 + st["n_records"] * 96, "k_coords"),
+        # records read + written
+        "k_rec_sort": per(st["n_records"] * 96 * 2, "k_rec_sort"),
     }
 
 
@@ -135,12 +137,12 @@ def main():
 
     total_bases = comm.sum(bases_rank) * args.steps
     value = total_bases / elapsed
-    stage_ms = {"seed": st["ms_seed"], "group": st["ms_group"], "chain": st["ms_lis"], "records": st["ms_records"]}
-    stage_launches = {"seed": st["launches_seed"], "group": st["launches_group"], "chain": st["launches_lis"],
-                      "records": st["launches_records"]}
-    kb = _kernel_bytes(st, args.steps)
-    dom = max(stage_ms, key=lambda s: stage_ms[s])
-    avg_ms = stage_ms[dom] / max(1, stage_launches[dom])
+    stage_ms = {"seed": st["ms_seed"], "group": st["ms_group"], "lis": st["ms_lis"], "fit": st["ms_fit"],
+                "records": st["ms_records"]}
+    kb = _kernel_bytes(st)
+    kms, kn = st["kernel_ms"], st["kernel_launches"]
+    dom = max(kb, key=lambda k: kms[k])
+    avg_ms = kms[dom] / max(1, kn[dom])
     achieved = kb[dom] / (avg_ms * 1e-3) / 1e9
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_{dom}.json")
@@ -193,6 +195,8 @@ def main():
                           "device_bytes": info["device_bytes"], "build_s": round(t_index, 3),
                           "generate_s": round(t_gen, 3)},
                 "stage_ms_per_step": {s: round(v / args.steps, 3) for s, v in stage_ms.items()},
+                "kernel_ms_per_launch": {k: round(kms[k] / max(1, kn[k]), 3) for k in kms},
+                "kernel_launches": dict(kn),
                 "counters_per_step": {n: st[n] // args.steps for n in
                                       ("n_kmers", "n_probes", "n_kept", "n_hits", "n_chains", "n_lis_tests",
                                        "n_records")},

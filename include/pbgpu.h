@@ -168,7 +168,17 @@ pbgpu_status pbgpu_align_resident(pbgpu_aligner* al, const pbgpu_reads* reads);
 pbgpu_status pbgpu_download(pbgpu_aligner* al, pbgpu_coords_batch** out);
 
 /* Per-stage device time (HIP events on the aligner's stream, summed over
- * launches since the last reset) and algorithmic counters. */
+ * calls since the last reset), per-kernel time (events immediately around a
+ * single launch of the named kernel: the first-tier k_group launch, k_lis,
+ * k_coords, k_seed, k_rec_sort) and algorithmic counters. */
+enum {
+  PBGPU_KERNEL_SEED = 0,
+  PBGPU_KERNEL_GROUP = 1,
+  PBGPU_KERNEL_LIS = 2,
+  PBGPU_KERNEL_COORDS = 3,
+  PBGPU_KERNEL_REC_SORT = 4,
+  PBGPU_KERNEL_N = 8
+};
 typedef struct {
   uint64_t n_batches;
   uint64_t n_reads, n_bases;
@@ -179,8 +189,9 @@ typedef struct {
   uint64_t n_chains;       /* (read, super-read) chains */
   uint64_t n_lis_tests;    /* LIS predecessor tests */
   uint64_t n_records;
-  double   ms_seed, ms_group, ms_lis, ms_records, ms_other;
-  uint64_t launches_seed, launches_group, launches_lis, launches_records;
+  double   ms_seed, ms_group, ms_lis, ms_fit, ms_records;
+  double   kernel_ms[PBGPU_KERNEL_N];
+  uint64_t kernel_launches[PBGPU_KERNEL_N];
 } pbgpu_stats;
 pbgpu_status pbgpu_aligner_get_stats(const pbgpu_aligner* al, pbgpu_stats* s);
 pbgpu_status pbgpu_aligner_reset_stats(pbgpu_aligner* al);

@@ -37,10 +37,21 @@ void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const ui
                   uint32_t hcap_log2, uint32_t* gtable, GroupOut O, unsigned long long* stats, hipStream_t st);
 uint64_t group_table_words(uint32_t hcap_log2);
 constexpr uint32_t kGroupLdsMaxLog2 = 13;  // 8192-slot table, 112 KiB of LDS
-void launch_chain_hist(const ChainDesc* chains, uint32_t n, uint32_t* hist, hipStream_t st);
-void launch_chain_perm(const ChainDesc* chains, uint32_t n, uint32_t* cursor, uint32_t* perm, hipStream_t st);
-void launch_chain(IndexView ix, AlignParamsDev P, LisParams lp, const ChainDesc* chains, const uint32_t* perm,
-                  uint32_t n, Node* nodes, const uint64_t* roff, ChainOut O, hipStream_t st);
+void launch_init_slen(const ChainDesc* chains, uint32_t n_chains, uint32_t* slen, hipStream_t st);
+void launch_strand_order(const uint32_t* slen, uint32_t n_items, uint32_t* hist, uint32_t* cursor, uint32_t* perm,
+                         int phase, hipStream_t st);
+void launch_chain_order(const uint32_t* lisl, uint32_t n, uint32_t* hist, uint32_t* cursor, uint32_t* perm, int phase,
+                        hipStream_t st);
+void launch_lis(bool big_nodes, const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen,
+                const int2* X, uint8_t* N, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx,
+                unsigned long long* stats, hipStream_t st);
+void launch_coords(IndexView ix, AlignParamsDev P, const ChainDesc* chains, const uint32_t* list, uint32_t n,
+                   const uint64_t* roff, uint32_t emit, ChainOut O, hipStream_t st);
+void launch_discard(const ChainDesc* chains, const uint32_t* list, uint32_t n, const uint32_t* lisl, uint32_t* slen,
+                    int2* X, const uint8_t* N, uint32_t* items_small, uint32_t* n_small, uint32_t* items_big,
+                    uint32_t* n_big, hipStream_t st);
+uint32_t len_buckets();
+uint32_t big_bucket();
 void launch_rec_hist(const Rec* recs, uint32_t n, uint32_t* per_read, hipStream_t st);
 void launch_rec_scatter(const Rec* recs, uint32_t n, const uint64_t* rec_off, uint32_t* cursor, uint32_t* order,
                         hipStream_t st);
@@ -453,7 +464,10 @@ struct pbgpu_aligner {
   dbuf<int2> hits;
   dbuf<ChainDesc> chains;
   dbuf<uint32_t> perm;
-  dbuf<Node> nodes;
+  dbuf<int2> X, pts;
+  dbuf<uint8_t> nodes;
+  dbuf<uint32_t> lisl, hist, slen;
+  dbuf<uint32_t> redo[3];
   dbuf<Rec> recs, recs_sorted;
   dbuf<int32_t> info_m, info_b;
   dbuf<uint8_t> tmp;
@@ -464,7 +478,7 @@ struct pbgpu_aligner {
   bool have_result = false;
   // stats
   pbgpu_stats acc{};
-  hipEvent_t ev[8]{};
+  hipEvent_t ev[16]{};
   uint64_t hit_budget = 1200000000ull, rec_hint = 0, info_per_chain = 32;
   dbuf<uint32_t> ovf_list, read_list;
 };
@@ -614,17 +628,19 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
   const uint32_t hcap_log2 = 11;
   al->ovf_reads.ensure(n);
   uint64_t rec_done = 0, info_done = 0;
-  double ms_group = 0, ms_chain = 0;
+  double ms_group = 0, ms_lis = 0, ms_fit = 0;
+  double k_ms[PBGPU_KERNEL_N] = {};
+  uint64_t k_n[PBGPU_KERNEL_N] = {};
   uint64_t n_chains = 0, n_tests = 0;
   for (uint32_t r0 = 0; r0 < n;) {
     uint32_t r1 = r0 + 1;
     while (r1 < n && hoff[r1 + 1] - hoff[r0] <= budget) ++r1;
     const uint64_t Hs = hoff[r1] - hoff[r0];
     const uint32_t nr = r1 - r0;
-    al->nodes.ensure(Hs + 1);
+    al->X.ensure(Hs + 1); al->pts.ensure(Hs + 1); al->nodes.ensure((Hs + 1) * NODE_BYTES);
     al->chains.ensure(std::min<uint64_t>(Hs, (uint64_t)nr << 10) + 1);  // grown below if a batch needs more
     GroupOut O;
-    O.nodes = al->nodes.p; O.chains = al->chains.p;
+    O.X = al->X.p; O.chains = al->chains.p;
     O.chain_count = al->counters.p;
     O.chain_cap = (uint32_t)std::min<uint64_t>(al->chains.n, 0xFFFFFFFFu);
     O.n_overflow = al->counters.p + 3;
@@ -644,9 +660,11 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
       HIPCHK(hipMemsetAsync(al->counters.p, 0, 16 * 4, st));
       static_assert(ST_LIS_TESTS == ST_CHAINS + 1, "per-attempt stat slots are adjacent");
       HIPCHK(hipMemsetAsync(al->stats.p + ST_CHAINS, 0, 16, st));  // redone on a retry: counted per attempt
+      HIPCHK(hipEventRecord(al->ev[8], st));
       launch_group(v, al->krec.p, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0, al->read_list.p, nr,
                    hcap_log2, nullptr, O, al->stats.p, st);
       HIPCHK(hipGetLastError());
+      HIPCHK(hipEventRecord(al->ev[9], st));
       uint32_t cnt[4];
       HIPCHK(hipMemcpyAsync(cnt, al->counters.p, 16, hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
@@ -693,18 +711,45 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
         continue;
       }
       HIPCHK(hipEventRecord(al->ev[6], st));
-      // length-bucketed order (longest first), record/info capacity
-      uint32_t* hist = al->counters.p + 16;  // 32 buckets + 32 cursors
-      HIPCHK(hipMemsetAsync(hist, 0, 64 * 4, st));
-      launch_chain_hist(al->chains.p, nch, hist, st);
-      uint32_t h[32];
-      HIPCHK(hipMemcpyAsync(h, hist, 128, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
-      uint32_t cur[32], acc = 0;
-      for (int b = 31; b >= 0; --b) { cur[b] = acc; acc += h[b]; }
-      HIPCHK(hipMemcpyAsync(hist + 32, cur, 128, hipMemcpyHostToDevice, st));
-      al->perm.ensure(nch + 1);
-      launch_chain_perm(al->chains.p, nch, hist + 32, al->perm.p, st);
+      // strands (chain, fwd|bwd) in length order -> k_lis (16-bit nodes; 32-bit for the longest strands)
+      const uint32_t NB = len_buckets();
+      al->hist.ensure(2 * NB);
+      al->perm.ensure(2ull * nch + 1);
+      al->lisl.ensure(2ull * nch + 1);
+      al->slen.ensure(2ull * nch + 1);
+      uint32_t n_big = 0;
+      auto order = [&](int which, uint32_t n_in) -> uint32_t {  // returns the number of items placed
+        HIPCHK(hipMemsetAsync(al->hist.p, 0, NB * 4, st));
+        if (which == 0) launch_strand_order(al->slen.p, n_in, al->hist.p, nullptr, nullptr, 0, st);
+        else launch_chain_order(al->lisl.p, n_in, al->hist.p, nullptr, nullptr, 0, st);
+        std::vector<uint32_t> h(NB), cur(NB);
+        HIPCHK(hipMemcpyAsync(h.data(), al->hist.p, NB * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        uint32_t acc = 0;
+        for (int b = (int)NB - 1; b >= 1; --b) {  // longest first; bucket 0 = empty
+          cur[b] = acc; acc += h[b];
+          if ((uint32_t)b == big_bucket()) n_big = acc;  // items in buckets >= big_bucket(): > LIS_U16_MAX hits
+        }
+        cur[0] = acc;
+        HIPCHK(hipMemcpyAsync(al->hist.p + NB, cur.data(), NB * 4, hipMemcpyHostToDevice, st));
+        if (which == 0) launch_strand_order(al->slen.p, n_in, nullptr, al->hist.p + NB, al->perm.p, 1, st);
+        else launch_chain_order(al->lisl.p, n_in, nullptr, al->hist.p + NB, al->perm.p, 1, st);
+        HIPCHK(hipGetLastError());
+        return acc;
+      };
+      launch_init_slen(al->chains.p, nch, al->slen.p, st);
+      HIPCHK(hipMemsetAsync(al->lisl.p, 0, 2ull * nch * 4, st));
+      const uint32_t n_strands = order(0, 2 * nch);
+      const uint32_t nbig = n_big;
+      HIPCHK(hipEventRecord(al->ev[11], st));
+      launch_lis(true, al->chains.p, al->perm.p, nbig, al->slen.p, al->X.p, al->nodes.p, al->pts.p, al->lisl.p, al->lp,
+                 al->P.max_match, al->stats.p, st);
+      launch_lis(false, al->chains.p, al->perm.p + nbig, n_strands - nbig, al->slen.p, al->X.p, al->nodes.p, al->pts.p,
+                 al->lisl.p, al->lp, al->P.max_match, al->stats.p, st);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipEventRecord(al->ev[12], st));
+      // chains in lis-length order -> k_coords; record/info capacity
+      const uint32_t n_fit = order(1, nch);
       const uint64_t rec_need = rec_done + (uint64_t)nch * (al->P.max_match ? 2 : 1) + 1024 * (attempt + 1);
       al->recs.grow_keep(std::max<uint64_t>(rec_need, al->rec_hint), rec_done, st);
       if (al->P.unitigs_k) {
@@ -719,13 +764,48 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
       unsigned long long ic = info_done;
       HIPCHK(hipMemcpyAsync(al->info_count.p, &ic, 8, hipMemcpyHostToDevice, st));
       HIPCHK(hipMemsetAsync(al->stats.p + ST_REC_OVERFLOW, 0, 8, st));
+      if (al->P.max_match) { al->redo[0].ensure(nch + 1); al->redo[1].ensure(nch + 1); al->redo[2].ensure(nch + 1); }
+      uint32_t* n_redo = al->counters.p + 8;  // [8] redo count, [9] small items, [10] big items
+      HIPCHK(hipMemsetAsync(n_redo, 0, 12, st));
       ChainOut CO;
+      CO.pts = al->pts.p; CO.lisl = al->lisl.p;
+      CO.redo = al->P.max_match ? al->redo[0].p : nullptr; CO.n_redo = n_redo;
       CO.recs = al->recs.p; CO.rec_count = al->counters.p + 4;
       CO.rec_cap = (uint32_t)std::min<uint64_t>(al->recs.n, 0xFFFFFFFFu);
       CO.info_m = al->info_m.p; CO.info_b = al->info_b.p; CO.info_count = al->info_count.p; CO.info_cap = al->info_m.n;
       CO.stats = al->stats.p;
-      launch_chain(v, al->P, al->lp, al->chains.p, al->perm.p, nch, al->nodes.p, rd->off.p, CO, st);
+      HIPCHK(hipEventRecord(al->ev[13], st));
+      launch_coords(v, al->P, al->chains.p, al->perm.p, n_fit, rd->off.p, 0, CO, st);
       HIPCHK(hipGetLastError());
+      HIPCHK(hipEventRecord(al->ev[14], st));
+      // --max-match rounds: discard the emitted lis, redo the strand's LIS, emit again
+      for (uint32_t round = 1, cur = 0; al->P.max_match; ++round) {
+        uint32_t nr3[3];
+        HIPCHK(hipMemcpyAsync(nr3, n_redo, 12, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        const uint32_t nre = nr3[0];
+        if (!nre) break;
+        uint32_t* list = al->redo[cur].p;
+        uint32_t* small = al->perm.p;            // free after the coords order pass consumed it
+        uint32_t* big = al->perm.p + nch;
+        HIPCHK(hipMemsetAsync(n_redo, 0, 12, st));
+        launch_discard(al->chains.p, list, nre, al->lisl.p, al->slen.p, al->X.p, al->nodes.p, small, n_redo + 1, big,
+                       n_redo + 2, st);
+        HIPCHK(hipMemcpyAsync(nr3, n_redo, 12, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        launch_lis(false, al->chains.p, small, nr3[1], al->slen.p, al->X.p, al->nodes.p, al->pts.p, al->lisl.p, al->lp,
+                   1, al->stats.p, st);
+        launch_lis(true, al->chains.p, big, nr3[2], al->slen.p, al->X.p, al->nodes.p, al->pts.p, al->lisl.p, al->lp,
+                   1, al->stats.p, st);
+        cur ^= 1;
+        CO.redo = al->redo[cur].p;
+        HIPCHK(hipMemsetAsync(n_redo, 0, 4, st));
+        // the chain list of this round is the previous round's redo list
+        HIPCHK(hipMemcpyAsync(al->redo[2].p, list, (size_t)nre * 4, hipMemcpyDeviceToDevice, st));
+        launch_coords(v, al->P, al->chains.p, al->redo[2].p, nre, rd->off.p, round, CO, st);
+        HIPCHK(hipGetLastError());
+      }
+      HIPCHK(hipEventRecord(al->ev[14], st));
       HIPCHK(hipEventRecord(al->ev[7], st));
       uint32_t nrec = 0;
       unsigned long long ninfo = 0, ovf = 0;
@@ -736,7 +816,12 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
       HIPCHK(hipMemcpyAsync(sub, al->stats.p + ST_CHAINS, 16, hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
       ms_group += ev_ms(al->ev[5], al->ev[6]);
-      ms_chain += ev_ms(al->ev[6], al->ev[7]);
+      ms_lis += ev_ms(al->ev[6], al->ev[12]);
+      ms_fit += ev_ms(al->ev[12], al->ev[7]);
+      k_ms[PBGPU_KERNEL_GROUP] += ev_ms(al->ev[8], al->ev[9]);
+      k_ms[PBGPU_KERNEL_LIS] += ev_ms(al->ev[11], al->ev[12]);
+      k_ms[PBGPU_KERNEL_COORDS] += ev_ms(al->ev[13], al->ev[14]);
+      k_n[PBGPU_KERNEL_GROUP]++; k_n[PBGPU_KERNEL_LIS]++; k_n[PBGPU_KERNEL_COORDS]++;
       if (ovf == 0 && nrec <= al->recs.n) {
         rec_done = nrec; info_done = ninfo;
         n_chains += sub[0]; n_tests += sub[1];
@@ -773,6 +858,7 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
   al->sort_scratch.ensure(2ull * nrec + 2);
   al->recs_sorted.ensure(nrec + 1);
   launch_rec_scatter(al->recs.p, nrec, al->rec_off.p, al->rec_cursor.p, al->order.p, st);
+  HIPCHK(hipEventRecord(al->ev[15], st));
   launch_rec_sort(al->recs.p, al->rec_off.p, al->order.p, al->sort_scratch.p, n, al->recs_sorted.p, st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(al->ev[4], st));
@@ -784,9 +870,12 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
   al->acc.n_records += nrec;
   al->acc.ms_seed += ev_ms(al->ev[0], al->ev[1]);
   al->acc.ms_group += ms_group;
-  al->acc.ms_lis += ms_chain;
+  al->acc.ms_lis += ms_lis;
+  al->acc.ms_fit += ms_fit;
   al->acc.ms_records += ev_ms(al->ev[3], al->ev[4]);
-  al->acc.launches_seed += 1; al->acc.launches_group += 1; al->acc.launches_lis += 1; al->acc.launches_records += 1;
+  k_ms[PBGPU_KERNEL_SEED] += ev_ms(al->ev[0], al->ev[1]); k_n[PBGPU_KERNEL_SEED]++;
+  k_ms[PBGPU_KERNEL_REC_SORT] += ev_ms(al->ev[15], al->ev[4]); k_n[PBGPU_KERNEL_REC_SORT]++;
+  for (int i = 0; i < PBGPU_KERNEL_N; ++i) { al->acc.kernel_ms[i] += k_ms[i]; al->acc.kernel_launches[i] += k_n[i]; }
   al->have_result = true;
 }
 

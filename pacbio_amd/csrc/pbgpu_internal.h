@@ -61,15 +61,22 @@ struct ChainDesc {
   uint64_t hit_base;     // first fwd node; bwd nodes follow at hit_base + nf
 };
 
-// One hit = one LIS node (32 B).  The group kernel writes (pb, sr); the chain
-// kernel fills the list fields.  rpb/rsr cache the coordinates of the node's
-// chain root (span_full == X - root, lis_align.hpp:167), aux holds the lis.
-struct __align__(16) Node {
-  int32_t pb, sr;
-  int32_t rpb, rsr;
-  uint32_t nxt, len, P, aux;
+// Per-hit buffers of a sub-batch (hit index = read-local list position +
+// the read's hit offset):
+//   X    int2  (pb offset, signed sr offset), written by k_group in list order
+//   N    16 B  LIS node space per hit; strands of <= 65535 hits use 8-byte
+//              LNode<uint16_t> records packed at the start of their region,
+//              longer strands 16-byte LNode<uint32_t>
+//   pts  int2  the strand's LIS points X[lis[0..len)) after k_lis
+// LNode: singly linked list of lis_align::compute_L_P (lis_align.hpp:139-182);
+// nxt doubles as the lis index array after the forward pass (--max-match).
+template <typename I>
+struct LNode {
+  I nxt, len, P, root;
 };
-static_assert(sizeof(Node) == 32, "Node is one 32-byte record");
+static_assert(sizeof(LNode<uint16_t>) == 8 && sizeof(LNode<uint32_t>) == 16, "node sizes");
+constexpr uint32_t LIS_U16_MAX = 0xFFFFu;   // strands up to this many hits use 16-bit nodes
+constexpr uint32_t NODE_BYTES = 16;         // node space reserved per hit
 
 struct Rec {
   int32_t rs, re, qs, qe, nb_mers;
@@ -86,7 +93,7 @@ enum StatSlot {
 };
 
 struct GroupOut {
-  Node* nodes;
+  int2* X;
   ChainDesc* chains;
   uint32_t* chain_count;
   uint32_t chain_cap;
@@ -101,6 +108,10 @@ struct LisParams {
 };
 
 struct ChainOut {
+  const int2* pts;
+  const uint32_t* lisl;
+  uint32_t* redo;          // --max-match: chains to discard + redo
+  uint32_t* n_redo;
   Rec* recs;
   uint32_t* rec_count;
   uint32_t rec_cap;

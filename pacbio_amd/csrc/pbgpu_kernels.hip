@@ -508,7 +508,7 @@ __global__ __launch_bounds__(GROUP_BLOCK) void k_group(IndexView ix, const KRec*
             }
             __syncthreads();
           }
-          if (valid) *(int2*)&O.nodes[hbase + pos] = make_int2(pb, fwd ? so : -so);
+          if (valid) O.X[hbase + pos] = make_int2(pb, fwd ? so : -so);
         }
       }
       __syncthreads();
@@ -554,40 +554,94 @@ __global__ __launch_bounds__(GROUP_BLOCK) void k_group(IndexView ix, const KRec*
   }
 }
 
-// chains by descending length class (ceil log2 of nf + nb): long chains start
-// first and lanes of a wave get chains of similar length
-DEV uint32_t chain_bucket(const ChainDesc& d) {
-  const uint32_t t = d.nf + d.nb;
-  return t ? 31u - (uint32_t)__clz(t) : 0u;  // floor(log2)
+// Work ordering for the lane-per-item kernels: items by descending length
+// class so the lanes of a wave get items of nearly equal length (exact below
+// 128, 16 classes per octave above).
+constexpr uint32_t NLB = 528;
+DEV uint32_t len_bucket(uint32_t n) {
+  if (n < 128) return n;
+  const uint32_t l = 31u - (uint32_t)__clz(n);
+  return 128u + 16u * (l - 7u) + ((n >> (l - 4u)) & 15u);
 }
-__global__ void k_chain_hist(const ChainDesc* __restrict__ chains, uint32_t n, uint32_t* hist) {
-  __shared__ uint32_t h[32];
-  if (threadIdx.x < 32) h[threadIdx.x] = 0;
+struct StrandLen {  // item = chain << 1 | strand (0 fwd, 1 bwd)
+  const uint32_t* slen;
+  DEV uint32_t operator()(uint32_t i) const { return slen[i]; }
+};
+struct ChainLisLen {  // item = chain; the longer of its two lis
+  const uint32_t* lisl;
+  DEV uint32_t operator()(uint32_t c) const { const uint32_t a = lisl[2 * c], b = lisl[2 * c + 1]; return a > b ? a : b; }
+};
+template <typename F>
+__global__ __launch_bounds__(256) void k_len_hist(F f, uint32_t n, uint32_t* hist) {
+  __shared__ uint32_t h[NLB];
+  for (uint32_t i = threadIdx.x; i < NLB; i += 256) h[i] = 0;
   __syncthreads();
-  for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x)
-    atomicAdd(&h[chain_bucket(chains[c])], 1u);
+  for (uint32_t c = blockIdx.x * 256 + threadIdx.x; c < n; c += gridDim.x * 256) atomicAdd(&h[len_bucket(f(c))], 1u);
   __syncthreads();
-  if (threadIdx.x < 32 && h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+  for (uint32_t i = threadIdx.x; i < NLB; i += 256) if (h[i]) atomicAdd(&hist[i], h[i]);
 }
-__global__ void k_chain_perm(const ChainDesc* __restrict__ chains, uint32_t n, uint32_t* cursor, uint32_t* perm) {
-  // block-aggregated: one global atomic per (block, bucket)
-  __shared__ uint32_t cnt[32], base[32];
-  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (threadIdx.x < 32) cnt[threadIdx.x] = 0;
+// block-aggregated: one global atomic per (block, bucket); zero-length items are dropped
+template <typename F>
+__global__ __launch_bounds__(256) void k_len_perm(F f, uint32_t n, uint32_t* cursor, uint32_t* perm) {
+  __shared__ uint32_t cnt[NLB], base[NLB];
+  for (uint32_t i = threadIdx.x; i < NLB; i += 256) cnt[i] = 0;
   __syncthreads();
+  const uint32_t c = blockIdx.x * 256 + threadIdx.x;
   uint32_t b = 0, loc = 0;
-  if (c < n) { b = chain_bucket(chains[c]); loc = atomicAdd(&cnt[b], 1u); }
+  if (c < n) { b = len_bucket(f(c)); if (b) loc = atomicAdd(&cnt[b], 1u); }
   __syncthreads();
-  if (threadIdx.x < 32 && cnt[threadIdx.x]) base[threadIdx.x] = atomicAdd(&cursor[threadIdx.x], cnt[threadIdx.x]);
+  for (uint32_t i = threadIdx.x; i < NLB; i += 256) if (cnt[i]) base[i] = atomicAdd(&cursor[i], cnt[i]);
   __syncthreads();
-  if (c < n) perm[base[b] + loc] = c;
+  if (c < n && b) perm[base[b] + loc] = c;
 }
 
-// ================================================================= chain
-// One LANE per chain (read, super-read): both strands' LIS, the fit, the
-// filters and --max-match, i.e. coarse_aligner::align_sequence_max's loop body
-// (coarse_aligner.cc:42-60) for one frags_pos entry.  A wave runs 64 chains;
-// the typical LIS scan stops at the list head, which stays in registers.
+// ================================================================= lis / fit
+// Lane-per-item kernels whose per-lane streams are staged through LDS: a wave
+// owns 64 items of similar length and walks them in chunks of CH elements.
+// Each chunk's rows (CH consecutive elements of one item = one 128-byte
+// segment) are loaded / stored cooperatively, CH lanes per row, into a
+// transposed LDS tile, so every HBM access is a whole coalesced segment and
+// the serial per-lane work reads and writes LDS.
+constexpr uint32_t RS = 65;  // LDS tile row stride (elements): one padding column
+
+// all of this wave's LDS and memory operations complete and visible to its lanes
+DEV void wave_drain() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+}
+DEV uint64_t shfl_u64(uint64_t v, int src) {
+  const uint32_t lo = __shfl((uint32_t)v, src, 64), hi = __shfl((uint32_t)(v >> 32), src, 64);
+  return (uint64_t)hi << 32 | lo;
+}
+DEV uint32_t wave_max_u32(uint32_t v) {
+  for (int o = 32; o > 0; o >>= 1) { const uint32_t y = __shfl_xor(v, o, 64); v = y > v ? y : v; }
+  return v;
+}
+// tile[e][l] = src_l[e] for e < cnt_l (every lane passes its own row: base, count)
+template <int CH, typename T>
+DEV void rows_load(T* tile, const T* __restrict__ src, uint64_t base, uint32_t cnt) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int g = 0; g < 64; g += 64 / CH) {
+    const int l = g + lane / CH, e = lane % CH;
+    const uint64_t bl = shfl_u64(base, l);
+    const uint32_t cl = __shfl(cnt, l, 64);
+    if ((uint32_t)e < cl) tile[e * RS + l] = src[bl + e];
+  }
+}
+template <int CH, typename T>
+DEV void rows_store(const T* tile, T* __restrict__ dst, uint64_t base, uint32_t cnt) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int g = 0; g < 64; g += 64 / CH) {
+    const int l = g + lane / CH, e = lane % CH;
+    const uint64_t bl = shfl_u64(base, l);
+    const uint32_t cl = __shfl(cnt, l, 64);
+    if ((uint32_t)e < cl) dst[bl + e] = tile[e * RS + l];
+  }
+}
+
 DEV bool affine_ok(double a, double b, double C, double df, double ds) {
   // (s.first <= b + a*s.second) && (s.second <= b + a*s.first) && s.first <= C && s.second <= C
   return (df <= __dadd_rn(b, __dmul_rn(a, ds))) && (ds <= __dadd_rn(b, __dmul_rn(a, df))) && df <= C && ds <= C;
@@ -597,97 +651,181 @@ DEV bool linear_ok(double a, double df, double ds) {
 }
 
 // lis_align::compute_L_P (lis_align.hpp:139-182) + indices (:190-204),
-// restated literally: singly linked list L, first acceptable predecessor in
-// list order, insertion after the first node of minimal length seen before
-// it.  The window test uses X[i] - X[anc_{W-1}(j)], which equals
-// sum_buffer::test_sum exactly (all values are small integers).
-// Returns the LIS length; the ascending lis is left in A[0..len).aux.
-DEV uint32_t lane_lis(Node* __restrict__ A, uint32_t n, const LisParams& lp, uint64_t& tests) {
+// restated literally, one strand per lane: singly linked list L, first
+// acceptable predecessor in list order, insertion after the first node of
+// minimal length seen before it.  The window test uses X[i] - X[anc_{W-1}(j)],
+// which equals sum_buffer::test_sum exactly (all values are small integers);
+// span_full is X[i] - X[root].  The list head stays in registers (the typical
+// scan stops there); older nodes are read from the chunk tile or from HBM.
+// Forward pass, then a reverse chunk sweep along P writes the lis points
+// pts[0..len) (and, with keep_idx, the lis indices into N[t].nxt).
+template <typename I, int CH>
+__global__ __launch_bounds__(64) void k_lis(const ChainDesc* __restrict__ chains, const uint32_t* __restrict__ items,
+                                            uint32_t n_items, const uint32_t* __restrict__ slen,
+                                            const int2* __restrict__ X, uint8_t* __restrict__ Nraw,
+                                            int2* __restrict__ pts, uint32_t* __restrict__ lisl, LisParams lp,
+                                            int keep_idx, unsigned long long* stats) {
   constexpr uint32_t NONE = 0xFFFFFFFFu;
-  uint32_t head = NONE, longest = 0, longest_ind = 0;
-  int32_t hpb = 0, hsr = 0, hrpb = 0, hrsr = 0;  // head node cached in registers
-  uint32_t hnxt = NONE, hlen = 0;
-  for (uint32_t i = 0; i < n; ++i) {
-    const int2 xi = *(const int2*)&A[i];
-    uint32_t prev = NONE, prev_len = 0, prev_nxt = NONE, found = NONE;
-    uint32_t f_len = 0;
-    int32_t f_rpb = 0, f_rsr = 0;
-    if (head != NONE) {
-      uint32_t it = head, lj = hlen, nx = hnxt;
-      int32_t jpb = hpb, jsr = hsr, jrpb = hrpb, jrsr = hrsr;
-      for (;;) {
-        ++tests;
-        if (xi.y > jsr) {
-          bool ok;
-          if (lp.mer_all) ok = true;
-          else if (lp.W == 1) ok = affine_ok(lp.a, lp.b, lp.C, (double)(xi.x - jpb), (double)(xi.y - jsr));
-          else if (lp.W == 0 || lj < lp.W) ok = true;  // !will_be_filled()
-          else {
-            uint32_t anc = it;
-            for (uint32_t w = 1; w < lp.W; ++w) anc = A[anc].P;
-            const int2 xa = *(const int2*)&A[anc];
-            ok = affine_ok(lp.a, lp.b, lp.C, (double)(xi.x - xa.x), (double)(xi.y - xa.y));
+  constexpr I INONE = (I)~(I)0;
+  __shared__ int2 xs[CH * RS];
+  __shared__ LNode<I> ns[CH * RS];
+  const int lane = lane_id();
+  const uint32_t w = blockIdx.x * 64 + lane;
+  const bool act = w < n_items;
+  uint32_t item = 0, n = 0;
+  uint64_t base = 0;
+  if (act) {
+    item = items[w];
+    const ChainDesc d = chains[item >> 1];
+    base = d.hit_base + ((item & 1) ? d.nf : 0);
+    n = slen[item];
+  }
+  const int2* Xl = X + base;
+  LNode<I>* Nl = (LNode<I>*)(Nraw + base * NODE_BYTES);
+  LNode<I>* Ng = (LNode<I>*)Nraw;  // rows are addressed in node units from the strand base
+  const uint64_t nbase = base * (NODE_BYTES / sizeof(LNode<I>));
+  const uint32_t nmax = wave_max_u32(n);
+  auto wide = [](I v) -> uint32_t { return v == INONE ? NONE : (uint32_t)v; };
+  uint64_t tests = 0;
+  uint32_t head = NONE, hlen = 0, hnxt = NONE, hroot = 0, longest = 0, longest_ind = 0;
+  int2 hx = make_int2(0, 0), hrootx = make_int2(0, 0);
+  for (uint32_t c0 = 0; c0 < nmax; c0 += CH) {
+    const uint32_t cnt = n > c0 ? (n - c0 < CH ? n - c0 : CH) : 0;
+    rows_load<CH>(xs, X, base + c0, cnt);
+    wave_drain();
+    auto getX = [&](uint32_t j) -> int2 { return j >= c0 ? xs[(j - c0) * RS + lane] : Xl[j]; };
+    auto getN = [&](uint32_t j) -> LNode<I> { return j >= c0 ? ns[(j - c0) * RS + lane] : Nl[j]; };
+    for (uint32_t e = 0; e < cnt; ++e) {
+      const uint32_t i = c0 + e;
+      const int2 xi = xs[e * RS + lane];
+      uint32_t prev = NONE, prev_len = 0, prev_nxt = NONE, found = NONE, f_len = 0, f_root = 0;
+      bool f_head = false;
+      if (head != NONE) {
+        uint32_t it = head, lj = hlen, nx = hnxt, jroot = hroot;
+        int2 xj = hx;
+        bool at_head = true;
+        for (;;) {
+          ++tests;
+          if (xi.y > xj.y) {
+            bool ok;
+            if (lp.mer_all) ok = true;
+            else if (lp.W == 1) ok = affine_ok(lp.a, lp.b, lp.C, (double)(xi.x - xj.x), (double)(xi.y - xj.y));
+            else if (lp.W == 0 || lj < lp.W) ok = true;  // !will_be_filled()
+            else {
+              uint32_t anc = it;
+              for (uint32_t q = 1; q < lp.W; ++q) anc = wide(getN(anc).P);
+              const int2 xa = getX(anc);
+              ok = affine_ok(lp.a, lp.b, lp.C, (double)(xi.x - xa.x), (double)(xi.y - xa.y));
+            }
+            if (ok) { found = it; f_len = lj; f_root = jroot; f_head = at_head; break; }
           }
-          if (ok) { found = it; f_len = lj; f_rpb = jrpb; f_rsr = jrsr; break; }
+          if (prev == NONE || lj < prev_len) { prev = it; prev_len = lj; prev_nxt = nx; }
+          it = nx;
+          if (it == NONE) break;
+          const LNode<I> nd = getN(it);
+          xj = getX(it); lj = nd.len; nx = wide(nd.nxt); jroot = nd.root; at_head = false;
         }
-        if (prev == NONE || lj < prev_len) { prev = it; prev_len = lj; prev_nxt = nx; }
-        it = nx;
-        if (it == NONE) break;
-        const Node nd = A[it];
-        jpb = nd.pb; jsr = nd.sr; jrpb = nd.rpb; jrsr = nd.rsr; lj = nd.len; nx = nd.nxt;
+      }
+      LNode<I> en;
+      uint32_t elen, eroot;
+      int2 erootx = xi;
+      bool have_rootx = true;
+      if (found != NONE) {
+        elen = f_len + 1; eroot = f_root; en.P = (I)found;
+        if (f_head) erootx = hrootx; else have_rootx = false;
+      } else {
+        elen = 1; eroot = i; en.P = INONE;
+      }
+      en.len = (I)elen; en.root = (I)eroot;
+      if (prev == NONE) {  // insert at the head
+        if (!have_rootx) { erootx = getX(eroot); have_rootx = true; }
+        en.nxt = head == NONE ? INONE : (I)head;
+        hnxt = head; head = i; hx = xi; hlen = elen; hroot = eroot; hrootx = erootx;
+      } else {
+        en.nxt = prev_nxt == NONE ? INONE : (I)prev_nxt;
+        if (prev >= c0) ns[(prev - c0) * RS + lane].nxt = (I)i;
+        else Nl[prev].nxt = (I)i;
+        if (prev == head) hnxt = i;
+      }
+      ns[e * RS + lane] = en;
+      if (longest < elen) {
+        if (!have_rootx) erootx = getX(eroot);
+        if (lp.seq_all || linear_ok(lp.a, (double)(xi.x - erootx.x), (double)(xi.y - erootx.y))) {
+          longest = elen; longest_ind = i;
+        }
       }
     }
-    Node e;
-    e.pb = xi.x; e.sr = xi.y; e.aux = 0;
-    if (found != NONE) { e.len = f_len + 1; e.rpb = f_rpb; e.rsr = f_rsr; e.P = found; }
-    else { e.len = 1; e.rpb = xi.x; e.rsr = xi.y; e.P = NONE; }
-    if (prev == NONE) {  // insert at the head
-      e.nxt = head;
-      head = i; hpb = e.pb; hsr = e.sr; hrpb = e.rpb; hrsr = e.rsr; hnxt = e.nxt; hlen = e.len;
-    } else {
-      e.nxt = prev_nxt;
-      A[prev].nxt = i;
-      if (prev == head) hnxt = i;
-    }
-    A[i] = e;
-    if (longest < e.len &&
-        (lp.seq_all || linear_ok(lp.a, (double)(xi.x - e.rpb), (double)(xi.y - e.rsr)))) {
-      longest = e.len; longest_ind = i;
-    }
+    wave_drain();
+    rows_store<CH>(ns, Ng, nbase + c0, cnt);
+    wave_drain();
   }
-  uint32_t s = longest_ind;
-  for (uint32_t t = 0; t < longest; ++t) { A[longest - 1 - t].aux = s; s = A[s].P; }
-  return longest;
+  // reverse sweep along P: lis points in ascending order
+  uint32_t s = longest_ind, t = 0;
+  bool need = longest > 0;
+  int2* Pl = pts + base;
+  for (int64_t c0 = nmax ? (int64_t)((nmax - 1) / CH * CH) : -1; c0 >= 0; c0 -= CH) {
+    if (!__ballot(need)) break;
+    const bool here = need && s >= (uint32_t)c0;
+    const uint32_t cnt = here ? (n - (uint32_t)c0 < CH ? n - (uint32_t)c0 : CH) : 0;
+    rows_load<CH>(xs, X, base + c0, cnt);
+    rows_load<CH>(ns, Ng, nbase + c0, cnt);
+    wave_drain();
+    if (here) {
+      while (need && s >= (uint32_t)c0) {
+        const uint32_t o = longest - 1 - t;
+        Pl[o] = xs[(s - c0) * RS + lane];
+        const uint32_t ps = wide(ns[(s - c0) * RS + lane].P);
+        if (keep_idx) Nl[o].nxt = (I)s;  // nxt is dead after the forward pass; the sweep reads only P
+        s = ps;
+        if (++t == longest) need = false;
+      }
+    }
+    wave_drain();
+  }
+  if (act) lisl[item] = longest;
+  tests = wave_sum_u64(tests);
+  if (lane == 0 && tests) atomicAdd(&stats[ST_LIS_TESTS], (unsigned long long)tests);
 }
 
-// compute_kmers_info (pb_aligner.cc:84-143) along one lis.
-// ids: unitig ids of the fwd name; rev => bwd name (reversed list).
-DEV uint32_t kmers_info_run(const uint32_t* ids, uint32_t nsz, bool rev, const AlignParamsDev& P, const Node* A,
-                            uint32_t nlis, bool fwd_align, uint32_t ql, int32_t* mers, int32_t* bases) {
-  const int32_t k = (int32_t)P.k, uk = (int32_t)P.unitigs_k;
-  auto uid = [&](uint32_t i) -> uint32_t { return i >= nsz ? INVALID_UNITIG : (rev ? ids[nsz - 1 - i] : ids[i]); };
-  const uint32_t id0 = uid(0);
-  if (!(id0 != INVALID_UNITIG && id0 < P.n_ul)) return 0;
-  const uint32_t size = 2 * nsz - 1;
-  for (uint32_t i = 0; i < size; ++i) { mers[i] = 0; bases[i] = 0; }
-  uint32_t cunitig = 0;
-  int32_t cend = P.ul[id0];
-  int32_t prev_pos = (int32_t)(0u - P.k);
-  for (uint32_t t = 0; t < nlis; ++t) {
-    const int32_t so = A[A[t].aux].sr;
-    const int32_t pos = fwd_align ? so : (int32_t)(ql + (uint32_t)so - P.k + 2u);
-    const int32_t sr_pos = pos < 0 ? -pos : pos;
+// compute_kmers_info (pb_aligner.cc:84-143) along one lis, one point at a
+// time.  ids: unitig ids of the fwd name; rev => bwd name (reversed list).
+// Any error leaves n_info == 0 (the reference clears both vectors).
+struct KmersInfo {
+  const uint32_t* ids;
+  uint32_t nsz;
+  bool rev, ok;
+  int32_t k, uk;
+  const int32_t* ul;
+  uint64_t n_ul;
+  int32_t* mers;
+  int32_t* bases;
+  uint32_t cunitig;
+  int32_t cend, prev_pos;
+  DEV uint32_t uid(uint32_t i) const { return i >= nsz ? INVALID_UNITIG : (rev ? ids[nsz - 1 - i] : ids[i]); }
+  DEV void init(const AlignParamsDev& P, const uint32_t* ids_, uint32_t nsz_, bool rev_, int32_t* m, int32_t* b) {
+    ids = ids_; nsz = nsz_; rev = rev_; k = (int32_t)P.k; uk = (int32_t)P.unitigs_k; ul = P.ul; n_ul = P.n_ul;
+    mers = m; bases = b;
+    const uint32_t id0 = uid(0);
+    ok = id0 != INVALID_UNITIG && id0 < n_ul;
+    if (!ok) return;
+    for (uint32_t i = 0; i < 2 * nsz - 1; ++i) { mers[i] = 0; bases[i] = 0; }
+    cunitig = 0;
+    cend = ul[id0];
+    prev_pos = (int32_t)(0u - (uint32_t)k);
+  }
+  DEV void add(int32_t sr_pos) {
+    if (!ok) return;
     const int32_t new_bases = k < sr_pos - prev_pos ? k : sr_pos - prev_pos;
     while (sr_pos + k > cend + 1) {
       if (cend >= sr_pos) {
-        if (cunitig >= nsz - 1) return 0;
+        if (cunitig >= nsz - 1) { ok = false; return; }
         const int32_t mx = sr_pos > prev_pos + k ? sr_pos : prev_pos + k;
         const int32_t nbb = cend - mx + 1;
         bases[2 * cunitig] += nbb; bases[2 * cunitig + 1] += nbb;
       }
       const uint32_t id = uid(++cunitig);
-      if (id == INVALID_UNITIG || id >= P.n_ul) return 0;
-      cend = (int32_t)((uint32_t)cend + (uint32_t)P.ul[id] - (uint32_t)uk + 1u);
+      if (id == INVALID_UNITIG || id >= n_ul) { ok = false; return; }
+      cend = (int32_t)((uint32_t)cend + (uint32_t)ul[id] - (uint32_t)uk + 1u);
     }
     ++mers[2 * cunitig];
     bases[2 * cunitig] += new_bases;
@@ -699,41 +837,18 @@ DEV uint32_t kmers_info_run(const uint32_t* ids, uint32_t nsz, bool rev, const A
       const int32_t nbb = new_bases < tt ? new_bases : tt;
       bases[2 * i + 1] += nbb; bases[2 * i + 2] += nbb;
       const uint32_t id = uid(i + 1);
-      if (id != INVALID_UNITIG && id < P.n_ul) cendi = (int32_t)((uint32_t)cendi + (uint32_t)P.ul[id] - (uint32_t)uk + 1u);
-      else return 0;
+      if (id != INVALID_UNITIG && id < n_ul) cendi = (int32_t)((uint32_t)cendi + (uint32_t)ul[id] - (uint32_t)uk + 1u);
+      else { ok = false; return; }
     }
     prev_pos = sr_pos;
   }
-  return size;
-}
+};
 
-// compute_coords_info (pb_aligner.cc:11-82) + the filters of
-// align_sequence_max (coarse_aligner.cc:46-54). Returns true if kept.
-DEV bool coords_record(const IndexView& ix, const AlignParamsDev& P, const ChainDesc& d, uint32_t rl,
-                       const Node* A, uint32_t nlis, bool fwd_align, Rec& R) {
-  const uint32_t k = P.k;
-  const uint32_t ql = (uint32_t)(ix.sr_start[d.sr + 1] - ix.sr_start[d.sr]);
-  R.nb_mers = (int32_t)nlis; R.pb_cons = 0; R.sr_cons = 0; R.pb_cover = k; R.sr_cover = k;
-  R.ql = ql; R.sr = d.sr; R.read = d.read; R.flags = (P.forward && !fwd_align) ? 2u : 0u;
-  R.n_info = 0; R.reserved = 0; R.info_off = 0; R.emit = 0;
-  R.stretch = 0; R.offset = 0; R.avg_err = 0;
-  if (nlis == 0) return false;
-  // least_square_2d::add (least_square_2d.hpp:47-67), x = sr offset, y = pb offset
+// least_square_2d::add (least_square_2d.hpp:47-67), x = sr offset, y = pb offset
+struct Lsq {
   double EX = 0, EY = 0, EXX = 0, EXY = 0, VX = 0, CXY = 0, NB = 0;
   long n = 0;
-  int2 prev = *(const int2*)&A[A[0].aux];
-  const int2 first = prev;
-  for (uint32_t t = 0; t < nlis; ++t) {
-    const int2 c = *(const int2*)&A[A[t].aux];
-    if (t) {
-      const uint32_t pb_diff = (uint32_t)(c.x - prev.x);
-      R.pb_cons += pb_diff == 1u;
-      R.pb_cover += k < pb_diff ? k : pb_diff;
-      const uint32_t sr_diff = (uint32_t)(c.y - prev.y);
-      R.sr_cons += sr_diff == 1u;
-      R.sr_cover += k < sr_diff ? k : sr_diff;
-    }
-    const double x = (double)c.y, y = (double)c.x;
+  DEV void add(double x, double y) {
     ++n;
     const double dn = (double)n;
     const double deltaX = __dadd_rn(x, -EX);
@@ -749,25 +864,14 @@ DEV bool coords_record(const IndexView& ix, const AlignParamsDev& P, const Chain
     EXY = __dadd_rn(EXY, __ddiv_rn(deltaXY, dn));
     CXY = __dadd_rn(CXY, __dmul_rn(deltaX, ndeltaY));
     NB = __dadd_rn(NB, __dadd_rn(__dmul_rn(deltaXY, ndeltaX), -__dmul_rn(deltaXX, ndeltaY)));
-    prev = c;
   }
-  const int2 last = prev;
-  if (n == 1) {
-    R.stretch = 1.0; R.offset = __dadd_rn(EY, -EX); R.avg_err = 0;
-  } else {
-    const double a = __ddiv_rn(CXY, VX), b = __ddiv_rn(NB, VX);
-    R.stretch = a; R.offset = b;
-    double e = 0;
-    for (uint32_t t = 0; t < nlis; ++t) {
-      const int2 c = *(const int2*)&A[A[t].aux];
-      e = __dadd_rn(e, fabs(__dadd_rn(__dadd_rn(__dmul_rn(a, (double)c.y), b), -(double)c.x)));
-    }
-    R.avg_err = __ddiv_rn(e, (double)n);
-  }
-  R.rs = first.x;
-  R.re = (int32_t)((uint32_t)last.x + k - 1u);
-  R.qs = first.y; R.qe = last.y;
-  // coords_info::canonicalize (pb_aligner.hpp:151-167)
+};
+
+// coords_info::canonicalize (pb_aligner.hpp:151-167) and the filters of
+// align_sequence_max (coarse_aligner.cc:46-54): fabs(stretch)==0, min_mers
+// (-M), min_bases (-B) (pb_aligner.hpp:169-174).  Returns true if kept.
+DEV bool coords_finish(const AlignParamsDev& P, uint32_t rl, Rec& R) {
+  const uint32_t k = P.k, ql = R.ql;
   if (R.qs < 0) {
     if (P.forward) {
       R.qs = (int32_t)(uint32_t)((uint64_t)ql + (uint64_t)(int64_t)R.qs - (uint64_t)k + 2ull);
@@ -783,7 +887,6 @@ DEV bool coords_record(const IndexView& ix, const AlignParamsDev& P, const Chain
   } else {
     R.qe = (int32_t)((uint32_t)R.qe + k - 1u);
   }
-  // filters: fabs(stretch)==0, min_mers (-M), min_bases (-B)  (pb_aligner.hpp:169-174)
   if (fabs(R.stretch) == 0.0) return false;
   const double drl = (double)rl;
   double vs = __dadd_rn(R.stretch, R.offset);
@@ -799,62 +902,168 @@ DEV bool coords_record(const IndexView& ix, const AlignParamsDev& P, const Chain
   return true;
 }
 
-__global__ __launch_bounds__(256) void k_chain(IndexView ix, AlignParamsDev P, LisParams lp,
-                                               const ChainDesc* __restrict__ chains, const uint32_t* __restrict__ perm,
-                                               uint32_t n_chains, Node* __restrict__ nodes,
-                                               const uint64_t* __restrict__ roff, ChainOut O) {
-  uint64_t tests = 0;
-  for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < n_chains; w += gridDim.x * blockDim.x) {
-    const ChainDesc d = chains[perm ? perm[w] : w];
-    Node* F = nodes + d.hit_base;
-    Node* B = F + d.nf;
-    uint32_t nf = d.nf, nb = d.nb;
-    uint32_t lf = lane_lis(F, nf, lp, tests);
-    uint32_t lb = lane_lis(B, nb, lp, tests);
-    const uint32_t rl = (uint32_t)(roff[d.read + 1] - roff[d.read]);
-    for (uint32_t emit = 0;; ++emit) {
-      const bool fwd_align = lf >= lb;
-      const uint32_t nl = fwd_align ? lf : lb;
-      if (nl == 0) break;
-      const Node* A = fwd_align ? F : B;
-      Rec R;
-      if (!coords_record(ix, P, d, rl, A, nl, fwd_align, R)) break;
-      R.emit = emit;
-      bool ok = true;
-      if (P.unitigs_k) {
-        const uint32_t u0 = ix.sr_uoff[d.sr], nsz = ix.sr_uoff[d.sr + 1] - u0;
-        const uint32_t need = nsz ? 2 * nsz - 1 : 0;
-        if (need) {
-          const unsigned long long io = atomicAdd(O.info_count, (unsigned long long)need);
-          if (io + need <= O.info_cap) {
-            R.n_info = kmers_info_run(ix.sr_uids + u0, nsz, (R.flags & 2u) != 0, P, A, nl, fwd_align, R.ql,
-                                      O.info_m + io, O.info_b + io);
-            R.info_off = io;
-          } else {
-            ok = false;
-          }
-        }
+// One lane per chain: coarse_aligner::align_sequence_max's loop body
+// (coarse_aligner.cc:42-60) for one emission -- pick the strand
+// (pb_aligner.cc:15, |fwd.lis| >= |bwd.lis|), compute_coords_info
+// (pb_aligner.cc:11-82) over its lis points (staged through LDS in chunks),
+// filters, kmers_info.  With --max-match, kept chains go to the redo list.
+template <int CH>
+__global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, const ChainDesc* __restrict__ chains,
+                                               const uint32_t* __restrict__ list, uint32_t n,
+                                               const uint64_t* __restrict__ roff, uint32_t emit, ChainOut O) {
+  __shared__ int2 ps[CH * RS];
+  const int lane = lane_id();
+  const uint32_t w = blockIdx.x * 64 + lane;
+  const bool act = w < n;
+  uint32_t c = 0, nl = 0;
+  uint64_t base = 0;
+  bool fwd_align = true;
+  ChainDesc d{};
+  if (act) {
+    c = list[w];
+    d = chains[c];
+    const uint32_t lf = O.lisl[2 * c], lb = O.lisl[2 * c + 1];
+    fwd_align = lf >= lb;
+    nl = fwd_align ? lf : lb;
+    base = d.hit_base + (fwd_align ? 0 : d.nf);
+  }
+  const uint32_t nmax = wave_max_u32(nl);
+  const uint32_t k = P.k;
+  Rec R;
+  R.nb_mers = (int32_t)nl; R.pb_cons = 0; R.sr_cons = 0; R.pb_cover = k; R.sr_cover = k;
+  R.ql = act ? (uint32_t)(ix.sr_start[d.sr + 1] - ix.sr_start[d.sr]) : 0;
+  R.sr = d.sr; R.read = d.read; R.flags = (P.forward && !fwd_align) ? 2u : 0u;
+  R.n_info = 0; R.reserved = 0; R.info_off = 0; R.emit = emit;
+  R.stretch = 0; R.offset = 0; R.avg_err = 0;
+  // pass 1: cons / cover and the least-squares fit, in lis order (pb_aligner.cc:19-47)
+  Lsq L;
+  int2 prev = make_int2(0, 0), first = make_int2(0, 0);
+  for (uint32_t c0 = 0; c0 < nmax; c0 += CH) {
+    const uint32_t cnt = nl > c0 ? (nl - c0 < CH ? nl - c0 : CH) : 0;
+    rows_load<CH>(ps, O.pts, base + c0, cnt);
+    wave_drain();
+    for (uint32_t e = 0; e < cnt; ++e) {
+      const int2 p = ps[e * RS + lane];
+      if (c0 + e == 0) {
+        first = p;
+      } else {
+        const uint32_t pb_diff = (uint32_t)(p.x - prev.x);
+        R.pb_cons += pb_diff == 1u;
+        R.pb_cover += k < pb_diff ? k : pb_diff;
+        const uint32_t sr_diff = (uint32_t)(p.y - prev.y);
+        R.sr_cons += sr_diff == 1u;
+        R.sr_cover += k < sr_diff ? k : sr_diff;
       }
-      const uint32_t ri = atomicAdd(O.rec_count, 1u);
-      if (ri < O.rec_cap && ok) O.recs[ri] = R;
-      else atomicAdd(&O.stats[ST_REC_OVERFLOW], 1ull);
-      if (!P.max_match) break;
-      // mer_lists::discard_update_LIS (pb_aligner.hpp:86-92): the longer lis, bwd on ties;
-      // off_lis::discard_LIS (pb_aligner.hpp:47-61) keeps the remaining offsets in order
-      Node* D = lf > lb ? F : B;
-      uint32_t& nD = lf > lb ? nf : nb;
-      uint32_t& lD = lf > lb ? lf : lb;
-      uint32_t wpos = 0, li = 0;
-      for (uint32_t rpos = 0; rpos < nD; ++rpos) {
-        if (li < lD && rpos == D[li].aux) { ++li; continue; }
-        *(int2*)&D[wpos++] = *(const int2*)&D[rpos];
+      L.add((double)p.y, (double)p.x);
+      prev = p;
+    }
+    wave_drain();
+  }
+  // pass 2: average error of the fit (least_square_2d.hpp:70-80 + pb_aligner.cc:49-60)
+  double a = 0, b = 0;
+  if (L.n == 1) {
+    R.stretch = 1.0; R.offset = __dadd_rn(L.EY, -L.EX); R.avg_err = 0;
+  } else if (L.n > 1) {
+    a = __ddiv_rn(L.CXY, L.VX); b = __ddiv_rn(L.NB, L.VX);
+    R.stretch = a; R.offset = b;
+  }
+  const uint32_t nl2 = L.n > 1 ? nl : 0;
+  const uint32_t nmax2 = wave_max_u32(nl2);
+  double err = 0;
+  for (uint32_t c0 = 0; c0 < nmax2; c0 += CH) {
+    const uint32_t cnt = nl2 > c0 ? (nl2 - c0 < CH ? nl2 - c0 : CH) : 0;
+    rows_load<CH>(ps, O.pts, base + c0, cnt);
+    wave_drain();
+    for (uint32_t e = 0; e < cnt; ++e) {
+      const int2 p = ps[e * RS + lane];
+      err = __dadd_rn(err, fabs(__dadd_rn(__dadd_rn(__dmul_rn(a, (double)p.y), b), -(double)p.x)));
+    }
+    wave_drain();
+  }
+  if (L.n > 1) R.avg_err = __ddiv_rn(err, (double)L.n);
+  R.rs = first.x;
+  R.re = (int32_t)((uint32_t)prev.x + k - 1u);
+  R.qs = first.y; R.qe = prev.y;
+  const uint32_t rl = act ? (uint32_t)(roff[d.read + 1] - roff[d.read]) : 0;
+  bool keep = act && nl > 0 && coords_finish(P, rl, R);
+  // pass 3: kmers_info along the lis (pb_aligner.cc:62-81)
+  KmersInfo KI;
+  uint32_t nl3 = 0;
+  bool info_ok = true;
+  if (keep && P.unitigs_k) {
+    const uint32_t u0 = ix.sr_uoff[d.sr], nsz = ix.sr_uoff[d.sr + 1] - u0;
+    const uint32_t need = nsz ? 2 * nsz - 1 : 0;
+    if (need) {
+      const unsigned long long io = atomicAdd(O.info_count, (unsigned long long)need);
+      if (io + need <= O.info_cap) {
+        KI.init(P, ix.sr_uids + u0, nsz, (R.flags & 2u) != 0, O.info_m + io, O.info_b + io);
+        R.info_off = io;
+        if (KI.ok) nl3 = nl; else R.n_info = 0;
+        R.n_info = KI.ok ? 2 * nsz - 1 : 0;
+      } else {
+        info_ok = false;
       }
-      nD -= lD;
-      lD = lane_lis(D, nD, lp, tests);
     }
   }
-  tests = wave_sum_u64(tests);
-  if (lane_id() == 0 && tests) atomicAdd(&O.stats[ST_LIS_TESTS], (unsigned long long)tests);
+  const uint32_t nmax3 = wave_max_u32(nl3);
+  for (uint32_t c0 = 0; c0 < nmax3; c0 += CH) {
+    const uint32_t cnt = nl3 > c0 ? (nl3 - c0 < CH ? nl3 - c0 : CH) : 0;
+    rows_load<CH>(ps, O.pts, base + c0, cnt);
+    wave_drain();
+    for (uint32_t e = 0; e < cnt; ++e) {
+      const int32_t so = ps[e * RS + lane].y;
+      const int32_t pos = fwd_align ? so : (int32_t)(R.ql + (uint32_t)so - k + 2u);
+      KI.add(pos < 0 ? -pos : pos);
+    }
+    wave_drain();
+  }
+  if (nl3 && !KI.ok) R.n_info = 0;
+  if (keep) {
+    const uint32_t ri = atomicAdd(O.rec_count, 1u);
+    if (ri < O.rec_cap && info_ok) O.recs[ri] = R;
+    else atomicAdd(&O.stats[ST_REC_OVERFLOW], 1ull);
+    if (P.max_match) O.redo[atomicAdd(O.n_redo, 1u)] = c;
+  }
+}
+
+// --max-match: mer_lists::discard_update_LIS (pb_aligner.hpp:86-92) drops the
+// longer lis (bwd on ties) from its strand; off_lis::discard_LIS
+// (pb_aligner.hpp:47-61) keeps the remaining offsets in order.  The strand
+// goes to the small- or big-node k_lis list for the next round.
+__global__ void k_discard(const ChainDesc* __restrict__ chains, const uint32_t* __restrict__ list, uint32_t n,
+                          const uint32_t* __restrict__ lisl, uint32_t* __restrict__ slen, int2* __restrict__ X,
+                          const uint8_t* __restrict__ Nraw, uint32_t* items_small, uint32_t* n_small,
+                          uint32_t* items_big, uint32_t* n_big) {
+  for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < n; w += gridDim.x * blockDim.x) {
+    const uint32_t c = list[w];
+    const ChainDesc d = chains[c];
+    const uint32_t lf = lisl[2 * c], lb = lisl[2 * c + 1];
+    const bool dF = lf > lb;
+    const uint32_t item = 2 * c + (dF ? 0u : 1u);
+    const uint64_t base = d.hit_base + (dF ? 0 : d.nf);
+    const uint32_t nD = slen[item], lD = dF ? lf : lb;
+    int2* XD = X + base;
+    const uint8_t* ND = Nraw + base * NODE_BYTES;
+    auto lis_at = [&](uint32_t t) -> uint32_t {
+      return nD <= LIS_U16_MAX ? ((const LNode<uint16_t>*)ND)[t].nxt : ((const LNode<uint32_t>*)ND)[t].nxt;
+    };
+    uint32_t wpos = 0, li = 0, next = lD ? lis_at(0) : 0xFFFFFFFFu;
+    for (uint32_t rpos = 0; rpos < nD; ++rpos) {
+      if (rpos == next) { ++li; next = li < lD ? lis_at(li) : 0xFFFFFFFFu; continue; }
+      XD[wpos++] = XD[rpos];
+    }
+    const uint32_t nn = nD - lD;
+    slen[item] = nn;
+    if (nn <= LIS_U16_MAX) items_small[atomicAdd(n_small, 1u)] = item;
+    else items_big[atomicAdd(n_big, 1u)] = item;
+  }
+}
+
+__global__ void k_init_slen(const ChainDesc* __restrict__ chains, uint32_t n, uint32_t* slen) {
+  for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x) {
+    const ChainDesc d = chains[c];
+    slen[2 * c] = d.nf; slen[2 * c + 1] = d.nb;
+  }
 }
 
 // =============================================================== records
@@ -966,18 +1175,53 @@ static uint32_t grid_for(uint32_t n, uint32_t block, uint32_t cap = 65536) {
   uint64_t g = ((uint64_t)n + block - 1) / block;
   return (uint32_t)(g < 1 ? 1 : (g > cap ? cap : g));
 }
-void launch_chain_hist(const ChainDesc* chains, uint32_t n, uint32_t* hist, hipStream_t st) {
-  if (!n) return;
-  hipLaunchKernelGGL(k_chain_hist, dim3(grid_for(n, 256, 2048)), dim3(256), 0, st, chains, n, hist);
+void launch_init_slen(const ChainDesc* chains, uint32_t n_chains, uint32_t* slen, hipStream_t st) {
+  if (!n_chains) return;
+  hipLaunchKernelGGL(k_init_slen, dim3(grid_for(n_chains, 256)), dim3(256), 0, st, chains, n_chains, slen);
 }
-void launch_chain_perm(const ChainDesc* chains, uint32_t n, uint32_t* cursor, uint32_t* perm, hipStream_t st) {
-  if (!n) return;
-  hipLaunchKernelGGL(k_chain_perm, dim3((n + 255) / 256), dim3(256), 0, st, chains, n, cursor, perm);
+void launch_strand_order(const uint32_t* slen, uint32_t n_items, uint32_t* hist, uint32_t* cursor, uint32_t* perm,
+                         int phase, hipStream_t st) {
+  if (!n_items) return;
+  StrandLen f{slen};
+  if (phase == 0) hipLaunchKernelGGL((k_len_hist<StrandLen>), dim3(grid_for(n_items, 256, 2048)), dim3(256), 0, st, f, n_items, hist);
+  else hipLaunchKernelGGL((k_len_perm<StrandLen>), dim3((n_items + 255) / 256), dim3(256), 0, st, f, n_items, cursor, perm);
 }
-void launch_chain(IndexView ix, AlignParamsDev P, LisParams lp, const ChainDesc* chains, const uint32_t* perm,
-                  uint32_t n, Node* nodes, const uint64_t* roff, ChainOut O, hipStream_t st) {
+void launch_chain_order(const uint32_t* lisl, uint32_t n, uint32_t* hist, uint32_t* cursor, uint32_t* perm, int phase,
+                        hipStream_t st) {
   if (!n) return;
-  hipLaunchKernelGGL(k_chain, dim3(grid_for(n, 256)), dim3(256), 0, st, ix, P, lp, chains, perm, n, nodes, roff, O);
+  ChainLisLen f{lisl};
+  if (phase == 0) hipLaunchKernelGGL((k_len_hist<ChainLisLen>), dim3(grid_for(n, 256, 2048)), dim3(256), 0, st, f, n, hist);
+  else hipLaunchKernelGGL((k_len_perm<ChainLisLen>), dim3((n + 255) / 256), dim3(256), 0, st, f, n, cursor, perm);
+}
+constexpr int LIS_CH16 = 16, LIS_CH32 = 8, FIT_CH = 16;
+void launch_lis(bool big_nodes, const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen,
+                const int2* X, uint8_t* N, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx,
+                unsigned long long* stats, hipStream_t st) {
+  if (!n_items) return;
+  const dim3 grid((n_items + 63) / 64);
+  if (big_nodes)
+    hipLaunchKernelGGL((k_lis<uint32_t, LIS_CH32>), grid, dim3(64), 0, st, chains, items, n_items, slen, X, N, pts, lisl,
+                       lp, keep_idx, stats);
+  else
+    hipLaunchKernelGGL((k_lis<uint16_t, LIS_CH16>), grid, dim3(64), 0, st, chains, items, n_items, slen, X, N, pts, lisl,
+                       lp, keep_idx, stats);
+}
+void launch_coords(IndexView ix, AlignParamsDev P, const ChainDesc* chains, const uint32_t* list, uint32_t n,
+                   const uint64_t* roff, uint32_t emit, ChainOut O, hipStream_t st) {
+  if (!n) return;
+  hipLaunchKernelGGL((k_coords<FIT_CH>), dim3((n + 63) / 64), dim3(64), 0, st, ix, P, chains, list, n, roff, emit, O);
+}
+void launch_discard(const ChainDesc* chains, const uint32_t* list, uint32_t n, const uint32_t* lisl, uint32_t* slen,
+                    int2* X, const uint8_t* N, uint32_t* items_small, uint32_t* n_small, uint32_t* items_big,
+                    uint32_t* n_big, hipStream_t st) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_discard, dim3(grid_for(n, 256)), dim3(256), 0, st, chains, list, n, lisl, slen, X, N, items_small,
+                     n_small, items_big, n_big);
+}
+uint32_t len_buckets() { return NLB; }
+uint32_t big_bucket() {  // first length class whose items all exceed LIS_U16_MAX
+  static_assert(LIS_U16_MAX == 65535u, "len_bucket(65536) starts a class");
+  return 128u + 16u * (16u - 7u);
 }
 
 void launch_rec_hist(const Rec* recs, uint32_t n, uint32_t* per_read, hipStream_t st) {

@@ -81,11 +81,18 @@ class CoordsBatch(C.Structure):
 class Stats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("n_batches", "n_reads", "n_bases", "n_kmers", "n_probes", "n_kept",
                                           "n_hits", "n_chains", "n_lis_tests", "n_records")] + \
-               [(n, C.c_double) for n in ("ms_seed", "ms_group", "ms_lis", "ms_records", "ms_other")] + \
-               [(n, C.c_uint64) for n in ("launches_seed", "launches_group", "launches_lis", "launches_records")]
+               [(n, C.c_double) for n in ("ms_seed", "ms_group", "ms_lis", "ms_fit", "ms_records")] + \
+               [("kernel_ms", C.c_double * 8), ("kernel_launches", C.c_uint64 * 8)]
 
     def as_dict(self):
-        return {n: getattr(self, n) for n, _ in self._fields_}
+        d = {n: getattr(self, n) for n, _ in self._fields_ if not n.startswith("kernel_")}
+        d["kernel_ms"] = {k: self.kernel_ms[i] for k, i in KERNELS.items()}
+        d["kernel_launches"] = {k: self.kernel_launches[i] for k, i in KERNELS.items()}
+        return d
+
+
+# pbgpu.h PBGPU_KERNEL_*: kernels timed individually
+KERNELS = {"k_seed": 0, "k_group": 1, "k_lis": 2, "k_coords": 3, "k_rec_sort": 4}
 
 
 _lib = None
