@@ -195,6 +195,10 @@ typedef struct {
 } pbgpu_stats;
 pbgpu_status pbgpu_aligner_get_stats(const pbgpu_aligner* al, pbgpu_stats* s);
 pbgpu_status pbgpu_aligner_reset_stats(pbgpu_aligner* al);
+/* Tuning: the maximum number of seed hits grouped and chained per device
+ * sub-batch (default 1.2e9, about 38 GB of working buffers).  A read whose
+ * hits exceed it forms a sub-batch of its own.  Results do not depend on it. */
+pbgpu_status pbgpu_aligner_set_hit_budget(pbgpu_aligner* al, uint64_t hits);
 
 /* --------------------------------------------------------------- output
  * print_coords_header + print_coords (jf_aligner.cc:32-70): headers are the

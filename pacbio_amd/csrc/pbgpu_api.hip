@@ -43,13 +43,13 @@ void launch_strand_order(const uint32_t* slen, uint32_t n_items, uint32_t* hist,
 void launch_chain_order(const uint32_t* lisl, uint32_t n, uint32_t* hist, uint32_t* cursor, uint32_t* perm, int phase,
                         hipStream_t st);
 void launch_lis(bool big_nodes, const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen,
-                const int2* X, uint8_t* N, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx,
+                const int2* X, void* N, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx,
                 unsigned long long* stats, hipStream_t st);
 void launch_coords(IndexView ix, AlignParamsDev P, const ChainDesc* chains, const uint32_t* list, uint32_t n,
                    const uint64_t* roff, uint32_t emit, ChainOut O, hipStream_t st);
 void launch_discard(const ChainDesc* chains, const uint32_t* list, uint32_t n, const uint32_t* lisl, uint32_t* slen,
-                    int2* X, const uint8_t* N, uint32_t* items_small, uint32_t* n_small, uint32_t* items_big,
-                    uint32_t* n_big, hipStream_t st);
+                    int2* X, const void* N16, const void* N32, uint32_t* items_small, uint32_t* n_small,
+                    uint32_t* items_big, uint32_t* n_big, hipStream_t st);
 uint32_t len_buckets();
 uint32_t big_bucket();
 void launch_rec_hist(const Rec* recs, uint32_t n, uint32_t* per_read, hipStream_t st);
@@ -465,7 +465,7 @@ struct pbgpu_aligner {
   dbuf<ChainDesc> chains;
   dbuf<uint32_t> perm;
   dbuf<int2> X, pts;
-  dbuf<uint8_t> nodes;
+  dbuf<uint8_t> nodes, nodes32;  // LNode<uint16_t> / LNode<uint32_t> per hit
   dbuf<uint32_t> lisl, hist, slen;
   dbuf<uint32_t> redo[3];
   dbuf<Rec> recs, recs_sorted;
@@ -637,7 +637,7 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
     while (r1 < n && hoff[r1 + 1] - hoff[r0] <= budget) ++r1;
     const uint64_t Hs = hoff[r1] - hoff[r0];
     const uint32_t nr = r1 - r0;
-    al->X.ensure(Hs + 1); al->pts.ensure(Hs + 1); al->nodes.ensure((Hs + 1) * NODE_BYTES);
+    al->X.ensure(Hs + 1); al->pts.ensure(Hs + 1); al->nodes.ensure((Hs + 1) * 8);
     al->chains.ensure(std::min<uint64_t>(Hs, (uint64_t)nr << 10) + 1);  // grown below if a batch needs more
     GroupOut O;
     O.X = al->X.p; O.chains = al->chains.p;
@@ -678,7 +678,7 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
         uint64_t mx = 0;
         for (uint32_t r : ovf) mx = std::max(mx, hoff[r + 1] - hoff[r]);
         if ((1ull << lg) > 2 * mx + 256) throw std::runtime_error("group table growth did not converge");
-        lg += 2;
+        lg += lg < kGroupLdsMaxLog2 ? 1 : 2;  // 2048 -> 4096 -> 8192 slots in LDS, then HBM tables
         al->ovf_list.ensure(n_ovf);
         HIPCHK(hipMemcpyAsync(al->ovf_list.p, ovf.data(), n_ovf * 4, hipMemcpyHostToDevice, st));
         HIPCHK(hipMemsetAsync(al->counters.p + 3, 0, 4, st));
@@ -741,8 +741,9 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
       HIPCHK(hipMemsetAsync(al->lisl.p, 0, 2ull * nch * 4, st));
       const uint32_t n_strands = order(0, 2 * nch);
       const uint32_t nbig = n_big;
+      if (nbig) al->nodes32.ensure((Hs + 1) * 16);
       HIPCHK(hipEventRecord(al->ev[11], st));
-      launch_lis(true, al->chains.p, al->perm.p, nbig, al->slen.p, al->X.p, al->nodes.p, al->pts.p, al->lisl.p, al->lp,
+      launch_lis(true, al->chains.p, al->perm.p, nbig, al->slen.p, al->X.p, al->nodes32.p, al->pts.p, al->lisl.p, al->lp,
                  al->P.max_match, al->stats.p, st);
       launch_lis(false, al->chains.p, al->perm.p + nbig, n_strands - nbig, al->slen.p, al->X.p, al->nodes.p, al->pts.p,
                  al->lisl.p, al->lp, al->P.max_match, al->stats.p, st);
@@ -789,13 +790,13 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
         uint32_t* small = al->perm.p;            // free after the coords order pass consumed it
         uint32_t* big = al->perm.p + nch;
         HIPCHK(hipMemsetAsync(n_redo, 0, 12, st));
-        launch_discard(al->chains.p, list, nre, al->lisl.p, al->slen.p, al->X.p, al->nodes.p, small, n_redo + 1, big,
-                       n_redo + 2, st);
+        launch_discard(al->chains.p, list, nre, al->lisl.p, al->slen.p, al->X.p, al->nodes.p, al->nodes32.p, small,
+                       n_redo + 1, big, n_redo + 2, st);
         HIPCHK(hipMemcpyAsync(nr3, n_redo, 12, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         launch_lis(false, al->chains.p, small, nr3[1], al->slen.p, al->X.p, al->nodes.p, al->pts.p, al->lisl.p, al->lp,
                    1, al->stats.p, st);
-        launch_lis(true, al->chains.p, big, nr3[2], al->slen.p, al->X.p, al->nodes.p, al->pts.p, al->lisl.p, al->lp,
+        launch_lis(true, al->chains.p, big, nr3[2], al->slen.p, al->X.p, al->nodes32.p, al->pts.p, al->lisl.p, al->lp,
                    1, al->stats.p, st);
         cur ^= 1;
         CO.redo = al->redo[cur].p;
@@ -937,6 +938,13 @@ pbgpu_status pbgpu_aligner_get_stats(const pbgpu_aligner* al, pbgpu_stats* s) {
 pbgpu_status pbgpu_aligner_reset_stats(pbgpu_aligner* al) {
   if (!al) return fail(PBGPU_ERR_INVALID, "null argument");
   memset(&al->acc, 0, sizeof al->acc);
+  return PBGPU_OK;
+}
+
+pbgpu_status pbgpu_aligner_set_hit_budget(pbgpu_aligner* al, uint64_t hits) {
+  if (!al) return fail(PBGPU_ERR_INVALID, "null argument");
+  if (hits == 0) return fail(PBGPU_ERR_INVALID, "hit budget must be > 0");
+  al->hit_budget = hits;
   return PBGPU_OK;
 }
 

@@ -64,9 +64,9 @@ struct ChainDesc {
 // Per-hit buffers of a sub-batch (hit index = read-local list position +
 // the read's hit offset):
 //   X    int2  (pb offset, signed sr offset), written by k_group in list order
-//   N    16 B  LIS node space per hit; strands of <= 65535 hits use 8-byte
-//              LNode<uint16_t> records packed at the start of their region,
-//              longer strands 16-byte LNode<uint32_t>
+//   N16  8 B   LIS node per hit, LNode<uint16_t> (strands of <= 65535 hits)
+//   N32  16 B  LIS node per hit, LNode<uint32_t> (longer strands; allocated
+//              only when a sub-batch has such strands)
 //   pts  int2  the strand's LIS points X[lis[0..len)) after k_lis
 // LNode: singly linked list of lis_align::compute_L_P (lis_align.hpp:139-182);
 // nxt doubles as the lis index array after the forward pass (--max-match).
@@ -76,7 +76,6 @@ struct LNode {
 };
 static_assert(sizeof(LNode<uint16_t>) == 8 && sizeof(LNode<uint32_t>) == 16, "node sizes");
 constexpr uint32_t LIS_U16_MAX = 0xFFFFu;   // strands up to this many hits use 16-bit nodes
-constexpr uint32_t NODE_BYTES = 16;         // node space reserved per hit
 
 struct Rec {
   int32_t rs, re, qs, qe, nb_mers;

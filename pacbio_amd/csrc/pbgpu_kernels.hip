@@ -618,29 +618,80 @@ DEV uint32_t wave_max_u32(uint32_t v) {
   for (int o = 32; o > 0; o >>= 1) { const uint32_t y = __shfl_xor(v, o, 64); v = y > v ? y : v; }
   return v;
 }
-// tile[e][l] = src_l[e] for e < cnt_l (every lane passes its own row: base, count)
+// tile[e][l] = src[row_l + e] for lo_l <= e < hi_l (every lane passes its own row)
 template <int CH, typename T>
-DEV void rows_load(T* tile, const T* __restrict__ src, uint64_t base, uint32_t cnt) {
+DEV void rows_load(T* tile, const T* __restrict__ src, uint64_t row, uint32_t lo, uint32_t hi) {
   const int lane = lane_id();
 #pragma unroll
   for (int g = 0; g < 64; g += 64 / CH) {
     const int l = g + lane / CH, e = lane % CH;
-    const uint64_t bl = shfl_u64(base, l);
-    const uint32_t cl = __shfl(cnt, l, 64);
-    if ((uint32_t)e < cl) tile[e * RS + l] = src[bl + e];
+    const uint64_t rl = shfl_u64(row, l);
+    const uint32_t lol = __shfl(lo, l, 64), hil = __shfl(hi, l, 64);
+    if ((uint32_t)e >= lol && (uint32_t)e < hil) tile[e * RS + l] = src[rl + e];
   }
 }
 template <int CH, typename T>
-DEV void rows_store(const T* tile, T* __restrict__ dst, uint64_t base, uint32_t cnt) {
+DEV void rows_store(const T* tile, T* __restrict__ dst, uint64_t row, uint32_t lo, uint32_t hi) {
   const int lane = lane_id();
 #pragma unroll
   for (int g = 0; g < 64; g += 64 / CH) {
     const int l = g + lane / CH, e = lane % CH;
-    const uint64_t bl = shfl_u64(base, l);
-    const uint32_t cl = __shfl(cnt, l, 64);
-    if ((uint32_t)e < cl) dst[bl + e] = tile[e * RS + l];
+    const uint64_t rl = shfl_u64(row, l);
+    const uint32_t lol = __shfl(lo, l, 64), hil = __shfl(hi, l, 64);
+    if ((uint32_t)e >= lol && (uint32_t)e < hil) dst[rl + e] = tile[e * RS + l];
   }
 }
+// Software-pipelined row load: issue() starts the global loads of one chunk
+// into registers (each lane holds 64/CH elements of the transposed tile),
+// commit() writes them to the LDS tile -- so the HBM latency of chunk j+1
+// overlaps the serial work on chunk j.
+template <int CH, typename T>
+struct RowPipe {
+  static constexpr int G = 64 / CH;
+  T v[G];
+  uint32_t mask;
+  DEV void issue(const T* __restrict__ src, uint64_t row, uint32_t lo, uint32_t hi) {
+    const int lane = lane_id();
+    mask = 0;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int l = g * CH + lane / CH, e = lane % CH;
+      const uint64_t rl = shfl_u64(row, l);
+      const uint32_t lol = __shfl(lo, l, 64), hil = __shfl(hi, l, 64);
+      if ((uint32_t)e >= lol && (uint32_t)e < hil) { v[g] = src[rl + e]; mask |= 1u << g; }
+    }
+  }
+  DEV void commit(T* tile) const {
+    const int lane = lane_id();
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int l = g * CH + lane / CH, e = lane % CH;
+      if (mask & (1u << g)) tile[e * RS + l] = v[g];
+    }
+  }
+};
+DEV void lds_fence() {
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS traffic done
+  __builtin_amdgcn_wave_barrier();
+}
+
+// A lane's item occupies [b, b + n) of a per-hit array; chunks follow the
+// absolute CH-aligned grid so that every row is one aligned segment.
+template <int CH>
+struct ChunkGrid {
+  uint64_t b, a0;   // item start, aligned start of chunk 0
+  uint32_t n;
+  DEV void init(uint64_t b_, uint32_t n_) { b = b_; n = n_; a0 = b_ & ~(uint64_t)(CH - 1); }
+  DEV uint32_t chunks() const { return n ? (uint32_t)((b - a0 + n + CH - 1) / CH) : 0; }
+  DEV uint64_t row(uint32_t j) const { return a0 + (uint64_t)j * CH; }
+  // valid element slots [lo, hi) of chunk j
+  DEV uint32_t lo(uint32_t j) const { const uint64_t r = row(j); return r >= b ? 0u : (uint32_t)(b - r); }
+  DEV uint32_t hi(uint32_t j) const {
+    const uint64_t r = row(j), e = b + n;
+    if (!n || r >= e) return 0u;
+    return e - r < CH ? (uint32_t)(e - r) : (uint32_t)CH;
+  }
+};
 
 DEV bool affine_ok(double a, double b, double C, double df, double ds) {
   // (s.first <= b + a*s.second) && (s.second <= b + a*s.first) && s.first <= C && s.second <= C
@@ -662,7 +713,7 @@ DEV bool linear_ok(double a, double df, double ds) {
 template <typename I, int CH>
 __global__ __launch_bounds__(64) void k_lis(const ChainDesc* __restrict__ chains, const uint32_t* __restrict__ items,
                                             uint32_t n_items, const uint32_t* __restrict__ slen,
-                                            const int2* __restrict__ X, uint8_t* __restrict__ Nraw,
+                                            const int2* __restrict__ X, LNode<I>* __restrict__ N,
                                             int2* __restrict__ pts, uint32_t* __restrict__ lisl, LisParams lp,
                                             int keep_idx, unsigned long long* stats) {
   constexpr uint32_t NONE = 0xFFFFFFFFu;
@@ -680,24 +731,37 @@ __global__ __launch_bounds__(64) void k_lis(const ChainDesc* __restrict__ chains
     base = d.hit_base + ((item & 1) ? d.nf : 0);
     n = slen[item];
   }
+  ChunkGrid<CH> G;
+  G.init(base, n);
   const int2* Xl = X + base;
-  LNode<I>* Nl = (LNode<I>*)(Nraw + base * NODE_BYTES);
-  LNode<I>* Ng = (LNode<I>*)Nraw;  // rows are addressed in node units from the strand base
-  const uint64_t nbase = base * (NODE_BYTES / sizeof(LNode<I>));
-  const uint32_t nmax = wave_max_u32(n);
+  LNode<I>* Nl = N + base;
+  const uint32_t nch = wave_max_u32(G.chunks());
   auto wide = [](I v) -> uint32_t { return v == INONE ? NONE : (uint32_t)v; };
   uint64_t tests = 0;
   uint32_t head = NONE, hlen = 0, hnxt = NONE, hroot = 0, longest = 0, longest_ind = 0;
   int2 hx = make_int2(0, 0), hrootx = make_int2(0, 0);
-  for (uint32_t c0 = 0; c0 < nmax; c0 += CH) {
-    const uint32_t cnt = n > c0 ? (n - c0 < CH ? n - c0 : CH) : 0;
-    rows_load<CH>(xs, X, base + c0, cnt);
-    wave_drain();
-    auto getX = [&](uint32_t j) -> int2 { return j >= c0 ? xs[(j - c0) * RS + lane] : Xl[j]; };
-    auto getN = [&](uint32_t j) -> LNode<I> { return j >= c0 ? ns[(j - c0) * RS + lane] : Nl[j]; };
-    for (uint32_t e = 0; e < cnt; ++e) {
+  RowPipe<CH, int2> px;
+  if (nch) px.issue(X, G.row(0), G.lo(0), G.hi(0));
+  for (uint32_t j = 0; j < nch; ++j) {
+    const uint32_t lo = G.lo(j), hi = G.hi(j);
+    const uint64_t row = G.row(j);
+    px.commit(xs);
+    if (j + 1 < nch) px.issue(X, G.row(j + 1), G.lo(j + 1), G.hi(j + 1));
+    lds_fence();
+    int2 xr[CH];
+#pragma unroll
+    for (int e = 0; e < CH; ++e) xr[e] = xs[e * RS + lane];
+    // local index of slot 0 of this chunk (wraps for the first chunk; only c0 + e with e >= lo is used)
+    const uint32_t c0 = (uint32_t)(row - base);
+    const uint32_t first = hi > lo ? c0 + lo : 0u;  // smallest local index held in the tile
+    auto in_tile = [&](uint32_t q) -> bool { return hi > lo && q >= first; };
+    auto getX = [&](uint32_t q) -> int2 { return in_tile(q) ? xs[(q - c0) * RS + lane] : Xl[q]; };
+    auto getN = [&](uint32_t q) -> LNode<I> { return in_tile(q) ? ns[(q - c0) * RS + lane] : Nl[q]; };
+#pragma unroll
+    for (int e = 0; e < CH; ++e) {
+      if ((uint32_t)e < lo || (uint32_t)e >= hi) continue;
       const uint32_t i = c0 + e;
-      const int2 xi = xs[e * RS + lane];
+      const int2 xi = xr[e];
       uint32_t prev = NONE, prev_len = 0, prev_nxt = NONE, found = NONE, f_len = 0, f_root = 0;
       bool f_head = false;
       if (head != NONE) {
@@ -743,7 +807,7 @@ __global__ __launch_bounds__(64) void k_lis(const ChainDesc* __restrict__ chains
         hnxt = head; head = i; hx = xi; hlen = elen; hroot = eroot; hrootx = erootx;
       } else {
         en.nxt = prev_nxt == NONE ? INONE : (I)prev_nxt;
-        if (prev >= c0) ns[(prev - c0) * RS + lane].nxt = (I)i;
+        if (in_tile(prev)) ns[(prev - c0) * RS + lane].nxt = (I)i;
         else Nl[prev].nxt = (I)i;
         if (prev == head) hnxt = i;
       }
@@ -755,23 +819,44 @@ __global__ __launch_bounds__(64) void k_lis(const ChainDesc* __restrict__ chains
         }
       }
     }
-    wave_drain();
-    rows_store<CH>(ns, Ng, nbase + c0, cnt);
-    wave_drain();
+    lds_fence();
+    rows_store<CH>(ns, N, row, lo, hi);
+    lds_fence();  // tile rows read before the next chunk overwrites them
   }
   // reverse sweep along P: lis points in ascending order
   uint32_t s = longest_ind, t = 0;
   bool need = longest > 0;
   int2* Pl = pts + base;
-  for (int64_t c0 = nmax ? (int64_t)((nmax - 1) / CH * CH) : -1; c0 >= 0; c0 -= CH) {
+  auto sweep_rows = [&](int64_t j, uint32_t& lo, uint32_t& hi) {
+    const bool here = need && (uint64_t)base + s >= G.row((uint32_t)j);
+    lo = here ? G.lo((uint32_t)j) : 0; hi = here ? G.hi((uint32_t)j) : 0;
+  };
+  RowPipe<CH, LNode<I>> pn;
+  int64_t j = (int64_t)nch - 1;
+  uint32_t lo_n = 0, hi_n = 0;
+  if (j >= 0) {
+    sweep_rows(j, lo_n, hi_n);
+    px.issue(X, G.row((uint32_t)j), lo_n, hi_n);
+    pn.issue(N, G.row((uint32_t)j), lo_n, hi_n);
+  }
+  for (; j >= 0; --j) {
     if (!__ballot(need)) break;
-    const bool here = need && s >= (uint32_t)c0;
-    const uint32_t cnt = here ? (n - (uint32_t)c0 < CH ? n - (uint32_t)c0 : CH) : 0;
-    rows_load<CH>(xs, X, base + c0, cnt);
-    rows_load<CH>(ns, Ng, nbase + c0, cnt);
-    wave_drain();
-    if (here) {
-      while (need && s >= (uint32_t)c0) {
+    const uint64_t row = G.row((uint32_t)j);
+    const uint32_t c0 = (uint32_t)(row - base);
+    px.commit(xs);
+    pn.commit(ns);
+    // the next chunk down: every lane still needing points reaches into it
+    if (j >= 1) {
+      const bool later = need;  // conservative: rows of lanes whose walk may continue below this chunk
+      const uint64_t r1 = G.row((uint32_t)(j - 1));
+      const uint32_t lo1 = later ? G.lo((uint32_t)(j - 1)) : 0, hi1 = later ? G.hi((uint32_t)(j - 1)) : 0;
+      (void)r1;
+      px.issue(X, r1, lo1, hi1);
+      pn.issue(N, r1, lo1, hi1);
+    }
+    lds_fence();
+    if (need && (uint64_t)base + s >= row) {
+      while (need && (uint64_t)base + s >= row) {
         const uint32_t o = longest - 1 - t;
         Pl[o] = xs[(s - c0) * RS + lane];
         const uint32_t ps = wide(ns[(s - c0) * RS + lane].P);
@@ -780,8 +865,9 @@ __global__ __launch_bounds__(64) void k_lis(const ChainDesc* __restrict__ chains
         if (++t == longest) need = false;
       }
     }
-    wave_drain();
+    lds_fence();
   }
+  (void)lo_n; (void)hi_n;
   if (act) lisl[item] = longest;
   tests = wave_sum_u64(tests);
   if (lane == 0 && tests) atomicAdd(&stats[ST_LIS_TESTS], (unsigned long long)tests);
@@ -797,18 +883,22 @@ struct KmersInfo {
   int32_t k, uk;
   const int32_t* ul;
   uint64_t n_ul;
-  int32_t* mers;
+  int32_t* mers;    // element i at mers[i * stride]
   int32_t* bases;
+  uint32_t stride;
   uint32_t cunitig;
   int32_t cend, prev_pos;
   DEV uint32_t uid(uint32_t i) const { return i >= nsz ? INVALID_UNITIG : (rev ? ids[nsz - 1 - i] : ids[i]); }
-  DEV void init(const AlignParamsDev& P, const uint32_t* ids_, uint32_t nsz_, bool rev_, int32_t* m, int32_t* b) {
+  DEV int32_t& M(uint32_t i) { return mers[i * stride]; }
+  DEV int32_t& B(uint32_t i) { return bases[i * stride]; }
+  DEV void init(const AlignParamsDev& P, const uint32_t* ids_, uint32_t nsz_, bool rev_, int32_t* m, int32_t* b,
+                uint32_t stride_) {
     ids = ids_; nsz = nsz_; rev = rev_; k = (int32_t)P.k; uk = (int32_t)P.unitigs_k; ul = P.ul; n_ul = P.n_ul;
-    mers = m; bases = b;
+    mers = m; bases = b; stride = stride_;
     const uint32_t id0 = uid(0);
     ok = id0 != INVALID_UNITIG && id0 < n_ul;
     if (!ok) return;
-    for (uint32_t i = 0; i < 2 * nsz - 1; ++i) { mers[i] = 0; bases[i] = 0; }
+    for (uint32_t i = 0; i < 2 * nsz - 1; ++i) { M(i) = 0; B(i) = 0; }
     cunitig = 0;
     cend = ul[id0];
     prev_pos = (int32_t)(0u - (uint32_t)k);
@@ -821,21 +911,21 @@ struct KmersInfo {
         if (cunitig >= nsz - 1) { ok = false; return; }
         const int32_t mx = sr_pos > prev_pos + k ? sr_pos : prev_pos + k;
         const int32_t nbb = cend - mx + 1;
-        bases[2 * cunitig] += nbb; bases[2 * cunitig + 1] += nbb;
+        B(2 * cunitig) += nbb; B(2 * cunitig + 1) += nbb;
       }
       const uint32_t id = uid(++cunitig);
       if (id == INVALID_UNITIG || id >= n_ul) { ok = false; return; }
       cend = (int32_t)((uint32_t)cend + (uint32_t)ul[id] - (uint32_t)uk + 1u);
     }
-    ++mers[2 * cunitig];
-    bases[2 * cunitig] += new_bases;
+    ++M(2 * cunitig);
+    B(2 * cunitig) += new_bases;
     int32_t cendi = cend;
     for (uint32_t i = cunitig; (i < nsz - 1) && ((uint32_t)sr_pos + (uint32_t)k > (uint32_t)cendi - (uint32_t)uk + 1u); ++i) {
       const int32_t full_mer = sr_pos + uk > cendi + 1;
-      mers[2 * i + 1] += full_mer; mers[2 * i + 2] += full_mer;
+      M(2 * i + 1) += full_mer; M(2 * i + 2) += full_mer;
       const int32_t tt = sr_pos + k - cendi + uk - 2;
       const int32_t nbb = new_bases < tt ? new_bases : tt;
-      bases[2 * i + 1] += nbb; bases[2 * i + 2] += nbb;
+      B(2 * i + 1) += nbb; B(2 * i + 2) += nbb;
       const uint32_t id = uid(i + 1);
       if (id != INVALID_UNITIG && id < n_ul) cendi = (int32_t)((uint32_t)cendi + (uint32_t)ul[id] - (uint32_t)uk + 1u);
       else { ok = false; return; }
@@ -905,13 +995,18 @@ DEV bool coords_finish(const AlignParamsDev& P, uint32_t rl, Rec& R) {
 // One lane per chain: coarse_aligner::align_sequence_max's loop body
 // (coarse_aligner.cc:42-60) for one emission -- pick the strand
 // (pb_aligner.cc:15, |fwd.lis| >= |bwd.lis|), compute_coords_info
-// (pb_aligner.cc:11-82) over its lis points (staged through LDS in chunks),
-// filters, kmers_info.  With --max-match, kept chains go to the redo list.
+// (pb_aligner.cc:11-82) over its lis points (staged through LDS in aligned
+// chunks), filters, kmers_info.  kmers_info of super-reads with at most
+// INFO_LDS_UNITIGS unitigs is accumulated in LDS during the first pass and
+// written once if the record is kept; longer names use a third pass that
+// updates the arrays in HBM.  With --max-match, kept chains go to the redo list.
+constexpr uint32_t INFO_LDS_UNITIGS = 8, INFO_LDS = 2 * INFO_LDS_UNITIGS - 1;
 template <int CH>
 __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, const ChainDesc* __restrict__ chains,
                                                const uint32_t* __restrict__ list, uint32_t n,
                                                const uint64_t* __restrict__ roff, uint32_t emit, ChainOut O) {
   __shared__ int2 ps[CH * RS];
+  __shared__ int32_t im[INFO_LDS * 64], ib[INFO_LDS * 64];
   const int lane = lane_id();
   const uint32_t w = blockIdx.x * 64 + lane;
   const bool act = w < n;
@@ -927,7 +1022,9 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
     nl = fwd_align ? lf : lb;
     base = d.hit_base + (fwd_align ? 0 : d.nf);
   }
-  const uint32_t nmax = wave_max_u32(nl);
+  ChunkGrid<CH> G;
+  G.init(base, nl);
+  const uint32_t nch = wave_max_u32(G.chunks());
   const uint32_t k = P.k;
   Rec R;
   R.nb_mers = (int32_t)nl; R.pb_cons = 0; R.sr_cons = 0; R.pb_cover = k; R.sr_cover = k;
@@ -935,16 +1032,26 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
   R.sr = d.sr; R.read = d.read; R.flags = (P.forward && !fwd_align) ? 2u : 0u;
   R.n_info = 0; R.reserved = 0; R.info_off = 0; R.emit = emit;
   R.stretch = 0; R.offset = 0; R.avg_err = 0;
-  // pass 1: cons / cover and the least-squares fit, in lis order (pb_aligner.cc:19-47)
+  // kmers_info setup (pb_aligner.cc:62-81): unitig list of the name used for the record
+  uint32_t u0 = 0, nsz = 0;
+  if (act && nl && P.unitigs_k) { u0 = ix.sr_uoff[d.sr]; nsz = ix.sr_uoff[d.sr + 1] - u0; }
+  const bool info_lds = nsz && nsz <= INFO_LDS_UNITIGS;
+  KmersInfo KI;
+  if (info_lds) KI.init(P, ix.sr_uids + u0, nsz, (R.flags & 2u) != 0, im + lane, ib + lane, 64);
+  auto info_pos = [&](int32_t so) -> int32_t {
+    const int32_t pos = fwd_align ? so : (int32_t)(R.ql + (uint32_t)so - k + 2u);
+    return pos < 0 ? -pos : pos;
+  };
+  // pass 1: cons / cover, the least-squares fit (pb_aligner.cc:19-47), kmers_info (LDS case)
   Lsq L;
   int2 prev = make_int2(0, 0), first = make_int2(0, 0);
-  for (uint32_t c0 = 0; c0 < nmax; c0 += CH) {
-    const uint32_t cnt = nl > c0 ? (nl - c0 < CH ? nl - c0 : CH) : 0;
-    rows_load<CH>(ps, O.pts, base + c0, cnt);
+  for (uint32_t j = 0; j < nch; ++j) {
+    const uint32_t lo = G.lo(j), hi = G.hi(j);
+    rows_load<CH>(ps, O.pts, G.row(j), lo, hi);
     wave_drain();
-    for (uint32_t e = 0; e < cnt; ++e) {
+    for (uint32_t e = lo; e < hi; ++e) {
       const int2 p = ps[e * RS + lane];
-      if (c0 + e == 0) {
+      if (L.n == 0) {
         first = p;
       } else {
         const uint32_t pb_diff = (uint32_t)(p.x - prev.x);
@@ -955,6 +1062,7 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
         R.sr_cover += k < sr_diff ? k : sr_diff;
       }
       L.add((double)p.y, (double)p.x);
+      if (info_lds) KI.add(info_pos(p.y));
       prev = p;
     }
     wave_drain();
@@ -967,14 +1075,15 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
     a = __ddiv_rn(L.CXY, L.VX); b = __ddiv_rn(L.NB, L.VX);
     R.stretch = a; R.offset = b;
   }
-  const uint32_t nl2 = L.n > 1 ? nl : 0;
-  const uint32_t nmax2 = wave_max_u32(nl2);
+  ChunkGrid<CH> G2;
+  G2.init(base, L.n > 1 ? nl : 0);
+  const uint32_t nch2 = wave_max_u32(G2.chunks());
   double err = 0;
-  for (uint32_t c0 = 0; c0 < nmax2; c0 += CH) {
-    const uint32_t cnt = nl2 > c0 ? (nl2 - c0 < CH ? nl2 - c0 : CH) : 0;
-    rows_load<CH>(ps, O.pts, base + c0, cnt);
+  for (uint32_t j = 0; j < nch2; ++j) {
+    const uint32_t lo = G2.lo(j), hi = G2.hi(j);
+    rows_load<CH>(ps, O.pts, G2.row(j), lo, hi);
     wave_drain();
-    for (uint32_t e = 0; e < cnt; ++e) {
+    for (uint32_t e = lo; e < hi; ++e) {
       const int2 p = ps[e * RS + lane];
       err = __dadd_rn(err, fabs(__dadd_rn(__dadd_rn(__dmul_rn(a, (double)p.y), b), -(double)p.x)));
     }
@@ -985,39 +1094,38 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
   R.re = (int32_t)((uint32_t)prev.x + k - 1u);
   R.qs = first.y; R.qe = prev.y;
   const uint32_t rl = act ? (uint32_t)(roff[d.read + 1] - roff[d.read]) : 0;
-  bool keep = act && nl > 0 && coords_finish(P, rl, R);
-  // pass 3: kmers_info along the lis (pb_aligner.cc:62-81)
-  KmersInfo KI;
-  uint32_t nl3 = 0;
-  bool info_ok = true;
-  if (keep && P.unitigs_k) {
-    const uint32_t u0 = ix.sr_uoff[d.sr], nsz = ix.sr_uoff[d.sr + 1] - u0;
-    const uint32_t need = nsz ? 2 * nsz - 1 : 0;
-    if (need) {
-      const unsigned long long io = atomicAdd(O.info_count, (unsigned long long)need);
-      if (io + need <= O.info_cap) {
-        KI.init(P, ix.sr_uids + u0, nsz, (R.flags & 2u) != 0, O.info_m + io, O.info_b + io);
-        R.info_off = io;
-        if (KI.ok) nl3 = nl; else R.n_info = 0;
-        R.n_info = KI.ok ? 2 * nsz - 1 : 0;
+  const bool keep = act && nl > 0 && coords_finish(P, rl, R);
+  // info arrays: allocate for kept records, copy the LDS case, or run pass 3 in HBM
+  bool info_ok = true, pass3 = false;
+  if (keep && nsz) {
+    const uint32_t need = 2 * nsz - 1;
+    const unsigned long long io = atomicAdd(O.info_count, (unsigned long long)need);
+    if (io + need <= O.info_cap) {
+      R.info_off = io;
+      if (info_lds) {
+        if (KI.ok) {
+          for (uint32_t q = 0; q < need; ++q) { O.info_m[io + q] = im[q * 64 + lane]; O.info_b[io + q] = ib[q * 64 + lane]; }
+          R.n_info = need;
+        }
       } else {
-        info_ok = false;
+        KI.init(P, ix.sr_uids + u0, nsz, (R.flags & 2u) != 0, O.info_m + io, O.info_b + io, 1);
+        pass3 = KI.ok;
       }
+    } else {
+      info_ok = false;
     }
   }
-  const uint32_t nmax3 = wave_max_u32(nl3);
-  for (uint32_t c0 = 0; c0 < nmax3; c0 += CH) {
-    const uint32_t cnt = nl3 > c0 ? (nl3 - c0 < CH ? nl3 - c0 : CH) : 0;
-    rows_load<CH>(ps, O.pts, base + c0, cnt);
+  ChunkGrid<CH> G3;
+  G3.init(base, pass3 ? nl : 0);
+  const uint32_t nch3 = wave_max_u32(G3.chunks());
+  for (uint32_t j = 0; j < nch3; ++j) {
+    const uint32_t lo = G3.lo(j), hi = G3.hi(j);
+    rows_load<CH>(ps, O.pts, G3.row(j), lo, hi);
     wave_drain();
-    for (uint32_t e = 0; e < cnt; ++e) {
-      const int32_t so = ps[e * RS + lane].y;
-      const int32_t pos = fwd_align ? so : (int32_t)(R.ql + (uint32_t)so - k + 2u);
-      KI.add(pos < 0 ? -pos : pos);
-    }
+    for (uint32_t e = lo; e < hi; ++e) KI.add(info_pos(ps[e * RS + lane].y));
     wave_drain();
   }
-  if (nl3 && !KI.ok) R.n_info = 0;
+  if (pass3 && KI.ok) R.n_info = 2 * nsz - 1;
   if (keep) {
     const uint32_t ri = atomicAdd(O.rec_count, 1u);
     if (ri < O.rec_cap && info_ok) O.recs[ri] = R;
@@ -1032,8 +1140,8 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
 // goes to the small- or big-node k_lis list for the next round.
 __global__ void k_discard(const ChainDesc* __restrict__ chains, const uint32_t* __restrict__ list, uint32_t n,
                           const uint32_t* __restrict__ lisl, uint32_t* __restrict__ slen, int2* __restrict__ X,
-                          const uint8_t* __restrict__ Nraw, uint32_t* items_small, uint32_t* n_small,
-                          uint32_t* items_big, uint32_t* n_big) {
+                          const LNode<uint16_t>* __restrict__ N16, const LNode<uint32_t>* __restrict__ N32,
+                          uint32_t* items_small, uint32_t* n_small, uint32_t* items_big, uint32_t* n_big) {
   for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < n; w += gridDim.x * blockDim.x) {
     const uint32_t c = list[w];
     const ChainDesc d = chains[c];
@@ -1043,10 +1151,7 @@ __global__ void k_discard(const ChainDesc* __restrict__ chains, const uint32_t* 
     const uint64_t base = d.hit_base + (dF ? 0 : d.nf);
     const uint32_t nD = slen[item], lD = dF ? lf : lb;
     int2* XD = X + base;
-    const uint8_t* ND = Nraw + base * NODE_BYTES;
-    auto lis_at = [&](uint32_t t) -> uint32_t {
-      return nD <= LIS_U16_MAX ? ((const LNode<uint16_t>*)ND)[t].nxt : ((const LNode<uint32_t>*)ND)[t].nxt;
-    };
+    auto lis_at = [&](uint32_t t) -> uint32_t { return nD <= LIS_U16_MAX ? N16[base + t].nxt : N32[base + t].nxt; };
     uint32_t wpos = 0, li = 0, next = lD ? lis_at(0) : 0xFFFFFFFFu;
     for (uint32_t rpos = 0; rpos < nD; ++rpos) {
       if (rpos == next) { ++li; next = li < lD ? lis_at(li) : 0xFFFFFFFFu; continue; }
@@ -1193,18 +1298,18 @@ void launch_chain_order(const uint32_t* lisl, uint32_t n, uint32_t* hist, uint32
   if (phase == 0) hipLaunchKernelGGL((k_len_hist<ChainLisLen>), dim3(grid_for(n, 256, 2048)), dim3(256), 0, st, f, n, hist);
   else hipLaunchKernelGGL((k_len_perm<ChainLisLen>), dim3((n + 255) / 256), dim3(256), 0, st, f, n, cursor, perm);
 }
-constexpr int LIS_CH16 = 16, LIS_CH32 = 8, FIT_CH = 16;
+constexpr int LIS_CH16 = 8, LIS_CH32 = 8, FIT_CH = 8;
 void launch_lis(bool big_nodes, const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen,
-                const int2* X, uint8_t* N, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx,
+                const int2* X, void* N, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx,
                 unsigned long long* stats, hipStream_t st) {
   if (!n_items) return;
   const dim3 grid((n_items + 63) / 64);
   if (big_nodes)
-    hipLaunchKernelGGL((k_lis<uint32_t, LIS_CH32>), grid, dim3(64), 0, st, chains, items, n_items, slen, X, N, pts, lisl,
-                       lp, keep_idx, stats);
+    hipLaunchKernelGGL((k_lis<uint32_t, LIS_CH32>), grid, dim3(64), 0, st, chains, items, n_items, slen, X,
+                       (LNode<uint32_t>*)N, pts, lisl, lp, keep_idx, stats);
   else
-    hipLaunchKernelGGL((k_lis<uint16_t, LIS_CH16>), grid, dim3(64), 0, st, chains, items, n_items, slen, X, N, pts, lisl,
-                       lp, keep_idx, stats);
+    hipLaunchKernelGGL((k_lis<uint16_t, LIS_CH16>), grid, dim3(64), 0, st, chains, items, n_items, slen, X,
+                       (LNode<uint16_t>*)N, pts, lisl, lp, keep_idx, stats);
 }
 void launch_coords(IndexView ix, AlignParamsDev P, const ChainDesc* chains, const uint32_t* list, uint32_t n,
                    const uint64_t* roff, uint32_t emit, ChainOut O, hipStream_t st) {
@@ -1212,11 +1317,11 @@ void launch_coords(IndexView ix, AlignParamsDev P, const ChainDesc* chains, cons
   hipLaunchKernelGGL((k_coords<FIT_CH>), dim3((n + 63) / 64), dim3(64), 0, st, ix, P, chains, list, n, roff, emit, O);
 }
 void launch_discard(const ChainDesc* chains, const uint32_t* list, uint32_t n, const uint32_t* lisl, uint32_t* slen,
-                    int2* X, const uint8_t* N, uint32_t* items_small, uint32_t* n_small, uint32_t* items_big,
-                    uint32_t* n_big, hipStream_t st) {
+                    int2* X, const void* N16, const void* N32, uint32_t* items_small, uint32_t* n_small,
+                    uint32_t* items_big, uint32_t* n_big, hipStream_t st) {
   if (!n) return;
-  hipLaunchKernelGGL(k_discard, dim3(grid_for(n, 256)), dim3(256), 0, st, chains, list, n, lisl, slen, X, N, items_small,
-                     n_small, items_big, n_big);
+  hipLaunchKernelGGL(k_discard, dim3(grid_for(n, 256)), dim3(256), 0, st, chains, list, n, lisl, slen, X,
+                     (const LNode<uint16_t>*)N16, (const LNode<uint32_t>*)N32, items_small, n_small, items_big, n_big);
 }
 uint32_t len_buckets() { return NLB; }
 uint32_t big_bucket() {  // first length class whose items all exceed LIS_U16_MAX

@@ -30,7 +30,7 @@ EXPORTS = [
     "pbgpu_align_params_default", "pbgpu_aligner_create", "pbgpu_aligner_free",
     "pbgpu_align_batch", "pbgpu_coords_free",
     "pbgpu_reads_upload", "pbgpu_reads_free", "pbgpu_align_resident", "pbgpu_download",
-    "pbgpu_aligner_get_stats", "pbgpu_aligner_reset_stats",
+    "pbgpu_aligner_get_stats", "pbgpu_aligner_reset_stats", "pbgpu_aligner_set_hit_budget",
     "pbgpu_format_coords", "pbgpu_free_text",
 ]
 
@@ -130,6 +130,7 @@ def lib():
         L.pbgpu_download.argtypes = [vp, C.POINTER(C.POINTER(CoordsBatch))]
         L.pbgpu_aligner_get_stats.argtypes = [vp, C.POINTER(Stats)]
         L.pbgpu_aligner_reset_stats.argtypes = [vp]
+        L.pbgpu_aligner_set_hit_budget.argtypes = [vp, C.c_uint64]
         L.pbgpu_format_coords.argtypes = [vp, C.POINTER(CoordsBatch), C.POINTER(C.c_char_p), C.POINTER(C.c_uint64),
                                           C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p),
                                           C.POINTER(C.c_uint64)]
@@ -236,6 +237,7 @@ class Coords:
         self.ptr = ptr
         c = ptr.contents
         n, nr = c.n_reads, c.n_records
+        self.n_reads, self.n_records = n, nr
         self.read_offsets = np.ctypeslib.as_array(c.read_offsets, shape=(n + 1,)).copy() if n + 1 else np.zeros(1, np.uint64)
         if nr:
             buf = (C.c_char * (nr * RECORD_DTYPE.itemsize)).from_address(c.records)
@@ -311,6 +313,9 @@ class Aligner:
 
     def reset_stats(self):
         _check(lib().pbgpu_aligner_reset_stats(self.h))
+
+    def set_hit_budget(self, hits):
+        _check(lib().pbgpu_aligner_set_hit_budget(self.h, C.c_uint64(int(hits))))
 
     def close(self):
         if self.h:

@@ -1,0 +1,131 @@
+"""GPU edge cases, each checked byte-for-byte against the CPU restatement
+(oracle/): degenerate reads, empty batches, determinism, the resident API,
+sub-batching with a tiny hit budget, reads that touch more super-reads than
+the LDS group tables hold (4096/8192-slot tiers and HBM tables), the
+max-count threshold on a repetitive genome, k = 31, and -0 output."""
+import pytest
+
+from tests._compare import assert_same_coords
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle(ds_names, ds_seqs, pnames, pseqs, k=17, ul=None, zero_match=False, **cfg):
+    from oracle.oracle import OracleIndex, params
+    oix = OracleIndex.from_records(ds_names, ds_seqs, k)
+    try:
+        return oix.align_format(params(k=k, unitig_lengths=ul, **cfg), pnames, pseqs, threads=8,
+                                zero_match=zero_match)
+    finally:
+        oix.close()
+
+
+def _gpu(ds_names, ds_seqs, pnames, pseqs, k=17, ul=None, zero_match=False, budget=None, **cfg):
+    from pacbio_amd import pbgpu
+    gix = pbgpu.Index.from_records(ds_names, ds_seqs, k)
+    al = pbgpu.Aligner(gix, k=k, unitig_lengths=ul, **cfg)
+    if budget:
+        al.set_hit_budget(budget)
+    co = al.align(pseqs)
+    txt = co.format(gix, pnames, [len(s) for s in pseqs], zero_match=zero_match)
+    st = al.stats()
+    return txt, st
+
+
+@pytest.fixture(scope="module")
+def small():
+    from tools.synth import Dataset
+    return Dataset("small", seed=11)
+
+
+@pytest.fixture(scope="module")
+def dense():
+    # 60 kb genome under ~330x of 1 kb super-reads; 40 kb reads touch >10k super-reads each
+    from tools.synth import Dataset
+    return Dataset("small", seed=5, genome_len=60_000, n_sr=20_000, n_pb=3, pb_len_mean=40_000, pb_len_sigma=0.0,
+                   err_ins=0.02, err_del=0.02, err_sub=0.01)
+
+
+def test_degenerate_reads(small):
+    real = small.pb_seqs()[:3]
+    r0 = real[0]
+    pseqs = [b"", b"ACG", b"N" * 5000, r0.lower(), r0[:3000] + b"N" * 40 + r0[3040:], r0.replace(b"A", b"R", 50),
+             b"ACGT" * 2000, b"A" * 3000, r0[:16], r0[:17], real[1], real[2]]
+    pnames = [f"edge{i}" for i in range(len(pseqs))]
+    names, seqs = small.sr_names(), small.sr_seqs()
+    for zm in (False, True):
+        exp = _oracle(names, seqs, pnames, pseqs, zero_match=zm)
+        got, _ = _gpu(names, seqs, pnames, pseqs, zero_match=zm)
+        assert_same_coords(got, exp, f"degenerate zero_match={zm}")
+
+
+def test_empty_batch(small):
+    from pacbio_amd import pbgpu
+    gix = pbgpu.Index.from_records(small.sr_names(), small.sr_seqs(), 17)
+    al = pbgpu.Aligner(gix, k=17)
+    co = al.align([])
+    assert co.n_reads == 0 and co.n_records == 0
+    co2 = al.align([b"", b"NNNN"])
+    assert co2.n_records == 0
+
+
+def test_determinism_and_resident_api(small):
+    from pacbio_amd import pbgpu
+    names, seqs = small.sr_names(), small.sr_seqs()
+    pnames, pseqs = small.pb_names(), small.pb_seqs()
+    gix = pbgpu.Index.from_records(names, seqs, 17)
+    al = pbgpu.Aligner(gix, k=17, forward=True, unitigs_k=31, unitig_lengths=small.unitig_lengths,
+                       bases_matching=15.0)
+    lens = [len(s) for s in pseqs]
+    a = al.align(pseqs).format(gix, pnames, lens)
+    b = al.align(pseqs).format(gix, pnames, lens)
+    assert a == b
+    rr = al.upload(pseqs)
+    for _ in range(2):
+        al.align_resident(rr)
+        c = al.download().format(gix, pnames, lens)
+        assert c == a
+    rr.close()
+
+
+@pytest.mark.parametrize("budget", [1, 5000, 200_000])
+def test_sub_batches(small, budget):
+    names, seqs = small.sr_names(), small.sr_seqs()
+    pnames, pseqs = small.pb_names(), small.pb_seqs()
+    cfg = dict(forward=True, unitigs_k=31, bases_matching=15.0, max_match=True)
+    exp = _oracle(names, seqs, pnames, pseqs, ul=small.unitig_lengths, **cfg)
+    got, _ = _gpu(names, seqs, pnames, pseqs, ul=small.unitig_lengths, budget=budget, **cfg)
+    assert_same_coords(got, exp, f"budget={budget}")
+
+
+# ~330x coverage: max_count 400 filters part of the k-mers and moves the 99% threshold
+@pytest.mark.parametrize("cfg", [dict(), dict(max_count=400), dict(forward=True, max_match=True)],
+                         ids=["default", "maxcount400", "fwd_maxmatch"])
+def test_dense_group_overflow(dense, cfg):
+    names, seqs = dense.sr_names(), dense.sr_seqs()
+    pnames, pseqs = dense.pb_names(), dense.pb_seqs()
+    exp = _oracle(names, seqs, pnames, pseqs, **cfg)
+    got, st = _gpu(names, seqs, pnames, pseqs, **cfg)
+    if not cfg:
+        assert st["n_chains"] > 3 * 8192, "reads must touch more super-reads than the largest LDS table"
+    assert_same_coords(got, exp, f"dense {cfg}")
+
+
+def test_repeats_threshold():
+    from tools.synth import Dataset
+    ds = Dataset("small", seed=3, repeat_frac=0.2, n_pb=30)
+    names, seqs = ds.sr_names(), ds.sr_seqs()
+    pnames, pseqs = ds.pb_names(), ds.pb_seqs()
+    for mc in (30, 5000):
+        exp = _oracle(names, seqs, pnames, pseqs, max_count=mc)
+        got, _ = _gpu(names, seqs, pnames, pseqs, max_count=mc)
+        assert_same_coords(got, exp, f"repeats max_count={mc}")
+
+
+def test_k31(small):
+    names, seqs = small.sr_names(), small.sr_seqs()
+    pnames, pseqs = small.pb_names(), small.pb_seqs()
+    exp = _oracle(names, seqs, pnames, pseqs, k=31)
+    got, _ = _gpu(names, seqs, pnames, pseqs, k=31)
+    assert exp.count("\n") > 5
+    assert_same_coords(got, exp, "k31")
