@@ -67,6 +67,20 @@ def build_pbgpu(force=False):
     return lib
 
 
+def build_pbgpu_prof():
+    """Phase-profiling variant (-DPBGPU_PROF) for tools/prof_lis.py; never the product library."""
+    objdir = os.path.join(ROOT, "build", "prof")
+    os.makedirs(objdir, exist_ok=True)
+    objs = []
+    for s in ["pbgpu_kernels.hip", "pbgpu_api.hip"]:
+        obj = os.path.join(objdir, s + ".o")
+        _run([HIPCC] + HIPFLAGS + ["-DPBGPU_PROF", "-c", os.path.join(CSRC, s), "-o", obj])
+        objs.append(obj)
+    lib = os.path.join(PKG, "libpbgpu_prof.so")
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + objs + ["-lpthread"])
+    return lib
+
+
 def build_oracle():
     odir = os.path.join(ROOT, "oracle")
     _run(["make", "-s", "-j8", "-C", odir, "all"])

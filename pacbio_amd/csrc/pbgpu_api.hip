@@ -50,6 +50,10 @@ void launch_coords(IndexView ix, AlignParamsDev P, const ChainDesc* chains, cons
 void launch_discard(const ChainDesc* chains, const uint32_t* list, uint32_t n, const uint32_t* lisl, uint32_t* slen,
                     int2* X, const void* N16, const void* N32, uint32_t* items_small, uint32_t* n_small,
                     uint32_t* items_big, uint32_t* n_big, hipStream_t st);
+void launch_lis_wave(bool large, const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen,
+                     const int2* X, void* N16, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx,
+                     unsigned long long* stats, hipStream_t st);
+uint32_t lis_class_bounds(int which);
 uint32_t len_buckets();
 uint32_t big_bucket();
 void launch_rec_hist(const Rec* recs, uint32_t n, uint32_t* per_read, hipStream_t st);
@@ -717,7 +721,7 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
       al->perm.ensure(2ull * nch + 1);
       al->lisl.ensure(2ull * nch + 1);
       al->slen.ensure(2ull * nch + 1);
-      uint32_t n_big = 0;
+      uint32_t n_big = 0, n_mid = 0, n_w2 = 0;  // items in classes above LIS_U16_MAX / LISW_LARGE / LISW_SMALL
       auto order = [&](int which, uint32_t n_in) -> uint32_t {  // returns the number of items placed
         HIPCHK(hipMemsetAsync(al->hist.p, 0, NB * 4, st));
         if (which == 0) launch_strand_order(al->slen.p, n_in, al->hist.p, nullptr, nullptr, 0, st);
@@ -729,6 +733,8 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
         for (int b = (int)NB - 1; b >= 1; --b) {  // longest first; bucket 0 = empty
           cur[b] = acc; acc += h[b];
           if ((uint32_t)b == big_bucket()) n_big = acc;  // items in buckets >= big_bucket(): > LIS_U16_MAX hits
+          if ((uint32_t)b == lis_class_bounds(1)) n_mid = acc;
+          if ((uint32_t)b == lis_class_bounds(0)) n_w2 = acc;
         }
         cur[0] = acc;
         HIPCHK(hipMemcpyAsync(al->hist.p + NB, cur.data(), NB * 4, hipMemcpyHostToDevice, st));
@@ -745,8 +751,14 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
       HIPCHK(hipEventRecord(al->ev[11], st));
       launch_lis(true, al->chains.p, al->perm.p, nbig, al->slen.p, al->X.p, al->nodes32.p, al->pts.p, al->lisl.p, al->lp,
                  al->P.max_match, al->stats.p, st);
-      launch_lis(false, al->chains.p, al->perm.p + nbig, n_strands - nbig, al->slen.p, al->X.p, al->nodes.p, al->pts.p,
+      // 4095 < n <= 65535: lane-per-strand chunked kernel; n <= 4095: wave-per-strand kernels
+      const uint32_t nmid = n_mid, nw2 = n_w2;
+      launch_lis(false, al->chains.p, al->perm.p + nbig, nmid - nbig, al->slen.p, al->X.p, al->nodes.p, al->pts.p,
                  al->lisl.p, al->lp, al->P.max_match, al->stats.p, st);
+      launch_lis_wave(true, al->chains.p, al->perm.p + nmid, nw2 - nmid, al->slen.p, al->X.p, al->nodes.p, al->pts.p,
+                      al->lisl.p, al->lp, al->P.max_match, al->stats.p, st);
+      launch_lis_wave(false, al->chains.p, al->perm.p + nw2, n_strands - nw2, al->slen.p, al->X.p, al->nodes.p,
+                      al->pts.p, al->lisl.p, al->lp, al->P.max_match, al->stats.p, st);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(al->ev[12], st));
       // chains in lis-length order -> k_coords; record/info capacity

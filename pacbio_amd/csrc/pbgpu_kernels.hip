@@ -14,11 +14,23 @@
 // use explicit __dadd_rn / __dmul_rn so that no FMA is ever formed.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <algorithm>
 #include "pbgpu_internal.h"
 
 namespace pbgpu {
 
 #define DEV __device__ __forceinline__
+
+// Optional phase profiling of k_lis (build with -DPBGPU_PROF; tools/prof_lis.py):
+// per-wave s_memtime deltas summed into g_prof.
+#ifdef PBGPU_PROF
+__device__ unsigned long long g_prof[16];
+#define PROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define PROF_ADD(slot, v) do { if (lane_id() == 0) atomicAdd(&g_prof[slot], (unsigned long long)(v)); } while (0)
+#else
+#define PROF_T(v)
+#define PROF_ADD(slot, v)
+#endif
 
 // ------------------------------------------------------------------ utils
 DEV uint64_t fmix64(uint64_t k) {
@@ -740,30 +752,62 @@ __global__ __launch_bounds__(64) void k_lis(const ChainDesc* __restrict__ chains
   uint64_t tests = 0;
   uint32_t head = NONE, hlen = 0, hnxt = NONE, hroot = 0, longest = 0, longest_ind = 0;
   int2 hx = make_int2(0, 0), hrootx = make_int2(0, 0);
+  PROF_T(t_start);
+#ifdef PBGPU_PROF
+  uint64_t p_load = 0, p_fetch = 0, p_elem = 0, p_store = 0;
+#endif
   RowPipe<CH, int2> px;
   if (nch) px.issue(X, G.row(0), G.lo(0), G.hi(0));
   for (uint32_t j = 0; j < nch; ++j) {
     const uint32_t lo = G.lo(j), hi = G.hi(j);
     const uint64_t row = G.row(j);
+    PROF_T(t0);
     px.commit(xs);
     if (j + 1 < nch) px.issue(X, G.row(j + 1), G.lo(j + 1), G.hi(j + 1));
+    PROF_T(t1);
     lds_fence();
     int2 xr[CH];
 #pragma unroll
     for (int e = 0; e < CH; ++e) xr[e] = xs[e * RS + lane];
+    lds_fence();
+    PROF_T(t2);
+#ifdef PBGPU_PROF
+    p_load += t1 - t0; p_fetch += t2 - t1;
+#endif
     // local index of slot 0 of this chunk (wraps for the first chunk; only c0 + e with e >= lo is used)
     const uint32_t c0 = (uint32_t)(row - base);
     const uint32_t first = hi > lo ? c0 + lo : 0u;  // smallest local index held in the tile
     auto in_tile = [&](uint32_t q) -> bool { return hi > lo && q >= first; };
-    auto getX = [&](uint32_t q) -> int2 { return in_tile(q) ? xs[(q - c0) * RS + lane] : Xl[q]; };
-    auto getN = [&](uint32_t q) -> LNode<I> { return in_tile(q) ? ns[(q - c0) * RS + lane] : Nl[q]; };
+    // Older elements live in HBM.  Those reads are rare (deep list scans) but
+    // each one must drain vmcnt; the drain stays inside the rare branch so that
+    // the common path never waits on the row prefetch or the row stores.
+    auto getX = [&](uint32_t q) -> int2 {
+      int2 v;
+      if (in_tile(q)) {
+        v = xs[(q - c0) * RS + lane];
+      } else {
+        v = Xl[q];
+        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+      }
+      return v;
+    };
+    auto getN = [&](uint32_t q) -> LNode<I> {
+      LNode<I> v;
+      if (in_tile(q)) {
+        v = ns[(q - c0) * RS + lane];
+      } else {
+        v = Nl[q];
+        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+      }
+      return v;
+    };
 #pragma unroll
     for (int e = 0; e < CH; ++e) {
       if ((uint32_t)e < lo || (uint32_t)e >= hi) continue;
       const uint32_t i = c0 + e;
       const int2 xi = xr[e];
       uint32_t prev = NONE, prev_len = 0, prev_nxt = NONE, found = NONE, f_len = 0, f_root = 0;
-      bool f_head = false;
+      int2 f_rootx = hrootx;
       if (head != NONE) {
         uint32_t it = head, lj = hlen, nx = hnxt, jroot = hroot;
         int2 xj = hx;
@@ -781,7 +825,11 @@ __global__ __launch_bounds__(64) void k_lis(const ChainDesc* __restrict__ chains
               const int2 xa = getX(anc);
               ok = affine_ok(lp.a, lp.b, lp.C, (double)(xi.x - xa.x), (double)(xi.y - xa.y));
             }
-            if (ok) { found = it; f_len = lj; f_root = jroot; f_head = at_head; break; }
+            if (ok) {
+              found = it; f_len = lj; f_root = jroot;
+              if (!at_head) f_rootx = getX(jroot);  // the head's root is cached in registers
+              break;
+            }
           }
           if (prev == NONE || lj < prev_len) { prev = it; prev_len = lj; prev_nxt = nx; }
           it = nx;
@@ -792,17 +840,14 @@ __global__ __launch_bounds__(64) void k_lis(const ChainDesc* __restrict__ chains
       }
       LNode<I> en;
       uint32_t elen, eroot;
-      int2 erootx = xi;
-      bool have_rootx = true;
+      int2 erootx;
       if (found != NONE) {
-        elen = f_len + 1; eroot = f_root; en.P = (I)found;
-        if (f_head) erootx = hrootx; else have_rootx = false;
+        elen = f_len + 1; eroot = f_root; en.P = (I)found; erootx = f_rootx;
       } else {
-        elen = 1; eroot = i; en.P = INONE;
+        elen = 1; eroot = i; en.P = INONE; erootx = xi;
       }
       en.len = (I)elen; en.root = (I)eroot;
       if (prev == NONE) {  // insert at the head
-        if (!have_rootx) { erootx = getX(eroot); have_rootx = true; }
         en.nxt = head == NONE ? INONE : (I)head;
         hnxt = head; head = i; hx = xi; hlen = elen; hroot = eroot; hrootx = erootx;
       } else {
@@ -813,16 +858,21 @@ __global__ __launch_bounds__(64) void k_lis(const ChainDesc* __restrict__ chains
       }
       ns[e * RS + lane] = en;
       if (longest < elen) {
-        if (!have_rootx) erootx = getX(eroot);
         if (lp.seq_all || linear_ok(lp.a, (double)(xi.x - erootx.x), (double)(xi.y - erootx.y))) {
           longest = elen; longest_ind = i;
         }
       }
     }
     lds_fence();
+    PROF_T(t3);
     rows_store<CH>(ns, N, row, lo, hi);
     lds_fence();  // tile rows read before the next chunk overwrites them
+    PROF_T(t4);
+#ifdef PBGPU_PROF
+    p_elem += t3 - t2; p_store += t4 - t3;
+#endif
   }
+  PROF_T(t_fwd);
   // reverse sweep along P: lis points in ascending order
   uint32_t s = longest_ind, t = 0;
   bool need = longest > 0;
@@ -868,7 +918,195 @@ __global__ __launch_bounds__(64) void k_lis(const ChainDesc* __restrict__ chains
     lds_fence();
   }
   (void)lo_n; (void)hi_n;
+  PROF_T(t_end);
+  PROF_ADD(0, p_load); PROF_ADD(1, p_fetch); PROF_ADD(2, p_elem); PROF_ADD(3, p_store);
+  PROF_ADD(4, t_end - t_fwd); PROF_ADD(5, t_end - t_start); PROF_ADD(6, nch); PROF_ADD(7, 1);
   if (act) lisl[item] = longest;
+  tests = wave_sum_u64(tests);
+  if (lane == 0 && tests) atomicAdd(&stats[ST_LIS_TESTS], (unsigned long long)tests);
+}
+
+// ------------------------------------------------------------------------
+// k_lis_w: one WAVE per strand, the whole strand (X and the list nodes) in
+// LDS.  Same algorithm (compute_L_P, lis_align.hpp:139-182), evaluated with
+// the wave's 64 lanes on 64 consecutive elements at a time:
+//  * "clean" step: element i's first test is against the current list head.
+//    If every element of a run passes that test, each is found at the head
+//    and inserted at the head (prev stays before_begin), so for the run
+//    head(i) = i-1, len(i) = len(head)+1+(i-start), root(i) = root(head),
+//    P(i) = i-1.  Lanes test their element against X[i-1] (lane 0 against
+//    the real head) and a ballot finds the first element that is not clean;
+//    the clean prefix is committed in parallel, including the longest update
+//    (len grows by one per element, so the last lane whose span passes
+//    `linear` with len > longest wins, exactly as the sequential loop).
+//  * any other element runs the literal list scan, wave-uniformly.
+// Backtracking (indices, :190-204) walks maximal runs with P(e) = e-1 at
+// once: run starts are kept per node.  Only the default window (W = 1,
+// accept_mer = affine_capped) takes the clean step; other windows and the
+// test-only accept_all variants use the literal scan for every element.
+// HBM traffic: X once (coalesced, prefetched for the next strand while the
+// current one is processed), the lis points (and, for --max-match, the lis
+// indices) once.
+template <int SMAX, int WPB>
+__global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict__ chains,
+                                                    const uint32_t* __restrict__ items, uint32_t n_items,
+                                                    const uint32_t* __restrict__ slen, const int2* __restrict__ X,
+                                                    LNode<uint16_t>* __restrict__ N16, int2* __restrict__ pts,
+                                                    uint32_t* __restrict__ lisl, LisParams lp, int keep_idx,
+                                                    unsigned long long* stats) {
+  constexpr uint32_t NONE = 0xFFFFu;
+  constexpr int PF = (SMAX + 63) / 64;  // prefetch registers per lane
+  __shared__ int2 s_x[WPB][SMAX];
+  __shared__ uint16_t s_nxt[WPB][SMAX], s_len[WPB][SMAX], s_P[WPB][SMAX], s_root[WPB][SMAX], s_rs[WPB][SMAX];
+  const int lane = lane_id();
+  const uint32_t wv = threadIdx.x >> 6;
+  int2* sx = s_x[wv];
+  uint16_t *snxt = s_nxt[wv], *sln = s_len[wv], *sP = s_P[wv], *sroot = s_root[wv], *srs = s_rs[wv];
+  const uint32_t nwaves = gridDim.x * WPB;
+  const bool fast = lp.W == 1 && !lp.mer_all;
+  uint64_t tests = 0;
+  auto strand = [&](uint32_t w, uint64_t& base, uint32_t& n, uint32_t& item) {
+    item = items[w];
+    const ChainDesc d = chains[item >> 1];
+    base = d.hit_base + ((item & 1) ? d.nf : 0);
+    n = slen[item];
+  };
+  // strands are prefetched into registers one strand ahead (small SMAX only)
+  constexpr bool PREFETCH = PF <= 8;
+  uint32_t w = blockIdx.x * WPB + wv;
+  int2 pf[PREFETCH ? PF : 1];
+  uint64_t nbase = 0;
+  uint32_t nn = 0, nitem = 0;
+  if (w < n_items) {
+    strand(w, nbase, nn, nitem);
+    if constexpr (PREFETCH) {
+#pragma unroll
+      for (int q = 0; q < PF; ++q) { const uint32_t j = q * 64 + lane; if (j < nn) pf[q] = X[nbase + j]; }
+    }
+  }
+  for (; w < n_items; w += nwaves) {
+    const uint64_t base = nbase;
+    const uint32_t n = nn, item = nitem;
+    if constexpr (PREFETCH) {
+#pragma unroll
+      for (int q = 0; q < PF; ++q) { const uint32_t j = q * 64 + lane; if (j < n) sx[j] = pf[q]; }
+    } else {
+      for (uint32_t j = lane; j < n; j += 64) sx[j] = X[base + j];
+    }
+    // issue the next strand's loads now; they land while this strand is processed
+    if (w + nwaves < n_items) {
+      strand(w + nwaves, nbase, nn, nitem);
+      if constexpr (PREFETCH) {
+#pragma unroll
+        for (int q = 0; q < PF; ++q) { const uint32_t j = q * 64 + lane; if (j < nn) pf[q] = X[nbase + j]; }
+      }
+    }
+    lds_fence();
+    // ---- forward pass (compute_L_P)
+    uint32_t head = NONE, longest = 0, longest_ind = 0;
+    uint32_t cur = 0;
+    while (cur < n) {
+      const uint32_t pend = cur + 64 < n ? cur + 64 : n;
+      uint32_t m = 0;
+      if (fast && head != NONE) {
+        const uint32_t i = cur + lane;
+        bool clean = false;
+        int2 xi = make_int2(0, 0);
+        if (i < pend) {
+          const uint32_t hj = lane == 0 ? head : i - 1;
+          xi = sx[i];
+          const int2 xj = sx[hj];
+          clean = xi.y > xj.y && affine_ok(lp.a, lp.b, lp.C, (double)(xi.x - xj.x), (double)(xi.y - xj.y));
+        }
+        const uint64_t bad = __ballot(i < pend && !clean);
+        m = bad ? (uint32_t)__ffsll((unsigned long long)bad) - 1 : pend - cur;
+        if (m) {
+          const uint32_t hl = sln[head], hr = sroot[head];
+          const uint32_t rsr = head + 1 == cur ? srs[head] : cur;  // run of P(e) = e-1 links
+          const int2 hrx = sx[hr];
+          bool cand = false;
+          if ((uint32_t)lane < m) {
+            const uint32_t elen = hl + 1 + lane;
+            const uint32_t P = lane == 0 ? head : i - 1;
+            snxt[i] = (uint16_t)P; sln[i] = (uint16_t)elen; sP[i] = (uint16_t)P; sroot[i] = (uint16_t)hr;
+            srs[i] = (uint16_t)(P + 1 == i ? rsr : i);
+            cand = elen > longest &&
+                   (lp.seq_all || linear_ok(lp.a, (double)(xi.x - hrx.x), (double)(xi.y - hrx.y)));
+          }
+          const uint64_t cb = __ballot(cand);
+          if (cb) {
+            const uint32_t top = 63u - (uint32_t)__clzll((long long)cb);
+            longest = hl + 1 + top; longest_ind = cur + top;
+          }
+          head = cur + m - 1;
+          tests += m;
+          cur += m;
+          lds_fence();
+        }
+      }
+      if (cur < pend) {
+        // ---- literal step for element cur (wave-uniform)
+        const uint32_t i = cur;
+        const int2 xi = sx[i];
+        uint32_t prev = NONE, prev_len = 0, prev_nxt = NONE, found = NONE;
+        for (uint32_t it = head; it != NONE;) {
+          ++tests;
+          const uint32_t lj = sln[it];
+          const int2 xj = sx[it];
+          if (xi.y > xj.y) {
+            bool ok;
+            if (lp.mer_all) ok = true;
+            else if (lp.W == 1) ok = affine_ok(lp.a, lp.b, lp.C, (double)(xi.x - xj.x), (double)(xi.y - xj.y));
+            else if (lp.W == 0 || lj < lp.W) ok = true;  // !will_be_filled()
+            else {
+              uint32_t anc = it;
+              for (uint32_t q = 1; q < lp.W; ++q) anc = sP[anc];
+              const int2 xa = sx[anc];
+              ok = affine_ok(lp.a, lp.b, lp.C, (double)(xi.x - xa.x), (double)(xi.y - xa.y));
+            }
+            if (ok) { found = it; break; }
+          }
+          const uint32_t nx = snxt[it];
+          if (prev == NONE || lj < prev_len) { prev = it; prev_len = lj; prev_nxt = nx; }
+          it = nx;
+        }
+        uint32_t elen, eroot, P;
+        if (found != NONE) { elen = sln[found] + 1u; eroot = sroot[found]; P = found; }
+        else { elen = 1; eroot = i; P = NONE; }
+        uint32_t enxt;
+        if (prev == NONE) { enxt = head; head = i; }
+        else { enxt = prev_nxt; if (lane == 0) snxt[prev] = (uint16_t)i; }
+        if (lane == 0) {
+          snxt[i] = (uint16_t)enxt; sln[i] = (uint16_t)elen; sP[i] = (uint16_t)P; sroot[i] = (uint16_t)eroot;
+          srs[i] = (uint16_t)(P + 1 == i ? srs[i - 1] : i);
+        }
+        if (elen > longest) {
+          const int2 xr = sx[eroot];
+          if (lp.seq_all || linear_ok(lp.a, (double)(xi.x - xr.x), (double)(xi.y - xr.y))) {
+            longest = elen; longest_ind = i;
+          }
+        }
+        ++cur;
+        lds_fence();
+      }
+    }
+    // ---- backtracking (indices): whole P(e) = e-1 runs at a time, lis points in ascending order
+    uint32_t t = longest, s = longest_ind;
+    int2* Pl = pts + base;
+    while (t > 0) {
+      const uint32_t r = srs[s];
+      const uint32_t run = s - r + 1, cnt = run < t ? run : t;
+      for (uint32_t j = lane; j < cnt; j += 64) {
+        Pl[t - 1 - j] = sx[s - j];
+        if (keep_idx) N16[base + t - 1 - j].nxt = (uint16_t)(s - j);
+      }
+      t -= cnt;
+      if (t) s = cnt == run ? sP[r] : s - cnt;
+    }
+    if (lane == 0) lisl[item] = longest;
+    lds_fence();  // LDS reads of this strand done before the next strand's commit
+  }
+  tests = lane == 0 ? tests : 0;
   tests = wave_sum_u64(tests);
   if (lane == 0 && tests) atomicAdd(&stats[ST_LIS_TESTS], (unsigned long long)tests);
 }
@@ -1311,6 +1549,39 @@ void launch_lis(bool big_nodes, const ChainDesc* chains, const uint32_t* items, 
     hipLaunchKernelGGL((k_lis<uint16_t, LIS_CH16>), grid, dim3(64), 0, st, chains, items, n_items, slen, X,
                        (LNode<uint16_t>*)N, pts, lisl, lp, keep_idx, stats);
 }
+constexpr uint32_t LISW_SMALL = 511, LISW_LARGE = 4095;
+static uint32_t resident_blocks(const void* fn, int block) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    hipDeviceProp_t pr;
+    cus = hipGetDeviceProperties(&pr, dev) == hipSuccess ? pr.multiProcessorCount : 256;
+  }
+  int per = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, block, 0) != hipSuccess || per < 1) per = 1;
+  return (uint32_t)(per * cus);
+}
+void launch_lis_wave(bool large, const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen,
+                     const int2* X, void* N16, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx,
+                     unsigned long long* stats, hipStream_t st) {
+  if (!n_items) return;
+  if (large) {
+    const void* fn = (const void*)k_lis_w<LISW_LARGE, 1>;
+    const uint32_t g = std::min<uint32_t>(resident_blocks(fn, 64), n_items);
+    hipLaunchKernelGGL((k_lis_w<LISW_LARGE, 1>), dim3(g), dim3(64), 0, st, chains, items, n_items, slen, X,
+                       (LNode<uint16_t>*)N16, pts, lisl, lp, keep_idx, stats);
+  } else {
+    const void* fn = (const void*)k_lis_w<LISW_SMALL, 4>;
+    const uint32_t g = std::min<uint32_t>(resident_blocks(fn, 256), (n_items + 3) / 4);
+    hipLaunchKernelGGL((k_lis_w<LISW_SMALL, 4>), dim3(g), dim3(256), 0, st, chains, items, n_items, slen, X,
+                       (LNode<uint16_t>*)N16, pts, lisl, lp, keep_idx, stats);
+  }
+}
+// length classes (len_bucket) at the kernel boundaries
+uint32_t lis_class_bounds(int which) {  // first class of: 0 = > LISW_SMALL, 1 = > LISW_LARGE, 2 = > LIS_U16_MAX
+  return which == 0 ? 128u + 16u * (9u - 7u) : which == 1 ? 128u + 16u * (12u - 7u) : 128u + 16u * (16u - 7u);
+}
 void launch_coords(IndexView ix, AlignParamsDev P, const ChainDesc* chains, const uint32_t* list, uint32_t n,
                    const uint64_t* roff, uint32_t emit, ChainOut O, hipStream_t st) {
   if (!n) return;
@@ -1324,6 +1595,17 @@ void launch_discard(const ChainDesc* chains, const uint32_t* list, uint32_t n, c
                      (const LNode<uint16_t>*)N16, (const LNode<uint32_t>*)N32, items_small, n_small, items_big, n_big);
 }
 uint32_t len_buckets() { return NLB; }
+#ifdef PBGPU_PROF
+extern "C" int pbgpu_debug_prof(unsigned long long* out, int n, int reset) {
+  if (n > 16) n = 16;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), n * sizeof(unsigned long long)) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 uint32_t big_bucket() {  // first length class whose items all exceed LIS_U16_MAX
   static_assert(LIS_U16_MAX == 65535u, "len_bucket(65536) starts a class");
   return 128u + 16u * (16u - 7u);

@@ -17,7 +17,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpbgpu.so")
+LIB_PATH = os.environ.get("PBGPU_LIB") or os.path.join(_HERE, "libpbgpu.so")  # PBGPU_LIB: profiling builds only
 
 PBGPU_OK = 0
 STATUS = {0: "OK", 1: "INVALID", 2: "IO", 3: "NOMEM", 4: "DEVICE", 5: "UNSUPPORTED", 6: "INTERNAL"}

@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Phase profile of k_lis (s_memtime per wave, summed): run with the
+-DPBGPU_PROF library, e.g.
+  PBGPU_LIB=pacbio_amd/libpbgpu_prof.so python tools/prof_lis.py --reads 10000"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reads", type=int, default=10000)
+    ap.add_argument("--workload", default="C2")
+    a = ap.parse_args()
+    from pacbio_amd import pbgpu
+    from tools.synth import Dataset
+    ds = Dataset(a.workload, seed=42, threads=16, n_pb=a.reads)
+    ix = pbgpu.Index.from_records(ds.sr_names(), ds.sr_seqs(), 17)
+    al = pbgpu.Aligner(ix, k=17, forward=True, unitigs_k=31, unitig_lengths=ds.unitig_lengths,
+                       bases_matching=15.0, max_count=5000, stretch_cap=10000.0)
+    blob, off = ds.pb_blob()
+    rr = al.upload(blob=blob, offsets=off)
+    al.align_resident(rr)
+    L = pbgpu.lib()
+    f = L.pbgpu_debug_prof
+    f.argtypes = [C.POINTER(C.c_ulonglong), C.c_int, C.c_int]
+    buf = (C.c_ulonglong * 16)()
+    f(buf, 16, 1)
+    al.reset_stats()
+    al.align_resident(rr)
+    pbgpu.device_synchronize(0)
+    f(buf, 16, 1)
+    st = al.stats()
+    names = ["row_load_issue", "lds_fetch", "element_loop", "row_store", "sweep", "wave_total", "chunks", "waves"]
+    v = list(buf)[:8]
+    waves = max(1, v[7])
+    print(f"k_lis: {st['kernel_ms']['k_lis']:.2f} ms, waves={waves}, chunks/wave={v[6] / waves:.1f}, "
+          f"hits={st['n_hits']}, tests={st['n_lis_tests']}")
+    for n, x in zip(names[:6], v[:6]):
+        print(f"  {n:16s} {x / waves:12.0f} ticks/wave  ({100.0 * x / max(1, v[5]):5.1f}%)")
+
+
+if __name__ == "__main__":
+    main()
