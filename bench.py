@@ -98,6 +98,7 @@ def main():
     ap.add_argument("--cpu-sample-reads", type=int, default=0, help="CPU baseline sample (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
     args = ap.parse_args()
 
     rank, world, local = _dist()
@@ -160,13 +161,27 @@ def main():
         oix = OracleIndex.from_records(names, seqs, k, threads=cthreads)
         p = params(k=k, forward=True, unitigs_k=31, unitig_lengths=ds.unitig_lengths, bases_matching=15.0,
                    max_count=5000, stretch_cap=10000.0)
-        nsamp = args.cpu_sample_reads or max(1, min(len(off) - 1, 8 * cthreads))
-        pseqs = ds.pb_seqs()[:nsamp]
+        allp = ds.pb_seqs()
+        if args.cpu_sample_reads:
+            nsamp = min(len(allp), args.cpu_sample_reads)
+        else:
+            # bounded sample: a pilot sizes it to about --cpu-seconds of oracle work
+            pilot = allp[:max(1, min(len(allp), 4 * cthreads))]
+            psec, _ = oix.align_timed(p, pilot, threads=cthreads)
+            rate = sum(len(x) for x in pilot) / max(psec, 1e-6)
+            want = rate * args.cpu_seconds
+            nsamp, acc = 0, 0
+            while nsamp < len(allp) and acc < want:
+                acc += len(allp[nsamp])
+                nsamp += 1
+            nsamp = max(nsamp, len(pilot))
+        pseqs = allp[:nsamp]
         sec, nrec = oix.align_timed(p, pseqs, threads=cthreads)
-        sbases = sum(len(s) for s in pseqs)
+        sbases = sum(len(x) for x in pseqs)
         cpu = {"value": sbases / sec, "unit": "bases/s", "cores": cthreads, "kind": "port",
-               "sample": f"first {nsamp} reads of the rank-0 shard ({sbases} bases) against the full "
-                         f"{args.workload} index, oracle/ C restatement, {cthreads} threads, {sec:.2f} s"}
+               "sample": f"first {nsamp} reads of the rank-0 shard ({sbases} bases, {nrec} records) against the full "
+                         f"{args.workload} index; oracle/ C restatement (bit-identical output), {cthreads} threads, "
+                         f"{sec:.2f} s"}
         oix.close()
 
     if rank == 0:

@@ -484,6 +484,7 @@ struct pbgpu_aligner {
   pbgpu_stats acc{};
   hipEvent_t ev[16]{};
   uint64_t hit_budget = 1200000000ull, rec_hint = 0, info_per_chain = 32;
+  double chains_per_hit = 1.0 / 16;  // routing estimate for k_group tiers, refined after every batch
   dbuf<uint32_t> ovf_list, read_list;
 };
 
@@ -649,40 +650,56 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
     O.chain_cap = (uint32_t)std::min<uint64_t>(al->chains.n, 0xFFFFFFFFu);
     O.n_overflow = al->counters.p + 3;
     O.overflow_reads = al->ovf_reads.p;
-    // reads longest first (hits), so the long-read tail starts early
+    // reads longest first (hits), so the long-read tail starts early; reads whose
+    // predicted super-read count (hits x chains-per-hit of earlier batches) would
+    // overflow the 2048-slot table go straight to the 8192-slot tier
+    std::vector<uint32_t> rl_small, rl_big;
     {
       std::vector<uint32_t> rl(nr);
       for (uint32_t i = 0; i < nr; ++i) rl[i] = r0 + i;
       std::stable_sort(rl.begin(), rl.end(), [&](uint32_t a, uint32_t b) {
         return hoff[a + 1] - hoff[a] > hoff[b + 1] - hoff[b];
       });
+      const double limit = (double)((1u << hcap_log2) - (1u << hcap_log2) / 4);  // the small table's fill limit
+      for (uint32_t r : rl) ((double)(hoff[r + 1] - hoff[r]) * al->chains_per_hit > limit ? rl_big : rl_small).push_back(r);
       al->read_list.ensure(nr);
-      HIPCHK(hipMemcpyAsync(al->read_list.p, rl.data(), (size_t)nr * 4, hipMemcpyHostToDevice, st));
+      if (!rl_small.empty())
+        HIPCHK(hipMemcpyAsync(al->read_list.p, rl_small.data(), rl_small.size() * 4, hipMemcpyHostToDevice, st));
+      if (!rl_big.empty())
+        HIPCHK(hipMemcpyAsync(al->read_list.p + rl_small.size(), rl_big.data(), rl_big.size() * 4,
+                              hipMemcpyHostToDevice, st));
     }
+    const uint32_t n_small = (uint32_t)rl_small.size(), n_bigr = (uint32_t)rl_big.size();
     for (int attempt = 0;; ++attempt) {
       HIPCHK(hipEventRecord(al->ev[5], st));
       HIPCHK(hipMemsetAsync(al->counters.p, 0, 16 * 4, st));
       static_assert(ST_LIS_TESTS == ST_CHAINS + 1, "per-attempt stat slots are adjacent");
       HIPCHK(hipMemsetAsync(al->stats.p + ST_CHAINS, 0, 16, st));  // redone on a retry: counted per attempt
       HIPCHK(hipEventRecord(al->ev[8], st));
-      launch_group(v, al->krec.p, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0, al->read_list.p, nr,
+      launch_group(v, al->krec.p, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0, al->read_list.p, n_small,
                    hcap_log2, nullptr, O, al->stats.p, st);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(al->ev[9], st));
+      launch_group(v, al->krec.p, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0,
+                   al->read_list.p + n_small, n_bigr, kGroupLdsMaxLog2, nullptr, O, al->stats.p, st);
+      HIPCHK(hipGetLastError());
       uint32_t cnt[4];
       HIPCHK(hipMemcpyAsync(cnt, al->counters.p, 16, hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
-      // reads touching more super-reads than the table holds: a 4x LDS table, then
-      // global tables growing until they fit
-      uint32_t lg = hcap_log2;
+      // reads touching more super-reads than their table holds: the 8192-slot LDS
+      // table, then HBM tables growing until they fit
       uint32_t n_ovf = cnt[3];
+      uint32_t lg = hcap_log2;
       while (n_ovf) {
         std::vector<uint32_t> ovf(n_ovf);
         HIPCHK(hipMemcpy(ovf.data(), al->ovf_reads.p, n_ovf * 4, hipMemcpyDeviceToHost));
         uint64_t mx = 0;
         for (uint32_t r : ovf) mx = std::max(mx, hoff[r + 1] - hoff[r]);
-        if ((1ull << lg) > 2 * mx + 256) throw std::runtime_error("group table growth did not converge");
-        lg += lg < kGroupLdsMaxLog2 ? 1 : 2;  // 2048 -> 4096 -> 8192 slots in LDS, then HBM tables
+        // next tier: the 8192-slot LDS table, then HBM tables x4 each round (a read
+        // from the 8192 tier may retry it once; results do not depend on the tier)
+        lg = lg < kGroupLdsMaxLog2 ? kGroupLdsMaxLog2 : lg + 2;
+        if (lg > kGroupLdsMaxLog2 && (1ull << (lg - 2)) > 2 * mx + 256)
+          throw std::runtime_error("group table growth did not converge");
         al->ovf_list.ensure(n_ovf);
         HIPCHK(hipMemcpyAsync(al->ovf_list.p, ovf.data(), n_ovf * 4, hipMemcpyHostToDevice, st));
         HIPCHK(hipMemsetAsync(al->counters.p + 3, 0, 4, st));
@@ -838,6 +855,7 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
       if (ovf == 0 && nrec <= al->recs.n) {
         rec_done = nrec; info_done = ninfo;
         n_chains += sub[0]; n_tests += sub[1];
+        if (Hs) al->chains_per_hit = std::max(1e-4, 1.1 * (double)nch / (double)Hs);
         break;
       }
       if (attempt > 8) throw std::runtime_error("record buffer growth did not converge");

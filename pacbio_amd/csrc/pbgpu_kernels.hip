@@ -380,18 +380,19 @@ __global__ __launch_bounds__(BLOCK) void k_seed(IndexView ix, const uint8_t* __r
 // holds), and scatter every hit to its (read, SR, strand) list with an
 // order-preserving multisplit.  Each list comes out in exactly the
 // reference's frags_pos order (coarse_aligner.cc:128-140) -- no sort needed.
-constexpr uint32_t GROUP_BLOCK = 256;  // 4 waves share one read's table
+// 4 waves share one read's table; reads touching many super-reads use a
+// 16-wave block over the largest LDS table.
+constexpr uint32_t GROUP_BLOCK = 256, GROUP_BLOCK_BIG = 1024;
 
-template <bool GLOBAL_TABLE>
-__global__ __launch_bounds__(GROUP_BLOCK) void k_group(IndexView ix, const KRec* __restrict__ krec,
+template <bool GLOBAL_TABLE, uint32_t B>
+__global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restrict__ krec,
                                                        const uint64_t* __restrict__ roff, const uint32_t* __restrict__ n_kept,
                                                        const uint32_t* __restrict__ thr_in, const uint64_t* __restrict__ hit_off,
                                                        uint64_t node_base, uint32_t r0, const uint32_t* __restrict__ read_list,
                                                        uint32_t n_list, uint32_t hcap_log2, uint32_t* gtable, GroupOut O,
                                                        unsigned long long* stats) {
-  constexpr uint32_t B = GROUP_BLOCK;
   extern __shared__ uint32_t s_dyn[];
-  __shared__ uint32_t s_nf[B], s_nb[B], s_off[B + 1], s_scan[8];
+  __shared__ uint32_t s_nf[B], s_nb[B], s_off[B + 1], s_scan[B / 64];
   __shared__ int32_t s_pb[B];
   __shared__ uint64_t s_pf[B], s_pbk[B];
   __shared__ uint32_t s_flag, s_used, s_cbase;
@@ -659,15 +660,16 @@ DEV void rows_store(const T* tile, T* __restrict__ dst, uint64_t row, uint32_t l
 // overlaps the serial work on chunk j.
 template <int CH, typename T>
 struct RowPipe {
-  static constexpr int G = 64 / CH;
-  T v[G];
+  static constexpr int NG = CH;        // load instructions per chunk
+  static constexpr int SPG = 64 / CH;  // rows (items) per instruction
+  T v[NG];
   uint32_t mask;
   DEV void issue(const T* __restrict__ src, uint64_t row, uint32_t lo, uint32_t hi) {
     const int lane = lane_id();
     mask = 0;
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const int l = g * CH + lane / CH, e = lane % CH;
+    for (int g = 0; g < NG; ++g) {
+      const int l = g * SPG + lane / CH, e = lane % CH;
       const uint64_t rl = shfl_u64(row, l);
       const uint32_t lol = __shfl(lo, l, 64), hil = __shfl(hi, l, 64);
       if ((uint32_t)e >= lol && (uint32_t)e < hil) { v[g] = src[rl + e]; mask |= 1u << g; }
@@ -676,8 +678,8 @@ struct RowPipe {
   DEV void commit(T* tile) const {
     const int lane = lane_id();
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const int l = g * CH + lane / CH, e = lane % CH;
+    for (int g = 0; g < NG; ++g) {
+      const int l = g * SPG + lane / CH, e = lane % CH;
       if (mask & (1u << g)) tile[e * RS + l] = v[g];
     }
   }
@@ -686,6 +688,13 @@ DEV void lds_fence() {
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS traffic done
   __builtin_amdgcn_wave_barrier();
 }
+
+template <int CH>
+struct ChunkGrid;
+// Streams every lane's item through the LDS tile chunk by chunk, the next
+// chunk's rows in flight while f() consumes the current one.
+template <int CH, typename F>
+DEV void stream_rows(const int2* __restrict__ src, const ChunkGrid<CH>& G, uint32_t nch, int2* tile, F&& f);
 
 // A lane's item occupies [b, b + n) of a per-hit array; chunks follow the
 // absolute CH-aligned grid so that every row is one aligned segment.
@@ -704,6 +713,21 @@ struct ChunkGrid {
     return e - r < CH ? (uint32_t)(e - r) : (uint32_t)CH;
   }
 };
+
+template <int CH, typename F>
+DEV void stream_rows(const int2* __restrict__ src, const ChunkGrid<CH>& G, uint32_t nch, int2* tile, F&& f) {
+  const int lane = lane_id();
+  RowPipe<CH, int2> pp;
+  if (nch) pp.issue(src, G.row(0), G.lo(0), G.hi(0));
+  for (uint32_t j = 0; j < nch; ++j) {
+    const uint32_t lo = G.lo(j), hi = G.hi(j);
+    pp.commit(tile);
+    if (j + 1 < nch) pp.issue(src, G.row(j + 1), G.lo(j + 1), G.hi(j + 1));
+    lds_fence();
+    for (uint32_t e = lo; e < hi; ++e) f(tile[e * RS + lane]);
+    lds_fence();
+  }
+}
 
 DEV bool affine_ok(double a, double b, double C, double df, double ds) {
   // (s.first <= b + a*s.second) && (s.second <= b + a*s.first) && s.first <= C && s.second <= C
@@ -1124,21 +1148,35 @@ struct KmersInfo {
   int32_t* mers;    // element i at mers[i * stride]
   int32_t* bases;
   uint32_t stride;
+  const int32_t* cl;  // optional cache: length of unitig i at cl[i * stride], UL_INVALID if unusable
   uint32_t cunitig;
   int32_t cend, prev_pos;
+  static constexpr int32_t UL_INVALID = INT32_MIN;
   DEV uint32_t uid(uint32_t i) const { return i >= nsz ? INVALID_UNITIG : (rev ? ids[nsz - 1 - i] : ids[i]); }
+  DEV int32_t ulen_direct(uint32_t i) const {
+    const uint32_t id = uid(i);
+    return (id == INVALID_UNITIG || id >= n_ul) ? UL_INVALID : ul[id];
+  }
+  DEV int32_t ulen(uint32_t i) const {
+    if (cl) return i < nsz ? cl[i * stride] : UL_INVALID;
+    return ulen_direct(i);
+  }
   DEV int32_t& M(uint32_t i) { return mers[i * stride]; }
   DEV int32_t& B(uint32_t i) { return bases[i * stride]; }
   DEV void init(const AlignParamsDev& P, const uint32_t* ids_, uint32_t nsz_, bool rev_, int32_t* m, int32_t* b,
-                uint32_t stride_) {
+                uint32_t stride_, int32_t* cache = nullptr) {
     ids = ids_; nsz = nsz_; rev = rev_; k = (int32_t)P.k; uk = (int32_t)P.unitigs_k; ul = P.ul; n_ul = P.n_ul;
-    mers = m; bases = b; stride = stride_;
-    const uint32_t id0 = uid(0);
-    ok = id0 != INVALID_UNITIG && id0 < n_ul;
+    mers = m; bases = b; stride = stride_; cl = nullptr;
+    if (cache) {
+      for (uint32_t i = 0; i < nsz; ++i) cache[i * stride] = ulen_direct(i);
+      cl = cache;
+    }
+    const int32_t l0 = ulen(0);
+    ok = l0 != UL_INVALID;
     if (!ok) return;
     for (uint32_t i = 0; i < 2 * nsz - 1; ++i) { M(i) = 0; B(i) = 0; }
     cunitig = 0;
-    cend = ul[id0];
+    cend = l0;
     prev_pos = (int32_t)(0u - (uint32_t)k);
   }
   DEV void add(int32_t sr_pos) {
@@ -1151,9 +1189,9 @@ struct KmersInfo {
         const int32_t nbb = cend - mx + 1;
         B(2 * cunitig) += nbb; B(2 * cunitig + 1) += nbb;
       }
-      const uint32_t id = uid(++cunitig);
-      if (id == INVALID_UNITIG || id >= n_ul) { ok = false; return; }
-      cend = (int32_t)((uint32_t)cend + (uint32_t)ul[id] - (uint32_t)uk + 1u);
+      const int32_t l = ulen(++cunitig);
+      if (l == UL_INVALID) { ok = false; return; }
+      cend = (int32_t)((uint32_t)cend + (uint32_t)l - (uint32_t)uk + 1u);
     }
     ++M(2 * cunitig);
     B(2 * cunitig) += new_bases;
@@ -1164,8 +1202,8 @@ struct KmersInfo {
       const int32_t tt = sr_pos + k - cendi + uk - 2;
       const int32_t nbb = new_bases < tt ? new_bases : tt;
       B(2 * i + 1) += nbb; B(2 * i + 2) += nbb;
-      const uint32_t id = uid(i + 1);
-      if (id != INVALID_UNITIG && id < n_ul) cendi = (int32_t)((uint32_t)cendi + (uint32_t)ul[id] - (uint32_t)uk + 1u);
+      const int32_t l = ulen(i + 1);
+      if (l != UL_INVALID) cendi = (int32_t)((uint32_t)cendi + (uint32_t)l - (uint32_t)uk + 1u);
       else { ok = false; return; }
     }
     prev_pos = sr_pos;
@@ -1244,7 +1282,7 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
                                                const uint32_t* __restrict__ list, uint32_t n,
                                                const uint64_t* __restrict__ roff, uint32_t emit, ChainOut O) {
   __shared__ int2 ps[CH * RS];
-  __shared__ int32_t im[INFO_LDS * 64], ib[INFO_LDS * 64];
+  __shared__ int32_t im[INFO_LDS * 64], ib[INFO_LDS * 64], iul[INFO_LDS_UNITIGS * 64];
   const int lane = lane_id();
   const uint32_t w = blockIdx.x * 64 + lane;
   const bool act = w < n;
@@ -1275,7 +1313,7 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
   if (act && nl && P.unitigs_k) { u0 = ix.sr_uoff[d.sr]; nsz = ix.sr_uoff[d.sr + 1] - u0; }
   const bool info_lds = nsz && nsz <= INFO_LDS_UNITIGS;
   KmersInfo KI;
-  if (info_lds) KI.init(P, ix.sr_uids + u0, nsz, (R.flags & 2u) != 0, im + lane, ib + lane, 64);
+  if (info_lds) KI.init(P, ix.sr_uids + u0, nsz, (R.flags & 2u) != 0, im + lane, ib + lane, 64, iul + lane);
   auto info_pos = [&](int32_t so) -> int32_t {
     const int32_t pos = fwd_align ? so : (int32_t)(R.ql + (uint32_t)so - k + 2u);
     return pos < 0 ? -pos : pos;
@@ -1283,28 +1321,21 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
   // pass 1: cons / cover, the least-squares fit (pb_aligner.cc:19-47), kmers_info (LDS case)
   Lsq L;
   int2 prev = make_int2(0, 0), first = make_int2(0, 0);
-  for (uint32_t j = 0; j < nch; ++j) {
-    const uint32_t lo = G.lo(j), hi = G.hi(j);
-    rows_load<CH>(ps, O.pts, G.row(j), lo, hi);
-    wave_drain();
-    for (uint32_t e = lo; e < hi; ++e) {
-      const int2 p = ps[e * RS + lane];
-      if (L.n == 0) {
-        first = p;
-      } else {
-        const uint32_t pb_diff = (uint32_t)(p.x - prev.x);
-        R.pb_cons += pb_diff == 1u;
-        R.pb_cover += k < pb_diff ? k : pb_diff;
-        const uint32_t sr_diff = (uint32_t)(p.y - prev.y);
-        R.sr_cons += sr_diff == 1u;
-        R.sr_cover += k < sr_diff ? k : sr_diff;
-      }
-      L.add((double)p.y, (double)p.x);
-      if (info_lds) KI.add(info_pos(p.y));
-      prev = p;
+  stream_rows<CH>(O.pts, G, nch, ps, [&](const int2 p) {
+    if (L.n == 0) {
+      first = p;
+    } else {
+      const uint32_t pb_diff = (uint32_t)(p.x - prev.x);
+      R.pb_cons += pb_diff == 1u;
+      R.pb_cover += k < pb_diff ? k : pb_diff;
+      const uint32_t sr_diff = (uint32_t)(p.y - prev.y);
+      R.sr_cons += sr_diff == 1u;
+      R.sr_cover += k < sr_diff ? k : sr_diff;
     }
-    wave_drain();
-  }
+    L.add((double)p.y, (double)p.x);
+    if (info_lds) KI.add(info_pos(p.y));
+    prev = p;
+  });
   // pass 2: average error of the fit (least_square_2d.hpp:70-80 + pb_aligner.cc:49-60)
   double a = 0, b = 0;
   if (L.n == 1) {
@@ -1317,16 +1348,9 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
   G2.init(base, L.n > 1 ? nl : 0);
   const uint32_t nch2 = wave_max_u32(G2.chunks());
   double err = 0;
-  for (uint32_t j = 0; j < nch2; ++j) {
-    const uint32_t lo = G2.lo(j), hi = G2.hi(j);
-    rows_load<CH>(ps, O.pts, G2.row(j), lo, hi);
-    wave_drain();
-    for (uint32_t e = lo; e < hi; ++e) {
-      const int2 p = ps[e * RS + lane];
-      err = __dadd_rn(err, fabs(__dadd_rn(__dadd_rn(__dmul_rn(a, (double)p.y), b), -(double)p.x)));
-    }
-    wave_drain();
-  }
+  stream_rows<CH>(O.pts, G2, nch2, ps, [&](const int2 p) {
+    err = __dadd_rn(err, fabs(__dadd_rn(__dadd_rn(__dmul_rn(a, (double)p.y), b), -(double)p.x)));
+  });
   if (L.n > 1) R.avg_err = __ddiv_rn(err, (double)L.n);
   R.rs = first.x;
   R.re = (int32_t)((uint32_t)prev.x + k - 1u);
@@ -1356,13 +1380,7 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
   ChunkGrid<CH> G3;
   G3.init(base, pass3 ? nl : 0);
   const uint32_t nch3 = wave_max_u32(G3.chunks());
-  for (uint32_t j = 0; j < nch3; ++j) {
-    const uint32_t lo = G3.lo(j), hi = G3.hi(j);
-    rows_load<CH>(ps, O.pts, G3.row(j), lo, hi);
-    wave_drain();
-    for (uint32_t e = lo; e < hi; ++e) KI.add(info_pos(ps[e * RS + lane].y));
-    wave_drain();
-  }
+  stream_rows<CH>(O.pts, G3, nch3, ps, [&](const int2 p) { KI.add(info_pos(p.y)); });
   if (pass3 && KI.ok) R.n_info = 2 * nsz - 1;
   if (keep) {
     const uint32_t ri = atomicAdd(O.rec_count, 1u);
@@ -1498,18 +1516,25 @@ void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const ui
                   const uint64_t* hit_off, uint64_t node_base, uint32_t r0, const uint32_t* read_list, uint32_t n_list,
                   uint32_t hcap_log2, uint32_t* gtable, GroupOut O, unsigned long long* stats, hipStream_t st) {
   if (!n_list) return;
-  if (!gtable) {  // LDS table: hcap_log2 <= 13
+  if (!gtable) {  // LDS table: hcap_log2 <= 13; the 8192-slot table gets a 16-wave block
     const size_t lds = ((size_t)7 << hcap_log2) / 2 * sizeof(uint32_t);
     static bool attr = false;
     if (!attr) {
-      (void)hipFuncSetAttribute((const void*)k_group<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 16 * 1024);
+      (void)hipFuncSetAttribute((const void*)k_group<false, GROUP_BLOCK>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                120 * 1024);
+      (void)hipFuncSetAttribute((const void*)k_group<false, GROUP_BLOCK_BIG>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
       attr = true;
     }
-    hipLaunchKernelGGL((k_group<false>), dim3(n_list), dim3(GROUP_BLOCK), lds, st, ix, krec, roff, n_kept, thr, hit_off,
-                       node_base, r0, read_list, n_list, hcap_log2, gtable, O, stats);
+    if (hcap_log2 >= 13)
+      hipLaunchKernelGGL((k_group<false, GROUP_BLOCK_BIG>), dim3(n_list), dim3(GROUP_BLOCK_BIG), lds, st, ix, krec, roff,
+                         n_kept, thr, hit_off, node_base, r0, read_list, n_list, hcap_log2, gtable, O, stats);
+    else
+      hipLaunchKernelGGL((k_group<false, GROUP_BLOCK>), dim3(n_list), dim3(GROUP_BLOCK), lds, st, ix, krec, roff, n_kept,
+                         thr, hit_off, node_base, r0, read_list, n_list, hcap_log2, gtable, O, stats);
   } else {
-    hipLaunchKernelGGL((k_group<true>), dim3(n_list), dim3(GROUP_BLOCK), 0, st, ix, krec, roff, n_kept, thr, hit_off,
-                       node_base, r0, read_list, n_list, hcap_log2, gtable, O, stats);
+    hipLaunchKernelGGL((k_group<true, GROUP_BLOCK_BIG>), dim3(n_list), dim3(GROUP_BLOCK_BIG), 0, st, ix, krec, roff,
+                       n_kept, thr, hit_off, node_base, r0, read_list, n_list, hcap_log2, gtable, O, stats);
   }
 }
 uint64_t group_table_words(uint32_t hcap_log2) { return ((uint64_t)7 << hcap_log2) / 2; }
@@ -1536,7 +1561,7 @@ void launch_chain_order(const uint32_t* lisl, uint32_t n, uint32_t* hist, uint32
   if (phase == 0) hipLaunchKernelGGL((k_len_hist<ChainLisLen>), dim3(grid_for(n, 256, 2048)), dim3(256), 0, st, f, n, hist);
   else hipLaunchKernelGGL((k_len_perm<ChainLisLen>), dim3((n + 255) / 256), dim3(256), 0, st, f, n, cursor, perm);
 }
-constexpr int LIS_CH16 = 8, LIS_CH32 = 8, FIT_CH = 8;
+constexpr int LIS_CH16 = 8, LIS_CH32 = 8, FIT_CH = 16;
 void launch_lis(bool big_nodes, const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen,
                 const int2* X, void* N, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx,
                 unsigned long long* stats, hipStream_t st) {
