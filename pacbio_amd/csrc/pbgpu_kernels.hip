@@ -1561,7 +1561,7 @@ void launch_chain_order(const uint32_t* lisl, uint32_t n, uint32_t* hist, uint32
   if (phase == 0) hipLaunchKernelGGL((k_len_hist<ChainLisLen>), dim3(grid_for(n, 256, 2048)), dim3(256), 0, st, f, n, hist);
   else hipLaunchKernelGGL((k_len_perm<ChainLisLen>), dim3((n + 255) / 256), dim3(256), 0, st, f, n, cursor, perm);
 }
-constexpr int LIS_CH16 = 8, LIS_CH32 = 8, FIT_CH = 16;
+constexpr int LIS_CH16 = 8, LIS_CH32 = 8, FIT_CH = 8;
 void launch_lis(bool big_nodes, const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen,
                 const int2* X, void* N, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx,
                 unsigned long long* stats, hipStream_t st) {
