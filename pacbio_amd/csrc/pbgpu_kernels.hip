@@ -442,22 +442,34 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
       s_off[tid] = block_excl_scan<B>(nf + nb, s_scan, total);
       if (tid == 0) s_off[B] = total;
       __syncthreads();
+      // hit h -> (record, strand, occurrence address); the occurrence of the next
+      // 256-hit step is loaded one step ahead so its latency overlaps the table work
+      auto locate = [&](uint32_t h, uint32_t& rec, bool& fwd, int32_t& pb) -> uint64_t {
+        uint32_t lo = 0, hi = B;  // last record with s_off <= h
+        while (hi - lo > 1) { const uint32_t md = (lo + hi) >> 1; if (s_off[md] <= h) lo = md; else hi = md; }
+        rec = lo;
+        const uint32_t local = h - s_off[lo];
+        fwd = local < s_nf[lo];
+        pb = s_pb[lo];
+        return fwd ? s_pf[lo] + local : s_pbk[lo] + (local - s_nf[lo]);
+      };
+      uint64_t e_nx = 0;
+      uint32_t rec_nx = 0xFFFFFFFFu;
+      bool fwd_nx = true;
+      int32_t pb_nx = 0;
+      if (tid < total) e_nx = ix.occ[locate(tid, rec_nx, fwd_nx, pb_nx)];
       for (uint32_t h0 = 0; h0 < total; h0 += B) {
         const uint32_t h = h0 + tid;
         const bool valid = h < total;
         uint32_t sr = 0, slot = 0, rec = 0xFFFFFFFFu;
         int32_t so = 0, pb = 0;
         bool fwd = true;
+        const uint64_t e = e_nx;
+        if (valid) { rec = rec_nx; fwd = fwd_nx; pb = pb_nx; }
+        if (h + B < total) e_nx = ix.occ[locate(h + B, rec_nx, fwd_nx, pb_nx)];
         if (valid) {
-          uint32_t lo = 0, hi = B;  // last record with s_off <= h
-          while (hi - lo > 1) { const uint32_t md = (lo + hi) >> 1; if (s_off[md] <= h) lo = md; else hi = md; }
-          rec = lo;
-          const uint32_t local = h - s_off[lo];
-          fwd = local < s_nf[lo];
-          const uint64_t e = ix.occ[fwd ? s_pf[lo] + local : s_pbk[lo] + (local - s_nf[lo])];
           sr = (uint32_t)(e >> 32);
           so = (int32_t)(uint32_t)(e & 0xFFFFFFFFull);
-          pb = s_pb[lo];
           slot = (sr * 0x9E3779B1u) >> (32 - hcap_log2);
         }
         if (pass == 0) {
@@ -491,8 +503,8 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
                 const bool in_seg = rec == lrec;
                 const uint64_t seg = __ballot(in_seg);
                 if (in_seg) tag[key] = (uint8_t)lane;
-                if (GLOBAL_TABLE) __threadfence_block();
-                __builtin_amdgcn_s_waitcnt(0);
+                if (GLOBAL_TABLE) { __threadfence_block(); __builtin_amdgcn_s_waitcnt(0); }
+                else __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the tag writes landed
                 __builtin_amdgcn_wave_barrier();
                 const bool dup = in_seg && tag[key] != (uint8_t)lane;
                 if (!__ballot(dup)) {
@@ -513,8 +525,8 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
                     act2 &= ~peers;
                   }
                 }
-                if (GLOBAL_TABLE) __threadfence_block();
-                __builtin_amdgcn_s_waitcnt(0);
+                if (GLOBAL_TABLE) { __threadfence_block(); __builtin_amdgcn_s_waitcnt(0); }
+                else __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the tag writes landed
                 __builtin_amdgcn_wave_barrier();
                 active &= ~seg;
               }
