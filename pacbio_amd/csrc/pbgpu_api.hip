@@ -484,8 +484,10 @@ struct pbgpu_aligner {
   pbgpu_stats acc{};
   hipEvent_t ev[16]{};
   uint64_t hit_budget = 1200000000ull, rec_hint = 0, info_per_chain = 32;
-  double chains_per_hit = 1.0 / 16;  // routing estimate for k_group tiers, refined after every batch
+  double chains_per_hit = 1.0 / 48;  // k_group partition estimate, refined after every batch
   dbuf<uint32_t> ovf_list, read_list;
+  dbuf<uint8_t> nparts;
+  dbuf<uint2> prog;
 };
 
 static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd);
@@ -650,31 +652,42 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
     O.chain_cap = (uint32_t)std::min<uint64_t>(al->chains.n, 0xFFFFFFFFu);
     O.n_overflow = al->counters.p + 3;
     O.overflow_reads = al->ovf_reads.p;
-    // reads longest first (hits), so the long-read tail starts early; reads whose
-    // predicted super-read count (hits x chains-per-hit of earlier batches) would
-    // overflow the 2048-slot table go straight to the 8192-slot tier
-    std::vector<uint32_t> rl_small, rl_big;
+    // Reads longest first (hits), so the long-read tail starts early.  The predicted
+    // super-read count of a read (hits x chains-per-hit of earlier batches) picks its
+    // table: 2048 LDS slots (4 waves), 8192 LDS slots (16 waves), and beyond that the
+    // 8192-slot table over several hash partitions of its super-reads.  A misprediction
+    // only costs time: an overflowing read resumes in the next tier.
+    uint32_t n_small = 0, n_bigr = 0;
     {
-      std::vector<uint32_t> rl(nr);
+      std::vector<uint32_t> rl(nr), rs, rb;
+      std::vector<uint8_t> parts(nr);
       for (uint32_t i = 0; i < nr; ++i) rl[i] = r0 + i;
       std::stable_sort(rl.begin(), rl.end(), [&](uint32_t a, uint32_t b) {
         return hoff[a + 1] - hoff[a] > hoff[b + 1] - hoff[b];
       });
-      const double limit = (double)((1u << hcap_log2) - (1u << hcap_log2) / 4);  // the small table's fill limit
-      for (uint32_t r : rl) ((double)(hoff[r + 1] - hoff[r]) * al->chains_per_hit > limit ? rl_big : rl_small).push_back(r);
+      const double fill_small = 0.95 * (double)((1u << hcap_log2) - (1u << hcap_log2) / 4);
+      const double fill_big = 0.95 * (double)((1u << kGroupLdsMaxLog2) - (1u << kGroupLdsMaxLog2) / 4);
+      for (uint32_t r : rl) {
+        const double pred = (double)(hoff[r + 1] - hoff[r]) * al->chains_per_hit;
+        parts[r - r0] = (uint8_t)std::min(255.0, std::max(1.0, std::ceil(pred / fill_big)));
+        (pred > fill_small ? rb : rs).push_back(r);
+      }
+      n_small = (uint32_t)rs.size(); n_bigr = (uint32_t)rb.size();
+      rs.insert(rs.end(), rb.begin(), rb.end());
       al->read_list.ensure(nr);
-      if (!rl_small.empty())
-        HIPCHK(hipMemcpyAsync(al->read_list.p, rl_small.data(), rl_small.size() * 4, hipMemcpyHostToDevice, st));
-      if (!rl_big.empty())
-        HIPCHK(hipMemcpyAsync(al->read_list.p + rl_small.size(), rl_big.data(), rl_big.size() * 4,
-                              hipMemcpyHostToDevice, st));
+      al->nparts.ensure(n);
+      al->prog.ensure(n);
+      HIPCHK(hipMemcpyAsync(al->read_list.p, rs.data(), (size_t)nr * 4, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(al->nparts.p + r0, parts.data(), nr, hipMemcpyHostToDevice, st));
     }
-    const uint32_t n_small = (uint32_t)rl_small.size(), n_bigr = (uint32_t)rl_big.size();
+    O.nparts = al->nparts.p;
+    O.prog = al->prog.p;
     for (int attempt = 0;; ++attempt) {
       HIPCHK(hipEventRecord(al->ev[5], st));
       HIPCHK(hipMemsetAsync(al->counters.p, 0, 16 * 4, st));
       static_assert(ST_LIS_TESTS == ST_CHAINS + 1, "per-attempt stat slots are adjacent");
       HIPCHK(hipMemsetAsync(al->stats.p + ST_CHAINS, 0, 16, st));  // redone on a retry: counted per attempt
+      O.resume = 0;
       HIPCHK(hipEventRecord(al->ev[8], st));
       launch_group(v, al->krec.p, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0, al->read_list.p, n_small,
                    hcap_log2, nullptr, O, al->stats.p, st);
@@ -683,6 +696,7 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
       launch_group(v, al->krec.p, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0,
                    al->read_list.p + n_small, n_bigr, kGroupLdsMaxLog2, nullptr, O, al->stats.p, st);
       HIPCHK(hipGetLastError());
+      O.resume = 1;
       uint32_t cnt[4];
       HIPCHK(hipMemcpyAsync(cnt, al->counters.p, 16, hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));

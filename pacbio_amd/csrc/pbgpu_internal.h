@@ -98,6 +98,9 @@ struct GroupOut {
   uint32_t chain_cap;
   uint32_t* overflow_reads;
   uint32_t* n_overflow;
+  const uint8_t* nparts;   // per read: super-read hash partitions grouped one after the other (null = 1)
+  uint2* prog;             // per read: {next partition, hits placed} when its table overflowed
+  int resume;              // continue each read from prog[] (overflow relaunch)
 };
 
 struct LisParams {

@@ -24,7 +24,7 @@ namespace pbgpu {
 // Optional phase profiling of k_lis (build with -DPBGPU_PROF; tools/prof_lis.py):
 // per-wave s_memtime deltas summed into g_prof.
 #ifdef PBGPU_PROF
-__device__ unsigned long long g_prof[16];
+__device__ unsigned long long g_prof[32];
 #define PROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define PROF_ADD(slot, v) do { if (lane_id() == 0) atomicAdd(&g_prof[slot], (unsigned long long)(v)); } while (0)
 #else
@@ -407,19 +407,37 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
   uint32_t* tcf = tkey + hcap;
   uint32_t* tcb = tcf + hcap;
   uint8_t* tag = (uint8_t*)(tcb + hcap);
-  if (!GLOBAL_TABLE)  // the global variant is zeroed by hipMemsetAsync
-    for (uint32_t i = tid; i < hcap; i += B) { tkey[i] = 0; tcf[i] = 0; tcb[i] = 0; }
-  if (tid == 0) { s_flag = 0; s_used = 0; }
-  __syncthreads();
   const uint64_t kbase = roff[r];
   const uint32_t nk = n_kept[r], thr = thr_in[r];
   const uint64_t hbase = hit_off[r] - node_base;
   const uint32_t used_limit = hcap - hcap / 4;
   const uint64_t lt_mask = (1ull << lane) - 1ull;
+  // Reads touching many super-reads are grouped in P passes over hash partitions
+  // of the super-read ids; each partition's lists are placed after the previous
+  // ones, so every list is still contiguous and in reference order.
+  const uint32_t P = O.nparts ? O.nparts[r] : 1u;
+  uint32_t part0 = 0, placed = 0;
+  if (O.resume) { const uint2 pg = O.prog[r]; part0 = pg.x; placed = pg.y; }
+  auto part_of = [&](uint32_t sr) -> uint32_t {
+    return P == 1 ? 0u : (uint32_t)(((uint64_t)(sr * 0x85EBCA77u) * P) >> 32);
+  };
+  for (uint32_t part = part0; part < P; ++part) {
+  uint32_t part_hits = 0;
+  for (uint32_t i = tid; i < hcap; i += B) { tkey[i] = 0; tcf[i] = 0; tcb[i] = 0; }
+  if (tid == 0) { s_flag = 0; s_used = 0; }
+  if (GLOBAL_TABLE) __threadfence_block();
+  __syncthreads();
+#ifdef PBGPU_PROF
+  uint64_t pr_setup[2] = {0, 0}, pr_steps[2] = {0, 0}, pr_compact = 0;
+  const uint64_t pr_t0 = __builtin_amdgcn_s_memtime();
+#endif
 
   for (int pass = 0; pass < 2; ++pass) {
     for (uint32_t g0 = 0; g0 < nk; g0 += B) {
       if (s_flag) break;  // uniform (written before the last barrier)
+#ifdef PBGPU_PROF
+      const uint64_t pr_a = __builtin_amdgcn_s_memtime();
+#endif
       const uint32_t i = g0 + tid;
       uint32_t nf = 0, nb = 0;
       if (i < nk) {
@@ -442,6 +460,10 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
       s_off[tid] = block_excl_scan<B>(nf + nb, s_scan, total);
       if (tid == 0) s_off[B] = total;
       __syncthreads();
+#ifdef PBGPU_PROF
+      const uint64_t pr_b = __builtin_amdgcn_s_memtime();
+      pr_setup[pass] += pr_b - pr_a;
+#endif
       // hit h -> (record, strand, occurrence address); the occurrence of the next
       // 256-hit step is loaded one step ahead so its latency overlaps the table work
       auto locate = [&](uint32_t h, uint32_t& rec, bool& fwd, int32_t& pb) -> uint64_t {
@@ -467,14 +489,16 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
         const uint64_t e = e_nx;
         if (valid) { rec = rec_nx; fwd = fwd_nx; pb = pb_nx; }
         if (h + B < total) e_nx = ix.occ[locate(h + B, rec_nx, fwd_nx, pb_nx)];
+        bool mine = valid;
         if (valid) {
           sr = (uint32_t)(e >> 32);
           so = (int32_t)(uint32_t)(e & 0xFFFFFFFFull);
           slot = (sr * 0x9E3779B1u) >> (32 - hcap_log2);
+          mine = part_of(sr) == part;
         }
         if (pass == 0) {
           // order-free: distinct super-reads and per-strand list lengths
-          if (valid) {
+          if (mine) {
             bool ok = true;
             for (;;) {
               const uint32_t old = atomicCAS(&tkey[slot], 0u, sr + 1);
@@ -485,7 +509,7 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
             if (ok) atomicAdd(fwd ? &tcf[slot] : &tcb[slot], 1u);
           }
         } else {
-          if (valid) while (tkey[slot] != sr + 1) slot = (slot + 1) & (hcap - 1);
+          if (mine) while (tkey[slot] != sr + 1) slot = (slot + 1) & (hcap - 1);
           // Order-preserving multisplit over (slot, strand) keys.  The four waves hold
           // consecutive 64-hit runs; they take the list cursors in wave order (LDS only,
           // after all loads are in flight).  Within a wave, hits of one k-mer record hit
@@ -496,11 +520,11 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
           uint32_t pos = 0;
           for (uint32_t w = 0; w < B / 64; ++w) {
             if (wave == w) {
-              uint64_t active = __ballot(valid);
+              uint64_t active = __ballot(mine);
               while (active) {
                 const int leader = __ffsll((unsigned long long)active) - 1;
                 const uint32_t lrec = __builtin_amdgcn_readlane(rec, leader);
-                const bool in_seg = rec == lrec;
+                const bool in_seg = mine && rec == lrec;
                 const uint64_t seg = __ballot(in_seg);
                 if (in_seg) tag[key] = (uint8_t)lane;
                 if (GLOBAL_TABLE) { __threadfence_block(); __builtin_amdgcn_s_waitcnt(0); }
@@ -533,14 +557,24 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
             }
             __syncthreads();
           }
-          if (valid) O.X[hbase + pos] = make_int2(pb, fwd ? so : -so);
+          if (mine) O.X[hbase + pos] = make_int2(pb, fwd ? so : -so);
         }
       }
       __syncthreads();
+#ifdef PBGPU_PROF
+      pr_steps[pass] += __builtin_amdgcn_s_memtime() - pr_b;
+#endif
     }
     if (pass == 0) {
-      if (s_flag) {  // table too full: this read is redone with a larger table
-        if (tid == 0) { const uint32_t o = atomicAdd(O.n_overflow, 1u); O.overflow_reads[o] = r; }
+#ifdef PBGPU_PROF
+      const uint64_t pr_c = __builtin_amdgcn_s_memtime();
+#endif
+      if (s_flag) {  // table too full: this read continues from this partition with a larger table
+        if (tid == 0) {
+          O.prog[r] = make_uint2(part, placed);
+          const uint32_t o = atomicAdd(O.n_overflow, 1u);
+          O.overflow_reads[o] = r;
+        }
         return;
       }
       // chain descriptors, slot order; cursors become read-local list starts
@@ -552,13 +586,14 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
       }
       uint32_t tsum, tn;
       const uint32_t esum = block_excl_scan<B>(sum, s_scan, tsum);
+      part_hits = tsum;
       const uint32_t enn = block_excl_scan<B>(nn, s_scan, tn);
       if (tid == 0) {
         s_cbase = atomicAdd(O.chain_count, tn);
         atomicAdd(&stats[ST_CHAINS], (unsigned long long)tn);
       }
       __syncthreads();
-      uint32_t b0 = esum, ci = s_cbase + enn;
+      uint32_t b0 = placed + esum, ci = s_cbase + enn;
       for (uint32_t j = 0; j < per; ++j) {
         const uint32_t sl = tid * per + j;
         if (!tkey[sl]) continue;
@@ -575,8 +610,24 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
       }
       if (GLOBAL_TABLE) __threadfence_block();
       __syncthreads();
+#ifdef PBGPU_PROF
+      pr_compact += __builtin_amdgcn_s_memtime() - pr_c;
+#endif
     }
   }
+  placed += part_hits;
+  }  // partitions
+#ifdef PBGPU_PROF
+  if (tid == 0 && !GLOBAL_TABLE) {
+    const int sb = B == 256 ? 8 : 14;
+    atomicAdd(&g_prof[sb + 0], (unsigned long long)pr_setup[0] + pr_setup[1]);
+    atomicAdd(&g_prof[sb + 1], (unsigned long long)pr_steps[0]);
+    atomicAdd(&g_prof[sb + 2], (unsigned long long)pr_steps[1]);
+    atomicAdd(&g_prof[sb + 3], (unsigned long long)pr_compact);
+    atomicAdd(&g_prof[sb + 4], (unsigned long long)(__builtin_amdgcn_s_memtime() - pr_t0));
+    atomicAdd(&g_prof[sb + 5], 1ull);
+  }
+#endif
 }
 
 // Work ordering for the lane-per-item kernels: items by descending length
@@ -1634,10 +1685,10 @@ void launch_discard(const ChainDesc* chains, const uint32_t* list, uint32_t n, c
 uint32_t len_buckets() { return NLB; }
 #ifdef PBGPU_PROF
 extern "C" int pbgpu_debug_prof(unsigned long long* out, int n, int reset) {
-  if (n > 16) n = 16;
+  if (n > 32) n = 32;
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), n * sizeof(unsigned long long)) != hipSuccess) return -1;
   if (reset) {
-    unsigned long long z[16] = {};
+    unsigned long long z[32] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof z) != hipSuccess) return -1;
   }
   return 0;

@@ -28,12 +28,12 @@ def main():
     L = pbgpu.lib()
     f = L.pbgpu_debug_prof
     f.argtypes = [C.POINTER(C.c_ulonglong), C.c_int, C.c_int]
-    buf = (C.c_ulonglong * 16)()
-    f(buf, 16, 1)
+    buf = (C.c_ulonglong * 32)()
+    f(buf, 32, 1)
     al.reset_stats()
     al.align_resident(rr)
     pbgpu.device_synchronize(0)
-    f(buf, 16, 1)
+    f(buf, 32, 1)
     st = al.stats()
     names = ["row_load_issue", "lds_fetch", "element_loop", "row_store", "sweep", "wave_total", "chunks", "waves"]
     v = list(buf)[:8]
@@ -42,6 +42,12 @@ def main():
           f"hits={st['n_hits']}, tests={st['n_lis_tests']}")
     for n, x in zip(names[:6], v[:6]):
         print(f"  {n:16s} {x / waves:12.0f} ticks/wave  ({100.0 * x / max(1, v[5]):5.1f}%)")
+    g = list(buf)
+    for label, sb in (("k_group 2048-slot tier", 8), ("k_group 8192-slot tier", 14)):
+        blocks = max(1, g[sb + 5])
+        print(f"{label}: blocks={g[sb + 5]} (ms: tier0 {st['kernel_ms']['k_group']:.2f})")
+        for n, x in zip(["setup", "pass0 steps", "pass1 steps", "compaction", "block_total"], g[sb:sb + 5]):
+            print(f"  {n:16s} {x / blocks:12.0f} ticks/block ({100.0 * x / max(1, g[sb + 4]):5.1f}%)")
 
 
 if __name__ == "__main__":
