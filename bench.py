@@ -67,6 +67,11 @@ class Comm:
         return float(t.item())
 
 
+# the rocprofv3 kernel each timed slot corresponds to (tools/pmc_summary.py file names)
+ROCPROF_FILE = {"k_seed": "k_seed_256_8", "k_group": "k_group_false_256u", "k_lis": "k_lis_w_511_4",
+                "k_coords": "k_coords_8", "k_rec_sort": "k_rec_sort_256_2048"}
+
+
 def _kernel_bytes(st):
     """Algorithmic HBM bytes per launch of each individually timed kernel
     (DESIGN.md "Roofline"): every byte the algorithm must move at least once,
@@ -76,9 +81,10 @@ def _kernel_bytes(st):
     return {
         # read bases (1 B), one 64-B bucket per probe, kept k-mer records (16 B) written
         "k_seed": per(st["n_bases"] + st["n_probes"] * 64 + st["n_kept"] * 16, "k_seed"),
-        # k-mer records (16 B) + occurrence headers (16 B) read, every occurrence (8 B) read,
-        # every hit (8 B) written, chain descriptors (24 B) written
-        "k_group": per(st["n_kept"] * 32 + st["n_hits"] * 16 + st["n_chains"] * 24, "k_group"),
+        # first-tier launches only (the timed ones): k-mer records (16 B) + occurrence headers
+        # (16 B) read, every occurrence (8 B) read once, every hit (8 B) written, chain
+        # descriptors (24 B) written -- counted by the kernel for the reads it completed
+        "k_group": per(st["g0_kept"] * 32 + st["g0_hits"] * 16 + st["g0_chains"] * 24, "k_group"),
         # every hit read (8 B), a node written per hit (8 B), lis points written (<= 8 B/hit)
         "k_lis": per(st["n_hits"] * 24 + st["n_chains"] * 24, "k_lis"),
         # chain descriptors + lis lengths read, lis points read, records written
@@ -97,6 +103,7 @@ def main():
     ap.add_argument("--reads", type=int, default=0, help="override reads per GPU")
     ap.add_argument("--cpu-sample-reads", type=int, default=0, help="CPU baseline sample (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-brand", action="store_true", help="skip the B_rand gather microbenchmark")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
     args = ap.parse_args()
@@ -105,6 +112,9 @@ def main():
     comm = Comm(world)
     from pacbio_amd import pbgpu
     from tools.synth import Dataset, PRESETS
+
+    # B_rand: random 64-B sector gathers over a 64 GB buffer, this GPU, this run
+    b_rand = pbgpu.measure_gather(local, 64 << 30) if not args.no_brand else None
 
     k = 21 if args.workload == "C3" else 17
     n_pb = args.reads or PRESETS[args.workload]["n_pb"]
@@ -146,7 +156,7 @@ def main():
     avg_ms = kms[dom] / max(1, kn[dom])
     achieved = kb[dom] / (avg_ms * 1e-3) / 1e9
     traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{dom}.json")
+    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{ROCPROF_FILE[dom]}.json")
     if os.path.exists(pmc_path):
         try:
             with open(pmc_path) as f:
@@ -217,9 +227,10 @@ def main():
                                        "n_records")},
                 "fit_dtype": "f64",
             },
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
+            "roofline": {"bound": "hbm", "kernel": dom, "rocprof_kernel": ROCPROF_FILE[dom], "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "alg_bytes_per_launch": kb[dom], "avg_launch_ms": avg_ms},
+                         "alg_bytes_per_launch": kb[dom], "avg_launch_ms": avg_ms,
+                         "b_rand_gbs": b_rand, "frac_of_b_rand": (achieved / b_rand) if b_rand else None},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -55,6 +55,10 @@ const char* pbgpu_last_error(void);
 int         pbgpu_device_count(void);
 /* hipDeviceSynchronize on `device` (bench brackets its timed region with it) */
 pbgpu_status pbgpu_device_synchronize(int device);
+/* Measurement aid (no reference counterpart): bandwidth of uniformly random
+ * 64-byte sector loads over a fresh device buffer of buffer_bytes, all CUs
+ * (SURVEY 8(d) B_rand, the random-access roofline).  Frees the buffer. */
+pbgpu_status pbgpu_measure_gather(int device, uint64_t buffer_bytes, double* gbps);
 
 /* ------------------------------------------------------------------ index
  * Replaces superread_parse() + sequence_psa (superread_parser.hpp:53-224):
@@ -192,6 +196,9 @@ typedef struct {
   double   ms_seed, ms_group, ms_lis, ms_fit, ms_records;
   double   kernel_ms[PBGPU_KERNEL_N];
   uint64_t kernel_launches[PBGPU_KERNEL_N];
+  /* work completed inside the timed first-tier k_group launches (kept k-mers
+   * of the reads they finished, hits scattered, chains emitted) */
+  uint64_t g0_kept, g0_hits, g0_chains;
 } pbgpu_stats;
 pbgpu_status pbgpu_aligner_get_stats(const pbgpu_aligner* al, pbgpu_stats* s);
 pbgpu_status pbgpu_aligner_reset_stats(pbgpu_aligner* al);

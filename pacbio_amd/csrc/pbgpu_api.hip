@@ -60,7 +60,7 @@ void launch_rec_hist(const Rec* recs, uint32_t n, uint32_t* per_read, hipStream_
 void launch_rec_scatter(const Rec* recs, uint32_t n, const uint64_t* rec_off, uint32_t* cursor, uint32_t* order,
                         hipStream_t st);
 int rec_sort_lcap();
-void launch_rec_sort(const Rec* recs, const uint64_t* rec_off, const uint32_t* order, uint32_t* gscratch,
+void launch_rec_sort(const Rec* recs, const uint64_t* rec_off, const uint32_t* order, uint64_t* gscratch,
                      uint32_t n_reads, Rec* out, hipStream_t st);
 }  // namespace pbgpu
 
@@ -375,6 +375,65 @@ pbgpu_status pbgpu_device_synchronize(int device) {
   API_CATCH
 }
 
+// Random 64-B sector gather over a large buffer: SURVEY 8(d)'s B_rand, the
+// roofline of the index probes and occurrence-list reads.  Four lanes load one
+// sector (16 B each); every lane keeps UNR sectors in flight.
+namespace {
+constexpr int GATHER_UNR = 8;
+__global__ __launch_bounds__(256) void k_gather_sectors(const uint4* __restrict__ buf, uint64_t n_sectors,
+                                                        uint32_t iters, uint32_t seed, uint4* __restrict__ sink) {
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t grp = gid >> 2;
+  const uint32_t part = threadIdx.x & 3;
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  for (uint32_t it = 0; it < iters; ++it) {
+    uint4 v[GATHER_UNR];
+#pragma unroll
+    for (int u = 0; u < GATHER_UNR; ++u) {
+      uint64_t h = (grp * GATHER_UNR + u) * 0x9E3779B97F4A7C15ull + ((uint64_t)(it + 1) * seed);
+      h ^= h >> 31; h *= 0xD6E8FEB86659FD93ull; h ^= h >> 32;
+      v[u] = buf[(h % n_sectors) * 4 + part];
+    }
+#pragma unroll
+    for (int u = 0; u < GATHER_UNR; ++u) { acc.x ^= v[u].x; acc.y ^= v[u].y; acc.z ^= v[u].z; acc.w ^= v[u].w; }
+  }
+  if ((acc.x & 0xFFFFF) == 0x12345) sink[gid & 1023] = acc;  // keeps the loads live, practically never stores
+}
+}  // namespace
+
+pbgpu_status pbgpu_measure_gather(int device, uint64_t buffer_bytes, double* gbps) {
+  if (!gbps || buffer_bytes < (1u << 20)) return fail(PBGPU_ERR_INVALID, "bad argument");
+  API_TRY
+  HIPCHK(hipSetDevice(device));
+  dbuf<uint4> buf, sink;
+  const uint64_t n_sectors = buffer_bytes / 64;
+  buf.ensure(n_sectors * 4);
+  sink.ensure(1024);
+  hipDeviceProp_t pr;
+  HIPCHK(hipGetDeviceProperties(&pr, device));
+  const uint32_t blocks = (uint32_t)pr.multiProcessorCount * 8, iters = 64;
+  hipStream_t st;
+  HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  hipEvent_t e0, e1;
+  HIPCHK(hipEventCreate(&e0)); HIPCHK(hipEventCreate(&e1));
+  hipLaunchKernelGGL(k_gather_sectors, dim3(blocks), dim3(256), 0, st, buf.p, n_sectors, iters, 7u, sink.p);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(e0, st));
+  const int reps = 3;
+  for (int r = 0; r < reps; ++r)
+    hipLaunchKernelGGL(k_gather_sectors, dim3(blocks), dim3(256), 0, st, buf.p, n_sectors, iters, 11u + 2u * r, sink.p);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(e1, st));
+  HIPCHK(hipEventSynchronize(e1));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+  const double bytes = (double)reps * blocks * 256 / 4 * GATHER_UNR * iters * 64.0;
+  *gbps = bytes / (ms * 1e-3) / 1e9;
+  (void)hipEventDestroy(e0); (void)hipEventDestroy(e1); (void)hipStreamDestroy(st);
+  return PBGPU_OK;
+  API_CATCH
+}
+
 pbgpu_status pbgpu_index_build_fasta(const char* const* paths, size_t n_paths, const pbgpu_index_params* params,
                                      pbgpu_index** out) {
   if (!out || (!paths && n_paths)) return fail(PBGPU_ERR_INVALID, "null argument");
@@ -463,7 +522,8 @@ struct pbgpu_aligner {
   dbuf<int32_t> ul;
   // per-batch buffers
   dbuf<KRec> krec;
-  dbuf<uint32_t> n_kept, thr, rec_per_read, rec_cursor, order, sort_scratch, ovf_reads, counters;
+  dbuf<uint32_t> n_kept, thr, rec_per_read, rec_cursor, order, ovf_reads, counters;
+  dbuf<uint64_t> sort_scratch;  // k_rec_sort keys of reads above its LDS capacity: 6 words per record
   dbuf<uint64_t> nhits, hit_off, rec_off, huge_elems;
   dbuf<int2> hits;
   dbuf<ChainDesc> chains;
@@ -900,7 +960,7 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(temp_storage(al->tmp, tb), tb, in, al->rec_off.p, (uint64_t)n + 1, st));
   }
   al->order.ensure(nrec + 1);
-  al->sort_scratch.ensure(2ull * nrec + 2);
+  al->sort_scratch.ensure(6ull * nrec + 6);
   al->recs_sorted.ensure(nrec + 1);
   launch_rec_scatter(al->recs.p, nrec, al->rec_off.p, al->rec_cursor.p, al->order.p, st);
   HIPCHK(hipEventRecord(al->ev[15], st));
@@ -913,6 +973,7 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
   al->acc.n_kmers += sv[ST_KMERS]; al->acc.n_probes += sv[ST_PROBES]; al->acc.n_kept += sv[ST_KEPT];
   al->acc.n_hits += sv[ST_HITS]; al->acc.n_chains += n_chains; al->acc.n_lis_tests += n_tests;
   al->acc.n_records += nrec;
+  al->acc.g0_kept += sv[ST_G0_KEPT]; al->acc.g0_hits += sv[ST_G0_HITS]; al->acc.g0_chains += sv[ST_G0_CHAINS];
   al->acc.ms_seed += ev_ms(al->ev[0], al->ev[1]);
   al->acc.ms_group += ms_group;
   al->acc.ms_lis += ms_lis;

@@ -88,7 +88,9 @@ static_assert(sizeof(Rec) == 96, "Rec layout must match pbgpu_record");
 
 enum StatSlot {
   ST_KMERS = 0, ST_PROBES, ST_KEPT, ST_HITS, ST_CHAINS, ST_LIS_TESTS, ST_RECORDS,
-  ST_REC_OVERFLOW, ST_INFO_USED, ST_GROUP_OVERFLOW, ST_N
+  ST_REC_OVERFLOW, ST_INFO_USED, ST_GROUP_OVERFLOW,
+  ST_G0_KEPT, ST_G0_HITS, ST_G0_CHAINS,  // work completed by first-tier (4-wave LDS) k_group launches
+  ST_N
 };
 
 struct GroupOut {

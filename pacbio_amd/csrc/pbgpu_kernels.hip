@@ -416,7 +416,7 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
   // of the super-read ids; each partition's lists are placed after the previous
   // ones, so every list is still contiguous and in reference order.
   const uint32_t P = O.nparts ? O.nparts[r] : 1u;
-  uint32_t part0 = 0, placed = 0;
+  uint32_t part0 = 0, placed = 0, read_chains = 0;
   if (O.resume) { const uint2 pg = O.prog[r]; part0 = pg.x; placed = pg.y; }
   auto part_of = [&](uint32_t sr) -> uint32_t {
     return P == 1 ? 0u : (uint32_t)(((uint64_t)(sr * 0x85EBCA77u) * P) >> 32);
@@ -588,6 +588,7 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
       const uint32_t esum = block_excl_scan<B>(sum, s_scan, tsum);
       part_hits = tsum;
       const uint32_t enn = block_excl_scan<B>(nn, s_scan, tn);
+      read_chains += tn;
       if (tid == 0) {
         s_cbase = atomicAdd(O.chain_count, tn);
         atomicAdd(&stats[ST_CHAINS], (unsigned long long)tn);
@@ -617,6 +618,11 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
   }
   placed += part_hits;
   }  // partitions
+  if (!GLOBAL_TABLE && B == GROUP_BLOCK && tid == 0) {  // per-launch algorithmic counters (bench roofline)
+    atomicAdd(&stats[ST_G0_KEPT], (unsigned long long)nk);
+    atomicAdd(&stats[ST_G0_HITS], (unsigned long long)placed);
+    atomicAdd(&stats[ST_G0_CHAINS], (unsigned long long)read_chains);
+  }
 #ifdef PBGPU_PROF
   if (tid == 0 && !GLOBAL_TABLE) {
     const int sb = B == 256 ? 8 : 14;
@@ -1502,22 +1508,42 @@ __global__ void k_rec_scatter(const Rec* recs, uint32_t n, const uint64_t* rec_o
   }
 }
 
-DEV bool rec_less(const Rec& a, const Rec& b) {
-  if (a.rs != b.rs) return a.rs < b.rs;
-  if (a.re != b.re) return a.re < b.re;
-  if (a.ql != b.ql) return a.ql < b.ql;
-  if (a.sr != b.sr) return a.sr < b.sr;
-  return a.emit < b.emit;
+// Sort key of a record within its read: (rs, re, ql, sr, emit) as two u64 words
+// plus a tie word (emit, then the read-local slot, which never decides since
+// (sr, emit) is unique per read).  Signed rs/re are biased so u64 order = int order.
+DEV uint64_t rec_key_hi(const Rec& r) {
+  return ((uint64_t)((uint32_t)r.rs ^ 0x80000000u) << 32) | (uint32_t)((uint32_t)r.re ^ 0x80000000u);
+}
+DEV uint64_t rec_key_lo(const Rec& r) { return ((uint64_t)r.ql << 32) | r.sr; }
+
+// Bitonic network over staged keys: pair p -> (i, i + j), all threads busy.
+template <int BLOCK, typename EX>
+DEV void bitonic_keys(uint64_t* hi, uint64_t* lo, EX* ex, uint32_t np2) {
+  for (uint32_t kk = 2; kk <= np2; kk <<= 1) {
+    for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+      for (uint32_t p = threadIdx.x; p < (np2 >> 1); p += BLOCK) {
+        const uint32_t i = ((p & ~(j - 1)) << 1) | (p & (j - 1)), l = i + j;
+        const uint64_t h0 = hi[i], h1 = hi[l], l0 = lo[i], l1 = lo[l];
+        const EX e0 = ex[i], e1 = ex[l];
+        const bool gt = h0 != h1 ? h0 > h1 : l0 != l1 ? l0 > l1 : e0 > e1;
+        if (gt == ((i & kk) == 0)) { hi[i] = h1; hi[l] = h0; lo[i] = l1; lo[l] = l0; ex[i] = e1; ex[l] = e0; }
+      }
+      __syncthreads();
+    }
+  }
 }
 
-// One block per read: sort the read's record indices by (rs, re, ql, sr, emit)
-// with an odd-even merge (bitonic) network over LDS (or global for big reads),
-// then gather the records in that order.
+// One block per read: stage the sort keys of the read's records once (LDS, or
+// a global scratch region for reads with more than LCAP records), sort them
+// with a bitonic network, then gather the records in that order.  Padding
+// entries carry all-ones keys and sort last.
 template <int BLOCK, int LCAP>
 __global__ __launch_bounds__(BLOCK) void k_rec_sort(const Rec* __restrict__ recs, const uint64_t* __restrict__ rec_off,
-                                                    const uint32_t* __restrict__ order_in, uint32_t* gscratch,
+                                                    const uint32_t* __restrict__ order_in, uint64_t* gscratch,
                                                     uint32_t n_reads, Rec* __restrict__ out) {
-  __shared__ uint32_t s_idx[LCAP];
+  static_assert(LCAP <= 4096, "LDS tie word holds a 12-bit slot");
+  __shared__ uint64_t s_hi[LCAP], s_lo[LCAP];
+  __shared__ uint32_t s_ex[LCAP];
   const uint32_t r = blockIdx.x;
   if (r >= n_reads) return;
   const uint64_t b = rec_off[r];
@@ -1525,27 +1551,36 @@ __global__ __launch_bounds__(BLOCK) void k_rec_sort(const Rec* __restrict__ recs
   if (n == 0) return;
   uint32_t np2 = 1;
   while (np2 < n) np2 <<= 1;
-  uint32_t* a = np2 <= LCAP ? s_idx : gscratch + 2 * b;  // host reserves 2x per read for the global case
-  for (uint32_t i = threadIdx.x; i < np2; i += BLOCK) a[i] = i < n ? order_in[b + i] : 0xFFFFFFFFu;
-  __syncthreads();
-  for (uint32_t kk = 2; kk <= np2; kk <<= 1) {
-    for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
-      for (uint32_t i = threadIdx.x; i < np2; i += BLOCK) {
-        const uint32_t l = i ^ j;
-        if (l > i) {
-          const uint32_t x = a[i], y = a[l];
-          bool gt;  // x > y ?
-          if (x == 0xFFFFFFFFu) gt = y != 0xFFFFFFFFu;
-          else if (y == 0xFFFFFFFFu) gt = false;
-          else gt = rec_less(recs[y], recs[x]);
-          const bool up = (i & kk) == 0;
-          if (gt == up) { a[i] = y; a[l] = x; }
-        }
+  if (np2 <= LCAP) {
+    for (uint32_t i = threadIdx.x; i < np2; i += BLOCK) {
+      if (i < n) {
+        const Rec& R = recs[order_in[b + i]];
+        s_hi[i] = rec_key_hi(R); s_lo[i] = rec_key_lo(R); s_ex[i] = (R.emit << 12) | i;
+      } else {
+        s_hi[i] = ~0ull; s_lo[i] = ~0ull; s_ex[i] = ~0u;
       }
-      __syncthreads();
     }
+    __syncthreads();
+    bitonic_keys<BLOCK>(s_hi, s_lo, s_ex, np2);
+    for (uint32_t i = threadIdx.x; i < n; i += BLOCK) out[b + i] = recs[order_in[b + (s_ex[i] & 0xFFFu)]];
+  } else {
+    // host reserves 6 words per record: np2 <= 2n entries of {hi, lo, ex}
+    uint64_t* hi = gscratch + 6 * b;
+    uint64_t* lo = hi + np2;
+    uint64_t* ex = lo + np2;
+    for (uint32_t i = threadIdx.x; i < np2; i += BLOCK) {
+      if (i < n) {
+        const Rec& R = recs[order_in[b + i]];
+        hi[i] = rec_key_hi(R); lo[i] = rec_key_lo(R); ex[i] = ((uint64_t)R.emit << 32) | i;
+      } else {
+        hi[i] = ~0ull; lo[i] = ~0ull; ex[i] = ~0ull;
+      }
+    }
+    __threadfence_block();
+    __syncthreads();
+    bitonic_keys<BLOCK>(hi, lo, ex, np2);
+    for (uint32_t i = threadIdx.x; i < n; i += BLOCK) out[b + i] = recs[order_in[b + (uint32_t)ex[i]]];
   }
-  for (uint32_t i = threadIdx.x; i < n; i += BLOCK) out[b + i] = recs[a[i]];
 }
 
 }  // namespace pbgpu
@@ -1708,9 +1743,9 @@ void launch_rec_scatter(const Rec* recs, uint32_t n, const uint64_t* rec_off, ui
   if (!n) return;
   hipLaunchKernelGGL(k_rec_scatter, dim3(1024), dim3(256), 0, st, recs, n, rec_off, cursor, order);
 }
-constexpr int REC_BLOCK = 256, REC_LCAP = 4096;
+constexpr int REC_BLOCK = 256, REC_LCAP = 2048;
 int rec_sort_lcap() { return REC_LCAP; }
-void launch_rec_sort(const Rec* recs, const uint64_t* rec_off, const uint32_t* order, uint32_t* gscratch,
+void launch_rec_sort(const Rec* recs, const uint64_t* rec_off, const uint32_t* order, uint64_t* gscratch,
                      uint32_t n_reads, Rec* out, hipStream_t st) {
   if (!n_reads) return;
   hipLaunchKernelGGL((k_rec_sort<REC_BLOCK, REC_LCAP>), dim3(n_reads), dim3(REC_BLOCK), 0, st, recs, rec_off, order,

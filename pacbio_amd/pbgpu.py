@@ -25,6 +25,7 @@ STATUS = {0: "OK", 1: "INVALID", 2: "IO", 3: "NOMEM", 4: "DEVICE", 5: "UNSUPPORT
 # every symbol include/pbgpu.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "pbgpu_abi_version", "pbgpu_last_error", "pbgpu_device_count", "pbgpu_device_synchronize",
+    "pbgpu_measure_gather",
     "pbgpu_index_build_fasta", "pbgpu_index_build", "pbgpu_index_free", "pbgpu_index_get_info",
     "pbgpu_index_sr_name", "pbgpu_index_sr_len",
     "pbgpu_align_params_default", "pbgpu_aligner_create", "pbgpu_aligner_free",
@@ -82,7 +83,8 @@ class Stats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("n_batches", "n_reads", "n_bases", "n_kmers", "n_probes", "n_kept",
                                           "n_hits", "n_chains", "n_lis_tests", "n_records")] + \
                [(n, C.c_double) for n in ("ms_seed", "ms_group", "ms_lis", "ms_fit", "ms_records")] + \
-               [("kernel_ms", C.c_double * 8), ("kernel_launches", C.c_uint64 * 8)]
+               [("kernel_ms", C.c_double * 8), ("kernel_launches", C.c_uint64 * 8)] + \
+               [(n, C.c_uint64) for n in ("g0_kept", "g0_hits", "g0_chains")]
 
     def as_dict(self):
         d = {n: getattr(self, n) for n, _ in self._fields_ if not n.startswith("kernel_")}
@@ -109,6 +111,7 @@ def lib():
         L.pbgpu_last_error.restype = C.c_char_p
         L.pbgpu_device_count.restype = C.c_int
         L.pbgpu_device_synchronize.argtypes = [C.c_int]
+        L.pbgpu_measure_gather.argtypes = [C.c_int, C.c_uint64, C.POINTER(C.c_double)]
         L.pbgpu_index_build_fasta.argtypes = [C.POINTER(C.c_char_p), C.c_size_t, C.POINTER(IndexParams), C.POINTER(vp)]
         L.pbgpu_index_build.argtypes = [C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.POINTER(C.c_uint64),
                                         C.c_size_t, C.POINTER(IndexParams), C.POINTER(vp)]
@@ -147,6 +150,13 @@ def _check(st):
 
 def device_synchronize(device=0):
     _check(lib().pbgpu_device_synchronize(device))
+
+
+def measure_gather(device=0, buffer_bytes=64 << 30):
+    """GB/s of uniformly random 64-B sector loads over a buffer of buffer_bytes (B_rand)."""
+    g = C.c_double()
+    _check(lib().pbgpu_measure_gather(device, buffer_bytes, C.byref(g)))
+    return g.value
 
 
 def _cstrs(items):

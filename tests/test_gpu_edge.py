@@ -108,6 +108,9 @@ def test_dense_group_overflow(dense, cfg):
     got, st = _gpu(names, seqs, pnames, pseqs, **cfg)
     if not cfg:
         assert st["n_chains"] > 3 * 8192, "reads must touch more super-reads than the largest LDS table"
+        from tests._compare import split_reads
+        # k_rec_sort stages keys in LDS up to 2048 records per read, in HBM above
+        assert max(len(v) for v in split_reads(got)[1].values()) > 2048
     assert_same_coords(got, exp, f"dense {cfg}")
 
 

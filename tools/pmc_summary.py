@@ -22,6 +22,11 @@ def short(name):
     return base + tmpl
 
 
+def fname(k):
+    """file-name form of a (template) kernel name: k_group<false, 256u> -> k_group_false_256u"""
+    return re.sub(r"[^A-Za-z0-9]+", "_", k).strip("_")
+
+
 def load_trace(d):
     p = os.path.join(d, "kt", "run_kernel_trace.csv")
     out = collections.defaultdict(list)
@@ -71,7 +76,7 @@ def main():
             print(f"    {cn:28s} {c[cn]:.4g}")
         if a.json_out and hbm is not None:
             os.makedirs(a.json_out, exist_ok=True)
-            with open(os.path.join(a.json_out, f"pmc_{k.split('<')[0]}.json"), "w") as f:
+            with open(os.path.join(a.json_out, f"pmc_{fname(k)}.json"), "w") as f:
                 json.dump({"kernel": k, "launches": len(ds), "mean_ms": mean, "hbm_bytes_per_launch": hbm,
                            "hbm_formula": "2*FETCH_SIZE + WRITE_SIZE (KiB -> B), MI355X_MICROARCH.md HBM [CDNA4]",
                            "counters_per_launch": c}, f, indent=1)
