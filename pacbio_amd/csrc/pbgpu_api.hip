@@ -36,7 +36,7 @@ void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const ui
                   const uint64_t* hit_off, uint64_t node_base, uint32_t r0, const uint32_t* read_list, uint32_t n_list,
                   uint32_t hcap_log2, uint32_t* gtable, GroupOut O, unsigned long long* stats, hipStream_t st);
 uint64_t group_table_words(uint32_t hcap_log2);
-constexpr uint32_t kGroupLdsMaxLog2 = 13;  // 8192-slot table, 112 KiB of LDS
+constexpr uint32_t kGroupLdsMaxLog2 = 13;  // 8192-slot table, 96 KiB of LDS
 void launch_init_slen(const ChainDesc* chains, uint32_t n_chains, uint32_t* slen, hipStream_t st);
 void launch_strand_order(const uint32_t* slen, uint32_t n_items, uint32_t* hist, uint32_t* cursor, uint32_t* perm,
                          int phase, hipStream_t st);
@@ -51,10 +51,12 @@ void launch_discard(const ChainDesc* chains, const uint32_t* list, uint32_t n, c
                     int2* X, const void* N16, const void* N32, uint32_t* items_small, uint32_t* n_small,
                     uint32_t* items_big, uint32_t* n_big, hipStream_t st);
 void launch_lis_wave(bool large, const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen,
-                     const int2* X, void* N16, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx,
+                     int2* X, void* N16, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx,
                      unsigned long long* stats, hipStream_t st);
 uint32_t lis_class_bounds(int which);
 uint32_t len_buckets();
+void launch_strand_order(const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen, int2* X,
+                         hipStream_t st);
 uint32_t big_bucket();
 void launch_rec_hist(const Rec* recs, uint32_t n, uint32_t* per_read, hipStream_t st);
 void launch_rec_scatter(const Rec* recs, uint32_t n, const uint64_t* rec_off, uint32_t* cursor, uint32_t* order,
@@ -839,6 +841,8 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
       const uint32_t n_strands = order(0, 2 * nch);
       const uint32_t nbig = n_big;
       if (nbig) al->nodes32.ensure((Hs + 1) * 16);
+      // strands longer than k_lis_w's LDS capacity: restore list order in place first
+      launch_strand_order(al->chains.p, al->perm.p, n_mid, al->slen.p, al->X.p, st);
       HIPCHK(hipEventRecord(al->ev[11], st));
       launch_lis(true, al->chains.p, al->perm.p, nbig, al->slen.p, al->X.p, al->nodes32.p, al->pts.p, al->lisl.p, al->lp,
                  al->P.max_match, al->stats.p, st);

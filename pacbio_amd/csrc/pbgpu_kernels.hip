@@ -398,20 +398,17 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
   __shared__ uint32_t s_flag, s_used, s_cbase;
   if (blockIdx.x >= n_list) return;
   const uint32_t tid = threadIdx.x;
-  const int lane = lane_id();
   const uint32_t wave = tid >> 6;
   const uint32_t r = read_list ? read_list[blockIdx.x] : r0 + blockIdx.x;
   const uint32_t hcap = 1u << hcap_log2;
-  // table: key (sr + 1, 0 = empty), fwd count/cursor, bwd count/cursor, 2*hcap byte tags
-  uint32_t* tkey = GLOBAL_TABLE ? gtable + (uint64_t)blockIdx.x * (7u * hcap / 2) : s_dyn;
+  // table: key (sr + 1, 0 = empty), fwd count/cursor, bwd count/cursor
+  uint32_t* tkey = GLOBAL_TABLE ? gtable + (uint64_t)blockIdx.x * (3u * hcap) : s_dyn;
   uint32_t* tcf = tkey + hcap;
   uint32_t* tcb = tcf + hcap;
-  uint8_t* tag = (uint8_t*)(tcb + hcap);
   const uint64_t kbase = roff[r];
   const uint32_t nk = n_kept[r], thr = thr_in[r];
   const uint64_t hbase = hit_off[r] - node_base;
   const uint32_t used_limit = hcap - hcap / 4;
-  const uint64_t lt_mask = (1ull << lane) - 1ull;
   // Reads touching many super-reads are grouped in P passes over hash partitions
   // of the super-read ids; each partition's lists are placed after the previous
   // ones, so every list is still contiguous and in reference order.
@@ -421,16 +418,16 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
   auto part_of = [&](uint32_t sr) -> uint32_t {
     return P == 1 ? 0u : (uint32_t)(((uint64_t)(sr * 0x85EBCA77u) * P) >> 32);
   };
+#ifdef PBGPU_PROF
+  uint64_t pr_setup[2] = {0, 0}, pr_steps[2] = {0, 0}, pr_compact = 0;
+  const uint64_t pr_t0 = __builtin_amdgcn_s_memtime();
+#endif
   for (uint32_t part = part0; part < P; ++part) {
   uint32_t part_hits = 0;
   for (uint32_t i = tid; i < hcap; i += B) { tkey[i] = 0; tcf[i] = 0; tcb[i] = 0; }
   if (tid == 0) { s_flag = 0; s_used = 0; }
   if (GLOBAL_TABLE) __threadfence_block();
   __syncthreads();
-#ifdef PBGPU_PROF
-  uint64_t pr_setup[2] = {0, 0}, pr_steps[2] = {0, 0}, pr_compact = 0;
-  const uint64_t pr_t0 = __builtin_amdgcn_s_memtime();
-#endif
 
   for (int pass = 0; pass < 2; ++pass) {
     for (uint32_t g0 = 0; g0 < nk; g0 += B) {
@@ -483,7 +480,7 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
       for (uint32_t h0 = 0; h0 < total; h0 += B) {
         const uint32_t h = h0 + tid;
         const bool valid = h < total;
-        uint32_t sr = 0, slot = 0, rec = 0xFFFFFFFFu;
+        uint32_t sr = 0, slot = 0, rec = 0xFFFFFFFFu;  // rec: the hit's k-mer record (unused after locate)
         int32_t so = 0, pb = 0;
         bool fwd = true;
         const uint64_t e = e_nx;
@@ -509,52 +506,23 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
             if (ok) atomicAdd(fwd ? &tcf[slot] : &tcb[slot], 1u);
           }
         } else {
-          if (mine) while (tkey[slot] != sr + 1) slot = (slot + 1) & (hcap - 1);
-          // Order-preserving multisplit over (slot, strand) keys.  The four waves hold
-          // consecutive 64-hit runs; they take the list cursors in wave order (LDS only,
-          // after all loads are in flight).  Within a wave, hits of one k-mer record hit
-          // distinct super-reads (except SRs holding the k-mer twice), so the run is
-          // processed record segment by record segment (usually 1-2), each segment in
-          // one conflict-free step; a tag check catches in-record repeats.
-          const uint32_t key = (slot << 1) | (fwd ? 0u : 1u);
+          // Scatter: each hit takes the next slot of its (super-read, strand) list.  All
+          // hits of one list inside this 256-hit step land in one contiguous run of
+          // slots, in arbitrary order within the run; steps are ordered by the
+          // barriers.  The consumers restore the reference order (pb offset ascending,
+          // then occurrence order = |sr offset| descending) with a transposition pass
+          // that is bounded by the run lengths (k_lis_w, k_strand_order).
+          // The waves take their slots in wave order (one barrier each), so a run is
+          // out of order only where the LDS unit does not serve one wave's same-address
+          // atomics in lane order: usually no consumer work at all.
+          uint32_t* cur = nullptr;
+          if (mine) {
+            while (tkey[slot] != sr + 1) slot = (slot + 1) & (hcap - 1);
+            cur = fwd ? &tcf[slot] : &tcb[slot];
+          }
           uint32_t pos = 0;
           for (uint32_t w = 0; w < B / 64; ++w) {
-            if (wave == w) {
-              uint64_t active = __ballot(mine);
-              while (active) {
-                const int leader = __ffsll((unsigned long long)active) - 1;
-                const uint32_t lrec = __builtin_amdgcn_readlane(rec, leader);
-                const bool in_seg = mine && rec == lrec;
-                const uint64_t seg = __ballot(in_seg);
-                if (in_seg) tag[key] = (uint8_t)lane;
-                if (GLOBAL_TABLE) { __threadfence_block(); __builtin_amdgcn_s_waitcnt(0); }
-                else __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the tag writes landed
-                __builtin_amdgcn_wave_barrier();
-                const bool dup = in_seg && tag[key] != (uint8_t)lane;
-                if (!__ballot(dup)) {
-                  if (in_seg) { uint32_t* cur = fwd ? &tcf[slot] : &tcb[slot]; pos = *cur; *cur = pos + 1; }
-                } else {
-                  const uint32_t k2 = in_seg ? key : 0xFFFFFFFFu;
-                  uint64_t act2 = seg;
-                  while (act2) {
-                    const int l2 = __ffsll((unsigned long long)act2) - 1;
-                    const uint32_t lk = __builtin_amdgcn_readlane(k2, l2);
-                    const uint64_t peers = __ballot(k2 == lk);
-                    uint32_t* cur = (lk & 1) ? &tcb[lk >> 1] : &tcf[lk >> 1];
-                    if (k2 == lk) {
-                      const uint32_t b = *cur;
-                      pos = b + (uint32_t)__popcll(peers & lt_mask);
-                      if (lane == l2) *cur = b + (uint32_t)__popcll(peers);
-                    }
-                    act2 &= ~peers;
-                  }
-                }
-                if (GLOBAL_TABLE) { __threadfence_block(); __builtin_amdgcn_s_waitcnt(0); }
-                else __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the tag writes landed
-                __builtin_amdgcn_wave_barrier();
-                active &= ~seg;
-              }
-            }
+            if (wave == w && mine) pos = atomicAdd(cur, 1u);
             __syncthreads();
           }
           if (mine) O.X[hbase + pos] = make_int2(pb, fwd ? so : -so);
@@ -1040,10 +1008,48 @@ __global__ __launch_bounds__(64) void k_lis(const ChainDesc* __restrict__ chains
 // HBM traffic: X once (coalesced, prefetched for the next strand while the
 // current one is processed), the lis points (and, for --max-match, the lis
 // indices) once.
+// List order of a strand (coarse_aligner.cc:128-140): pb offset
+// ascending, then occurrence order, which within one super-read and strand is
+// |sr offset| descending.  (pb, |so|) pairs are unique within a list.
+DEV bool hit_after(int2 a, int2 b) {
+  return a.x != b.x ? a.x > b.x : abs(a.y) < abs(b.y);
+}
+
+// Restores list order for strands too long for k_lis_w's LDS (one block per
+// strand, in place): odd-even transposition rounds until one swaps nothing.
+// k_group leaves only short unordered runs, so a few rounds suffice.
+__global__ __launch_bounds__(256) void k_strand_order(const ChainDesc* __restrict__ chains,
+                                                      const uint32_t* __restrict__ items, uint32_t n_items,
+                                                      const uint32_t* __restrict__ slen, int2* X) {
+  __shared__ uint32_t s_sw[2];
+  for (uint32_t w = blockIdx.x; w < n_items; w += gridDim.x) {
+    const uint32_t item = items[w];
+    const ChainDesc d = chains[item >> 1];
+    int2* x = X + d.hit_base + ((item & 1) ? d.nf : 0);
+    const uint32_t n = slen[item];
+    for (uint32_t round = 0;; ++round) {
+      if (threadIdx.x == 0) s_sw[round & 1] = 0;  // the other flag is still being read
+      bool sw = false;
+      for (uint32_t par = 0; par < 2; ++par) {
+        for (uint32_t j = 2 * threadIdx.x + par; j + 1 < n; j += 512) {
+          const int2 a = x[j], b = x[j + 1];
+          if (hit_after(a, b)) { x[j] = b; x[j + 1] = a; sw = true; }
+        }
+        __threadfence_block();
+        __syncthreads();
+      }
+      if (sw) s_sw[round & 1] = 1;
+      __syncthreads();
+      if (!s_sw[round & 1]) break;
+    }
+    __syncthreads();
+  }
+}
+
 template <int SMAX, int WPB>
 __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict__ chains,
                                                     const uint32_t* __restrict__ items, uint32_t n_items,
-                                                    const uint32_t* __restrict__ slen, const int2* __restrict__ X,
+                                                    const uint32_t* __restrict__ slen, int2* X,
                                                     LNode<uint16_t>* __restrict__ N16, int2* __restrict__ pts,
                                                     uint32_t* __restrict__ lisl, LisParams lp, int keep_idx,
                                                     unsigned long long* stats) {
@@ -1095,6 +1101,27 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
       }
     }
     lds_fence();
+    // ---- list order: k_group leaves each 256-hit step's run of a list unordered.
+    // Odd-even transposition in LDS until a round swaps nothing (an ordered strand
+    // costs one compare per element); written back to X when anything moved, for
+    // k_discard and the --max-match redo rounds.
+    {
+      bool moved = false;
+      for (;;) {
+        bool sw = false;
+        for (uint32_t par = 0; par < 2; ++par) {
+          for (uint32_t j = 2 * lane + par; j + 1 < n; j += 128) {
+            const int2 a = sx[j], b = sx[j + 1];
+            if (hit_after(a, b)) { sx[j] = b; sx[j + 1] = a; sw = true; }
+          }
+          lds_fence();
+        }
+        if (!__ballot(sw)) break;
+        moved = true;
+      }
+      if (moved)
+        for (uint32_t j = lane; j < n; j += 64) X[base + j] = sx[j];
+    }
     // ---- forward pass (compute_L_P)
     uint32_t head = NONE, longest = 0, longest_ind = 0;
     uint32_t cur = 0;
@@ -1615,7 +1642,7 @@ void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const ui
                   uint32_t hcap_log2, uint32_t* gtable, GroupOut O, unsigned long long* stats, hipStream_t st) {
   if (!n_list) return;
   if (!gtable) {  // LDS table: hcap_log2 <= 13; the 8192-slot table gets a 16-wave block
-    const size_t lds = ((size_t)7 << hcap_log2) / 2 * sizeof(uint32_t);
+    const size_t lds = ((size_t)3 << hcap_log2) * sizeof(uint32_t);
     static bool attr = false;
     if (!attr) {
       (void)hipFuncSetAttribute((const void*)k_group<false, GROUP_BLOCK>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1635,7 +1662,7 @@ void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const ui
                        n_kept, thr, hit_off, node_base, r0, read_list, n_list, hcap_log2, gtable, O, stats);
   }
 }
-uint64_t group_table_words(uint32_t hcap_log2) { return ((uint64_t)7 << hcap_log2) / 2; }
+uint64_t group_table_words(uint32_t hcap_log2) { return (uint64_t)3 << hcap_log2; }
 
 static uint32_t grid_for(uint32_t n, uint32_t block, uint32_t cap = 65536) {
   uint64_t g = ((uint64_t)n + block - 1) / block;
@@ -1686,7 +1713,7 @@ static uint32_t resident_blocks(const void* fn, int block) {
   return (uint32_t)(per * cus);
 }
 void launch_lis_wave(bool large, const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen,
-                     const int2* X, void* N16, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx,
+                     int2* X, void* N16, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx,
                      unsigned long long* stats, hipStream_t st) {
   if (!n_items) return;
   if (large) {
@@ -1718,6 +1745,12 @@ void launch_discard(const ChainDesc* chains, const uint32_t* list, uint32_t n, c
                      (const LNode<uint16_t>*)N16, (const LNode<uint32_t>*)N32, items_small, n_small, items_big, n_big);
 }
 uint32_t len_buckets() { return NLB; }
+void launch_strand_order(const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen, int2* X,
+                         hipStream_t st) {
+  if (!n_items) return;
+  hipLaunchKernelGGL(k_strand_order, dim3(std::min<uint32_t>(n_items, 2048)), dim3(256), 0, st, chains, items, n_items,
+                     slen, X);
+}
 #ifdef PBGPU_PROF
 extern "C" int pbgpu_debug_prof(unsigned long long* out, int n, int reset) {
   if (n > 32) n = 32;

@@ -132,3 +132,25 @@ def test_k31(small):
     got, _ = _gpu(names, seqs, pnames, pseqs, k=31)
     assert exp.count("\n") > 5
     assert_same_coords(got, exp, "k31")
+
+
+@pytest.fixture(scope="module")
+def long_strands():
+    # 44 kb mean (up to 100 kb) super-reads, 90 kb low-error reads: strands of 4k-76k hits
+    # exercise k_strand_order, the lane-per-strand k_lis and its 32-bit nodes (> 65535 hits)
+    from tools.synth import Dataset
+    return Dataset("small", seed=21, genome_len=400_000, n_sr=300, unitig_mean=4000, unitig_min=1000,
+                   sr_max_unitigs=24, n_pb=6, pb_len_mean=90_000, pb_len_sigma=0.0, err_ins=0.003, err_del=0.003,
+                   err_sub=0.002, n_run_rate=0.0)
+
+
+@pytest.mark.parametrize("cfg", [dict(), dict(forward=True, max_match=True)], ids=["default", "fwd_maxmatch"])
+def test_long_strands(long_strands, cfg):
+    ds = long_strands
+    names, seqs = ds.sr_names(), ds.sr_seqs()
+    pnames, pseqs = ds.pb_names(), ds.pb_seqs()
+    exp = _oracle(names, seqs, pnames, pseqs, **cfg)
+    nb = [int(line.split()[4]) for line in exp.splitlines() if not line.startswith(">")]
+    assert max(nb) > 65535 and sum(1 for x in nb if 4095 < x <= 65535) > 10
+    got, _ = _gpu(names, seqs, pnames, pseqs, **cfg)
+    assert_same_coords(got, exp, f"long strands {cfg}")
