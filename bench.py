@@ -68,7 +68,7 @@ class Comm:
 
 
 # the rocprofv3 kernel each timed slot corresponds to (tools/pmc_summary.py file names)
-ROCPROF_FILE = {"k_seed": "k_seed_256_8", "k_group": "k_group_false_256u", "k_lis": "k_lis_w_511_4",
+ROCPROF_FILE = {"k_seed": "k_seed_256_8", "k_group": "k_group_false_256u", "k_lis": "k_lis_w_255_8",
                 "k_coords": "k_coords_8", "k_rec_sort": "k_rec_sort_256_2048"}
 
 
@@ -85,8 +85,10 @@ def _kernel_bytes(st):
         # (16 B) read, every occurrence (8 B) read once, every hit (8 B) written, chain
         # descriptors (24 B) written -- counted by the kernel for the reads it completed
         "k_group": per(st["g0_kept"] * 32 + st["g0_hits"] * 16 + st["g0_chains"] * 24, "k_group"),
-        # every hit read (8 B), a node written per hit (8 B), lis points written (<= 8 B/hit)
-        "k_lis": per(st["n_hits"] * 24 + st["n_chains"] * 24, "k_lis"),
+        # tier-0 k_lis_w (strands <= 255 hits), counted by the kernel: every hit read (8 B)
+        # and its lis point written (<= 8 B); per strand its item, chain descriptor (24 B),
+        # length and lis length (12 B)
+        "k_lis": per(st["l0_hits"] * 16 + st["l0_strands"] * 36, "k_lis"),
         # chain descriptors + lis lengths read, lis points read, records written
         "k_coords": per(st["n_chains"] * 32 + st["n_records"] * 96, "k_coords"),
         # records read + written

@@ -173,8 +173,9 @@ pbgpu_status pbgpu_download(pbgpu_aligner* al, pbgpu_coords_batch** out);
 
 /* Per-stage device time (HIP events on the aligner's stream, summed over
  * calls since the last reset), per-kernel time (events immediately around a
- * single launch of the named kernel: the first-tier k_group launch, k_lis,
- * k_coords, k_seed, k_rec_sort) and algorithmic counters. */
+ * single launch of the named kernel: the first-tier k_group launch, the
+ * tier-0 k_lis_w launch, k_coords, k_seed, k_rec_sort) and algorithmic
+ * counters. */
 enum {
   PBGPU_KERNEL_SEED = 0,
   PBGPU_KERNEL_GROUP = 1,
@@ -199,6 +200,9 @@ typedef struct {
   /* work completed inside the timed first-tier k_group launches (kept k-mers
    * of the reads they finished, hits scattered, chains emitted) */
   uint64_t g0_kept, g0_hits, g0_chains;
+  /* work of the timed k_lis slot (the tier-0 wave-per-strand launches, strands
+   * of <= 255 hits): hits and strands */
+  uint64_t l0_hits, l0_strands;
 } pbgpu_stats;
 pbgpu_status pbgpu_aligner_get_stats(const pbgpu_aligner* al, pbgpu_stats* s);
 pbgpu_status pbgpu_aligner_reset_stats(pbgpu_aligner* al);

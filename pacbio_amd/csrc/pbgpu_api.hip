@@ -50,7 +50,7 @@ void launch_coords(IndexView ix, AlignParamsDev P, const ChainDesc* chains, cons
 void launch_discard(const ChainDesc* chains, const uint32_t* list, uint32_t n, const uint32_t* lisl, uint32_t* slen,
                     int2* X, const void* N16, const void* N32, uint32_t* items_small, uint32_t* n_small,
                     uint32_t* items_big, uint32_t* n_big, hipStream_t st);
-void launch_lis_wave(bool large, const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen,
+void launch_lis_wave(int tier, const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen,
                      int2* X, void* N16, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx,
                      unsigned long long* stats, hipStream_t st);
 uint32_t lis_class_bounds(int which);
@@ -814,7 +814,7 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
       al->perm.ensure(2ull * nch + 1);
       al->lisl.ensure(2ull * nch + 1);
       al->slen.ensure(2ull * nch + 1);
-      uint32_t n_big = 0, n_mid = 0, n_w2 = 0;  // items in classes above LIS_U16_MAX / LISW_LARGE / LISW_SMALL
+      uint32_t n_big = 0, n_mid = 0, n_w2 = 0, n_w1 = 0;  // items in classes above LIS_U16_MAX / LISW_LARGE / LISW_SMALL / LISW_TINY
       auto order = [&](int which, uint32_t n_in) -> uint32_t {  // returns the number of items placed
         HIPCHK(hipMemsetAsync(al->hist.p, 0, NB * 4, st));
         if (which == 0) launch_strand_order(al->slen.p, n_in, al->hist.p, nullptr, nullptr, 0, st);
@@ -822,12 +822,18 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
         std::vector<uint32_t> h(NB), cur(NB);
         HIPCHK(hipMemcpyAsync(h.data(), al->hist.p, NB * 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
+        if (getenv("PBGPU_DUMP_LEN_HIST")) {  // diagnostics: length-class histogram of this ordering pass
+          fprintf(stderr, "len_hist %s:", which == 0 ? "strands" : "chains");
+          for (uint32_t b = 0; b < NB; ++b) if (h[b]) fprintf(stderr, " %u:%u", b, h[b]);
+          fprintf(stderr, "\n");
+        }
         uint32_t acc = 0;
         for (int b = (int)NB - 1; b >= 1; --b) {  // longest first; bucket 0 = empty
           cur[b] = acc; acc += h[b];
           if ((uint32_t)b == big_bucket()) n_big = acc;  // items in buckets >= big_bucket(): > LIS_U16_MAX hits
           if ((uint32_t)b == lis_class_bounds(1)) n_mid = acc;
           if ((uint32_t)b == lis_class_bounds(0)) n_w2 = acc;
+          if ((uint32_t)b == lis_class_bounds(3)) n_w1 = acc;
         }
         cur[0] = acc;
         HIPCHK(hipMemcpyAsync(al->hist.p + NB, cur.data(), NB * 4, hipMemcpyHostToDevice, st));
@@ -847,12 +853,15 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
       launch_lis(true, al->chains.p, al->perm.p, nbig, al->slen.p, al->X.p, al->nodes32.p, al->pts.p, al->lisl.p, al->lp,
                  al->P.max_match, al->stats.p, st);
       // 4095 < n <= 65535: lane-per-strand chunked kernel; n <= 4095: wave-per-strand kernels
-      const uint32_t nmid = n_mid, nw2 = n_w2;
+      const uint32_t nmid = n_mid, nw2 = n_w2, nw1 = n_w1;
       launch_lis(false, al->chains.p, al->perm.p + nbig, nmid - nbig, al->slen.p, al->X.p, al->nodes.p, al->pts.p,
                  al->lisl.p, al->lp, al->P.max_match, al->stats.p, st);
-      launch_lis_wave(true, al->chains.p, al->perm.p + nmid, nw2 - nmid, al->slen.p, al->X.p, al->nodes.p, al->pts.p,
+      launch_lis_wave(2, al->chains.p, al->perm.p + nmid, nw2 - nmid, al->slen.p, al->X.p, al->nodes.p, al->pts.p,
                       al->lisl.p, al->lp, al->P.max_match, al->stats.p, st);
-      launch_lis_wave(false, al->chains.p, al->perm.p + nw2, n_strands - nw2, al->slen.p, al->X.p, al->nodes.p,
+      launch_lis_wave(1, al->chains.p, al->perm.p + nw2, nw1 - nw2, al->slen.p, al->X.p, al->nodes.p,
+                      al->pts.p, al->lisl.p, al->lp, al->P.max_match, al->stats.p, st);
+      HIPCHK(hipEventRecord(al->ev[10], st));  // the timed k_lis slot: tier-0 k_lis_w alone
+      launch_lis_wave(0, al->chains.p, al->perm.p + nw1, n_strands - nw1, al->slen.p, al->X.p, al->nodes.p,
                       al->pts.p, al->lisl.p, al->lp, al->P.max_match, al->stats.p, st);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(al->ev[12], st));
@@ -927,7 +936,7 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
       ms_lis += ev_ms(al->ev[6], al->ev[12]);
       ms_fit += ev_ms(al->ev[12], al->ev[7]);
       k_ms[PBGPU_KERNEL_GROUP] += ev_ms(al->ev[8], al->ev[9]);
-      k_ms[PBGPU_KERNEL_LIS] += ev_ms(al->ev[11], al->ev[12]);
+      k_ms[PBGPU_KERNEL_LIS] += ev_ms(al->ev[10], al->ev[12]);
       k_ms[PBGPU_KERNEL_COORDS] += ev_ms(al->ev[13], al->ev[14]);
       k_n[PBGPU_KERNEL_GROUP]++; k_n[PBGPU_KERNEL_LIS]++; k_n[PBGPU_KERNEL_COORDS]++;
       if (ovf == 0 && nrec <= al->recs.n) {
@@ -978,6 +987,7 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
   al->acc.n_hits += sv[ST_HITS]; al->acc.n_chains += n_chains; al->acc.n_lis_tests += n_tests;
   al->acc.n_records += nrec;
   al->acc.g0_kept += sv[ST_G0_KEPT]; al->acc.g0_hits += sv[ST_G0_HITS]; al->acc.g0_chains += sv[ST_G0_CHAINS];
+  al->acc.l0_hits += sv[ST_L0_HITS]; al->acc.l0_strands += sv[ST_L0_STRANDS];
   al->acc.ms_seed += ev_ms(al->ev[0], al->ev[1]);
   al->acc.ms_group += ms_group;
   al->acc.ms_lis += ms_lis;

@@ -90,6 +90,7 @@ enum StatSlot {
   ST_KMERS = 0, ST_PROBES, ST_KEPT, ST_HITS, ST_CHAINS, ST_LIS_TESTS, ST_RECORDS,
   ST_REC_OVERFLOW, ST_INFO_USED, ST_GROUP_OVERFLOW,
   ST_G0_KEPT, ST_G0_HITS, ST_G0_CHAINS,  // work completed by first-tier (4-wave LDS) k_group launches
+  ST_L0_HITS, ST_L0_STRANDS,             // work of the tier-0 (n <= 255) k_lis_w launches
   ST_N
 };
 

@@ -1046,6 +1046,7 @@ __global__ __launch_bounds__(256) void k_strand_order(const ChainDesc* __restric
   }
 }
 
+constexpr int LISW_TINY_N = 255;  // SMAX of the timed tier-0 k_lis_w
 template <int SMAX, int WPB>
 __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict__ chains,
                                                     const uint32_t* __restrict__ items, uint32_t n_items,
@@ -1063,7 +1064,7 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
   uint16_t *snxt = s_nxt[wv], *sln = s_len[wv], *sP = s_P[wv], *sroot = s_root[wv], *srs = s_rs[wv];
   const uint32_t nwaves = gridDim.x * WPB;
   const bool fast = lp.W == 1 && !lp.mer_all;
-  uint64_t tests = 0;
+  uint64_t tests = 0, my_hits = 0, my_strands = 0;
   auto strand = [&](uint32_t w, uint64_t& base, uint32_t& n, uint32_t& item) {
     item = items[w];
     const ChainDesc d = chains[item >> 1];
@@ -1086,6 +1087,7 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
   for (; w < n_items; w += nwaves) {
     const uint64_t base = nbase;
     const uint32_t n = nn, item = nitem;
+    my_hits += n; ++my_strands;
     if constexpr (PREFETCH) {
 #pragma unroll
       for (int q = 0; q < PF; ++q) { const uint32_t j = q * 64 + lane; if (j < n) sx[j] = pf[q]; }
@@ -1229,6 +1231,10 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
   tests = lane == 0 ? tests : 0;
   tests = wave_sum_u64(tests);
   if (lane == 0 && tests) atomicAdd(&stats[ST_LIS_TESTS], (unsigned long long)tests);
+  if (SMAX == LISW_TINY_N && lane == 0 && my_strands) {  // per-launch work of the timed tier (bench roofline)
+    atomicAdd(&stats[ST_L0_HITS], (unsigned long long)my_hits);
+    atomicAdd(&stats[ST_L0_STRANDS], (unsigned long long)my_strands);
+  }
 }
 
 // compute_kmers_info (pb_aligner.cc:84-143) along one lis, one point at a
@@ -1699,7 +1705,7 @@ void launch_lis(bool big_nodes, const ChainDesc* chains, const uint32_t* items, 
     hipLaunchKernelGGL((k_lis<uint16_t, LIS_CH16>), grid, dim3(64), 0, st, chains, items, n_items, slen, X,
                        (LNode<uint16_t>*)N, pts, lisl, lp, keep_idx, stats);
 }
-constexpr uint32_t LISW_SMALL = 511, LISW_LARGE = 4095;
+constexpr uint32_t LISW_TINY = LISW_TINY_N, LISW_SMALL = 511, LISW_LARGE = 4095;
 static uint32_t resident_blocks(const void* fn, int block) {
   static int cus = 0;
   if (!cus) {
@@ -1712,25 +1718,28 @@ static uint32_t resident_blocks(const void* fn, int block) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, block, 0) != hipSuccess || per < 1) per = 1;
   return (uint32_t)(per * cus);
 }
-void launch_lis_wave(bool large, const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen,
+template <int SMAX, int WPB>
+static void launch_lis_w(const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen,
+                         int2* X, void* N16, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx,
+                         unsigned long long* stats, hipStream_t st) {
+  const void* fn = (const void*)k_lis_w<SMAX, WPB>;
+  const uint32_t g = std::min<uint32_t>(resident_blocks(fn, 64 * WPB), (n_items + WPB - 1) / WPB);
+  hipLaunchKernelGGL((k_lis_w<SMAX, WPB>), dim3(g), dim3(64 * WPB), 0, st, chains, items, n_items, slen, X,
+                     (LNode<uint16_t>*)N16, pts, lisl, lp, keep_idx, stats);
+}
+// tier 0: n <= 255 (8 waves per block), 1: n <= 511 (4 waves), 2: n <= 4095 (1 wave)
+void launch_lis_wave(int tier, const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen,
                      int2* X, void* N16, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx,
                      unsigned long long* stats, hipStream_t st) {
   if (!n_items) return;
-  if (large) {
-    const void* fn = (const void*)k_lis_w<LISW_LARGE, 1>;
-    const uint32_t g = std::min<uint32_t>(resident_blocks(fn, 64), n_items);
-    hipLaunchKernelGGL((k_lis_w<LISW_LARGE, 1>), dim3(g), dim3(64), 0, st, chains, items, n_items, slen, X,
-                       (LNode<uint16_t>*)N16, pts, lisl, lp, keep_idx, stats);
-  } else {
-    const void* fn = (const void*)k_lis_w<LISW_SMALL, 4>;
-    const uint32_t g = std::min<uint32_t>(resident_blocks(fn, 256), (n_items + 3) / 4);
-    hipLaunchKernelGGL((k_lis_w<LISW_SMALL, 4>), dim3(g), dim3(256), 0, st, chains, items, n_items, slen, X,
-                       (LNode<uint16_t>*)N16, pts, lisl, lp, keep_idx, stats);
-  }
+  if (tier == 2) launch_lis_w<LISW_LARGE, 1>(chains, items, n_items, slen, X, N16, pts, lisl, lp, keep_idx, stats, st);
+  else if (tier == 1) launch_lis_w<LISW_SMALL, 4>(chains, items, n_items, slen, X, N16, pts, lisl, lp, keep_idx, stats, st);
+  else launch_lis_w<LISW_TINY, 8>(chains, items, n_items, slen, X, N16, pts, lisl, lp, keep_idx, stats, st);
 }
 // length classes (len_bucket) at the kernel boundaries
-uint32_t lis_class_bounds(int which) {  // first class of: 0 = > LISW_SMALL, 1 = > LISW_LARGE, 2 = > LIS_U16_MAX
-  return which == 0 ? 128u + 16u * (9u - 7u) : which == 1 ? 128u + 16u * (12u - 7u) : 128u + 16u * (16u - 7u);
+uint32_t lis_class_bounds(int which) {  // first class of: 0 = > LISW_SMALL, 1 = > LISW_LARGE, 2 = > LIS_U16_MAX, 3 = > LISW_TINY
+  return which == 0 ? 128u + 16u * (9u - 7u) : which == 1 ? 128u + 16u * (12u - 7u)
+       : which == 2 ? 128u + 16u * (16u - 7u) : 128u + 16u * (8u - 7u);
 }
 void launch_coords(IndexView ix, AlignParamsDev P, const ChainDesc* chains, const uint32_t* list, uint32_t n,
                    const uint64_t* roff, uint32_t emit, ChainOut O, hipStream_t st) {

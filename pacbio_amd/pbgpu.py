@@ -84,7 +84,7 @@ class Stats(C.Structure):
                                           "n_hits", "n_chains", "n_lis_tests", "n_records")] + \
                [(n, C.c_double) for n in ("ms_seed", "ms_group", "ms_lis", "ms_fit", "ms_records")] + \
                [("kernel_ms", C.c_double * 8), ("kernel_launches", C.c_uint64 * 8)] + \
-               [(n, C.c_uint64) for n in ("g0_kept", "g0_hits", "g0_chains")]
+               [(n, C.c_uint64) for n in ("g0_kept", "g0_hits", "g0_chains", "l0_hits", "l0_strands")]
 
     def as_dict(self):
         d = {n: getattr(self, n) for n, _ in self._fields_ if not n.startswith("kernel_")}
