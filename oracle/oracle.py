@@ -15,7 +15,8 @@ class OracleParams(C.Structure):
                 ("stretch_factor", C.c_double), ("stretch_cap", C.c_double), ("window_size", C.c_uint32),
                 ("forward", C.c_int), ("max_match", C.c_int), ("max_count", C.c_int32),
                 ("mers_matching", C.c_double), ("bases_matching", C.c_double), ("unitigs_k", C.c_uint32),
-                ("unitig_lengths", C.POINTER(C.c_int32)), ("n_unitigs", C.c_size_t), ("legacy_no_filter", C.c_int)]
+                ("unitig_lengths", C.POINTER(C.c_int32)), ("n_unitigs", C.c_size_t), ("legacy_no_filter", C.c_int),
+                ("fine_k", C.c_uint32)]
 
 
 class OracleRecord(C.Structure):
@@ -56,6 +57,12 @@ def lib():
                                           C.POINTER(C.c_uint64), C.c_size_t, C.c_int, C.c_int, C.c_int, C.c_int,
                                           C.POINTER(C.c_size_t)]
         L.oracle_align_format.restype = C.c_void_p
+        L.oracle_align_format_ex.argtypes = L.oracle_align_format.argtypes + [C.POINTER(C.c_void_p),
+                                                                               C.POINTER(C.c_size_t)]
+        L.oracle_align_format_ex.restype = C.c_void_p
+        L.oracle_index_build_fine.argtypes = [vp, C.c_uint32, C.c_int]
+        L.oracle_index_lookup_fine.argtypes = [vp, C.c_uint64, C.POINTER(C.c_uint64), C.c_uint64]
+        L.oracle_index_lookup_fine.restype = C.c_uint64
         L.oracle_align_timed.argtypes = [vp, C.POINTER(OracleParams), C.POINTER(C.c_char_p), C.POINTER(C.c_uint64),
                                          C.c_size_t, C.c_int, C.POINTER(C.c_uint64)]
         L.oracle_align_timed.restype = C.c_double
@@ -90,13 +97,14 @@ def _cstrs(items):
 
 def params(k=17, stretch_factor=1.3, stretch_constant=10, stretch_cap=10000.0, window_size=1, forward=False,
            max_match=False, max_count=5000, mers_matching=0.0, bases_matching=17.0, unitigs_k=0,
-           unitig_lengths=None, legacy_no_filter=False, psa_min=13):
+           unitig_lengths=None, legacy_no_filter=False, psa_min=13, fine_k=0):
     p = OracleParams()
     lib().oracle_params_default(C.byref(p))
     p.k = k; p.psa_min = psa_min; p.stretch_constant = stretch_constant; p.stretch_factor = stretch_factor
     p.stretch_cap = stretch_cap; p.window_size = window_size; p.forward = int(bool(forward))
     p.max_match = int(bool(max_match)); p.max_count = max_count; p.mers_matching = mers_matching
     p.bases_matching = bases_matching; p.unitigs_k = unitigs_k; p.legacy_no_filter = int(bool(legacy_no_filter))
+    p.fine_k = fine_k
     keep = None
     if unitig_lengths is not None:
         keep = np.ascontiguousarray(unitig_lengths, dtype=np.int32)
@@ -125,19 +133,36 @@ class OracleIndex:
         n = lib().oracle_index_lookup(self.h, code, out, cap)
         return n, [out[i] for i in range(min(n, cap))]
 
+    def build_fine(self, fine_k, threads=8):
+        if lib().oracle_index_build_fine(self.h, fine_k, threads) != 0:
+            raise ValueError(f"fine_k={fine_k} outside [1, k={self.k}]")
+        return self
+
+    def lookup_fine(self, code, cap=1 << 16):
+        out = (C.c_uint64 * cap)()
+        n = lib().oracle_index_lookup_fine(self.h, code, out, cap)
+        return n, [out[i] for i in range(min(n, cap))]
+
     def sr_name(self, i, bwd=False):
         return lib().oracle_index_sr_name(self.h, i, int(bwd)).decode()
 
-    def align_format(self, p, names, seqs, threads=1, compact=True, header=False, zero_match=False):
+    def align_format(self, p, names, seqs, threads=1, compact=True, header=False, zero_match=False, details=False):
+        """coords text; with details=True a (coords, details) pair."""
         bs = [s if isinstance(s, bytes) else s.encode() for s in seqs]
         lens = (C.c_uint64 * max(1, len(bs)))(*[len(b) for b in bs])
-        n = C.c_size_t()
-        t = lib().oracle_align_format(self.h, C.byref(p), _cstrs(names), _cstrs(bs), lens, len(bs), threads,
-                                      int(compact), int(header), int(zero_match), C.byref(n))
+        n, dn, dt = C.c_size_t(), C.c_size_t(), C.c_void_p()
+        t = lib().oracle_align_format_ex(self.h, C.byref(p), _cstrs(names), _cstrs(bs), lens, len(bs), threads,
+                                         int(compact), int(header), int(zero_match), C.byref(n),
+                                         C.byref(dt) if details else None, C.byref(dn))
         try:
-            return C.string_at(t, n.value).decode()
+            text = C.string_at(t, n.value).decode()
+            if details:
+                return text, C.string_at(dt.value, dn.value).decode() if dn.value else ""
+            return text
         finally:
             lib().free(C.c_void_p(t))
+            if dt.value:
+                lib().free(dt)
 
     def align_timed(self, p, seqs, threads=1):
         bs = [s if isinstance(s, bytes) else s.encode() for s in seqs]

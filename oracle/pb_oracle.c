@@ -148,6 +148,12 @@ struct oracle_index {
   uint64_t* pos;        /* positions, same order */
   uint32_t dir_bits;
   uint64_t* dir;        /* bucket directory over the top dir_bits of the code */
+  /* fine (-F) sub-index (oracle_index_build_fine) */
+  uint32_t fk, fshift, fdir_bits;
+  uint64_t fn_pos;
+  uint64_t* fkeys;      /* (T[x, x+k) zero-padded past n) << 1 | (x + k <= n), sorted */
+  uint64_t* fpos;
+  uint64_t* fdir;       /* directory over the top fdir_bits of the fine_k-mer */
 };
 
 typedef struct {
@@ -317,7 +323,8 @@ void oracle_index_free(oracle_index* ix) {
     free(ix->sr[i].name_fwd); free(ix->sr[i].name_bwd);
     free(ix->sr[i].fwd.id); free(ix->sr[i].fwd.ori);
   }
-  free(ix->sr); free(ix->text); free(ix->keys); free(ix->pos); free(ix->dir); free(ix);
+  free(ix->sr); free(ix->text); free(ix->keys); free(ix->pos); free(ix->dir);
+  free(ix->fkeys); free(ix->fpos); free(ix->fdir); free(ix);
 }
 size_t oracle_index_nb_sr(const oracle_index* ix) { return ix->n_sr; }
 uint64_t oracle_index_text_len(const oracle_index* ix) { return ix->n; }
@@ -342,6 +349,70 @@ uint64_t oracle_index_lookup(const oracle_index* ix, uint64_t code, uint64_t* po
   uint64_t lo, hi;
   index_range(ix, code, &lo, &hi);
   for (uint64_t i = lo; i < hi && i - lo < cap; ++i) pos_out[i - lo] = ix->pos[i];
+  return hi - lo;
+}
+
+/* ----------------------------------------------------------------------
+ * Fine sub-index.  For a pattern P of fine_k bases the reference searches the
+ * PSA built with mer_size = min(fine_k, psa_min) and max_size = k
+ * (jf_aligner.cc:202-203).  Its matches are the x with T[x, x+fine_k) == P,
+ * x <= n - fine_k, in SA order: sort_one_mer (mer_sa_imp.hpp:351-364)
+ * compares T[x+mer_size, min(n, x+k)) lexicographically (a proper prefix
+ * first) and breaks ties by x descending; the bases mer_size..fine_k are P's
+ * own, so the order is that of the extension T[x+fine_k, min(n, x+k)).
+ * Key = the k bases at x, zero-padded past n, << 1 | (x + k <= n): a
+ * truncated extension sorts before any full one it prefixes, and two
+ * truncated ones with equal padded keys keep x descending (the shorter one,
+ * at the larger x, first), as the reference's comparator does.
+ * ------------------------------------------------------------------------ */
+int oracle_index_build_fine(oracle_index* ix, uint32_t fk, int threads) {
+  const uint32_t k = ix->k;
+  if (fk < 1 || fk > k || k > 31) return -1;
+  free(ix->fkeys); free(ix->fpos); free(ix->fdir);
+  ix->fk = fk;
+  ix->fshift = 2 * (k - fk) + 1;
+  const uint64_t n = ix->n;
+  const uint64_t np = n >= fk ? n - fk + 1 : 0;
+  ix->fn_pos = np;
+  uint64_t* keys = xmalloc((np ? np : 1) * sizeof(uint64_t));
+  uint64_t* pos = xmalloc((np ? np : 1) * sizeof(uint64_t));
+  const uint64_t mask = mer_mask(k);
+  uint64_t m = 0;
+  for (uint32_t i = 0; i + 1 < k; ++i) m = (m << 2) | (i < n ? ix->text[i] : 0);
+  for (uint64_t x = 0; x < np; ++x) {
+    const uint64_t q = x + k - 1;
+    m = ((m << 2) | (q < n ? ix->text[q] : 0)) & mask;
+    keys[np - 1 - x] = (m << 1) | (x + k <= n ? 1u : 0u);
+    pos[np - 1 - x] = x;
+  }
+  radix_sort(&keys, &pos, np, 2 * k + 1, threads);
+  ix->fkeys = keys; ix->fpos = pos;
+  ix->fdir_bits = 2 * fk < 20 ? 2 * fk : 20;
+  const size_t nd = ((size_t)1 << ix->fdir_bits) + 1;
+  ix->fdir = xcalloc(nd, sizeof(uint64_t));
+  const uint32_t sh = ix->fshift + 2 * fk - ix->fdir_bits;
+  for (uint64_t i = 0; i < np; ++i) ix->fdir[(keys[i] >> sh) + 1]++;
+  for (size_t i = 1; i < nd; ++i) ix->fdir[i] += ix->fdir[i - 1];
+  return 0;
+}
+
+static void fine_range(const oracle_index* ix, uint64_t code, uint64_t* plo, uint64_t* phi) {
+  const uint32_t sh = 2 * ix->fk - ix->fdir_bits;
+  const uint64_t b = code >> sh;
+  uint64_t l = ix->fdir[b], h = ix->fdir[b + 1];
+  const uint64_t hi0 = h;
+  while (l < h) { uint64_t md = l + (h - l) / 2; if ((ix->fkeys[md] >> ix->fshift) < code) l = md + 1; else h = md; }
+  const uint64_t first = l;
+  h = hi0;
+  while (l < h) { uint64_t md = l + (h - l) / 2; if ((ix->fkeys[md] >> ix->fshift) <= code) l = md + 1; else h = md; }
+  *plo = first; *phi = l;
+}
+
+uint64_t oracle_index_lookup_fine(const oracle_index* ix, uint64_t code, uint64_t* pos_out, uint64_t cap) {
+  if (!ix->fkeys) DIE("fine sub-index not built");
+  uint64_t lo, hi;
+  fine_range(ix, code, &lo, &hi);
+  for (uint64_t i = lo; i < hi && i - lo < cap; ++i) pos_out[i - lo] = ix->fpos[i];
   return hi - lo;
 }
 
@@ -727,6 +798,25 @@ static void do_lis(offlist* l, size_t W, const accept_t* ac, lis_scratch* sc) {
   l->nlis = lis_run(l->off, l->n, W, ac, sc, l->lis);
 }
 
+/* growable text buffer (formatting of coords and details) */
+typedef struct { char* s; size_t n, cap; } sbuf;
+static void sb_reserve(sbuf* b, size_t extra) {
+  if (b->n + extra + 1 > b->cap) { size_t nc = b->cap ? b->cap : 4096; while (nc < b->n + extra + 1) nc *= 2; b->s = xrealloc(b->s, nc); b->cap = nc; }
+}
+static void sb_printf(sbuf* b, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+static void sb_printf(sbuf* b, const char* fmt, ...) {
+  va_list ap;
+  for (;;) {
+    sb_reserve(b, 256);
+    va_start(ap, fmt);
+    int r = vsnprintf(b->s + b->n, b->cap - b->n, fmt, ap);
+    va_end(ap);
+    if (r < 0) DIE("vsnprintf");
+    if ((size_t)r < b->cap - b->n) { b->n += (size_t)r; return; }
+    sb_reserve(b, (size_t)r + 1);
+  }
+}
+
 /* ======================================================================
  * Per-read aligner: fetch_super_reads (coarse_aligner.cc:81-141) +
  * align_sequence_max (coarse_aligner.cc:42-60).
@@ -747,17 +837,29 @@ typedef struct {
   uint64_t* cnts; size_t cap_cnts;
   lis_scratch sc;
   size_t n_sr;
+  /* fine (-F) windows: one per coarse record (fine_aligner.hpp:50-58) */
+  struct fine_win* fw; uint32_t cap_fw;
+  int32_t* fhead;        /* n_sr: first window of the super-read, -1 = none */
 } worker_t;
+
+typedef struct fine_win {
+  uint32_t sr; int32_t next;  /* next window of the same super-read */
+  double begin, end;          /* sr_local_ml (fine_aligner.hpp:12-17) */
+  offlist fwd, bwd;
+} fine_win;
 
 static void worker_init(worker_t* w, size_t n_sr) {
   memset(w, 0, sizeof(*w));
   w->n_sr = n_sr;
   w->slot_of_sr = xmalloc((n_sr ? n_sr : 1) * sizeof(int32_t));
-  for (size_t i = 0; i < n_sr; ++i) w->slot_of_sr[i] = -1;
+  w->fhead = xmalloc((n_sr ? n_sr : 1) * sizeof(int32_t));
+  for (size_t i = 0; i < n_sr; ++i) { w->slot_of_sr[i] = -1; w->fhead[i] = -1; }
 }
 static void worker_free(worker_t* w) {
   for (uint32_t i = 0; i < w->cap_lists; ++i) { free(w->fwd[i].off); free(w->fwd[i].lis); free(w->bwd[i].off); free(w->bwd[i].lis); }
   free(w->fwd); free(w->bwd); free(w->touched); free(w->slot_of_sr); free(w->ent); free(w->cnts);
+  for (uint32_t i = 0; i < w->cap_fw; ++i) { free(w->fw[i].fwd.off); free(w->fw[i].fwd.lis); free(w->fw[i].bwd.off); free(w->fw[i].bwd.lis); }
+  free(w->fw); free(w->fhead);
   lis_scratch_free(&w->sc);
 }
 
@@ -790,8 +892,112 @@ static int cmp_rec(const void* a, const void* b) {
   return x->emit < y->emit ? -1 : x->emit > y->emit;
 }
 
+/* print_details (jf_aligner.cc:72-108) for one super-read of frags_pos, in
+ * its final state: fwd and bwd lists merged by pb offset (fwd first on
+ * ties), the elements of the longer lis (fwd only if strictly longer) in
+ * brackets. */
+static void details_line(sbuf* det, const char* pbname, size_t pbname_len, const char* srname,
+                         const offlist* F, const offlist* B) {
+  sb_printf(det, "%.*s %s", (int)pbname_len, pbname, srname);
+  const int fa = F->nlis > B->nlis;
+  const offlist* L = fa ? F : B;
+  uint32_t li = 0, fi = 0, bi = 0;
+  while (fi < F->n || bi < B->n) {
+    int32_t pb, so; int in_lis;
+    if (fi < F->n && (bi == B->n || F->off[2 * fi] <= B->off[2 * bi])) {
+      pb = F->off[2 * fi]; so = F->off[2 * fi + 1];
+      in_lis = fa && li < L->nlis && L->lis[li] == fi;
+      ++fi;
+    } else {
+      pb = B->off[2 * bi]; so = B->off[2 * bi + 1];
+      in_lis = !fa && li < L->nlis && L->lis[li] == bi;
+      ++bi;
+    }
+    if (in_lis) { sb_printf(det, " [%d:%d]", pb, so); ++li; }
+    else sb_printf(det, " %d:%d", pb, so);
+  }
+  sb_printf(det, "\n");
+}
+
+/* fine_aligner::thread::align_sequence (fine_aligner.cc:38-51): one window
+ * per coarse record (prime_frags_pos, fine_aligner.hpp:50-58), every
+ * fine_k-mer of the read looked up (no SSR / toggle / count filters) and its
+ * hits kept in each window of the super-read whose [begin, end] holds the pb
+ * offset (fetch_local_super_reads, fine_aligner.cc:7-36), LIS with
+ * accept_all and window 1, compute_coords_info(forward = true) with
+ * align_k = fine_k and no filters.  Replaces coarse[0..nc) by the fine
+ * records (malloc'd, *nf).  A window without hits gives nb_mers = 0, whose
+ * rs/re/qs/qe the reference leaves uninitialized (pb_aligner.cc:27 returns
+ * before setting them): they are 0 here. */
+static oracle_record* fine_align_read(const oracle_index* ix, const oracle_params* p, worker_t* w,
+                                      const char* seq, size_t len, const oracle_record* coarse, size_t nc,
+                                      size_t* nf) {
+  const uint32_t fk = ix->fk;
+  if (w->cap_fw < nc) {
+    w->fw = xrealloc(w->fw, nc * sizeof(fine_win));
+    for (uint32_t i = w->cap_fw; i < nc; ++i) memset(&w->fw[i], 0, sizeof(fine_win));
+    w->cap_fw = (uint32_t)nc;
+  }
+  for (size_t i = nc; i-- > 0;) {  /* window lists per super-read, in coarse order */
+    const oracle_record* c = &coarse[i];
+    fine_win* fw = &w->fw[i];
+    fw->sr = c->sr_index;
+    const double b = c->stretch + c->offset - c->avg_err;
+    const double e = c->stretch * (double)c->ql + c->offset + c->avg_err - (double)fk;
+    fw->begin = 0.0 < b ? b : 0.0;                       /* std::max((double)0, b) */
+    fw->end = e < (double)c->rl ? e : (double)c->rl;     /* std::min((double)rl, e) */
+    fw->fwd.n = fw->bwd.n = 0; fw->fwd.nlis = fw->bwd.nlis = 0;
+    fw->next = w->fhead[fw->sr];
+    w->fhead[fw->sr] = (int32_t)i;
+  }
+  const uint64_t mask = mer_mask(fk);
+  uint64_t m = 0, rm = 0; uint32_t rlen = 0;
+  for (size_t i = 0; i < len; ++i) {
+    const int c = jf_code((unsigned char)seq[i]);
+    if (c < 0) { rlen = 0; continue; }
+    ++rlen;
+    m = ((m << 2) | (uint64_t)c) & mask;
+    rm = (rm >> 2) | ((uint64_t)(3 - c) << (2 * (fk - 1)));
+    if (rlen < fk) continue;
+    const int canon = m < rm;
+    const int32_t pb_off = (int32_t)(i + 1) - (int32_t)fk + 1;
+    for (int half = 0; half < 2; ++half) {
+      uint64_t lo, hi;
+      fine_range(ix, half ? (canon ? rm : m) : (canon ? m : rm), &lo, &hi);
+      for (uint64_t q = lo; q < hi; ++q) {
+        const uint64_t x = ix->fpos[q];
+        const size_t s = sr_of(ix, x);
+        if (w->fhead[s] < 0) continue;
+        if (x + fk > ix->sr[s].start + ix->sr[s].len) continue;
+        const int32_t off = (int32_t)(x - ix->sr[s].start + 1);
+        const int32_t it_off = half ? -off : off;
+        const int32_t fin = canon ? it_off : -it_off;
+        for (int32_t wi = w->fhead[s]; wi >= 0; wi = w->fw[wi].next) {
+          fine_win* fw = &w->fw[wi];
+          if ((double)pb_off >= fw->begin && (double)pb_off <= fw->end)
+            offlist_push(fin > 0 ? &fw->fwd : &fw->bwd, pb_off, fin);
+        }
+      }
+    }
+  }
+  accept_t all = { 1, 0, 0, 0, 1, 0 };
+  cinfo_ctx cx = { fk, p->unitigs_k, p->unitig_lengths, p->n_unitigs, 1 };
+  oracle_record* recs = xmalloc((nc ? nc : 1) * sizeof(oracle_record));
+  for (size_t i = 0; i < nc; ++i) {
+    fine_win* fw = &w->fw[i];
+    do_lis(&fw->fwd, 1, &all, &w->sc);
+    do_lis(&fw->bwd, 1, &all, &w->sc);
+    compute_coords_info(&ix->sr[fw->sr], fw->sr, &fw->fwd, &fw->bwd, (uint64_t)len, &cx, &recs[i]);
+    recs[i].emit = (uint32_t)i;
+    w->fhead[fw->sr] = -1;
+  }
+  *nf = nc;
+  return recs;
+}
+
 static int align_read_w(const oracle_index* ix, const oracle_params* p, worker_t* w,
-                        const char* seq, size_t len, oracle_read_result* out) {
+                        const char* seq, size_t len, oracle_read_result* out,
+                        sbuf* det, const char* pbname, size_t pbname_len) {
   const uint32_t k = ix->k;
   const uint64_t mask = mer_mask(k);
   const int32_t max_count = p->max_count ? p->max_count : INT_MAX;
@@ -884,7 +1090,15 @@ static int align_read_w(const oracle_index* ix, const oracle_params* p, worker_t
       discard_lis(D);
       do_lis(D, p->window_size, &ac, &w->sc);
     }
+    if (det) details_line(det, pbname, pbname_len, ix->sr[sr].name_fwd, F, B);
     w->slot_of_sr[sr] = -1;
+  }
+  if (p->fine_k) {
+    size_t nf = 0;
+    oracle_record* fr = fine_align_read(ix, p, w, seq, len, recs, nrec, &nf);
+    for (size_t i = 0; i < nrec; ++i) { free(recs[i].kmers_info); free(recs[i].bases_info); }
+    free(recs);
+    recs = fr; nrec = nf;
   }
   qsort(recs, nrec, sizeof(oracle_record), cmp_rec);
   out->n = nrec; out->recs = recs;
@@ -893,8 +1107,9 @@ static int align_read_w(const oracle_index* ix, const oracle_params* p, worker_t
 
 int oracle_align_read(const oracle_index* ix, const oracle_params* p, const char* seq, size_t len, oracle_read_result* out) {
   if (p->k != ix->k) DIE("params.k != index k");
+  if (p->fine_k && p->fine_k != ix->fk) DIE("params.fine_k != the index's fine sub-index");
   worker_t w; worker_init(&w, ix->n_sr);
-  int r = align_read_w(ix, p, &w, seq, len, out);
+  int r = align_read_w(ix, p, &w, seq, len, out, NULL, NULL, 0);
   worker_free(&w);
   return r;
 }
@@ -907,23 +1122,6 @@ void oracle_read_result_free(oracle_read_result* r) {
 /* ======================================================================
  * Formatting (jf_aligner.cc:32-70) and the threaded driver.
  * ==================================================================== */
-typedef struct { char* s; size_t n, cap; } sbuf;
-static void sb_reserve(sbuf* b, size_t extra) {
-  if (b->n + extra + 1 > b->cap) { size_t nc = b->cap ? b->cap : 4096; while (nc < b->n + extra + 1) nc *= 2; b->s = xrealloc(b->s, nc); b->cap = nc; }
-}
-static void sb_printf(sbuf* b, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
-static void sb_printf(sbuf* b, const char* fmt, ...) {
-  va_list ap;
-  for (;;) {
-    sb_reserve(b, 256);
-    va_start(ap, fmt);
-    int r = vsnprintf(b->s + b->n, b->cap - b->n, fmt, ap);
-    va_end(ap);
-    if (r < 0) DIE("vsnprintf");
-    if ((size_t)r < b->cap - b->n) { b->n += (size_t)r; return; }
-    sb_reserve(b, (size_t)r + 1);
-  }
-}
 static void format_read(sbuf* b, const oracle_index* ix, const char* header, uint64_t pb_size,
                         const oracle_read_result* r, int compact, int zero_match) {
   if (r->n == 0 && !zero_match) return;
@@ -947,7 +1145,7 @@ typedef struct {
   const oracle_index* ix; const oracle_params* p;
   const char* const* names; const char* const* seqs; const uint64_t* lens; size_t n;
   int compact, zero_match, do_format;
-  sbuf* outs; atomic_size_t next; atomic_ullong nrec;
+  sbuf* outs; sbuf* dets; atomic_size_t next; atomic_ullong nrec;
 } drv_t;
 
 static void* drv_worker(void* arg) {
@@ -957,7 +1155,9 @@ static void* drv_worker(void* arg) {
     size_t i = atomic_fetch_add(&d->next, 1);
     if (i >= d->n) break;
     oracle_read_result r;
-    align_read_w(d->ix, d->p, &w, d->seqs[i], d->lens[i], &r);
+    sbuf* det = d->dets ? &d->dets[i] : NULL;
+    const char* nm = d->names ? d->names[i] : "";
+    align_read_w(d->ix, d->p, &w, d->seqs[i], d->lens[i], &r, det, nm, strcspn(nm, " \t\n\v\f\r"));
     atomic_fetch_add(&d->nrec, r.n);
     if (d->do_format) format_read(&d->outs[i], d->ix, d->names[i], d->lens[i], &r, d->compact, d->zero_match);
     oracle_read_result_free(&r);
@@ -974,33 +1174,49 @@ static void run_driver(drv_t* d, int threads) {
   free(th);
 }
 
-char* oracle_align_format(const oracle_index* ix, const oracle_params* p, const char* const* names,
-                          const char* const* seqs, const uint64_t* lens, size_t n, int threads,
-                          int compact, int header, int zero_match, size_t* out_len) {
-  if (p->k != ix->k) DIE("params.k != index k");
-  drv_t d; memset(&d, 0, sizeof(d));
-  d.ix = ix; d.p = p; d.names = names; d.seqs = seqs; d.lens = lens; d.n = n;
-  d.compact = compact; d.zero_match = zero_match; d.do_format = 1;
-  d.outs = xcalloc(n ? n : 1, sizeof(sbuf));
-  atomic_init(&d.next, 0); atomic_init(&d.nrec, 0);
-  run_driver(&d, threads);
+static char* join_parts(sbuf* parts, size_t n, const char* head, size_t* out_len) {
   sbuf all = { 0, 0, 0 };
-  if (header)
-    sb_printf(&all, "Rstart Rend Qstart Qend Nmers Rcons Qcons Rcover Qcover Rlen Qlen Stretch Offset Err%s Qname\n",
-              compact ? "" : " Rname");
+  if (head) sb_printf(&all, "%s", head);
   for (size_t i = 0; i < n; ++i) {
-    if (d.outs[i].n) { sb_reserve(&all, d.outs[i].n); memcpy(all.s + all.n, d.outs[i].s, d.outs[i].n); all.n += d.outs[i].n; }
-    free(d.outs[i].s);
+    if (parts[i].n) { sb_reserve(&all, parts[i].n); memcpy(all.s + all.n, parts[i].s, parts[i].n); all.n += parts[i].n; }
+    free(parts[i].s);
   }
-  free(d.outs);
+  free(parts);
   sb_reserve(&all, 0);
   all.s[all.n] = 0;
   *out_len = all.n;
   return all.s;
 }
 
+char* oracle_align_format(const oracle_index* ix, const oracle_params* p, const char* const* names,
+                          const char* const* seqs, const uint64_t* lens, size_t n, int threads,
+                          int compact, int header, int zero_match, size_t* out_len) {
+  return oracle_align_format_ex(ix, p, names, seqs, lens, n, threads, compact, header, zero_match, out_len, NULL, NULL);
+}
+
+char* oracle_align_format_ex(const oracle_index* ix, const oracle_params* p, const char* const* names,
+                             const char* const* seqs, const uint64_t* lens, size_t n, int threads,
+                             int compact, int header, int zero_match, size_t* out_len,
+                             char** details, size_t* details_len) {
+  if (p->k != ix->k) DIE("params.k != index k");
+  if (p->fine_k && p->fine_k != ix->fk) DIE("params.fine_k != the index's fine sub-index");
+  drv_t d; memset(&d, 0, sizeof(d));
+  d.ix = ix; d.p = p; d.names = names; d.seqs = seqs; d.lens = lens; d.n = n;
+  d.compact = compact; d.zero_match = zero_match; d.do_format = 1;
+  d.outs = xcalloc(n ? n : 1, sizeof(sbuf));
+  if (details) d.dets = xcalloc(n ? n : 1, sizeof(sbuf));
+  atomic_init(&d.next, 0); atomic_init(&d.nrec, 0);
+  run_driver(&d, threads);
+  char head[160];
+  snprintf(head, sizeof head, "Rstart Rend Qstart Qend Nmers Rcons Qcons Rcover Qcover Rlen Qlen Stretch Offset Err%s Qname\n",
+           compact ? "" : " Rname");
+  if (details) *details = join_parts(d.dets, n, NULL, details_len);
+  return join_parts(d.outs, n, header ? head : NULL, out_len);
+}
+
 double oracle_align_timed(const oracle_index* ix, const oracle_params* p, const char* const* seqs,
                           const uint64_t* lens, size_t n, int threads, uint64_t* n_records) {
+  if (p->fine_k && p->fine_k != ix->fk) DIE("params.fine_k != the index's fine sub-index");
   drv_t d; memset(&d, 0, sizeof(d));
   d.ix = ix; d.p = p; d.seqs = seqs; d.lens = lens; d.n = n;
   atomic_init(&d.next, 0); atomic_init(&d.nrec, 0);

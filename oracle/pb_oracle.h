@@ -58,6 +58,9 @@ typedef struct {
   /* test-only knob: 1 => skip SSR / toggle / count threshold (the
    * semantics tests/test_pb_aligner.cc:68 was written against) */
   int      legacy_no_filter;
+  /* -F: fine_aligner k (0 = off).  The index must carry the fine sub-index
+   * (oracle_index_build_fine) for this k. */
+  uint32_t fine_k;
 } oracle_params;
 
 void oracle_params_default(oracle_params* p);
@@ -88,6 +91,15 @@ int      oracle_index_base(const oracle_index* ix, uint64_t pos);
  * positions in reference order (descending text position). */
 uint64_t oracle_index_lookup(const oracle_index* ix, uint64_t code,
                              uint64_t* pos_out, uint64_t cap);
+
+/* Fine (-F) sub-index over the short mer size fine_k <= k: every position in
+ * SA order for a fine_k-mer pattern (sort_one_mer, mer_sa_imp.hpp:351-364).
+ * Returns 0, or -1 if fine_k is outside [1, k] or k > 31. */
+int      oracle_index_build_fine(oracle_index* ix, uint32_t fine_k, int threads);
+/* Exact-match lookup of a fine_k-mer code in the fine sub-index: total count
+ * and up to `cap` positions in the reference's SA order. */
+uint64_t oracle_index_lookup_fine(const oracle_index* ix, uint64_t code,
+                                  uint64_t* pos_out, uint64_t cap);
 
 /* ---------------------------------------------------------------- records */
 typedef struct {
@@ -122,6 +134,16 @@ char* oracle_align_format(const oracle_index* ix, const oracle_params* p,
                           const uint64_t* lens, size_t n, int threads,
                           int compact, int header, int zero_match,
                           size_t* out_len);
+
+/* oracle_align_format, and with details != NULL also the --details text
+ * (print_details, jf_aligner.cc:72-108): per read, one line per super-read
+ * of the coarse frags_pos in first-hit order (the reference iterates an
+ * unordered_map).  Caller frees both texts. */
+char* oracle_align_format_ex(const oracle_index* ix, const oracle_params* p,
+                             const char* const* names, const char* const* seqs,
+                             const uint64_t* lens, size_t n, int threads,
+                             int compact, int header, int zero_match,
+                             size_t* out_len, char** details, size_t* details_len);
 
 /* Timing helper for the CPU baseline: aligns n reads with `threads`
  * workers, returns wall seconds (records discarded). */

@@ -97,7 +97,7 @@ static void read_reads(const char* path, readset* rs) {
 int main(int argc, char** argv) {
   oracle_params p; oracle_params_default(&p);
   int threads = 1, header = 1, zero = 0, compact = 1, s_given = 0, m_given = 0, k_given = 0;
-  const char* coords = NULL; const char* ul_path = NULL; const char* us_path = NULL;
+  const char* coords = NULL; const char* details = NULL; const char* ul_path = NULL; const char* us_path = NULL;
   const char** srs = NULL; size_t n_srs = 0;
   const char** pbs = NULL; size_t n_pbs = 0;
   enum { O_PSA = 256, O_SC, O_SF, O_CAP, O_WIN, O_DETAILS, O_COORDS, O_MAXM, O_MAXC, O_COMPACT, O_NOCOMPACT };
@@ -115,7 +115,7 @@ int main(int argc, char** argv) {
     switch (c) {
     case 's': s_given = 1; break; /* required, unused (legacy) */
     case 'm': p.k = (uint32_t)strtoul(optarg, NULL, 10); m_given = 1; break;
-    case 'F': usage_die("-F (fine aligner) is not restated in the oracle yet");
+    case 'F': p.fine_k = (uint32_t)strtoul(optarg, NULL, 10); break;
     case O_PSA: p.psa_min = (uint32_t)strtoul(optarg, NULL, 10); break;
     case 't': threads = atoi(optarg); break;
     case O_SC: p.stretch_constant = (double)atoi(optarg); break;
@@ -125,7 +125,7 @@ int main(int argc, char** argv) {
     case 'f': p.forward = 1; break;
     case 'B': p.bases_matching = strtod(optarg, NULL); break;
     case 'M': p.mers_matching = strtod(optarg, NULL); break;
-    case O_DETAILS: usage_die("--details is not restated in the oracle yet");
+    case O_DETAILS: details = optarg; break;
     case O_COORDS: coords = optarg; break;
     case O_MAXM: p.max_match = 1; break;
     case 'H': header = 0; break;
@@ -153,16 +153,26 @@ int main(int argc, char** argv) {
     p.unitigs_k = 0; /* unitigs_lengths() only called with -l/-u (jf_aligner.cc:215) */
   }
   oracle_index* ix = oracle_index_build_fasta(srs, n_srs, p.k, threads);
+  if (p.fine_k && oracle_index_build_fine(ix, p.fine_k, threads) != 0)
+    usage_die("-F must be in [1, -m] with -m <= 31 (PSA::search assumes the pattern is at most max_size, mer_sa_imp.hpp:366)");
   readset rs; memset(&rs, 0, sizeof(rs));
   for (size_t i = 0; i < n_pbs; ++i) read_reads(pbs[i], &rs);
-  size_t olen;
-  char* out = oracle_align_format(ix, &p, (const char* const*)rs.names, (const char* const*)rs.seqs, rs.lens, rs.n,
-                                  threads, compact, header, zero, &olen);
+  size_t olen, dlen = 0;
+  char* dtext = NULL;
+  char* out = oracle_align_format_ex(ix, &p, (const char* const*)rs.names, (const char* const*)rs.seqs, rs.lens, rs.n,
+                                     threads, compact, header, zero, &olen, details ? &dtext : NULL, &dlen);
   FILE* o = coords ? fopen(coords, "w") : stdout;
   if (!o) usage_die("can't open coords output");
   fwrite(out, 1, olen, o);
   if (coords) fclose(o);
   free(out);
+  if (details) {
+    FILE* d = fopen(details, "w");
+    if (!d) usage_die("can't open details output");
+    fwrite(dtext, 1, dlen, d);
+    fclose(d);
+    free(dtext);
+  }
   for (size_t i = 0; i < rs.n; ++i) { free(rs.names[i]); free(rs.seqs[i]); }
   free(rs.names); free(rs.seqs); free(rs.lens); free(ul); free(srs); free(pbs);
   oracle_index_free(ix);

@@ -10,6 +10,7 @@ Every expected value here comes from EXECUTING the reference's own sources
   encode_cases.json  compact_dna::copy_from_str    (src_psa/compact_dna.hpp)
   srname_cases.json  super_read_name parse/reverse (src_jf_aligner/super_read_name.cc)
   psa_cases.json     PSA::search hit sets + order  (src_psa/psa.hpp, mer_sa_imp.hpp)
+  psa_fine_cases.json  the same for -F patterns shorter than max_size
 The reference's own test data files (tests/aligner_output/*) are copied
 verbatim as input/expected-output fixtures (aligner_output/).
 """
@@ -150,6 +151,46 @@ def psa_cases(rng, k=17, min_size=13):
     return {"fasta": "psa_sr.fa", "k": k, "min_size": min_size, "cases": res}
 
 
+def psa_fine_cases(rng, k=17, psa_min=13):
+    """Short (-F) patterns: SA order of fine_k-mer matches in a PSA built the way
+    jf_aligner.cc:202-203 builds it (min_size = min(fine_k, psa_min), max_size = k).
+    Reuses psa_sr.fa (written by psa_cases) plus a text-end super-read so that
+    matches whose k-base extension is truncated at the end of the text occur."""
+    fa = os.path.join(HERE, "psa_fine_sr.fa")
+    text = []
+    with open(os.path.join(HERE, "psa_sr.fa")) as f, open(fa, "w") as o:
+        for line in f:
+            o.write(line)
+            if not line.startswith(">"):
+                text.append(line.strip())
+        tail = "ACGTTGCAACGTAC" + "ACGTTGCAAC"  # the last 10 bases repeat 10 bases seen just before
+        o.write(">tail\n" + tail + "\n")
+        text.append(tail)
+    text = "".join(text)
+    out = {"fasta": "psa_fine_sr.fa", "k": k, "psa_min": psa_min, "sets": []}
+    for fk in (11, 13, 15):
+        queries = set()
+        for _ in range(300):
+            p = rng.randint(0, len(text) - fk)
+            q = text[p:p + fk]
+            queries.add(q)
+            queries.add(q[::-1].translate(str.maketrans("ACGT", "TGCA")))
+        for p in range(len(text) - fk - k, len(text) - fk + 1):
+            queries.add(text[p:p + fk])
+        queries.add("A" * fk)
+        queries = sorted(queries)
+        mn = min(fk, psa_min)
+        o1 = run("ref_psa", "".join(q + "\n" for q in queries), fa, str(mn), str(k), "1").splitlines()
+        o4 = run("ref_psa", "".join(q + "\n" for q in queries), fa, str(mn), str(k), "4").splitlines()
+        assert o1 == o4, "fine hit order must not depend on the PSA build thread count"
+        cases = []
+        for q, line in zip(queries, o1):
+            v = [int(t) for t in line.split()]
+            cases.append({"q": q, "count": v[0], "pos": v[1:]})
+        out["sets"].append({"fine_k": fk, "min_size": mn, "cases": cases})
+    return out
+
+
 def main():
     if not os.path.isdir(REF):
         sys.exit("oracle/_ref missing: run `make -C oracle ref` in the build container")
@@ -160,10 +201,14 @@ def main():
         with open(os.path.join(HERE, name), "w") as f:
             json.dump(data, f, separators=(",", ":"))
         print(name, "ok")
+    # added later with its own generator so the fixtures above stay byte-identical
+    with open(os.path.join(HERE, "psa_fine_cases.json"), "w") as f:
+        json.dump(psa_fine_cases(random.Random(20261016)), f, separators=(",", ":"))
+    print("psa_fine_cases.json ok")
     dst = os.path.join(HERE, "aligner_output")
     os.makedirs(dst, exist_ok=True)
     for fn in ["test_super_reads.fa", "test_pacbio.fa", "test_unitigs_lengths", "coords_normal_expected",
-               "coords_forward_expected"]:
+               "coords_forward_expected", "details_normal_expected", "details_forward_expected"]:
         shutil.copyfile(os.path.join(REFSRC, "tests", "aligner_output", fn), os.path.join(dst, fn))
     print("aligner_output ok")
 

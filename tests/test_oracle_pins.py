@@ -104,6 +104,20 @@ def test_index_lookup_matches_reference_psa():
         assert pos == c["pos"], c["q"]  # descending text position == SA tie-break order
 
 
+def test_fine_index_lookup_matches_reference_psa():
+    """-F patterns shorter than max_size: the SA order within a match range is
+    the order of the (k - fine_k)-base extension, a truncated extension first,
+    then x descending (mer_sa_imp.hpp:351-364), executed from the reference."""
+    g = _load("psa_fine_cases.json")
+    for st in g["sets"]:
+        ix = O.OracleIndex.from_fasta([os.path.join(GOLD, g["fasta"])], g["k"], threads=2).build_fine(st["fine_k"])
+        for c in st["cases"]:
+            n, pos = ix.lookup_fine(_code(c["q"]))
+            assert n == c["count"], (st["fine_k"], c["q"])
+            assert pos == c["pos"], (st["fine_k"], c["q"])
+        ix.close()
+
+
 # tests/test_kmers_info.cc:12-113 / 115-172 (known answers, unitigs_k=31, k=17)
 KI_SIMPLE = [
     ("0F_1R_3F", [100, 100, 100], [20, 71, 85, 142, 170], [0, 0, 0, 0, 0], [0, 0, 0, 0, 0], "bad"),
