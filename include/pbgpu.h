@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PBGPU_ABI_VERSION 1
+#define PBGPU_ABI_VERSION 2
 
 typedef enum pbgpu_status {
   PBGPU_OK = 0,
@@ -72,6 +72,12 @@ typedef struct {
                         thread-order-dependent hit order upstream) */
   int32_t  device;   /* HIP device ordinal */
   int32_t  threads;  /* host threads for FASTA parsing (0 = all cores) */
+  uint32_t fine_k;   /* -F: also build the short-mer sub-index for the fine
+                        aligner (jf_aligner.cc:200-203), 1 <= fine_k <= k;
+                        0 = none.  Its occurrence lists follow the PSA order
+                        of a pattern shorter than max_size = k: the k - fine_k
+                        bases after each occurrence, then position descending
+                        (mer_sa_imp.hpp:351-364). */
 } pbgpu_index_params;
 
 /* superread_parser.cc:12-46: multi-line FASTA, full header line kept as the
@@ -115,7 +121,10 @@ typedef struct {
   uint32_t unitigs_k;         /* -k; 0 = no k-unitig accounting */
   const int32_t* unitig_lengths; /* -l table, index = line number (misc.cc:11-19); copied */
   uint64_t n_unitigs;
-  uint32_t fine_k;            /* -F; 0 = off (non-zero: PBGPU_ERR_UNSUPPORTED for now) */
+  uint32_t fine_k;            /* -F; 0 = off.  Must equal the index's fine_k.  The
+                                 coarse records then only define the windows of
+                                 fine_aligner (fine_aligner.hpp:24-63) and the
+                                 batch's records are the fine ones. */
 } pbgpu_align_params;
 
 void         pbgpu_align_params_default(pbgpu_align_params* p);
@@ -203,6 +212,9 @@ typedef struct {
   /* work of the timed k_lis slot (the tier-0 wave-per-strand launches, strands
    * of <= 255 hits): hits and strands */
   uint64_t l0_hits, l0_strands;
+  /* fine aligner (-F): windowed hits, windows (= fine records), device time */
+  uint64_t n_fine_hits, n_fine_windows;
+  double   ms_fine;
 } pbgpu_stats;
 pbgpu_status pbgpu_aligner_get_stats(const pbgpu_aligner* al, pbgpu_stats* s);
 pbgpu_status pbgpu_aligner_reset_stats(pbgpu_aligner* al);
@@ -210,6 +222,27 @@ pbgpu_status pbgpu_aligner_reset_stats(pbgpu_aligner* al);
  * sub-batch (default 1.2e9, about 38 GB of working buffers).  A read whose
  * hits exceed it forms a sub-batch of its own.  Results do not depend on it. */
 pbgpu_status pbgpu_aligner_set_hit_budget(pbgpu_aligner* al, uint64_t hits);
+
+/* ---------------------------------------------------------------- details
+ * --details (print_details, jf_aligner.cc:72-108): with details enabled, each
+ * alignment also keeps, per read, every super-read of the coarse frags_pos
+ * with its final fwd and bwd hit lists (after any --max-match discards) and
+ * the elements of the printed lis (the fwd lis if strictly longer, else the
+ * bwd one).  Lists of a read come in first-hit order; the reference iterates
+ * an unordered_map there. */
+pbgpu_status pbgpu_aligner_set_details(pbgpu_aligner* al, int enable);
+typedef struct {
+  uint64_t n_reads, n_lists, n_hits;
+  const uint64_t* read_offsets;  /* n_reads + 1 into the lists */
+  const uint32_t* list_sr;       /* super-read of each list */
+  const uint64_t* hit_offsets;   /* n_lists + 1 into hits: the fwd hits, then the bwd hits */
+  const uint32_t* n_fwd;         /* fwd hits of each list */
+  const int32_t*  hits;          /* (pb offset, signed sr offset) pairs */
+  const uint8_t*  in_lis;        /* per hit: 1 if part of the printed lis */
+} pbgpu_details_batch;
+/* details of the last alignment (PBGPU_ERR_INVALID if details were off) */
+pbgpu_status pbgpu_download_details(pbgpu_aligner* al, pbgpu_details_batch** out);
+pbgpu_status pbgpu_details_free(pbgpu_details_batch* d);
 
 /* --------------------------------------------------------------- output
  * print_coords_header + print_coords (jf_aligner.cc:32-70): headers are the
@@ -220,6 +253,12 @@ pbgpu_status pbgpu_format_coords(const pbgpu_index* ix, const pbgpu_coords_batch
                                  const char* const* read_headers, const uint64_t* read_lens,
                                  int compact, int header, int zero_match, int threads,
                                  char** text, uint64_t* len);
+/* print_details (jf_aligner.cc:72-108): "name sr_name pb:sr ... [pb:sr] ...",
+ * fwd and bwd hits merged by pb offset (fwd first on ties), lis hits in
+ * brackets. */
+pbgpu_status pbgpu_format_details(const pbgpu_index* ix, const pbgpu_details_batch* d,
+                                  const char* const* read_headers, int threads,
+                                  char** text, uint64_t* len);
 void         pbgpu_free_text(char* text);
 
 #ifdef __cplusplus

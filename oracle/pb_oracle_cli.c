@@ -142,6 +142,7 @@ int main(int argc, char** argv) {
     }
   }
   if (!s_given || !m_given) usage_die("-s and -m are required");
+  if (!details && !coords) usage_die("No output file given. Doing nothing ungracefully."); /* jf_aligner.cc:166-167 */
   if (ul_path && us_path) usage_die("-u conflicts with -l");
   if (p.max_count == 0) usage_die("--max-count 0 is undefined behaviour in the reference (coarse_aligner.cc:86)");
   int32_t* ul = NULL; size_t n_ul = 0;

@@ -2,9 +2,9 @@
 // (src_jf_aligner/jf_aligner.cc:161-233, options jf_aligner_cmdline.yaggo:1-77)
 // running the coarse aligner on an MI355X through the pbgpu C ABI.
 //
-// Same flags, same coords text.  Reads are processed in batches; output is
-// written in input order (what the reference prints with -t 1).  Not yet
-// implemented: -F/--fine-mer and --details (rejected with an error).
+// Same flags, same coords (and --details) text.  Reads are processed in
+// batches; output is written in input order (what the reference prints with
+// -t 1).  -F runs the fine aligner on the device after the coarse one.
 #include <getopt.h>
 
 #include <algorithm>
@@ -140,6 +140,7 @@ int main(int argc, char** argv) {
   uint32_t psa_min = 13, threads = 1;
   bool s_given = false, m_given = false, k_given = false, no_header = false, zero = false, compact = true;
   const char* coords_path = nullptr;
+  const char* details_path = nullptr;
   const char* ul_path = nullptr;
   const char* us_path = nullptr;
   std::vector<const char*> srs, pbs;
@@ -171,7 +172,7 @@ int main(int argc, char** argv) {
     case 'f': ap.forward = 1; break;
     case 'B': ap.bases_matching = parse_f64(optarg, "-B"); break;
     case 'M': ap.mers_matching = parse_f64(optarg, "-M"); break;
-    case O_DETAILS: die("--details is not implemented yet");
+    case O_DETAILS: details_path = optarg; break;
     case O_COORDS: coords_path = optarg; break;
     case O_MAXM: ap.max_match = 1; break;
     case 'H': no_header = true; break;
@@ -192,7 +193,7 @@ int main(int argc, char** argv) {
   if (!s_given) die("-s, --size is required");
   if (!m_given) die("-m, --mer is required");
   if (ul_path && us_path) die("-u conflicts with -l");
-  if (ap.fine_k) die("-F (fine aligner) is not implemented yet");
+  if (!details_path && !coords_path) die("No output file given. Doing nothing ungracefully.");  // jf_aligner.cc:166-167
   if (ap.max_count == 0) die("--max-count 0 is undefined behaviour in the reference (coarse_aligner.cc:86)");
   std::vector<int32_t> ul;
   if (ul_path || us_path) {
@@ -207,12 +208,15 @@ int main(int argc, char** argv) {
   }
   FILE* out = coords_path ? fopen(coords_path, "w") : stdout;
   if (!out) die(std::string("Failed to open coords file '") + coords_path + "'");
+  FILE* dout = details_path ? fopen(details_path, "w") : nullptr;
+  if (details_path && !dout) die(std::string("Failed to open details file '") + details_path + "'");
 
-  pbgpu_index_params ip{ap.k, psa_min, device, (int)threads};
+  pbgpu_index_params ip{ap.k, psa_min, device, (int)threads, ap.fine_k};
   pbgpu_index* ix = nullptr;
   check(pbgpu_index_build_fasta(srs.data(), srs.size(), &ip, &ix), "index");
   pbgpu_aligner* al = nullptr;
   check(pbgpu_aligner_create(ix, &ap, &al), "aligner");
+  if (dout) check(pbgpu_aligner_set_details(al, 1), "details");
 
   if (!no_header) {
     fputs("Rstart Rend Qstart Qend Nmers Rcons Qcons Rcover Qcover Rlen Qlen Stretch Offset Err", out);
@@ -246,8 +250,17 @@ int main(int argc, char** argv) {
     fwrite(text, 1, tl, out);
     pbgpu_free_text(text);
     pbgpu_coords_free(cb);
+    if (dout) {
+      pbgpu_details_batch* db = nullptr;
+      check(pbgpu_download_details(al, &db), "details");
+      check(pbgpu_format_details(ix, db, hp.data(), (int)std::max(1u, threads), &text, &tl), "format details");
+      fwrite(text, 1, tl, dout);
+      pbgpu_free_text(text);
+      pbgpu_details_free(db);
+    }
   }
   if (coords_path) fclose(out);
+  if (dout) fclose(dout);
   pbgpu_aligner_free(al);
   pbgpu_index_free(ix);
   return 0;

@@ -24,12 +24,13 @@
 
 namespace pbgpu {
 // kernels (pbgpu_kernels.hip)
-void launch_build_keys(IndexView ix, uint64_t N, uint64_t* keys, uint64_t* vals, hipStream_t st);
-void launch_runs(const uint64_t* keys, const uint64_t* uidx, uint64_t N, uint64_t* run_start, hipStream_t st);
+void launch_build_keys(IndexView ix, uint32_t km, uint32_t K, uint32_t ebits, uint64_t N, uint64_t* keys, uint64_t* vals,
+                       hipStream_t st);
+void launch_runs(const uint64_t* keys, const uint64_t* uidx, uint64_t N, uint32_t sh, uint64_t* run_start, hipStream_t st);
 void launch_occ_fill(const uint64_t* vals, const uint64_t* uidx, const uint64_t* kpos, uint64_t N, uint64_t* occ,
                      hipStream_t st);
 void launch_headers(const uint64_t* keys, const uint64_t* kpos, const uint64_t* run_start, uint64_t U, uint64_t* occ,
-                    ulonglong2* table, uint64_t bucket_mask, uint32_t k, hipStream_t st);
+                    ulonglong2* table, uint64_t bucket_mask, uint32_t k, uint32_t ebits, hipStream_t st);
 void launch_seed(IndexView ix, const uint8_t* seq, const uint64_t* roff, uint32_t n_reads, AlignParamsDev P,
                  KRec* krec, uint32_t* n_kept, uint32_t* thr, uint64_t* nhits, unsigned long long* stats, hipStream_t st);
 void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const uint32_t* n_kept, const uint32_t* thr,
@@ -58,6 +59,17 @@ uint32_t len_buckets();
 void launch_strand_order(const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen, int2* X,
                          hipStream_t st);
 uint32_t big_bucket();
+void launch_fine_windows(const Rec* recs, uint32_t n, uint64_t* keys, uint32_t* idx, int phase, const uint64_t* roff,
+                         uint32_t fk, FineWin* out, hipStream_t st);
+void launch_fine_hits(bool emit, IndexView fx, const uint8_t* seq, const uint64_t* roff, uint32_t r0, uint32_t nr,
+                      const FineWin* win, const uint64_t* woff, uint64_t* read_hits, const uint64_t* hit_off,
+                      uint64_t w_sub0, uint32_t* keys, int2* vals, unsigned long long* stats, hipStream_t st);
+void launch_list_bounds(const uint32_t* keys, uint64_t G, uint32_t* lstart, uint32_t* lend, hipStream_t st);
+void launch_fine_desc(IndexView ix, const Rec* recs, uint64_t w_sub0, uint32_t nwin, const uint32_t* lstart,
+                      const uint32_t* lend, int with_info, ChainDesc* chains, uint32_t* emit_of,
+                      unsigned long long* info_need, hipStream_t st);
+void launch_fine_empty(IndexView ix, uint32_t k, const ChainDesc* chains, uint32_t n, const uint32_t* lisl,
+                       const uint32_t* emit_of, ChainOut O, hipStream_t st);
 void launch_rec_hist(const Rec* recs, uint32_t n, uint32_t* per_read, hipStream_t st);
 void launch_rec_scatter(const Rec* recs, uint32_t n, const uint64_t* rec_off, uint32_t* cursor, uint32_t* order,
                         hipStream_t st);
@@ -130,6 +142,7 @@ struct dbuf {
     p = q; n = nn;
   }
   size_t bytes() const { return n * sizeof(T); }
+  void swap(dbuf& o) { std::swap(p, o.p); std::swap(n, o.n); }
 };
 
 static void* temp_storage(dbuf<uint8_t>& t, size_t bytes) {
@@ -169,14 +182,25 @@ struct pbgpu_index {
   dbuf<uint64_t> text, d_sr_start, occ;
   dbuf<ulonglong2> table;
   dbuf<uint32_t> sr_uoff, sr_uids;
+  // fine (-F) sub-index: same table / occurrence layout over fine_k-mers
+  uint32_t fk = 0;
+  uint64_t f_buckets = 0, f_kmers = 0, f_occ = 0;
+  dbuf<uint64_t> f_occv;
+  dbuf<ulonglong2> f_table;
   IndexView view() const {
     IndexView v;
     v.text = text.p; v.n = n; v.sr_start = d_sr_start.p; v.n_sr = (uint32_t)n_sr; v.k = k;
     v.table = table.p; v.bucket_mask = buckets - 1; v.occ = occ.p; v.sr_uoff = sr_uoff.p; v.sr_uids = sr_uids.p;
     return v;
   }
+  IndexView fine_view() const {
+    IndexView v = view();
+    v.k = fk; v.table = f_table.p; v.bucket_mask = f_buckets - 1; v.occ = f_occv.p;
+    return v;
+  }
   uint64_t device_bytes() const {
-    return text.bytes() + d_sr_start.bytes() + occ.bytes() + table.bytes() + sr_uoff.bytes() + sr_uids.bytes();
+    return text.bytes() + d_sr_start.bytes() + occ.bytes() + table.bytes() + sr_uoff.bytes() + sr_uids.bytes() +
+           f_occv.bytes() + f_table.bytes();
   }
 };
 
@@ -234,6 +258,84 @@ static void load_fasta(const char* path, text_builder& tb) {
   }
 }
 
+// Hash table + occurrence lists of the km-mers of the text (layout in
+// pbgpu_internal.h): sort keys (k_build_keys) -> radix sort -> runs of equal
+// canonical km-mer -> occurrence lists and headers -> table.  ebits > 0
+// orders each list by the K - km bases that follow (the fine sub-index).
+static void build_kmer_table(pbgpu_index* ix, uint32_t km, uint32_t K, uint32_t ebits, hipStream_t st,
+                             dbuf<ulonglong2>& table, dbuf<uint64_t>& occ, uint64_t& n_buckets, uint64_t& n_kmers,
+                             uint64_t& n_occ) {
+  const uint64_t N = ix->n >= km ? ix->n - km + 1 : 0;
+  IndexView v = ix->view();
+  if (N == 0) {
+    n_buckets = 1;
+    table.alloc(4);
+    HIPCHK(hipMemset(table.p, 0xFF, table.bytes()));
+    occ.alloc(2);
+    n_kmers = n_occ = 0;
+    return;
+  }
+  const int key_bits = (int)(2 * km + 1 + ebits);
+  dbuf<uint64_t> k0, k1, v0, v1;
+  k0.alloc(N); k1.alloc(N); v0.alloc(N); v1.alloc(N);
+  launch_build_keys(v, km, K, ebits, N, k0.p, v0.p, st);
+  HIPCHK(hipGetLastError());
+  dbuf<uint8_t> tmp;
+  size_t tbytes = 0;
+  hipcub::DoubleBuffer<uint64_t> dk(k0.p, k1.p), dv(v0.p, v1.p);
+  HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tbytes, dk, dv, N, 0, key_bits, st));
+  HIPCHK(hipcub::DeviceRadixSort::SortPairs(temp_storage(tmp, tbytes), tbytes, dk, dv, N, 0, key_bits, st));
+  uint64_t* keys = dk.Current();
+  uint64_t* vals = dv.Current();
+  uint64_t* spare_k = dk.Alternate();
+  uint64_t* spare_v = dv.Alternate();
+  const uint32_t sh = ebits + 1;  // keys >> sh = canonical km-mer
+  // uidx = inclusive scan of run heads (into spare_k), kpos = exclusive scan of keep (N+1, into a new buffer)
+  struct HeadOp {
+    const uint64_t* keys; uint32_t sh;
+    __host__ __device__ uint64_t operator()(const uint64_t& i) const {
+      return (i == 0 || (keys[i] >> sh) != (keys[i - 1] >> sh)) ? 1ull : 0ull;
+    }
+  };
+  struct KeepOp {
+    const uint64_t* vals; uint64_t N;
+    __host__ __device__ uint64_t operator()(const uint64_t& i) const { return (i < N && vals[i] != ~0ull) ? 1ull : 0ull; }
+  };
+  hipcub::CountingInputIterator<uint64_t> cnt(0);
+  hipcub::TransformInputIterator<uint64_t, HeadOp, hipcub::CountingInputIterator<uint64_t>> heads(cnt, HeadOp{keys, sh});
+  uint64_t* uidx = spare_k;
+  tbytes = 0;
+  HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tbytes, heads, uidx, N, st));
+  HIPCHK(hipcub::DeviceScan::InclusiveSum(temp_storage(tmp, tbytes), tbytes, heads, uidx, N, st));
+  dbuf<uint64_t> kpos;
+  kpos.alloc(N + 1);
+  hipcub::TransformInputIterator<uint64_t, KeepOp, hipcub::CountingInputIterator<uint64_t>> keeps(cnt, KeepOp{vals, N});
+  tbytes = 0;
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tbytes, keeps, kpos.p, N + 1, st));
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(temp_storage(tmp, tbytes), tbytes, keeps, kpos.p, N + 1, st));
+  uint64_t U = 0, kept = 0;
+  HIPCHK(hipMemcpyAsync(&U, uidx + N - 1, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&kept, kpos.p + N, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  uint64_t* run_start = spare_v;  // U + 1 <= N + 1 ... spare_v has N entries; U < N unless all distinct
+  dbuf<uint64_t> rs_extra;
+  if (U + 1 > N) { rs_extra.alloc(U + 1); run_start = rs_extra.p; }
+  launch_runs(keys, uidx, N, sh, run_start, st);
+  HIPCHK(hipMemcpyAsync(run_start + U, &N, 8, hipMemcpyHostToDevice, st));
+  n_kmers = U;
+  n_occ = kept;
+  occ.alloc(2 * U + kept);
+  uint64_t buckets = 1;
+  while (buckets * 2 < U) buckets <<= 1;  // slots = 4*buckets >= 2U: load <= 0.5
+  n_buckets = buckets;
+  table.alloc(4 * buckets);
+  HIPCHK(hipMemsetAsync(table.p, 0xFF, table.bytes(), st));
+  launch_occ_fill(vals, uidx, kpos.p, N, occ.p, st);
+  launch_headers(keys, kpos.p, run_start, U, occ.p, table.p, buckets - 1, km, ebits, st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(st));  // the temporaries above are freed on return
+}
+
 static void build_device_index(pbgpu_index* ix, text_builder& tb) {
   auto t0 = std::chrono::steady_clock::now();
   HIPCHK(hipSetDevice(ix->device));
@@ -276,72 +378,10 @@ static void build_device_index(pbgpu_index* ix, text_builder& tb) {
   ix->sr_uids.alloc(std::max<size_t>(uids.size(), 1));
   if (!uids.empty()) HIPCHK(hipMemcpy(ix->sr_uids.p, uids.data(), uids.size() * 4, hipMemcpyHostToDevice));
 
-  const uint64_t N = ix->n >= k ? ix->n - k + 1 : 0;
-  IndexView v = ix->view();
-  if (N == 0) {
-    ix->buckets = 1;
-    ix->table.alloc(4);
-    HIPCHK(hipMemset(ix->table.p, 0xFF, ix->table.bytes()));
-    ix->occ.alloc(2);
-    ix->build_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    return;
-  }
-  dbuf<uint64_t> k0, k1, v0, v1;
-  k0.alloc(N); k1.alloc(N); v0.alloc(N); v1.alloc(N);
-  launch_build_keys(v, N, k0.p, v0.p, st);
-  HIPCHK(hipGetLastError());
-  dbuf<uint8_t> tmp;
-  size_t tbytes = 0;
-  hipcub::DoubleBuffer<uint64_t> dk(k0.p, k1.p), dv(v0.p, v1.p);
-  HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tbytes, dk, dv, N, 0, (int)(2 * k + 1), st));
-  HIPCHK(hipcub::DeviceRadixSort::SortPairs(temp_storage(tmp, tbytes), tbytes, dk, dv, N, 0, (int)(2 * k + 1), st));
-  uint64_t* keys = dk.Current();
-  uint64_t* vals = dv.Current();
-  uint64_t* spare_k = dk.Alternate();
-  uint64_t* spare_v = dv.Alternate();
-  // uidx = inclusive scan of run heads (into spare_k), kpos = exclusive scan of keep (N+1, into a new buffer)
-  struct HeadOp {
-    const uint64_t* keys;
-    __host__ __device__ uint64_t operator()(const uint64_t& i) const {
-      return (i == 0 || (keys[i] >> 1) != (keys[i - 1] >> 1)) ? 1ull : 0ull;
-    }
-  };
-  struct KeepOp {
-    const uint64_t* vals; uint64_t N;
-    __host__ __device__ uint64_t operator()(const uint64_t& i) const { return (i < N && vals[i] != ~0ull) ? 1ull : 0ull; }
-  };
-  hipcub::CountingInputIterator<uint64_t> cnt(0);
-  hipcub::TransformInputIterator<uint64_t, HeadOp, hipcub::CountingInputIterator<uint64_t>> heads(cnt, HeadOp{keys});
-  uint64_t* uidx = spare_k;
-  tbytes = 0;
-  HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tbytes, heads, uidx, N, st));
-  HIPCHK(hipcub::DeviceScan::InclusiveSum(temp_storage(tmp, tbytes), tbytes, heads, uidx, N, st));
-  dbuf<uint64_t> kpos;
-  kpos.alloc(N + 1);
-  hipcub::TransformInputIterator<uint64_t, KeepOp, hipcub::CountingInputIterator<uint64_t>> keeps(cnt, KeepOp{vals, N});
-  tbytes = 0;
-  HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tbytes, keeps, kpos.p, N + 1, st));
-  HIPCHK(hipcub::DeviceScan::ExclusiveSum(temp_storage(tmp, tbytes), tbytes, keeps, kpos.p, N + 1, st));
-  uint64_t U = 0, kept = 0;
-  HIPCHK(hipMemcpyAsync(&U, uidx + N - 1, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(&kept, kpos.p + N, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  uint64_t* run_start = spare_v;  // U + 1 <= N + 1 ... spare_v has N entries; U < N unless all distinct
-  dbuf<uint64_t> rs_extra;
-  if (U + 1 > N) { rs_extra.alloc(U + 1); run_start = rs_extra.p; }
-  launch_runs(keys, uidx, N, run_start, st);
-  HIPCHK(hipMemcpyAsync(run_start + U, &N, 8, hipMemcpyHostToDevice, st));
-  ix->n_kmers = U;
-  ix->n_occ = kept;
-  ix->occ.alloc(2 * U + kept);
-  uint64_t buckets = 1;
-  while (buckets * 2 < U) buckets <<= 1;  // slots = 4*buckets >= 2U: load <= 0.5
-  ix->buckets = buckets;
-  ix->table.alloc(4 * buckets);
-  HIPCHK(hipMemsetAsync(ix->table.p, 0xFF, ix->table.bytes(), st));
-  launch_occ_fill(vals, uidx, kpos.p, N, ix->occ.p, st);
-  launch_headers(keys, kpos.p, run_start, U, ix->occ.p, ix->table.p, buckets - 1, k, st);
-  HIPCHK(hipGetLastError());
+  build_kmer_table(ix, k, k, 0, st, ix->table, ix->occ, ix->buckets, ix->n_kmers, ix->n_occ);
+  if (ix->fk)
+    build_kmer_table(ix, ix->fk, k, 2 * (k - ix->fk) + 1, st, ix->f_table, ix->f_occv, ix->f_buckets, ix->f_kmers,
+                     ix->f_occ);
   HIPCHK(hipStreamSynchronize(st));
   ix->build_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
@@ -349,6 +389,9 @@ static void build_device_index(pbgpu_index* ix, text_builder& tb) {
 static pbgpu_status index_common(const pbgpu_index_params* p) {
   if (!p) return fail(PBGPU_ERR_INVALID, "null params");
   if (p->k < 2 || p->k > 31) return fail(PBGPU_ERR_UNSUPPORTED, "k=%u outside [2,31]", p->k);
+  if (p->fine_k > p->k)
+    return fail(PBGPU_ERR_UNSUPPORTED, "fine_k (%u) > k (%u): PSA::search assumes the pattern is at most max_size "
+                "(mer_sa_imp.hpp:366)", p->fine_k, p->k);
   if (p->psa_min >= p->k)
     return fail(PBGPU_ERR_UNSUPPORTED,
                 "psa_min (%u) >= k (%u): the reference's hit order then depends on thread timing (mer_sa_imp.hpp:247)",
@@ -445,7 +488,7 @@ pbgpu_status pbgpu_index_build_fasta(const char* const* paths, size_t n_paths, c
   text_builder tb;
   for (size_t i = 0; i < n_paths; ++i) load_fasta(paths[i], tb);
   std::unique_ptr<pbgpu_index> ix(new pbgpu_index);
-  ix->device = params->device; ix->k = params->k; ix->psa_min = params->psa_min;
+  ix->device = params->device; ix->k = params->k; ix->psa_min = params->psa_min; ix->fk = params->fine_k;
   build_device_index(ix.get(), tb);
   *out = ix.release();
   return PBGPU_OK;
@@ -469,7 +512,7 @@ pbgpu_status pbgpu_index_build(const char* const* names, const char* const* seqs
     tb.end_record(names[i], start);
   }
   std::unique_ptr<pbgpu_index> ix(new pbgpu_index);
-  ix->device = params->device; ix->k = params->k; ix->psa_min = params->psa_min;
+  ix->device = params->device; ix->k = params->k; ix->psa_min = params->psa_min; ix->fk = params->fine_k;
   build_device_index(ix.get(), tb);
   *out = ix.release();
   return PBGPU_OK;
@@ -544,13 +587,73 @@ struct pbgpu_aligner {
   bool have_result = false;
   // stats
   pbgpu_stats acc{};
-  hipEvent_t ev[16]{};
+  hipEvent_t ev[18]{};
   uint64_t hit_budget = 1200000000ull, rec_hint = 0, info_per_chain = 32;
   double chains_per_hit = 1.0 / 48;  // k_group partition estimate, refined after every batch
   dbuf<uint32_t> ovf_list, read_list;
   dbuf<uint8_t> nparts;
   dbuf<uint2> prog;
+  // -F: fine aligner pass (params of k_coords with align_k = fine_k, forward, unfiltered)
+  bool fine = false;
+  AlignParamsDev PF{};
+  LisParams lpf{};
+  dbuf<FineWin> fwin;
+  dbuf<uint64_t> fwk[2], fread_hits;
+  dbuf<uint32_t> fwi[2], fkeys[2], lstart, lend, emit_of;
+  dbuf<int2> X2;
+  // --details: final coarse lists of the last alignment, in sub-batch chain order
+  bool details = false;
+  struct {
+    std::vector<uint32_t> read, sr, nf;
+    std::vector<uint64_t> hoff{0};
+    std::vector<int32_t> hits;
+    std::vector<uint8_t> lis;
+    void clear() { read.clear(); sr.clear(); nf.clear(); hoff.assign(1, 0); hits.clear(); lis.clear(); }
+  } det;
 };
+
+// print_details input (jf_aligner.cc:72-108) of one sub-batch: every (read,
+// super-read) chain's final fwd / bwd lists and the printed lis, marked by
+// walking the lis points (pairs are unique within a list) along the list.
+static void capture_details(pbgpu_aligner* al, uint32_t nch, uint64_t Hs) {
+  hipStream_t st = al->st;
+  std::vector<ChainDesc> ch(nch);
+  std::vector<uint32_t> sl(2ull * nch), ll(2ull * nch);
+  std::vector<int2> X(Hs), pts(Hs);
+  if (nch) {
+    HIPCHK(hipMemcpyAsync(ch.data(), al->chains.p, nch * sizeof(ChainDesc), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(sl.data(), al->slen.p, 2ull * nch * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(ll.data(), al->lisl.p, 2ull * nch * 4, hipMemcpyDeviceToHost, st));
+  }
+  if (Hs) {
+    HIPCHK(hipMemcpyAsync(X.data(), al->X.p, Hs * sizeof(int2), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(pts.data(), al->pts.p, Hs * sizeof(int2), hipMemcpyDeviceToHost, st));
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  auto& D = al->det;
+  for (uint32_t c = 0; c < nch; ++c) {
+    const ChainDesc& d = ch[c];
+    const uint32_t nF = sl[2 * c], nB = sl[2 * c + 1], lf = ll[2 * c], lb = ll[2 * c + 1];
+    const bool fa = lf > lb;  // print_details: fwd only if strictly longer (jf_aligner.cc:77)
+    D.read.push_back(d.read); D.sr.push_back(d.sr); D.nf.push_back(nF);
+    const int2* P = pts.data() + d.hit_base + (fa ? 0 : d.nf);
+    const uint32_t nl = fa ? lf : lb;
+    for (int strand = 0; strand < 2; ++strand) {
+      const int2* L = X.data() + d.hit_base + (strand ? d.nf : 0);
+      const uint32_t n = strand ? nB : nF;
+      uint32_t li = 0;
+      const bool mine = (strand == 0) == fa;
+      for (uint32_t i = 0; i < n; ++i) {
+        D.hits.push_back(L[i].x); D.hits.push_back(L[i].y);
+        const bool in = mine && li < nl && P[li].x == L[i].x && P[li].y == L[i].y;
+        D.lis.push_back(in ? 1 : 0);
+        li += in;
+      }
+      if (mine && li != nl) throw std::runtime_error("details: lis points not found in their list");
+    }
+    D.hoff.push_back(D.lis.size());
+  }
+}
 
 static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd);
 
@@ -563,7 +666,9 @@ pbgpu_status pbgpu_aligner_create(const pbgpu_index* ix, const pbgpu_align_param
     return fail(PBGPU_ERR_INVALID, "max_count must be > 0 (0 means INT_MAX upstream, which is undefined behaviour)");
   if (params->n_unitigs && !params->forward)
     return fail(PBGPU_ERR_INVALID, "Forward flag must be used if passing unitigs lengths");
-  if (params->fine_k) return fail(PBGPU_ERR_UNSUPPORTED, "fine aligner (-F) is not implemented yet");
+  if (params->fine_k && params->fine_k != ix->fk)
+    return fail(PBGPU_ERR_INVALID, "aligner fine_k (%u) != the index's fine sub-index k (%u): build the index with fine_k",
+                params->fine_k, ix->fk);
   if (params->unitigs_k && !params->unitig_lengths)
     return fail(PBGPU_ERR_INVALID, "unitigs_k given without unitig lengths");
   API_TRY
@@ -584,10 +689,17 @@ pbgpu_status pbgpu_aligner_create(const pbgpu_index* ix, const pbgpu_align_param
   P.unitigs_k = params->unitigs_k && params->n_unitigs ? params->unitigs_k : 0;
   P.ul = al->ul.p; P.n_ul = params->unitigs_k ? params->n_unitigs : 0;
   al->lp.W = params->window_size; al->lp.a = params->stretch_factor; al->lp.b = params->stretch_constant;
-  al->lp.C = params->stretch_cap; al->lp.mer_all = 0; al->lp.seq_all = 0;
+  al->lp.C = params->stretch_cap; al->lp.mer_all = 0; al->lp.seq_all = 0; al->lp.ordered = 0;
+  if (params->fine_k) {  // fine_aligner (fine_aligner.hpp:31-37): align_k = fine_k, compute_coords_info(forward = true)
+    al->fine = true;
+    al->PF = P;
+    al->PF.k = params->fine_k; al->PF.forward = 1; al->PF.max_match = 0; al->PF.fine = 1;
+    al->lpf = al->lp;
+    al->lpf.W = 1; al->lpf.mer_all = 1; al->lpf.seq_all = 1;  // lis_align::accept_all, window 1 (fine_aligner.cc:43-46)
+  }
   HIPCHK(hipStreamCreateWithFlags(&al->st, hipStreamNonBlocking));
   for (auto& e : al->ev) HIPCHK(hipEventCreate(&e));
-  al->stats.alloc(ST_N);
+  al->stats.alloc(ST_N + 1);  // + the fine stage's kmers_info capacity counter
   al->info_count.alloc(1);
   al->counters.alloc(128);
   *out = al.release();
@@ -653,6 +765,228 @@ static float ev_ms(hipEvent_t a, hipEvent_t b) {
   return ms;
 }
 
+// Strands (chain, fwd|bwd) in length order -> the LIS tiers (k_lis with
+// 32-bit nodes above LIS_U16_MAX hits, k_lis with 16-bit nodes above
+// LISW_LARGE, k_lis_w below), then the chains in lis-length order in al->perm
+// for k_coords.  restore: k_group's lists need their order restored
+// (k_strand_order / in k_lis_w); lists built in order (the fine aligner's) do
+// not.  timed: record the k_lis slot events.  Returns the chains placed.
+static uint32_t lis_stage(pbgpu_aligner* al, uint32_t nch, uint64_t Hs, const LisParams& lp0, int keep_idx,
+                          bool restore, bool timed) {
+  hipStream_t st = al->st;
+  LisParams lp = lp0;
+  lp.ordered = restore ? 0 : 1;
+  // strands (chain, fwd|bwd) in length order -> k_lis (16-bit nodes; 32-bit for the longest strands)
+  const uint32_t NB = len_buckets();
+  al->hist.ensure(2 * NB);
+  al->perm.ensure(2ull * nch + 1);
+  al->lisl.ensure(2ull * nch + 1);
+  al->slen.ensure(2ull * nch + 1);
+  uint32_t n_big = 0, n_mid = 0, n_w2 = 0, n_w1 = 0;  // items in classes above LIS_U16_MAX / LISW_LARGE / LISW_SMALL / LISW_TINY
+  auto order = [&](int which, uint32_t n_in) -> uint32_t {  // returns the number of items placed
+    HIPCHK(hipMemsetAsync(al->hist.p, 0, NB * 4, st));
+    if (which == 0) launch_strand_order(al->slen.p, n_in, al->hist.p, nullptr, nullptr, 0, st);
+    else launch_chain_order(al->lisl.p, n_in, al->hist.p, nullptr, nullptr, 0, st);
+    std::vector<uint32_t> h(NB), cur(NB);
+    HIPCHK(hipMemcpyAsync(h.data(), al->hist.p, NB * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (getenv("PBGPU_DUMP_LEN_HIST")) {  // diagnostics: length-class histogram of this ordering pass
+      fprintf(stderr, "len_hist %s:", which == 0 ? "strands" : "chains");
+      for (uint32_t b = 0; b < NB; ++b) if (h[b]) fprintf(stderr, " %u:%u", b, h[b]);
+      fprintf(stderr, "\n");
+    }
+    uint32_t acc = 0;
+    for (int b = (int)NB - 1; b >= 1; --b) {  // longest first; bucket 0 = empty
+      cur[b] = acc; acc += h[b];
+      if ((uint32_t)b == big_bucket()) n_big = acc;  // items in buckets >= big_bucket(): > LIS_U16_MAX hits
+      if ((uint32_t)b == lis_class_bounds(1)) n_mid = acc;
+      if ((uint32_t)b == lis_class_bounds(0)) n_w2 = acc;
+      if ((uint32_t)b == lis_class_bounds(3)) n_w1 = acc;
+    }
+    cur[0] = acc;
+    HIPCHK(hipMemcpyAsync(al->hist.p + NB, cur.data(), NB * 4, hipMemcpyHostToDevice, st));
+    if (which == 0) launch_strand_order(al->slen.p, n_in, nullptr, al->hist.p + NB, al->perm.p, 1, st);
+    else launch_chain_order(al->lisl.p, n_in, nullptr, al->hist.p + NB, al->perm.p, 1, st);
+    HIPCHK(hipGetLastError());
+    return acc;
+  };
+  launch_init_slen(al->chains.p, nch, al->slen.p, st);
+  HIPCHK(hipMemsetAsync(al->lisl.p, 0, 2ull * nch * 4, st));
+  const uint32_t n_strands = order(0, 2 * nch);
+  const uint32_t nbig = n_big;
+  if (nbig) al->nodes32.ensure((Hs + 1) * 16);
+  // strands longer than k_lis_w's LDS capacity: restore list order in place first
+  if (restore) launch_strand_order(al->chains.p, al->perm.p, n_mid, al->slen.p, al->X.p, st);
+  if (timed) HIPCHK(hipEventRecord(al->ev[11], st));
+  launch_lis(true, al->chains.p, al->perm.p, nbig, al->slen.p, al->X.p, al->nodes32.p, al->pts.p, al->lisl.p, lp,
+             keep_idx, al->stats.p, st);
+  // 4095 < n <= 65535: lane-per-strand chunked kernel; n <= 4095: wave-per-strand kernels
+  const uint32_t nmid = n_mid, nw2 = n_w2, nw1 = n_w1;
+  launch_lis(false, al->chains.p, al->perm.p + nbig, nmid - nbig, al->slen.p, al->X.p, al->nodes.p, al->pts.p,
+             al->lisl.p, lp, keep_idx, al->stats.p, st);
+  launch_lis_wave(2, al->chains.p, al->perm.p + nmid, nw2 - nmid, al->slen.p, al->X.p, al->nodes.p, al->pts.p,
+                  al->lisl.p, lp, keep_idx, al->stats.p, st);
+  launch_lis_wave(1, al->chains.p, al->perm.p + nw2, nw1 - nw2, al->slen.p, al->X.p, al->nodes.p,
+                  al->pts.p, al->lisl.p, lp, keep_idx, al->stats.p, st);
+  if (timed) HIPCHK(hipEventRecord(al->ev[10], st));  // the timed k_lis slot: tier-0 k_lis_w alone
+  launch_lis_wave(0, al->chains.p, al->perm.p + nw1, n_strands - nw1, al->slen.p, al->X.p, al->nodes.p,
+                  al->pts.p, al->lisl.p, lp, keep_idx, al->stats.p, st);
+  HIPCHK(hipGetLastError());
+  if (timed) HIPCHK(hipEventRecord(al->ev[12], st));
+  // chains in lis-length order -> k_coords; record/info capacity
+  const uint32_t n_fit = order(1, nch);
+  return n_fit;
+}
+
+// Records grouped per read and sorted by (rs, re, ql, sr, emit): al->recs[0..nrec)
+// -> al->recs_sorted, al->rec_off.  timed: event around the sort kernel.
+static void records_stage(pbgpu_aligner* al, uint32_t n, uint32_t nrec, bool timed) {
+  hipStream_t st = al->st;
+  al->rec_per_read.ensure(n); al->rec_cursor.ensure(n);
+  HIPCHK(hipMemsetAsync(al->rec_per_read.p, 0, n * 4, st));
+  HIPCHK(hipMemsetAsync(al->rec_cursor.p, 0, n * 4, st));
+  launch_rec_hist(al->recs.p, nrec, al->rec_per_read.p, st);
+  {
+    struct RecOp {
+      const uint32_t* c; uint64_t n;
+      __host__ __device__ uint64_t operator()(const uint64_t& i) const { return i < n ? (uint64_t)c[i] : 0ull; }
+    };
+    hipcub::CountingInputIterator<uint64_t> cnt0(0);
+    hipcub::TransformInputIterator<uint64_t, RecOp, hipcub::CountingInputIterator<uint64_t>> in(cnt0, RecOp{al->rec_per_read.p, n});
+    size_t tb = 0;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, al->rec_off.p, (uint64_t)n + 1, st));
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(temp_storage(al->tmp, tb), tb, in, al->rec_off.p, (uint64_t)n + 1, st));
+  }
+  al->order.ensure(nrec + 1);
+  al->sort_scratch.ensure(6ull * nrec + 6);
+  al->recs_sorted.ensure(nrec + 1);
+  launch_rec_scatter(al->recs.p, nrec, al->rec_off.p, al->rec_cursor.p, al->order.p, st);
+  if (timed) HIPCHK(hipEventRecord(al->ev[15], st));
+  launch_rec_sort(al->recs.p, al->rec_off.p, al->order.p, al->sort_scratch.p, n, al->recs_sorted.p, st);
+  HIPCHK(hipGetLastError());
+}
+
+// fine_aligner::thread::align_sequence (fine_aligner.cc:38-51) for the whole
+// batch, on the coarse records sorted per read (al->recs_sorted / rec_off):
+// windows -> per-read windowed hit counts -> sub-batches of <= hit_budget hits:
+// hits in list order -> stable sort by (window, strand) -> chains -> LIS
+// (accept_all) -> k_coords (align_k = fine_k, forward, unfiltered) + the
+// hit-less windows -> records.  The fine records replace the coarse ones.
+static void fine_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
+  const pbgpu_index* ix = al->ix;
+  const IndexView v = ix->view(), fv = ix->fine_view();
+  hipStream_t st = al->st;
+  const uint32_t n = (uint32_t)rd->n_reads;
+  const uint32_t nwin = (uint32_t)al->last_records;
+  std::vector<uint64_t> woff(n + 1);
+  HIPCHK(hipMemcpyAsync(woff.data(), al->rec_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, st));
+  // windows sorted by (read, super-read) (the lookup side of prime_frags_pos's std::map)
+  al->fwin.ensure(nwin + 1);
+  al->fwk[0].ensure(nwin + 1); al->fwk[1].ensure(nwin + 1); al->fwi[0].ensure(nwin + 1); al->fwi[1].ensure(nwin + 1);
+  launch_fine_windows(al->recs_sorted.p, nwin, al->fwk[0].p, al->fwi[0].p, 0, rd->off.p, al->PF.k, nullptr, st);
+  {
+    hipcub::DoubleBuffer<uint64_t> dk(al->fwk[0].p, al->fwk[1].p);
+    hipcub::DoubleBuffer<uint32_t> dv(al->fwi[0].p, al->fwi[1].p);
+    size_t tb = 0;
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, dk, dv, nwin, 0, 64, st));
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(temp_storage(al->tmp, tb), tb, dk, dv, nwin, 0, 64, st));
+    launch_fine_windows(al->recs_sorted.p, nwin, nullptr, dv.Current(), 1, rd->off.p, al->PF.k, al->fwin.p, st);
+  }
+  HIPCHK(hipGetLastError());
+  // windowed hits per read
+  al->fread_hits.ensure(n + 1);
+  launch_fine_hits(false, fv, rd->seq.p, rd->off.p, 0, n, al->fwin.p, al->rec_off.p, al->fread_hits.p, nullptr, 0,
+                   nullptr, nullptr, al->stats.p, st);
+  HIPCHK(hipGetLastError());
+  std::vector<uint64_t> rh(n), hoff(n + 1, 0);
+  HIPCHK(hipMemcpyAsync(rh.data(), al->fread_hits.p, (size_t)n * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  for (uint32_t r = 0; r < n; ++r) hoff[r + 1] = hoff[r] + rh[r];
+  const uint64_t budget = std::min<uint64_t>(al->hit_budget, 0xFFFFFFF0ull);
+  uint64_t rec_done = 0, info_done = 0;
+  unsigned long long* info_need = al->stats.p + ST_N;  // scratch slot past the stat slots
+  for (uint32_t r0 = 0; r0 < n;) {
+    uint32_t r1 = r0 + 1;
+    while (r1 < n && hoff[r1 + 1] - hoff[r0] <= budget) ++r1;
+    const uint64_t Hs = hoff[r1] - hoff[r0];
+    if (Hs > 0xFFFFFFF0ull) throw unsupported("a single read has more than 2^32 fine hits");
+    const uint64_t ws0 = woff[r0];
+    const uint32_t nws = (uint32_t)(woff[r1] - ws0);
+    if (nws == 0) { r0 = r1; continue; }
+    // sub-batch-relative hit offsets of its reads
+    std::vector<uint64_t> rel(r1 - r0);
+    for (uint32_t r = r0; r < r1; ++r) rel[r - r0] = hoff[r] - hoff[r0];
+    al->hit_off.ensure(n + 1);
+    HIPCHK(hipMemcpyAsync(al->hit_off.p + r0, rel.data(), rel.size() * 8, hipMemcpyHostToDevice, st));
+    al->fkeys[0].ensure(Hs + 1); al->fkeys[1].ensure(Hs + 1);
+    al->X.ensure(Hs + 1); al->X2.ensure(Hs + 1);
+    launch_fine_hits(true, fv, rd->seq.p, rd->off.p, r0, r1 - r0, al->fwin.p, al->rec_off.p, nullptr, al->hit_off.p,
+                     ws0, al->fkeys[0].p, al->X.p, al->stats.p, st);
+    HIPCHK(hipGetLastError());
+    int nbits = 1;
+    while ((1ull << nbits) < 2ull * nws) ++nbits;
+    {
+      hipcub::DoubleBuffer<uint32_t> dk(al->fkeys[0].p, al->fkeys[1].p);
+      hipcub::DoubleBuffer<uint64_t> dv((uint64_t*)al->X.p, (uint64_t*)al->X2.p);
+      size_t tb = 0;
+      HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, dk, dv, Hs, 0, nbits, st));
+      HIPCHK(hipcub::DeviceRadixSort::SortPairs(temp_storage(al->tmp, tb), tb, dk, dv, Hs, 0, nbits, st));
+      if (dk.Current() != al->fkeys[0].p) al->fkeys[0].swap(al->fkeys[1]);
+      if ((int2*)dv.Current() != al->X.p) al->X.swap(al->X2);
+    }
+    al->lstart.ensure(2ull * nws); al->lend.ensure(2ull * nws);
+    HIPCHK(hipMemsetAsync(al->lstart.p, 0, 2ull * nws * 4, st));
+    HIPCHK(hipMemsetAsync(al->lend.p, 0, 2ull * nws * 4, st));
+    launch_list_bounds(al->fkeys[0].p, Hs, al->lstart.p, al->lend.p, st);
+    al->chains.ensure(nws + 1); al->emit_of.ensure(nws + 1);
+    HIPCHK(hipMemsetAsync(info_need, 0, 8, st));
+    launch_fine_desc(v, al->recs_sorted.p, ws0, nws, al->lstart.p, al->lend.p, al->PF.unitigs_k != 0, al->chains.p,
+                     al->emit_of.p, info_need, st);
+    HIPCHK(hipGetLastError());
+    al->pts.ensure(Hs + 1); al->nodes.ensure((Hs + 1) * 8);
+    const uint32_t n_fit = lis_stage(al, nws, Hs, al->lpf, 0, false, false);
+    unsigned long long need = 0;
+    HIPCHK(hipMemcpyAsync(&need, info_need, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    al->recs.grow_keep(rec_done + nws + 1, rec_done, st);
+    if (al->PF.unitigs_k) {
+      al->info_m.grow_keep(info_done + need + 1, info_done, st);
+      al->info_b.grow_keep(info_done + need + 1, info_done, st);
+    } else {
+      al->info_m.ensure(1); al->info_b.ensure(1);
+    }
+    uint32_t rc32 = (uint32_t)rec_done;
+    HIPCHK(hipMemcpyAsync(al->counters.p + 4, &rc32, 4, hipMemcpyHostToDevice, st));
+    unsigned long long ic = info_done;
+    HIPCHK(hipMemcpyAsync(al->info_count.p, &ic, 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(al->stats.p + ST_REC_OVERFLOW, 0, 8, st));
+    ChainOut CO{};
+    CO.pts = al->pts.p; CO.lisl = al->lisl.p;
+    CO.redo = nullptr; CO.n_redo = al->counters.p + 8;
+    CO.recs = al->recs.p; CO.rec_count = al->counters.p + 4;
+    CO.rec_cap = (uint32_t)std::min<uint64_t>(al->recs.n, 0xFFFFFFFFu);
+    CO.info_m = al->info_m.p; CO.info_b = al->info_b.p; CO.info_count = al->info_count.p; CO.info_cap = al->info_m.n;
+    CO.stats = al->stats.p;
+    CO.emit_of = al->emit_of.p;
+    launch_coords(v, al->PF, al->chains.p, al->perm.p, n_fit, rd->off.p, 0, CO, st);
+    launch_fine_empty(v, al->PF.k, al->chains.p, nws, al->lisl.p, al->emit_of.p, CO, st);
+    HIPCHK(hipGetLastError());
+    uint32_t nrec = 0;
+    unsigned long long ninfo = 0, ovf = 0;
+    HIPCHK(hipMemcpyAsync(&nrec, al->counters.p + 4, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&ninfo, al->info_count.p, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&ovf, al->stats.p + ST_REC_OVERFLOW, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (ovf || nrec != rec_done + nws)
+      throw std::runtime_error("fine aligner: record / kmers_info capacity mismatch");
+    rec_done = nrec; info_done = ninfo;
+    r0 = r1;
+  }
+  al->last_records = rec_done;
+  al->last_info = info_done;
+  records_stage(al, n, (uint32_t)rec_done, false);
+}
+
 static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
   const pbgpu_index* ix = al->ix;
   const IndexView v = ix->view();
@@ -660,6 +994,7 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
   const uint32_t n = (uint32_t)rd->n_reads;
   al->have_result = false;
   al->last_reads = n;
+  al->det.clear();
   al->acc.n_batches++;
   al->acc.n_reads += n;
   al->acc.n_bases += rd->n_bases;
@@ -808,65 +1143,7 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
         continue;
       }
       HIPCHK(hipEventRecord(al->ev[6], st));
-      // strands (chain, fwd|bwd) in length order -> k_lis (16-bit nodes; 32-bit for the longest strands)
-      const uint32_t NB = len_buckets();
-      al->hist.ensure(2 * NB);
-      al->perm.ensure(2ull * nch + 1);
-      al->lisl.ensure(2ull * nch + 1);
-      al->slen.ensure(2ull * nch + 1);
-      uint32_t n_big = 0, n_mid = 0, n_w2 = 0, n_w1 = 0;  // items in classes above LIS_U16_MAX / LISW_LARGE / LISW_SMALL / LISW_TINY
-      auto order = [&](int which, uint32_t n_in) -> uint32_t {  // returns the number of items placed
-        HIPCHK(hipMemsetAsync(al->hist.p, 0, NB * 4, st));
-        if (which == 0) launch_strand_order(al->slen.p, n_in, al->hist.p, nullptr, nullptr, 0, st);
-        else launch_chain_order(al->lisl.p, n_in, al->hist.p, nullptr, nullptr, 0, st);
-        std::vector<uint32_t> h(NB), cur(NB);
-        HIPCHK(hipMemcpyAsync(h.data(), al->hist.p, NB * 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        if (getenv("PBGPU_DUMP_LEN_HIST")) {  // diagnostics: length-class histogram of this ordering pass
-          fprintf(stderr, "len_hist %s:", which == 0 ? "strands" : "chains");
-          for (uint32_t b = 0; b < NB; ++b) if (h[b]) fprintf(stderr, " %u:%u", b, h[b]);
-          fprintf(stderr, "\n");
-        }
-        uint32_t acc = 0;
-        for (int b = (int)NB - 1; b >= 1; --b) {  // longest first; bucket 0 = empty
-          cur[b] = acc; acc += h[b];
-          if ((uint32_t)b == big_bucket()) n_big = acc;  // items in buckets >= big_bucket(): > LIS_U16_MAX hits
-          if ((uint32_t)b == lis_class_bounds(1)) n_mid = acc;
-          if ((uint32_t)b == lis_class_bounds(0)) n_w2 = acc;
-          if ((uint32_t)b == lis_class_bounds(3)) n_w1 = acc;
-        }
-        cur[0] = acc;
-        HIPCHK(hipMemcpyAsync(al->hist.p + NB, cur.data(), NB * 4, hipMemcpyHostToDevice, st));
-        if (which == 0) launch_strand_order(al->slen.p, n_in, nullptr, al->hist.p + NB, al->perm.p, 1, st);
-        else launch_chain_order(al->lisl.p, n_in, nullptr, al->hist.p + NB, al->perm.p, 1, st);
-        HIPCHK(hipGetLastError());
-        return acc;
-      };
-      launch_init_slen(al->chains.p, nch, al->slen.p, st);
-      HIPCHK(hipMemsetAsync(al->lisl.p, 0, 2ull * nch * 4, st));
-      const uint32_t n_strands = order(0, 2 * nch);
-      const uint32_t nbig = n_big;
-      if (nbig) al->nodes32.ensure((Hs + 1) * 16);
-      // strands longer than k_lis_w's LDS capacity: restore list order in place first
-      launch_strand_order(al->chains.p, al->perm.p, n_mid, al->slen.p, al->X.p, st);
-      HIPCHK(hipEventRecord(al->ev[11], st));
-      launch_lis(true, al->chains.p, al->perm.p, nbig, al->slen.p, al->X.p, al->nodes32.p, al->pts.p, al->lisl.p, al->lp,
-                 al->P.max_match, al->stats.p, st);
-      // 4095 < n <= 65535: lane-per-strand chunked kernel; n <= 4095: wave-per-strand kernels
-      const uint32_t nmid = n_mid, nw2 = n_w2, nw1 = n_w1;
-      launch_lis(false, al->chains.p, al->perm.p + nbig, nmid - nbig, al->slen.p, al->X.p, al->nodes.p, al->pts.p,
-                 al->lisl.p, al->lp, al->P.max_match, al->stats.p, st);
-      launch_lis_wave(2, al->chains.p, al->perm.p + nmid, nw2 - nmid, al->slen.p, al->X.p, al->nodes.p, al->pts.p,
-                      al->lisl.p, al->lp, al->P.max_match, al->stats.p, st);
-      launch_lis_wave(1, al->chains.p, al->perm.p + nw2, nw1 - nw2, al->slen.p, al->X.p, al->nodes.p,
-                      al->pts.p, al->lisl.p, al->lp, al->P.max_match, al->stats.p, st);
-      HIPCHK(hipEventRecord(al->ev[10], st));  // the timed k_lis slot: tier-0 k_lis_w alone
-      launch_lis_wave(0, al->chains.p, al->perm.p + nw1, n_strands - nw1, al->slen.p, al->X.p, al->nodes.p,
-                      al->pts.p, al->lisl.p, al->lp, al->P.max_match, al->stats.p, st);
-      HIPCHK(hipGetLastError());
-      HIPCHK(hipEventRecord(al->ev[12], st));
-      // chains in lis-length order -> k_coords; record/info capacity
-      const uint32_t n_fit = order(1, nch);
+      const uint32_t n_fit = lis_stage(al, nch, Hs, al->lp, al->P.max_match, true, true);
       const uint64_t rec_need = rec_done + (uint64_t)nch * (al->P.max_match ? 2 : 1) + 1024 * (attempt + 1);
       al->recs.grow_keep(std::max<uint64_t>(rec_need, al->rec_hint), rec_done, st);
       if (al->P.unitigs_k) {
@@ -884,13 +1161,14 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
       if (al->P.max_match) { al->redo[0].ensure(nch + 1); al->redo[1].ensure(nch + 1); al->redo[2].ensure(nch + 1); }
       uint32_t* n_redo = al->counters.p + 8;  // [8] redo count, [9] small items, [10] big items
       HIPCHK(hipMemsetAsync(n_redo, 0, 12, st));
-      ChainOut CO;
+      ChainOut CO{};
       CO.pts = al->pts.p; CO.lisl = al->lisl.p;
       CO.redo = al->P.max_match ? al->redo[0].p : nullptr; CO.n_redo = n_redo;
       CO.recs = al->recs.p; CO.rec_count = al->counters.p + 4;
       CO.rec_cap = (uint32_t)std::min<uint64_t>(al->recs.n, 0xFFFFFFFFu);
       CO.info_m = al->info_m.p; CO.info_b = al->info_b.p; CO.info_count = al->info_count.p; CO.info_cap = al->info_m.n;
       CO.stats = al->stats.p;
+      CO.emit_of = nullptr;  // coarse: the round index is the emission index
       HIPCHK(hipEventRecord(al->ev[13], st));
       launch_coords(v, al->P, al->chains.p, al->perm.p, n_fit, rd->off.p, 0, CO, st);
       HIPCHK(hipGetLastError());
@@ -940,6 +1218,7 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
       k_ms[PBGPU_KERNEL_COORDS] += ev_ms(al->ev[13], al->ev[14]);
       k_n[PBGPU_KERNEL_GROUP]++; k_n[PBGPU_KERNEL_LIS]++; k_n[PBGPU_KERNEL_COORDS]++;
       if (ovf == 0 && nrec <= al->recs.n) {
+        if (al->details) capture_details(al, nch, Hs);
         rec_done = nrec; info_done = ninfo;
         n_chains += sub[0]; n_tests += sub[1];
         if (Hs) al->chains_per_hit = std::max(1e-4, 1.1 * (double)nch / (double)Hs);
@@ -955,31 +1234,14 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
   al->last_records = rec_done;
   al->last_info = info_done;
   HIPCHK(hipEventRecord(al->ev[3], st));
-  // ------------------------------------------------------------- records
   const uint32_t nrec = (uint32_t)al->last_records;
-  al->rec_per_read.ensure(n); al->rec_cursor.ensure(n);
-  HIPCHK(hipMemsetAsync(al->rec_per_read.p, 0, n * 4, st));
-  HIPCHK(hipMemsetAsync(al->rec_cursor.p, 0, n * 4, st));
-  launch_rec_hist(al->recs.p, nrec, al->rec_per_read.p, st);
-  {
-    struct RecOp {
-      const uint32_t* c; uint64_t n;
-      __host__ __device__ uint64_t operator()(const uint64_t& i) const { return i < n ? (uint64_t)c[i] : 0ull; }
-    };
-    hipcub::CountingInputIterator<uint64_t> cnt0(0);
-    hipcub::TransformInputIterator<uint64_t, RecOp, hipcub::CountingInputIterator<uint64_t>> in(cnt0, RecOp{al->rec_per_read.p, n});
-    size_t tb = 0;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, al->rec_off.p, (uint64_t)n + 1, st));
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(temp_storage(al->tmp, tb), tb, in, al->rec_off.p, (uint64_t)n + 1, st));
-  }
-  al->order.ensure(nrec + 1);
-  al->sort_scratch.ensure(6ull * nrec + 6);
-  al->recs_sorted.ensure(nrec + 1);
-  launch_rec_scatter(al->recs.p, nrec, al->rec_off.p, al->rec_cursor.p, al->order.p, st);
-  HIPCHK(hipEventRecord(al->ev[15], st));
-  launch_rec_sort(al->recs.p, al->rec_off.p, al->order.p, al->sort_scratch.p, n, al->recs_sorted.p, st);
-  HIPCHK(hipGetLastError());
+  records_stage(al, n, nrec, true);
   HIPCHK(hipEventRecord(al->ev[4], st));
+  if (al->fine) {
+    HIPCHK(hipEventRecord(al->ev[16], st));
+    fine_stage(al, rd);
+    HIPCHK(hipEventRecord(al->ev[17], st));
+  }
   unsigned long long sv[ST_N];
   HIPCHK(hipMemcpyAsync(sv, al->stats.p, sizeof sv, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
@@ -988,6 +1250,11 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
   al->acc.n_records += nrec;
   al->acc.g0_kept += sv[ST_G0_KEPT]; al->acc.g0_hits += sv[ST_G0_HITS]; al->acc.g0_chains += sv[ST_G0_CHAINS];
   al->acc.l0_hits += sv[ST_L0_HITS]; al->acc.l0_strands += sv[ST_L0_STRANDS];
+  if (al->fine) {
+    al->acc.n_fine_hits += sv[ST_FINE_HITS];
+    al->acc.n_fine_windows += nrec;
+    al->acc.ms_fine += ev_ms(al->ev[16], al->ev[17]);
+  }
   al->acc.ms_seed += ev_ms(al->ev[0], al->ev[1]);
   al->acc.ms_group += ms_group;
   al->acc.ms_lis += ms_lis;
@@ -1037,6 +1304,109 @@ pbgpu_status pbgpu_coords_free(pbgpu_coords_batch* c) {
   if (!c) return PBGPU_OK;
   delete reinterpret_cast<coords_holder*>(c);  // c is the first member
   return PBGPU_OK;
+}
+
+pbgpu_status pbgpu_aligner_set_details(pbgpu_aligner* al, int enable) {
+  if (!al) return fail(PBGPU_ERR_INVALID, "null argument");
+  al->details = enable != 0;
+  return PBGPU_OK;
+}
+
+}  // extern "C"
+
+struct details_holder {
+  pbgpu_details_batch d{};
+  std::vector<uint64_t> roff, hoff;
+  std::vector<uint32_t> sr, nf;
+  std::vector<int32_t> hits;
+  std::vector<uint8_t> lis;
+};
+
+extern "C" {
+
+pbgpu_status pbgpu_download_details(pbgpu_aligner* al, pbgpu_details_batch** out) {
+  if (!al || !out) return fail(PBGPU_ERR_INVALID, "null argument");
+  if (!al->have_result || !al->details) return fail(PBGPU_ERR_INVALID, "no details (enable them before aligning)");
+  API_TRY
+  std::unique_ptr<details_holder> h(new details_holder);
+  const auto& D = al->det;
+  const uint64_t n = al->last_reads, nl = D.read.size();
+  // lists grouped by read, first-hit (chain) order within a read
+  h->roff.assign(n + 1, 0);
+  for (uint64_t i = 0; i < nl; ++i) h->roff[D.read[i] + 1]++;
+  for (uint64_t r = 0; r < n; ++r) h->roff[r + 1] += h->roff[r];
+  std::vector<uint64_t> cur(h->roff.begin(), h->roff.end() - 1), order(nl);
+  for (uint64_t i = 0; i < nl; ++i) order[cur[D.read[i]]++] = i;
+  h->sr.resize(nl); h->nf.resize(nl); h->hoff.resize(nl + 1); h->hoff[0] = 0;
+  h->hits.resize(D.hits.size()); h->lis.resize(D.lis.size());
+  for (uint64_t j = 0; j < nl; ++j) {
+    const uint64_t i = order[j], a = D.hoff[i], b = D.hoff[i + 1], o = h->hoff[j];
+    h->sr[j] = D.sr[i]; h->nf[j] = D.nf[i];
+    std::copy(D.hits.begin() + 2 * a, D.hits.begin() + 2 * b, h->hits.begin() + 2 * o);
+    std::copy(D.lis.begin() + a, D.lis.begin() + b, h->lis.begin() + o);
+    h->hoff[j + 1] = o + (b - a);
+  }
+  auto& d = h->d;
+  d.n_reads = n; d.n_lists = nl; d.n_hits = h->lis.size();
+  d.read_offsets = h->roff.data(); d.list_sr = h->sr.data(); d.hit_offsets = h->hoff.data();
+  d.n_fwd = h->nf.data(); d.hits = h->hits.data(); d.in_lis = h->lis.data();
+  *out = &h.release()->d;
+  return PBGPU_OK;
+  API_CATCH
+}
+
+pbgpu_status pbgpu_details_free(pbgpu_details_batch* d) {
+  delete reinterpret_cast<details_holder*>(d);  // d is the first member
+  return PBGPU_OK;
+}
+
+// print_details (jf_aligner.cc:72-108)
+pbgpu_status pbgpu_format_details(const pbgpu_index* ix, const pbgpu_details_batch* d, const char* const* hdrs,
+                                  int threads, char** text, uint64_t* len) {
+  if (!ix || !d || !text || !len || (d->n_reads && !hdrs)) return fail(PBGPU_ERR_INVALID, "null argument");
+  API_TRY
+  const uint64_t n = d->n_reads;
+  if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
+  std::vector<std::string> parts(std::max<uint64_t>(1, (uint64_t)threads * 4));
+  const uint64_t np = parts.size();
+  std::atomic<uint64_t> next(0);
+  auto work = [&]() {
+    char buf[64];
+    for (;;) {
+      const uint64_t pi = next.fetch_add(1);
+      if (pi >= np) break;
+      std::string& o = parts[pi];
+      for (uint64_t r = n * pi / np; r < n * (pi + 1) / np; ++r) {
+        const char* h = hdrs[r];
+        const size_t nl = strcspn(h, " \t\n\v\f\r");
+        for (uint64_t l = d->read_offsets[r]; l < d->read_offsets[r + 1]; ++l) {
+          o.append(h, nl); o += ' '; o += ix->name_fwd[d->list_sr[l]];
+          const uint64_t a = d->hit_offsets[l], e = d->hit_offsets[l + 1], m = a + d->n_fwd[l];
+          uint64_t fi = a, bi = m;
+          while (fi < m || bi < e) {
+            const uint64_t i = (fi < m && (bi == e || d->hits[2 * fi] <= d->hits[2 * bi])) ? fi++ : bi++;
+            const int w = snprintf(buf, sizeof buf, d->in_lis[i] ? " [%d:%d]" : " %d:%d", d->hits[2 * i], d->hits[2 * i + 1]);
+            o.append(buf, (size_t)w);
+          }
+          o += '\n';
+        }
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < threads; ++t) th.emplace_back(work);
+  work();
+  for (auto& t : th) t.join();
+  uint64_t total = 0;
+  for (auto& p : parts) total += p.size();
+  char* t = (char*)malloc(total + 1);
+  if (!t) return fail(PBGPU_ERR_NOMEM, "host allocation failed");
+  uint64_t o = 0;
+  for (auto& p : parts) { memcpy(t + o, p.data(), p.size()); o += p.size(); }
+  t[o] = 0;
+  *text = t; *len = o;
+  return PBGPU_OK;
+  API_CATCH
 }
 
 pbgpu_status pbgpu_align_batch(pbgpu_aligner* al, const pbgpu_read_batch* b, pbgpu_coords_batch** out) {

@@ -46,6 +46,15 @@ struct AlignParamsDev {
   uint32_t unitigs_k;
   const int32_t* ul;
   uint64_t n_ul;
+  int32_t fine;            // fine_aligner pass: every chain emits a record, no filters (fine_aligner.cc:43-48)
+};
+
+// fine_aligner window (sr_local_ml, fine_aligner.hpp:12-17) of one coarse
+// record: implied first / last start base of a k-mer in the read.  Sorted by
+// (read, super-read); w = the coarse record (list id) it belongs to.
+struct FineWin {
+  uint32_t sr, w;
+  double begin, end;
 };
 
 // kept k-mer record, one per kept PB k-mer, in read order
@@ -91,6 +100,7 @@ enum StatSlot {
   ST_REC_OVERFLOW, ST_INFO_USED, ST_GROUP_OVERFLOW,
   ST_G0_KEPT, ST_G0_HITS, ST_G0_CHAINS,  // work completed by first-tier (4-wave LDS) k_group launches
   ST_L0_HITS, ST_L0_STRANDS,             // work of the tier-0 (n <= 255) k_lis_w launches
+  ST_FINE_HITS,                          // fine aligner: windowed hits
   ST_N
 };
 
@@ -109,7 +119,8 @@ struct GroupOut {
 struct LisParams {
   uint32_t W;
   double a, b, C;   // affine_capped; seq uses linear(a)
-  int mer_all, seq_all;
+  int mer_all, seq_all;  // accept_all (lis_align.hpp) for the step / whole-chain test (fine aligner)
+  int ordered;           // lists are already in list order (no k_group order restoration)
 };
 
 struct ChainOut {
@@ -125,6 +136,7 @@ struct ChainOut {
   unsigned long long* info_count;
   uint64_t info_cap;
   unsigned long long* stats;
+  const uint32_t* emit_of;  // fine pass: per chain, the emission index of its coarse record (else null)
 };
 
 }  // namespace pbgpu

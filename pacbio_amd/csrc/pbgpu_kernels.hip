@@ -140,27 +140,41 @@ DEV bool table_lookup(const IndexView& ix, uint64_t key, uint64_t& payload, uint
 }
 
 // ============================================================ index build
-__global__ void k_build_keys(IndexView ix, uint64_t N, uint64_t* keys, uint64_t* vals) {
-  const uint32_t k = ix.k;
+// Sort keys, one per text position x in [0, N), N = n - km + 1:
+//   (canonical km-mer << 1 | orientation) << ebits | extension
+// ebits = 0 for the coarse index (km = k: occurrences in descending x, the SA
+// tie-break of mer_sa_imp.hpp:363).  The fine (-F) sub-index (km = fine_k < K
+// = k) appends the K - km bases after the occurrence, zero-padded past n, and
+// a "full" bit (x + K <= n): the SA order of a pattern shorter than max_size
+// (sort_one_mer, mer_sa_imp.hpp:351-364: extension lexicographic, a truncated
+// one first, then x descending).  Positions are enumerated in descending
+// order so the stable radix sort keeps x descending among equal keys.
+__global__ void k_build_keys(IndexView ix, uint32_t km, uint32_t K, uint32_t ebits, uint64_t N, uint64_t* keys,
+                             uint64_t* vals) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < N; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t x = N - 1 - i;  // descending positions => stable sort keeps x desc
-    const uint64_t f = text_kmer(ix.text, x, k);
-    const uint64_t r = revcomp(f, k);
+    const uint64_t x = N - 1 - i;
+    const uint64_t f = text_kmer(ix.text, x, km);
+    const uint64_t r = revcomp(f, km);
     const uint64_t canon = f < r ? f : r;
     const uint64_t obit = f > r ? 1 : 0;
     // SR holding x: upper_bound(sr_start, x) - 1 (pos_iterator, superread_parser.hpp:110-140)
     uint32_t lo = 0, hi = ix.n_sr + 1;
     while (lo < hi) { uint32_t m = (lo + hi) >> 1; if (ix.sr_start[m] <= x) lo = m + 1; else hi = m; }
     const uint32_t s = lo - 1;
-    const bool cross = x + k > ix.sr_start[s + 1];
-    keys[i] = (canon << 1) | obit;
+    const bool cross = x + km > ix.sr_start[s + 1];
+    uint64_t key = (canon << 1) | obit;
+    if (ebits) {
+      const uint64_t ext = K > km ? text_kmer(ix.text, x + km, K - km) : 0;  // text is zero past n
+      key = (key << ebits) | (ext << 1) | (x + K <= ix.n ? 1u : 0u);
+    }
+    keys[i] = key;
     vals[i] = cross ? ~0ull : (((uint64_t)s << 32) | (uint32_t)(x - ix.sr_start[s] + 1));
   }
 }
 
-__global__ void k_runs(const uint64_t* keys, const uint64_t* uidx, uint64_t N, uint64_t* run_start) {
+__global__ void k_runs(const uint64_t* keys, const uint64_t* uidx, uint64_t N, uint32_t sh, uint64_t* run_start) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < N; i += (uint64_t)gridDim.x * blockDim.x) {
-    const bool head = i == 0 || (keys[i] >> 1) != (keys[i - 1] >> 1);
+    const bool head = i == 0 || (keys[i] >> sh) != (keys[i - 1] >> sh);
     if (head) run_start[uidx[i] - 1] = i;
   }
 }
@@ -173,13 +187,13 @@ __global__ void k_occ_fill(const uint64_t* vals, const uint64_t* uidx, const uin
 }
 
 __global__ void k_headers(const uint64_t* keys, const uint64_t* kpos, const uint64_t* run_start, uint64_t U,
-                          uint64_t* occ, ulonglong2* table, uint64_t bucket_mask, uint32_t k) {
+                          uint64_t* occ, ulonglong2* table, uint64_t bucket_mask, uint32_t k, uint32_t ebits) {
   for (uint64_t u = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; u < U; u += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t s = run_start[u], e = run_start[u + 1];
-    const uint64_t canon = keys[s] >> 1;
+    const uint64_t canon = keys[s] >> (ebits + 1);
     const bool pal = canon == revcomp(canon, k);
     uint64_t lo = s, hi = e;  // first index with orientation bit set
-    while (lo < hi) { uint64_t m = (lo + hi) >> 1; if (keys[m] & 1) hi = m; else lo = m + 1; }
+    while (lo < hi) { uint64_t m = (lo + hi) >> 1; if ((keys[m] >> ebits) & 1) hi = m; else lo = m + 1; }
     const uint64_t nA = kpos[lo] - kpos[s], nB = kpos[e] - kpos[lo];
     const uint64_t hb = 2 * u + kpos[s];
     const uint64_t count = (e - s) * (pal ? 2 : 1);
@@ -1106,8 +1120,9 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
     // ---- list order: k_group leaves each 256-hit step's run of a list unordered.
     // Odd-even transposition in LDS until a round swaps nothing (an ordered strand
     // costs one compare per element); written back to X when anything moved, for
-    // k_discard and the --max-match redo rounds.
-    {
+    // k_discard and the --max-match redo rounds.  The fine aligner's lists come in
+    // order (and follow another order rule), so they skip this.
+    if (!lp.ordered) {
       bool moved = false;
       for (;;) {
         bool sw = false;
@@ -1355,6 +1370,7 @@ DEV bool coords_finish(const AlignParamsDev& P, uint32_t rl, Rec& R) {
   } else {
     R.qe = (int32_t)((uint32_t)R.qe + k - 1u);
   }
+  if (P.fine) return true;  // fine_aligner.cc:47-48 pushes every window's info unfiltered
   if (fabs(R.stretch) == 0.0) return false;
   const double drl = (double)rl;
   double vs = __dadd_rn(R.stretch, R.offset);
@@ -1408,7 +1424,7 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
   R.nb_mers = (int32_t)nl; R.pb_cons = 0; R.sr_cons = 0; R.pb_cover = k; R.sr_cover = k;
   R.ql = act ? (uint32_t)(ix.sr_start[d.sr + 1] - ix.sr_start[d.sr]) : 0;
   R.sr = d.sr; R.read = d.read; R.flags = (P.forward && !fwd_align) ? 2u : 0u;
-  R.n_info = 0; R.reserved = 0; R.info_off = 0; R.emit = emit;
+  R.n_info = 0; R.reserved = 0; R.info_off = 0; R.emit = O.emit_of ? (act ? O.emit_of[c] : 0u) : emit;
   R.stretch = 0; R.offset = 0; R.avg_err = 0;
   // kmers_info setup (pb_aligner.cc:62-81): unitig list of the name used for the record
   uint32_t u0 = 0, nsz = 0;
@@ -1529,6 +1545,206 @@ __global__ void k_init_slen(const ChainDesc* __restrict__ chains, uint32_t n, ui
   }
 }
 
+// ============================================================= fine (-F)
+// fine_aligner::thread::align_sequence (fine_aligner.cc:38-51): one window per
+// coarse record (prime_frags_pos, fine_aligner.hpp:50-58), every fine_k-mer of
+// the read looked up in the fine sub-index with no SSR / toggle / count
+// filter, each occurrence kept in every window of its super-read whose
+// [begin, end] holds the k-mer's pb offset (fetch_local_super_reads,
+// fine_aligner.cc:7-36).  The windowed hits then go through the same LIS
+// (accept_all) and k_coords (forward, no filters) as the coarse chains.
+
+// windows sorted by (read, super-read): keys, then FineWin records
+__global__ void k_fine_win_keys(const Rec* __restrict__ recs, uint32_t n, uint64_t* keys, uint32_t* idx) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    keys[i] = (uint64_t)recs[i].read << 32 | recs[i].sr;
+    idx[i] = i;
+  }
+}
+__global__ void k_fine_win_fill(const Rec* __restrict__ recs, const uint32_t* __restrict__ idx, uint32_t n,
+                                const uint64_t* __restrict__ roff, uint32_t fk, FineWin* __restrict__ out) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t w = idx[i];
+    const Rec R = recs[w];
+    const double rl = (double)(roff[R.read + 1] - roff[R.read]);
+    // begin = max(0, stretch + offset - avg_err); end = min(rl, stretch * ql + offset + avg_err - align_k)
+    const double b = __dadd_rn(__dadd_rn(R.stretch, R.offset), -R.avg_err);
+    const double e = __dadd_rn(__dadd_rn(__dadd_rn(__dmul_rn(R.stretch, (double)R.ql), R.offset), R.avg_err), -(double)fk);
+    FineWin W;
+    W.sr = R.sr; W.w = w;
+    W.begin = 0.0 < b ? b : 0.0;
+    W.end = e < rl ? e : rl;
+    out[i] = W;
+  }
+}
+
+constexpr int FINE_BLOCK = 256;
+constexpr uint32_t FINE_LDS_WIN = 4096, FINE_BITS = 1u << 16;
+DEV uint32_t fine_hash(uint32_t sr) { return (sr * 0x9E3779B1u) >> 16; }
+
+// One workgroup per read, one fine_k-mer per thread and step.  EMIT = false:
+// the read's windowed hit count.  EMIT = true: each step counts its threads'
+// hits, scans, and writes them in (k-mer, occurrence) order -- the list
+// order of fetch_local_super_reads -- as (list key, (pb offset, sr offset)),
+// list key = 2 * window + (bwd).  A stable sort by key then yields every
+// window's fwd and bwd lists in order.
+template <bool EMIT>
+__global__ __launch_bounds__(FINE_BLOCK) void k_fine_hits(IndexView fx, const uint8_t* __restrict__ seq,
+                                                          const uint64_t* __restrict__ roff, uint32_t r0,
+                                                          const FineWin* __restrict__ win,
+                                                          const uint64_t* __restrict__ woff,
+                                                          uint64_t* __restrict__ read_hits,
+                                                          const uint64_t* __restrict__ hit_off, uint64_t w_sub0,
+                                                          uint32_t* __restrict__ keys, int2* __restrict__ vals,
+                                                          unsigned long long* stats) {
+  __shared__ uint32_t s_bits[FINE_BITS / 32];
+  __shared__ uint32_t s_sr[FINE_LDS_WIN];
+  __shared__ uint32_t s_tmp[FINE_BLOCK / 64];
+  __shared__ uint64_t s_tmp64[FINE_BLOCK / 64];
+  const uint32_t r = r0 + blockIdx.x;
+  const int tid = threadIdx.x;
+  const uint64_t w0 = woff[r];
+  const uint32_t nw = (uint32_t)(woff[r + 1] - w0);
+  if (nw == 0) {
+    if (!EMIT && tid == 0) read_hits[r] = 0;
+    return;
+  }
+  for (uint32_t i = tid; i < FINE_BITS / 32; i += FINE_BLOCK) s_bits[i] = 0;
+  __syncthreads();
+  const bool lds = nw <= FINE_LDS_WIN;
+  for (uint32_t i = tid; i < nw; i += FINE_BLOCK) {
+    const uint32_t sr = win[w0 + i].sr, h = fine_hash(sr);
+    atomicOr(&s_bits[h >> 5], 1u << (h & 31));
+    if (lds) s_sr[i] = sr;
+  }
+  __syncthreads();
+  auto sr_at = [&](uint32_t i) -> uint32_t { return lds ? s_sr[i] : win[w0 + i].sr; };
+  const uint64_t base = roff[r];
+  const int64_t L = (int64_t)(roff[r + 1] - base);
+  const uint32_t k = fx.k;
+  const uint32_t hs = 2 * (k - 1);
+  uint64_t out = EMIT ? hit_off[r] : 0, total = 0;
+  for (int64_t t0 = 0; t0 < L; t0 += FINE_BLOCK) {
+    const int64_t p = t0 + tid;  // k-mer start, 0-based
+    bool valid = p + (int64_t)k <= L;
+    uint64_t m = 0, rm = 0;
+    if (valid) {
+      for (uint32_t j = 0; j < k; ++j) {
+        const int c = base_code(seq[base + p + j]);
+        if (c < 0) { valid = false; break; }
+        m = (m << 2) | (uint64_t)c;
+        rm = (rm >> 2) | ((uint64_t)(3 - c) << hs);
+      }
+    }
+    uint64_t ptr = 0;
+    bool found = false;
+    if (valid) {
+      uint64_t payload; uint32_t pr = 0;
+      found = table_lookup(fx, m < rm ? m : rm, payload, pr);
+      ptr = payload >> 24;
+    }
+    const int32_t o = (int32_t)(p + 1);  // parser.offset<0>(), 1-based
+    const bool canon = m < rm;
+    // occ(a) then occ(b), a = the canonical k-mer (find_pos_size, superread_parser.hpp:183-192)
+    auto walk = [&](auto&& emit) {
+      if (!found) return;
+      const uint64_t h0 = fx.occ[ptr], h1 = fx.occ[ptr + 1];
+      const bool pal = (h0 >> 32) & 1;
+      const uint32_t nA = (uint32_t)h1, nB = (uint32_t)(h1 >> 32);
+      for (int half = 0; half < 2; ++half) {
+        const bool useB = half && !pal;
+        const uint64_t lst = ptr + 2 + (useB ? nA : 0);
+        const uint32_t nl = useB ? nB : nA;
+        for (uint32_t j = 0; j < nl; ++j) {
+          const uint64_t v = fx.occ[lst + j];
+          const uint32_t sr = (uint32_t)(v >> 32), h = fine_hash(sr);
+          if (!((s_bits[h >> 5] >> (h & 31)) & 1u)) continue;
+          uint32_t lo = 0, hi = nw;
+          while (lo < hi) { const uint32_t md = (lo + hi) >> 1; if (sr_at(md) < sr) lo = md + 1; else hi = md; }
+          if (lo == nw || sr_at(lo) != sr) continue;
+          const int32_t off = (int32_t)(uint32_t)v;
+          const int32_t it_off = half ? -off : off;
+          const int32_t fin = canon ? it_off : -it_off;
+          for (uint32_t q = lo; q < nw && sr_at(q) == sr; ++q) {
+            const FineWin W = win[w0 + q];
+            if ((double)o >= W.begin && (double)o <= W.end) emit(W.w, fin);
+          }
+        }
+      }
+    };
+    uint32_t cnt = 0;
+    walk([&](uint32_t, int32_t) { ++cnt; });
+    if constexpr (EMIT) {
+      uint32_t tot;
+      uint64_t at = out + block_excl_scan<FINE_BLOCK>(cnt, s_tmp, tot);
+      walk([&](uint32_t w, int32_t fin) {
+        keys[at] = 2u * (uint32_t)(w - w_sub0) + (fin < 0 ? 1u : 0u);
+        vals[at] = make_int2(o, fin);
+        ++at;
+      });
+      out += tot;
+      total += tot;
+    } else {
+      total += cnt;
+    }
+  }
+  if constexpr (EMIT) {
+    if (tid == 0 && total) atomicAdd(&stats[ST_FINE_HITS], (unsigned long long)total);
+  } else {
+    const uint64_t t = block_sum_u64<FINE_BLOCK>(total, s_tmp64);
+    if (tid == 0) read_hits[r] = t;
+  }
+}
+
+// first / one-past-last position of every list key in the sorted hits
+__global__ void k_list_bounds(const uint32_t* __restrict__ keys, uint64_t G, uint32_t* lstart, uint32_t* lend) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < G; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t key = keys[i];
+    if (i == 0 || keys[i - 1] != key) lstart[key] = (uint32_t)i;
+    if (i + 1 == G || keys[i + 1] != key) lend[key] = (uint32_t)(i + 1);
+  }
+}
+
+// one chain per window (its coarse record): lists, emission index, kmers_info capacity
+__global__ void k_fine_desc(IndexView ix, const Rec* __restrict__ recs, uint64_t w_sub0, uint32_t nwin,
+                            const uint32_t* __restrict__ lstart, const uint32_t* __restrict__ lend, int with_info,
+                            ChainDesc* chains, uint32_t* emit_of, unsigned long long* info_need) {
+  uint64_t need = 0;
+  for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < nwin; c += gridDim.x * blockDim.x) {
+    const Rec R = recs[w_sub0 + c];
+    const uint32_t nf = lend[2 * c] - lstart[2 * c], nb = lend[2 * c + 1] - lstart[2 * c + 1];
+    ChainDesc d;
+    d.read = R.read; d.sr = R.sr; d.nf = nf; d.nb = nb;
+    d.hit_base = nf ? lstart[2 * c] : lstart[2 * c + 1];
+    chains[c] = d;
+    emit_of[c] = R.emit;
+    const uint32_t nsz = ix.sr_uoff[R.sr + 1] - ix.sr_uoff[R.sr];
+    if (with_info && nsz && (nf || nb)) need += 2 * nsz - 1;
+  }
+  need = wave_sum_u64(need);
+  if (lane_id() == 0 && need) atomicAdd(info_need, (unsigned long long)need);
+}
+
+// windows without a hit: compute_coords_info returns right after the ctor
+// (pb_aligner.cc:27) and the record is still pushed (fine_aligner.cc:47).  Its
+// rs/re/qs/qe are uninitialized upstream; they are 0 here (as in the oracle).
+__global__ void k_fine_empty(IndexView ix, uint32_t k, const ChainDesc* __restrict__ chains, uint32_t n,
+                             const uint32_t* __restrict__ lisl, const uint32_t* __restrict__ emit_of, ChainOut O) {
+  for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x) {
+    if (lisl[2 * c] | lisl[2 * c + 1]) continue;
+    const ChainDesc d = chains[c];
+    Rec R;
+    R.rs = R.re = R.qs = R.qe = 0; R.nb_mers = 0;
+    R.pb_cons = R.sr_cons = 0; R.pb_cover = R.sr_cover = k;
+    R.ql = (uint32_t)(ix.sr_start[d.sr + 1] - ix.sr_start[d.sr]);
+    R.sr = d.sr; R.read = d.read; R.emit = emit_of[c]; R.flags = 0; R.n_info = 0; R.reserved = 0; R.info_off = 0;
+    R.stretch = 0; R.offset = 0; R.avg_err = 0;
+    const uint32_t ri = atomicAdd(O.rec_count, 1u);
+    if (ri < O.rec_cap) O.recs[ri] = R;
+    else atomicAdd(&O.stats[ST_REC_OVERFLOW], 1ull);
+  }
+}
+
 // =============================================================== records
 __global__ void k_rec_hist(const Rec* recs, uint32_t n, uint32_t* per_read) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
@@ -1621,19 +1837,20 @@ __global__ __launch_bounds__(BLOCK) void k_rec_sort(const Rec* __restrict__ recs
 // ====================================================== launch wrappers
 namespace pbgpu {
 
-void launch_build_keys(IndexView ix, uint64_t N, uint64_t* keys, uint64_t* vals, hipStream_t st) {
-  hipLaunchKernelGGL(k_build_keys, dim3(4096), dim3(256), 0, st, ix, N, keys, vals);
+void launch_build_keys(IndexView ix, uint32_t km, uint32_t K, uint32_t ebits, uint64_t N, uint64_t* keys, uint64_t* vals,
+                       hipStream_t st) {
+  hipLaunchKernelGGL(k_build_keys, dim3(4096), dim3(256), 0, st, ix, km, K, ebits, N, keys, vals);
 }
-void launch_runs(const uint64_t* keys, const uint64_t* uidx, uint64_t N, uint64_t* run_start, hipStream_t st) {
-  hipLaunchKernelGGL(k_runs, dim3(4096), dim3(256), 0, st, keys, uidx, N, run_start);
+void launch_runs(const uint64_t* keys, const uint64_t* uidx, uint64_t N, uint32_t sh, uint64_t* run_start, hipStream_t st) {
+  hipLaunchKernelGGL(k_runs, dim3(4096), dim3(256), 0, st, keys, uidx, N, sh, run_start);
 }
 void launch_occ_fill(const uint64_t* vals, const uint64_t* uidx, const uint64_t* kpos, uint64_t N, uint64_t* occ,
                      hipStream_t st) {
   hipLaunchKernelGGL(k_occ_fill, dim3(4096), dim3(256), 0, st, vals, uidx, kpos, N, occ);
 }
 void launch_headers(const uint64_t* keys, const uint64_t* kpos, const uint64_t* run_start, uint64_t U, uint64_t* occ,
-                    ulonglong2* table, uint64_t bucket_mask, uint32_t k, hipStream_t st) {
-  hipLaunchKernelGGL(k_headers, dim3(4096), dim3(256), 0, st, keys, kpos, run_start, U, occ, table, bucket_mask, k);
+                    ulonglong2* table, uint64_t bucket_mask, uint32_t k, uint32_t ebits, hipStream_t st) {
+  hipLaunchKernelGGL(k_headers, dim3(4096), dim3(256), 0, st, keys, kpos, run_start, U, occ, table, bucket_mask, k, ebits);
 }
 
 constexpr int SEED_BLOCK = 256, SEED_PER = 8;
@@ -1792,6 +2009,44 @@ void launch_rec_sort(const Rec* recs, const uint64_t* rec_off, const uint32_t* o
   if (!n_reads) return;
   hipLaunchKernelGGL((k_rec_sort<REC_BLOCK, REC_LCAP>), dim3(n_reads), dim3(REC_BLOCK), 0, st, recs, rec_off, order,
                      gscratch, n_reads, out);
+}
+
+// ------------------------------------------------------------ fine launchers
+void launch_fine_windows(const Rec* recs, uint32_t n, uint64_t* keys, uint32_t* idx, int phase, const uint64_t* roff,
+                         uint32_t fk, FineWin* out, hipStream_t st) {
+  const uint32_t g = std::max<uint32_t>(1, std::min<uint32_t>(4096, (n + 255) / 256));
+  if (phase == 0) hipLaunchKernelGGL(k_fine_win_keys, dim3(g), dim3(256), 0, st, recs, n, keys, idx);
+  else hipLaunchKernelGGL(k_fine_win_fill, dim3(g), dim3(256), 0, st, recs, idx, n, roff, fk, out);
+}
+void launch_fine_hits(bool emit, IndexView fx, const uint8_t* seq, const uint64_t* roff, uint32_t r0, uint32_t nr,
+                      const FineWin* win, const uint64_t* woff, uint64_t* read_hits, const uint64_t* hit_off,
+                      uint64_t w_sub0, uint32_t* keys, int2* vals, unsigned long long* stats, hipStream_t st) {
+  if (!nr) return;
+  if (emit)
+    hipLaunchKernelGGL(k_fine_hits<true>, dim3(nr), dim3(FINE_BLOCK), 0, st, fx, seq, roff, r0, win, woff, read_hits,
+                       hit_off, w_sub0, keys, vals, stats);
+  else
+    hipLaunchKernelGGL(k_fine_hits<false>, dim3(nr), dim3(FINE_BLOCK), 0, st, fx, seq, roff, r0, win, woff, read_hits,
+                       hit_off, w_sub0, keys, vals, stats);
+}
+void launch_list_bounds(const uint32_t* keys, uint64_t G, uint32_t* lstart, uint32_t* lend, hipStream_t st) {
+  if (!G) return;
+  const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192, (G + 255) / 256));
+  hipLaunchKernelGGL(k_list_bounds, dim3(g), dim3(256), 0, st, keys, G, lstart, lend);
+}
+void launch_fine_desc(IndexView ix, const Rec* recs, uint64_t w_sub0, uint32_t nwin, const uint32_t* lstart,
+                      const uint32_t* lend, int with_info, ChainDesc* chains, uint32_t* emit_of,
+                      unsigned long long* info_need, hipStream_t st) {
+  if (!nwin) return;
+  const uint32_t g = std::max<uint32_t>(1, std::min<uint32_t>(4096, (nwin + 255) / 256));
+  hipLaunchKernelGGL(k_fine_desc, dim3(g), dim3(256), 0, st, ix, recs, w_sub0, nwin, lstart, lend, with_info, chains,
+                     emit_of, info_need);
+}
+void launch_fine_empty(IndexView ix, uint32_t k, const ChainDesc* chains, uint32_t n, const uint32_t* lisl,
+                       const uint32_t* emit_of, ChainOut O, hipStream_t st) {
+  if (!n) return;
+  const uint32_t g = std::max<uint32_t>(1, std::min<uint32_t>(4096, (n + 255) / 256));
+  hipLaunchKernelGGL(k_fine_empty, dim3(g), dim3(256), 0, st, ix, k, chains, n, lisl, emit_of, O);
 }
 
 }  // namespace pbgpu

@@ -33,6 +33,7 @@ EXPORTS = [
     "pbgpu_reads_upload", "pbgpu_reads_free", "pbgpu_align_resident", "pbgpu_download",
     "pbgpu_aligner_get_stats", "pbgpu_aligner_reset_stats", "pbgpu_aligner_set_hit_budget",
     "pbgpu_format_coords", "pbgpu_free_text",
+    "pbgpu_aligner_set_details", "pbgpu_download_details", "pbgpu_details_free", "pbgpu_format_details",
 ]
 
 
@@ -43,7 +44,8 @@ class PbgpuError(RuntimeError):
 
 
 class IndexParams(C.Structure):
-    _fields_ = [("k", C.c_uint32), ("psa_min", C.c_uint32), ("device", C.c_int32), ("threads", C.c_int32)]
+    _fields_ = [("k", C.c_uint32), ("psa_min", C.c_uint32), ("device", C.c_int32), ("threads", C.c_int32),
+                ("fine_k", C.c_uint32)]
 
 
 class IndexInfo(C.Structure):
@@ -79,12 +81,20 @@ class CoordsBatch(C.Structure):
                 ("bases_info", C.POINTER(C.c_int32))]
 
 
+class DetailsBatch(C.Structure):
+    _fields_ = [("n_reads", C.c_uint64), ("n_lists", C.c_uint64), ("n_hits", C.c_uint64),
+                ("read_offsets", C.POINTER(C.c_uint64)), ("list_sr", C.POINTER(C.c_uint32)),
+                ("hit_offsets", C.POINTER(C.c_uint64)), ("n_fwd", C.POINTER(C.c_uint32)),
+                ("hits", C.POINTER(C.c_int32)), ("in_lis", C.POINTER(C.c_uint8))]
+
+
 class Stats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("n_batches", "n_reads", "n_bases", "n_kmers", "n_probes", "n_kept",
                                           "n_hits", "n_chains", "n_lis_tests", "n_records")] + \
                [(n, C.c_double) for n in ("ms_seed", "ms_group", "ms_lis", "ms_fit", "ms_records")] + \
                [("kernel_ms", C.c_double * 8), ("kernel_launches", C.c_uint64 * 8)] + \
-               [(n, C.c_uint64) for n in ("g0_kept", "g0_hits", "g0_chains", "l0_hits", "l0_strands")]
+               [(n, C.c_uint64) for n in ("g0_kept", "g0_hits", "g0_chains", "l0_hits", "l0_strands",
+                                          "n_fine_hits", "n_fine_windows")] + [("ms_fine", C.c_double)]
 
     def as_dict(self):
         d = {n: getattr(self, n) for n, _ in self._fields_ if not n.startswith("kernel_")}
@@ -137,6 +147,11 @@ def lib():
         L.pbgpu_format_coords.argtypes = [vp, C.POINTER(CoordsBatch), C.POINTER(C.c_char_p), C.POINTER(C.c_uint64),
                                           C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p),
                                           C.POINTER(C.c_uint64)]
+        L.pbgpu_aligner_set_details.argtypes = [vp, C.c_int]
+        L.pbgpu_download_details.argtypes = [vp, C.POINTER(C.POINTER(DetailsBatch))]
+        L.pbgpu_details_free.argtypes = [C.POINTER(DetailsBatch)]
+        L.pbgpu_format_details.argtypes = [vp, C.POINTER(DetailsBatch), C.POINTER(C.c_char_p), C.c_int,
+                                           C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]
         L.pbgpu_free_text.argtypes = [C.c_void_p]
         L.pbgpu_free_text.restype = None
         _lib = L
@@ -187,15 +202,15 @@ class Index:
         self.h = handle
 
     @classmethod
-    def from_fasta(cls, paths, k, psa_min=13, device=0, threads=0):
-        p = IndexParams(k, psa_min, device, threads)
+    def from_fasta(cls, paths, k, psa_min=13, device=0, threads=0, fine_k=0):
+        p = IndexParams(k, psa_min, device, threads, fine_k)
         h = C.c_void_p()
         _check(lib().pbgpu_index_build_fasta(_cstrs(paths), len(paths), C.byref(p), C.byref(h)))
         return cls(h)
 
     @classmethod
-    def from_records(cls, names, seqs, k, psa_min=13, device=0, threads=0):
-        p = IndexParams(k, psa_min, device, threads)
+    def from_records(cls, names, seqs, k, psa_min=13, device=0, threads=0, fine_k=0):
+        p = IndexParams(k, psa_min, device, threads, fine_k)
         bs = [s if isinstance(s, bytes) else s.encode() for s in seqs]
         lens = (C.c_uint64 * max(1, len(bs)))(*[len(b) for b in bs])
         h = C.c_void_p()
@@ -324,6 +339,14 @@ class Aligner:
     def reset_stats(self):
         _check(lib().pbgpu_aligner_reset_stats(self.h))
 
+    def set_details(self, on=True):
+        _check(lib().pbgpu_aligner_set_details(self.h, int(bool(on))))
+
+    def download_details(self):
+        out = C.POINTER(DetailsBatch)()
+        _check(lib().pbgpu_download_details(self.h, C.byref(out)))
+        return Details(out)
+
     def set_hit_budget(self, hits):
         _check(lib().pbgpu_aligner_set_hit_budget(self.h, C.c_uint64(int(hits))))
 
@@ -331,6 +354,33 @@ class Aligner:
         if self.h:
             lib().pbgpu_aligner_free(self.h)
             self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Details:
+    """--details lists of the last alignment (owns the C allocation)."""
+
+    def __init__(self, ptr):
+        self.ptr = ptr
+
+    def format(self, index, headers, threads=0):
+        t = C.c_void_p()
+        tl = C.c_uint64()
+        _check(lib().pbgpu_format_details(index.h, self.ptr, _cstrs(headers), threads, C.byref(t), C.byref(tl)))
+        try:
+            return C.string_at(t, tl.value).decode()
+        finally:
+            lib().pbgpu_free_text(t)
+
+    def close(self):
+        if self.ptr:
+            lib().pbgpu_details_free(self.ptr)
+            self.ptr = None
 
     def __del__(self):
         try:

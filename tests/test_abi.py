@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert pbgpu.lib().pbgpu_abi_version() == 1
+    assert pbgpu.lib().pbgpu_abi_version() == 2
 
 
 def test_record_layout_matches_header():
@@ -76,11 +76,10 @@ CLI = os.path.join(ROOT, "pacbio_amd", "bin", "jf_aligner")
 @pytest.mark.parametrize("args,msg", [
     ([], "-s, --size is required"),
     (["-s", "1"], "-m, --mer is required"),
-    (["-s", "1", "-m", "17", "--max-count", "0"], "undefined behaviour"),
+    (["-s", "1", "-m", "17"], "No output file given"),
+    (["-s", "1", "-m", "17", "--coords", "/dev/null", "--max-count", "0"], "undefined behaviour"),
     (["-s", "1", "-m", "17", "-l", "x", "-u", "y"], "conflicts"),
-    (["-s", "1", "-m", "17", "-l", "x"], "-k, --k-mer"),
-    (["-s", "1", "-m", "17", "-F", "13"], "-F"),
-    (["-s", "1", "-m", "17", "--details", "d"], "--details"),
+    (["-s", "1", "-m", "17", "--coords", "/dev/null", "-l", "x"], "-k, --k-mer"),
 ])
 def test_cli_argument_errors(args, msg):
     r = subprocess.run([CLI] + args, capture_output=True, text=True)

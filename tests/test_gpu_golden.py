@@ -29,7 +29,7 @@ def _norm_ours(text):
 
 def _run(*extra):
     args = [CLI, "-s", "10k", "-m", "17", "-r", os.path.join(GOLD, "test_super_reads.fa"), "-p",
-            os.path.join(GOLD, "test_pacbio.fa"), "--stretch-cap", "200", "--no-compact", *extra]
+            os.path.join(GOLD, "test_pacbio.fa"), "--stretch-cap", "200", "--no-compact", "--coords", "/dev/stdout", *extra]
     r = subprocess.run(args, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     return r.stdout

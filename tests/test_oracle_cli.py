@@ -27,7 +27,7 @@ def _norm_ours(text):
 
 def _run(*extra):
     args = [ORACLE, "-s", "10k", "-m", "17", "-r", os.path.join(GOLD, "test_super_reads.fa"), "-p",
-            os.path.join(GOLD, "test_pacbio.fa"), "--stretch-cap", "200", "--no-compact", *extra]
+            os.path.join(GOLD, "test_pacbio.fa"), "--stretch-cap", "200", "--no-compact", "--coords", "/dev/stdout", *extra]
     return subprocess.run(args, capture_output=True, text=True, check=True).stdout
 
 
@@ -103,5 +103,6 @@ def test_fine_aligner_reference_properties():
 
 
 def test_cli_rejects_max_count_zero():
-    r = subprocess.run([ORACLE, "-s", "1", "-m", "17", "--max-count", "0"], capture_output=True, text=True)
+    r = subprocess.run([ORACLE, "-s", "1", "-m", "17", "--coords", "/dev/null", "--max-count", "0"], capture_output=True,
+                       text=True)
     assert r.returncode != 0
