@@ -89,8 +89,10 @@ def _kernel_bytes(st):
         # and its lis point written (<= 8 B); per strand its item, chain descriptor (24 B),
         # length and lis length (12 B)
         "k_lis": per(st["l0_hits"] * 16 + st["l0_strands"] * 36, "k_lis"),
-        # chain descriptors + lis lengths read, lis points read, records written
-        "k_coords": per(st["n_chains"] * 32 + st["n_records"] * 96, "k_coords"),
+        # counted by the kernel: per chain its list entry (4 B), descriptor (24 B), both lis
+        # lengths (8 B), super-read length + unitig range (16 B) and read range (16 B); every lis
+        # point (8 B) read once; every record (96 B) written (kmers_info pairs not counted)
+        "k_coords": per(st["fit_chains"] * 68 + st["fit_points"] * 8 + st["n_records"] * 96, "k_coords"),
         # records read + written
         "k_rec_sort": per(st["n_records"] * 96 * 2, "k_rec_sort"),
     }

@@ -78,6 +78,9 @@ typedef struct {
                         of a pattern shorter than max_size = k: the k - fine_k
                         bases after each occurrence, then position descending
                         (mer_sa_imp.hpp:351-364). */
+  uint32_t shard;    /* n_shards > 1: build shard `shard` of an index sharded by */
+  uint32_t n_shards; /* super-read range; 0 or 1 = the whole set.  See
+                        "Sharded index" below. */
 } pbgpu_index_params;
 
 /* superread_parser.cc:12-46: multi-line FASTA, full header line kept as the
@@ -99,6 +102,7 @@ typedef struct {
   uint64_t table_buckets;   /* 64-byte hash buckets */
   uint64_t device_bytes;    /* resident index footprint */
   double   build_seconds;
+  uint64_t sr_begin, sr_end; /* super-reads held on the device (all of them unless sharded) */
 } pbgpu_index_info;
 pbgpu_status pbgpu_index_get_info(const pbgpu_index* ix, pbgpu_index_info* info);
 /* frag_info.hpp:18-35: fwd name = header line, bwd name = reversed unitigs */
@@ -215,6 +219,8 @@ typedef struct {
   /* fine aligner (-F): windowed hits, windows (= fine records), device time */
   uint64_t n_fine_hits, n_fine_windows;
   double   ms_fine;
+  /* work of the timed k_coords slot (coarse): chains fitted, lis points streamed */
+  uint64_t fit_chains, fit_points;
 } pbgpu_stats;
 pbgpu_status pbgpu_aligner_get_stats(const pbgpu_aligner* al, pbgpu_stats* s);
 pbgpu_status pbgpu_aligner_reset_stats(pbgpu_aligner* al);
@@ -222,6 +228,42 @@ pbgpu_status pbgpu_aligner_reset_stats(pbgpu_aligner* al);
  * sub-batch (default 1.2e9, about 38 GB of working buffers).  A read whose
  * hits exceed it forms a sub-batch of its own.  Results do not depend on it. */
 pbgpu_status pbgpu_aligner_set_hit_budget(pbgpu_aligner* al, uint64_t hits);
+
+/* ---------------------------------------------------------- sharded index
+ * For super-read sets whose index does not fit one GPU (the C5
+ * configuration).  Shard s of S (pbgpu_index_params.shard / n_shards) holds the
+ * super-reads whose text starts in [T*s/S, T*(s+1)/S) (T = total bases) plus
+ * the next k-1 bases, so every occurrence -- super-read-end crossing ones
+ * included -- is counted by exactly one shard; names of all super-reads stay
+ * on the host.  Every shard aligns every read of the batch:
+ *   1. pbgpu_shard_counts: this shard's count of each looked-up k-mer of the
+ *      batch, saturated at max_count + 1, into the aligner's count buffer (one
+ *      uint32 per base of the batch);
+ *   2. the counts are summed over the shards, in place: over RCCL/xGMI with
+ *      pbgpu_shard_counts_allreduce (ncclAllReduce, sum), or through host
+ *      memory (pbgpu_shard_counts_download / _upload).  The saturated sum
+ *      decides the max-count filter and the 99% threshold exactly as the
+ *      whole count does;
+ *   3. pbgpu_align_resident_shard: the rest of the path on this shard's
+ *      super-reads (chains never span super-reads); records carry the global
+ *      sr_index;
+ *   4. pbgpu_coords_merge of the shards' batches: each read's records merged in
+ *      (rs, re, ql, sr_index, emit) order.
+ * pbgpu_align_batch / pbgpu_align_resident reject a sharded index; -F and
+ * --details run on a whole index only. */
+typedef struct pbgpu_comm pbgpu_comm;
+pbgpu_status pbgpu_shard_counts(pbgpu_aligner* al, const pbgpu_reads* reads);
+pbgpu_status pbgpu_shard_counts_download(pbgpu_aligner* al, uint32_t* host, uint64_t n);
+pbgpu_status pbgpu_shard_counts_upload(pbgpu_aligner* al, const uint32_t* host, uint64_t n);
+/* RCCL: rank 0 makes the 128-byte id, the caller hands it to every rank (any
+ * host channel), each rank creates its communicator on its aligner's device. */
+pbgpu_status pbgpu_rccl_unique_id(uint8_t id[128]);
+pbgpu_status pbgpu_rccl_comm_create(int device, int n_ranks, int rank, const uint8_t id[128], pbgpu_comm** out);
+pbgpu_status pbgpu_rccl_comm_free(pbgpu_comm* comm);
+pbgpu_status pbgpu_shard_counts_allreduce(pbgpu_aligner* al, pbgpu_comm* comm);
+pbgpu_status pbgpu_align_resident_shard(pbgpu_aligner* al, const pbgpu_reads* reads);
+/* Host-side merge (no device work); the result is freed with pbgpu_coords_free. */
+pbgpu_status pbgpu_coords_merge(const pbgpu_coords_batch* const* parts, uint64_t n_parts, pbgpu_coords_batch** out);
 
 /* ---------------------------------------------------------------- details
  * --details (print_details, jf_aligner.cc:72-108): with details enabled, each

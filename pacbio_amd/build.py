@@ -56,7 +56,7 @@ def build_pbgpu(force=False):
     lib = os.path.join(PKG, "libpbgpu.so")
     if force or jobs or _newer(lib, objs):
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + objs +
-             ["-Wl,-soname,libpbgpu.so", "-lpthread"])
+             ["-Wl,-soname,libpbgpu.so", "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-lpthread"])
     bindir = os.path.join(PKG, "bin")
     os.makedirs(bindir, exist_ok=True)
     cli = os.path.join(bindir, "jf_aligner")
@@ -77,7 +77,8 @@ def build_pbgpu_prof():
         _run([HIPCC] + HIPFLAGS + ["-DPBGPU_PROF", "-c", os.path.join(CSRC, s), "-o", obj])
         objs.append(obj)
     lib = os.path.join(PKG, "libpbgpu_prof.so")
-    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + objs + ["-lpthread"])
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + objs +
+         ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-lpthread"])
     return lib
 
 

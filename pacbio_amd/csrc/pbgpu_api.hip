@@ -3,6 +3,7 @@
 // pipeline on one HIP stream, result download and coords formatting.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <atomic>
@@ -31,8 +32,10 @@ void launch_occ_fill(const uint64_t* vals, const uint64_t* uidx, const uint64_t*
                      hipStream_t st);
 void launch_headers(const uint64_t* keys, const uint64_t* kpos, const uint64_t* run_start, uint64_t U, uint64_t* occ,
                     ulonglong2* table, uint64_t bucket_mask, uint32_t k, uint32_t ebits, hipStream_t st);
-void launch_seed(IndexView ix, const uint8_t* seq, const uint64_t* roff, uint32_t n_reads, AlignParamsDev P,
-                 KRec* krec, uint32_t* n_kept, uint32_t* thr, uint64_t* nhits, unsigned long long* stats, hipStream_t st);
+enum { SEED_WHOLE = 0, SEED_COUNTS = 1, SEED_FINISH = 2 };  // k_seed modes (pbgpu_kernels.hip)
+void launch_seed(int mode, IndexView ix, const uint8_t* seq, const uint64_t* roff, uint32_t n_reads, AlignParamsDev P,
+                 KRec* krec, uint32_t* n_kept, uint32_t* thr, uint64_t* nhits, unsigned long long* stats,
+                 uint32_t* gcount, uint64_t null_ptr, hipStream_t st);
 void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const uint32_t* n_kept, const uint32_t* thr,
                   const uint64_t* hit_off, uint64_t node_base, uint32_t r0, const uint32_t* read_list, uint32_t n_list,
                   uint32_t hcap_log2, uint32_t* gtable, GroupOut O, unsigned long long* stats, hipStream_t st);
@@ -42,7 +45,7 @@ void launch_init_slen(const ChainDesc* chains, uint32_t n_chains, uint32_t* slen
 void launch_strand_order(const uint32_t* slen, uint32_t n_items, uint32_t* hist, uint32_t* cursor, uint32_t* perm,
                          int phase, hipStream_t st);
 void launch_chain_order(const uint32_t* lisl, uint32_t n, uint32_t* hist, uint32_t* cursor, uint32_t* perm, int phase,
-                        hipStream_t st);
+                        unsigned long long* sums, hipStream_t st);
 void launch_lis(bool big_nodes, const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen,
                 const int2* X, void* N, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx,
                 unsigned long long* stats, hipStream_t st);
@@ -105,9 +108,13 @@ struct hip_error : std::runtime_error {
     }                                                                                                  \
   } while (0)
 struct bad_input : std::runtime_error { using std::runtime_error::runtime_error; };
+struct pbgpu_comm {  // an RCCL communicator of the sharded-index count exchange
+  ncclComm_t comm = nullptr;
+  int device = 0;
+};
 struct unsupported : std::runtime_error { using std::runtime_error::runtime_error; };
 
-#define API_TRY try {
+#define API_TRY try { (void)hipGetLastError();  /* launch checks below see only this call's errors */
 #define API_CATCH                                                                 \
   }                                                                               \
   catch (const hip_error& e) {                                                    \
@@ -182,6 +189,12 @@ struct pbgpu_index {
   dbuf<uint64_t> text, d_sr_start, occ;
   dbuf<ulonglong2> table;
   dbuf<uint32_t> sr_uoff, sr_uids;
+  // index sharded by super-read range: this shard holds super-reads
+  // [sr_begin, sr_end) (device arrays use local ids) plus a k-1-base seam
+  uint32_t shard = 0, n_shards = 1;
+  uint64_t sr_begin = 0, sr_end = 0, n_total = 0;
+  std::vector<uint64_t> gstart;   // global text offsets of all super-reads (host)
+  uint64_t null_ptr = 0;          // empty occurrence header: k-mers absent from this shard
   // fine (-F) sub-index: same table / occurrence layout over fine_k-mers
   uint32_t fk = 0;
   uint64_t f_buckets = 0, f_kmers = 0, f_occ = 0;
@@ -189,7 +202,7 @@ struct pbgpu_index {
   dbuf<ulonglong2> f_table;
   IndexView view() const {
     IndexView v;
-    v.text = text.p; v.n = n; v.sr_start = d_sr_start.p; v.n_sr = (uint32_t)n_sr; v.k = k;
+    v.text = text.p; v.n = n; v.sr_start = d_sr_start.p; v.n_sr = (uint32_t)(sr_end - sr_begin); v.k = k;
     v.table = table.p; v.bucket_mask = buckets - 1; v.occ = occ.p; v.sr_uoff = sr_uoff.p; v.sr_uids = sr_uids.p;
     return v;
   }
@@ -272,6 +285,7 @@ static void build_kmer_table(pbgpu_index* ix, uint32_t km, uint32_t K, uint32_t 
     table.alloc(4);
     HIPCHK(hipMemset(table.p, 0xFF, table.bytes()));
     occ.alloc(2);
+    HIPCHK(hipMemset(occ.p, 0, occ.bytes()));  // the empty header (ix->null_ptr = 0)
     n_kmers = n_occ = 0;
     return;
   }
@@ -324,7 +338,8 @@ static void build_kmer_table(pbgpu_index* ix, uint32_t km, uint32_t K, uint32_t 
   HIPCHK(hipMemcpyAsync(run_start + U, &N, 8, hipMemcpyHostToDevice, st));
   n_kmers = U;
   n_occ = kept;
-  occ.alloc(2 * U + kept);
+  occ.alloc(2 * U + kept + 2);  // + an empty header {0, 0} at 2U + kept (index null_ptr)
+  HIPCHK(hipMemsetAsync(occ.p + 2 * U + kept, 0, 16, st));
   uint64_t buckets = 1;
   while (buckets * 2 < U) buckets <<= 1;  // slots = 4*buckets >= 2U: load <= 0.5
   n_buckets = buckets;
@@ -343,10 +358,10 @@ static void build_device_index(pbgpu_index* ix, text_builder& tb) {
   HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
   struct stream_guard { hipStream_t s; ~stream_guard() { (void)hipStreamDestroy(s); } } sg{st};
   const uint32_t k = ix->k;
-  ix->n = tb.n;
+  ix->n_total = tb.n;
   ix->n_sr = tb.names.size();
-  ix->sr_start = tb.starts;
-  // names, bwd names (frag_info.hpp:22-35), unitig ids
+  ix->gstart = tb.starts;
+  // names, bwd names (frag_info.hpp:22-35), unitig ids -- of every super-read (host)
   ix->name_fwd = std::move(tb.names);
   ix->name_bwd.resize(ix->n_sr);
   std::vector<uint32_t> uoff(ix->n_sr + 1, 0), uids, id;
@@ -368,17 +383,54 @@ static void build_device_index(pbgpu_index* ix, text_builder& tb) {
   }
   uoff[ix->n_sr] = (uint32_t)uids.size();
   tb.words.resize(tb.n / 32 + 2, 0);
-  ix->text.alloc(tb.words.size());
-  HIPCHK(hipMemcpy(ix->text.p, tb.words.data(), tb.words.size() * 8, hipMemcpyHostToDevice));
-  std::vector<uint64_t>().swap(tb.words);
+  // This device's super-reads: all of them, or shard `shard` of n_shards -- the
+  // super-reads starting in [total * s / S, total * (s + 1) / S) of the text --
+  // plus the next k - 1 bases (the seam), so that an occurrence crossing into the
+  // next shard is counted here, once.
+  const uint64_t total = tb.n;
+  auto first_sr_at = [&](uint64_t b) -> uint64_t {  // first super-read starting at or after base b
+    return (uint64_t)(std::lower_bound(ix->gstart.begin(), ix->gstart.end() - 1, b) - ix->gstart.begin());
+  };
+  ix->sr_begin = ix->n_shards > 1 ? first_sr_at(total * ix->shard / ix->n_shards) : 0;
+  ix->sr_end = ix->n_shards > 1 && ix->shard + 1 < ix->n_shards ? first_sr_at(total * (ix->shard + 1) / ix->n_shards)
+                                                                  : ix->n_sr;
+  const uint64_t b0 = ix->gstart[ix->sr_begin], b1 = ix->gstart[ix->sr_end];
+  const uint64_t seam = std::min<uint64_t>(k - 1, total - b1);
+  const uint64_t L = b1 - b0 + seam;
+  ix->n = L;
+  std::vector<uint64_t> words;
+  if (b0 == 0 && b1 + seam == total) {
+    words.swap(tb.words);
+  } else {  // re-align the slice [b0, b0 + L) of the packed text to base 0
+    const uint64_t W = tb.words.size(), j0 = b0 >> 5;
+    const uint32_t sh = (uint32_t)(b0 & 31) * 2;
+    words.assign(L / 32 + 2, 0);
+    for (uint64_t i = 0; i < words.size(); ++i) {
+      const uint64_t a = j0 + i < W ? tb.words[j0 + i] : 0, c = j0 + i + 1 < W ? tb.words[j0 + i + 1] : 0;
+      words[i] = sh ? (a << sh) | (c >> (64 - sh)) : a;
+    }
+    if (L & 31) words[L >> 5] &= ~0ull << (64 - 2 * (L & 31));
+    for (uint64_t i = (L >> 5) + 1; i < words.size(); ++i) words[i] = 0;
+    std::vector<uint64_t>().swap(tb.words);
+  }
+  ix->text.alloc(words.size());
+  HIPCHK(hipMemcpy(ix->text.p, words.data(), words.size() * 8, hipMemcpyHostToDevice));
+  std::vector<uint64_t>().swap(words);
+  const uint64_t nloc = ix->sr_end - ix->sr_begin;
+  ix->sr_start.resize(nloc + 1);
+  for (uint64_t i = 0; i <= nloc; ++i) ix->sr_start[i] = ix->gstart[ix->sr_begin + i] - b0;
   ix->d_sr_start.alloc(ix->sr_start.size());
   HIPCHK(hipMemcpy(ix->d_sr_start.p, ix->sr_start.data(), ix->sr_start.size() * 8, hipMemcpyHostToDevice));
-  ix->sr_uoff.alloc(uoff.size());
-  HIPCHK(hipMemcpy(ix->sr_uoff.p, uoff.data(), uoff.size() * 4, hipMemcpyHostToDevice));
-  ix->sr_uids.alloc(std::max<size_t>(uids.size(), 1));
-  if (!uids.empty()) HIPCHK(hipMemcpy(ix->sr_uids.p, uids.data(), uids.size() * 4, hipMemcpyHostToDevice));
+  std::vector<uint32_t> luoff(nloc + 1);
+  for (uint64_t i = 0; i <= nloc; ++i) luoff[i] = uoff[ix->sr_begin + i] - uoff[ix->sr_begin];
+  ix->sr_uoff.alloc(luoff.size());
+  HIPCHK(hipMemcpy(ix->sr_uoff.p, luoff.data(), luoff.size() * 4, hipMemcpyHostToDevice));
+  ix->sr_uids.alloc(std::max<size_t>(luoff[nloc], 1));
+  if (luoff[nloc])
+    HIPCHK(hipMemcpy(ix->sr_uids.p, uids.data() + uoff[ix->sr_begin], (size_t)luoff[nloc] * 4, hipMemcpyHostToDevice));
 
   build_kmer_table(ix, k, k, 0, st, ix->table, ix->occ, ix->buckets, ix->n_kmers, ix->n_occ);
+  ix->null_ptr = 2 * ix->n_kmers + ix->n_occ;
   if (ix->fk)
     build_kmer_table(ix, ix->fk, k, 2 * (k - ix->fk) + 1, st, ix->f_table, ix->f_occv, ix->f_buckets, ix->f_kmers,
                      ix->f_occ);
@@ -396,6 +448,10 @@ static pbgpu_status index_common(const pbgpu_index_params* p) {
     return fail(PBGPU_ERR_UNSUPPORTED,
                 "psa_min (%u) >= k (%u): the reference's hit order then depends on thread timing (mer_sa_imp.hpp:247)",
                 p->psa_min, p->k);
+  if (p->n_shards > 1 && p->shard >= p->n_shards)
+    return fail(PBGPU_ERR_INVALID, "shard %u out of range (n_shards %u)", p->shard, p->n_shards);
+  if (p->n_shards > 1 && p->fine_k)
+    return fail(PBGPU_ERR_UNSUPPORTED, "the fine aligner (-F) runs on a whole index only (n_shards = 1)");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(PBGPU_ERR_DEVICE, "no HIP device available");
   if (p->device < 0 || p->device >= ndev) return fail(PBGPU_ERR_INVALID, "device %d out of range", p->device);
@@ -489,6 +545,7 @@ pbgpu_status pbgpu_index_build_fasta(const char* const* paths, size_t n_paths, c
   for (size_t i = 0; i < n_paths; ++i) load_fasta(paths[i], tb);
   std::unique_ptr<pbgpu_index> ix(new pbgpu_index);
   ix->device = params->device; ix->k = params->k; ix->psa_min = params->psa_min; ix->fk = params->fine_k;
+  if (params->n_shards > 1) { ix->shard = params->shard; ix->n_shards = params->n_shards; }
   build_device_index(ix.get(), tb);
   *out = ix.release();
   return PBGPU_OK;
@@ -513,6 +570,7 @@ pbgpu_status pbgpu_index_build(const char* const* names, const char* const* seqs
   }
   std::unique_ptr<pbgpu_index> ix(new pbgpu_index);
   ix->device = params->device; ix->k = params->k; ix->psa_min = params->psa_min; ix->fk = params->fine_k;
+  if (params->n_shards > 1) { ix->shard = params->shard; ix->n_shards = params->n_shards; }
   build_device_index(ix.get(), tb);
   *out = ix.release();
   return PBGPU_OK;
@@ -529,6 +587,7 @@ pbgpu_status pbgpu_index_free(pbgpu_index* ix) {
 pbgpu_status pbgpu_index_get_info(const pbgpu_index* ix, pbgpu_index_info* info) {
   if (!ix || !info) return fail(PBGPU_ERR_INVALID, "null argument");
   info->n_sr = ix->n_sr; info->text_len = ix->n; info->n_kmers = ix->n_kmers; info->n_occurrences = ix->n_occ;
+  info->sr_begin = ix->sr_begin; info->sr_end = ix->sr_end;
   info->table_buckets = ix->buckets; info->device_bytes = ix->device_bytes(); info->build_seconds = ix->build_seconds;
   return PBGPU_OK;
 }
@@ -538,7 +597,7 @@ const char* pbgpu_index_sr_name(const pbgpu_index* ix, uint32_t sr, int bwd) {
 }
 uint32_t pbgpu_index_sr_len(const pbgpu_index* ix, uint32_t sr) {
   if (!ix || sr >= ix->n_sr) return 0;
-  return (uint32_t)(ix->sr_start[sr + 1] - ix->sr_start[sr]);
+  return (uint32_t)(ix->gstart[sr + 1] - ix->gstart[sr]);
 }
 
 void pbgpu_align_params_default(pbgpu_align_params* p) {
@@ -552,6 +611,7 @@ void pbgpu_align_params_default(pbgpu_align_params* p) {
 // ---------------------------------------------------------------- aligner
 struct pbgpu_reads {
   pbgpu_aligner* owner = nullptr;
+  int device = 0;  // kept here: the owner may be freed first
   uint64_t n_reads = 0, n_bases = 0;
   std::vector<uint64_t> h_off;
   dbuf<uint8_t> seq;
@@ -560,6 +620,7 @@ struct pbgpu_reads {
 
 struct pbgpu_aligner {
   const pbgpu_index* ix = nullptr;
+  int device = 0;
   pbgpu_align_params prm{};
   AlignParamsDev P{};
   LisParams lp{};
@@ -593,6 +654,9 @@ struct pbgpu_aligner {
   dbuf<uint32_t> ovf_list, read_list;
   dbuf<uint8_t> nparts;
   dbuf<uint2> prog;
+  // sharded index: per-base k-mer counts of the current batch (SEED_COUNTS, then summed)
+  dbuf<uint32_t> gcount;
+  uint64_t gcount_n = ~0ull;
   // -F: fine aligner pass (params of k_coords with align_k = fine_k, forward, unfiltered)
   bool fine = false;
   AlignParamsDev PF{};
@@ -655,7 +719,8 @@ static void capture_details(pbgpu_aligner* al, uint32_t nch, uint64_t Hs) {
   }
 }
 
-static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd);
+static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode = SEED_WHOLE,
+                             uint32_t* gcount = nullptr);
 
 extern "C" {
 
@@ -675,6 +740,7 @@ pbgpu_status pbgpu_aligner_create(const pbgpu_index* ix, const pbgpu_align_param
   HIPCHK(hipSetDevice(ix->device));
   std::unique_ptr<pbgpu_aligner> al(new pbgpu_aligner);
   al->ix = ix;
+  al->device = ix->device;
   al->prm = *params;
   al->prm.unitig_lengths = nullptr;
   if (params->unitigs_k && params->n_unitigs) {
@@ -709,7 +775,7 @@ pbgpu_status pbgpu_aligner_create(const pbgpu_index* ix, const pbgpu_align_param
 
 pbgpu_status pbgpu_aligner_free(pbgpu_aligner* al) {
   if (!al) return PBGPU_OK;
-  (void)hipSetDevice(al->ix->device);
+  (void)hipSetDevice(al->device);  // not al->ix: the index may be freed first
   for (auto& e : al->ev) if (e) (void)hipEventDestroy(e);
   if (al->st) (void)hipStreamDestroy(al->st);
   delete al;
@@ -722,6 +788,7 @@ pbgpu_status pbgpu_reads_upload(pbgpu_aligner* al, const pbgpu_read_batch* b, pb
   HIPCHK(hipSetDevice(al->ix->device));
   std::unique_ptr<pbgpu_reads> r(new pbgpu_reads);
   r->owner = al;
+  r->device = al->device;
   r->n_reads = b->n_reads;
   r->h_off.resize(b->n_reads + 1);
   const uint64_t o0 = b->n_reads ? b->offsets[0] : 0;
@@ -742,14 +809,115 @@ pbgpu_status pbgpu_reads_upload(pbgpu_aligner* al, const pbgpu_read_batch* b, pb
 
 pbgpu_status pbgpu_reads_free(pbgpu_reads* r) {
   if (!r) return PBGPU_OK;
-  (void)hipSetDevice(r->owner->ix->device);
+  (void)hipSetDevice(r->device);
   delete r;
   return PBGPU_OK;
+}
+
+pbgpu_status pbgpu_shard_counts(pbgpu_aligner* al, const pbgpu_reads* rd) {
+  if (!al || !rd) return fail(PBGPU_ERR_INVALID, "null argument");
+  if (rd->owner != al) return fail(PBGPU_ERR_INVALID, "reads were uploaded for another aligner");
+  API_TRY
+  HIPCHK(hipSetDevice(al->ix->device));
+  const uint32_t n = (uint32_t)rd->n_reads;
+  al->gcount.ensure(rd->n_bases + 1);
+  al->gcount_n = rd->n_bases;
+  HIPCHK(hipMemsetAsync(al->gcount.p, 0, (rd->n_bases + 1) * 4, al->st));
+  if (n) {
+    HIPCHK(hipMemsetAsync(al->stats.p, 0, ST_N * 8, al->st));
+    launch_seed(SEED_COUNTS, al->ix->view(), rd->seq.p, rd->off.p, n, al->P, nullptr, nullptr, nullptr, nullptr,
+                al->stats.p, al->gcount.p, al->ix->null_ptr, al->st);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipStreamSynchronize(al->st));
+  return PBGPU_OK;
+  API_CATCH
+}
+
+pbgpu_status pbgpu_shard_counts_download(pbgpu_aligner* al, uint32_t* host, uint64_t n) {
+  if (!al || (!host && n)) return fail(PBGPU_ERR_INVALID, "null argument");
+  if (n != al->gcount_n) return fail(PBGPU_ERR_INVALID, "count buffer holds %llu entries", (unsigned long long)al->gcount_n);
+  API_TRY
+  HIPCHK(hipSetDevice(al->ix->device));
+  if (n) HIPCHK(hipMemcpy(host, al->gcount.p, n * 4, hipMemcpyDeviceToHost));
+  return PBGPU_OK;
+  API_CATCH
+}
+
+pbgpu_status pbgpu_shard_counts_upload(pbgpu_aligner* al, const uint32_t* host, uint64_t n) {
+  if (!al || (!host && n)) return fail(PBGPU_ERR_INVALID, "null argument");
+  if (n != al->gcount_n) return fail(PBGPU_ERR_INVALID, "count buffer holds %llu entries", (unsigned long long)al->gcount_n);
+  API_TRY
+  HIPCHK(hipSetDevice(al->ix->device));
+  if (n) HIPCHK(hipMemcpy(al->gcount.p, host, n * 4, hipMemcpyHostToDevice));
+  return PBGPU_OK;
+  API_CATCH
+}
+
+pbgpu_status pbgpu_rccl_unique_id(uint8_t id[128]) {
+  if (!id) return fail(PBGPU_ERR_INVALID, "null argument");
+  static_assert(sizeof(ncclUniqueId) == 128, "RCCL unique id size");
+  ncclUniqueId u;
+  const ncclResult_t r = ncclGetUniqueId(&u);
+  if (r != ncclSuccess) return fail(PBGPU_ERR_DEVICE, "ncclGetUniqueId: %s", ncclGetErrorString(r));
+  memcpy(id, &u, 128);
+  return PBGPU_OK;
+}
+
+pbgpu_status pbgpu_rccl_comm_create(int device, int n_ranks, int rank, const uint8_t id[128], pbgpu_comm** out) {
+  if (!id || !out || n_ranks < 1 || rank < 0 || rank >= n_ranks) return fail(PBGPU_ERR_INVALID, "bad argument");
+  API_TRY
+  HIPCHK(hipSetDevice(device));
+  ncclUniqueId u;
+  memcpy(&u, id, 128);
+  std::unique_ptr<pbgpu_comm> c(new pbgpu_comm);
+  c->device = device;
+  const ncclResult_t r = ncclCommInitRank(&c->comm, n_ranks, u, rank);
+  if (r != ncclSuccess) return fail(PBGPU_ERR_DEVICE, "ncclCommInitRank: %s", ncclGetErrorString(r));
+  *out = c.release();
+  return PBGPU_OK;
+  API_CATCH
+}
+
+pbgpu_status pbgpu_rccl_comm_free(pbgpu_comm* c) {
+  if (!c) return PBGPU_OK;
+  (void)hipSetDevice(c->device);
+  (void)ncclCommDestroy(c->comm);
+  delete c;
+  return PBGPU_OK;
+}
+
+pbgpu_status pbgpu_shard_counts_allreduce(pbgpu_aligner* al, pbgpu_comm* c) {
+  if (!al || !c) return fail(PBGPU_ERR_INVALID, "null argument");
+  if (c->device != al->ix->device) return fail(PBGPU_ERR_INVALID, "communicator and aligner are on different devices");
+  API_TRY
+  HIPCHK(hipSetDevice(al->ix->device));
+  if (al->gcount_n) {
+    const ncclResult_t r = ncclAllReduce(al->gcount.p, al->gcount.p, al->gcount_n, ncclUint32, ncclSum, c->comm, al->st);
+    if (r != ncclSuccess) return fail(PBGPU_ERR_DEVICE, "ncclAllReduce: %s", ncclGetErrorString(r));
+  }
+  HIPCHK(hipStreamSynchronize(al->st));
+  return PBGPU_OK;
+  API_CATCH
+}
+
+pbgpu_status pbgpu_align_resident_shard(pbgpu_aligner* al, const pbgpu_reads* rd) {
+  if (!al || !rd) return fail(PBGPU_ERR_INVALID, "null argument");
+  if (rd->owner != al) return fail(PBGPU_ERR_INVALID, "reads were uploaded for another aligner");
+  if (al->fine || al->details) return fail(PBGPU_ERR_UNSUPPORTED, "-F and --details run on a whole index only");
+  if (al->gcount_n != rd->n_bases) return fail(PBGPU_ERR_INVALID, "no summed counts for this batch (pbgpu_shard_counts)");
+  API_TRY
+  HIPCHK(hipSetDevice(al->ix->device));
+  aligner_pipeline(al, rd, SEED_FINISH, al->gcount.p);
+  return PBGPU_OK;
+  API_CATCH
 }
 
 pbgpu_status pbgpu_align_resident(pbgpu_aligner* al, const pbgpu_reads* rd) {
   if (!al || !rd) return fail(PBGPU_ERR_INVALID, "null argument");
   if (rd->owner != al) return fail(PBGPU_ERR_INVALID, "reads were uploaded for another aligner");
+  if (al->ix->n_shards > 1)
+    return fail(PBGPU_ERR_INVALID, "sharded index: use pbgpu_shard_counts + pbgpu_align_resident_shard");
   API_TRY
   HIPCHK(hipSetDevice(al->ix->device));
   aligner_pipeline(al, rd);
@@ -786,7 +954,8 @@ static uint32_t lis_stage(pbgpu_aligner* al, uint32_t nch, uint64_t Hs, const Li
   auto order = [&](int which, uint32_t n_in) -> uint32_t {  // returns the number of items placed
     HIPCHK(hipMemsetAsync(al->hist.p, 0, NB * 4, st));
     if (which == 0) launch_strand_order(al->slen.p, n_in, al->hist.p, nullptr, nullptr, 0, st);
-    else launch_chain_order(al->lisl.p, n_in, al->hist.p, nullptr, nullptr, 0, st);
+    else launch_chain_order(al->lisl.p, n_in, al->hist.p, nullptr, nullptr, 0,
+                            timed ? al->stats.p + ST_FIT_CHAINS : nullptr, st);  // k_coords' work counters
     std::vector<uint32_t> h(NB), cur(NB);
     HIPCHK(hipMemcpyAsync(h.data(), al->hist.p, NB * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -806,7 +975,7 @@ static uint32_t lis_stage(pbgpu_aligner* al, uint32_t nch, uint64_t Hs, const Li
     cur[0] = acc;
     HIPCHK(hipMemcpyAsync(al->hist.p + NB, cur.data(), NB * 4, hipMemcpyHostToDevice, st));
     if (which == 0) launch_strand_order(al->slen.p, n_in, nullptr, al->hist.p + NB, al->perm.p, 1, st);
-    else launch_chain_order(al->lisl.p, n_in, nullptr, al->hist.p + NB, al->perm.p, 1, st);
+    else launch_chain_order(al->lisl.p, n_in, nullptr, al->hist.p + NB, al->perm.p, 1, nullptr, st);
     HIPCHK(hipGetLastError());
     return acc;
   };
@@ -815,7 +984,8 @@ static uint32_t lis_stage(pbgpu_aligner* al, uint32_t nch, uint64_t Hs, const Li
   const uint32_t n_strands = order(0, 2 * nch);
   const uint32_t nbig = n_big;
   if (nbig) al->nodes32.ensure((Hs + 1) * 16);
-  // strands longer than k_lis_w's LDS capacity: restore list order in place first
+  // strands longer than k_lis_w's LDS capacity: restore list order in place first.
+  // (Running the tiers on separate streams was measured slower: they contend.)
   if (restore) launch_strand_order(al->chains.p, al->perm.p, n_mid, al->slen.p, al->X.p, st);
   if (timed) HIPCHK(hipEventRecord(al->ev[11], st));
   launch_lis(true, al->chains.p, al->perm.p, nbig, al->slen.p, al->X.p, al->nodes32.p, al->pts.p, al->lisl.p, lp,
@@ -987,7 +1157,7 @@ static void fine_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   records_stage(al, n, (uint32_t)rec_done, false);
 }
 
-static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
+static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, uint32_t* gcount) {
   const pbgpu_index* ix = al->ix;
   const IndexView v = ix->view();
   hipStream_t st = al->st;
@@ -1010,7 +1180,8 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
   al->krec.ensure(rd->n_bases + 1);
   al->n_kept.ensure(n); al->thr.ensure(n); al->nhits.ensure(n); al->hit_off.ensure(n + 1);
   HIPCHK(hipEventRecord(al->ev[0], st));
-  launch_seed(v, rd->seq.p, rd->off.p, n, al->P, al->krec.p, al->n_kept.p, al->thr.p, al->nhits.p, al->stats.p, st);
+  launch_seed(seed_mode, v, rd->seq.p, rd->off.p, n, al->P, al->krec.p, al->n_kept.p, al->thr.p, al->nhits.p,
+              al->stats.p, gcount, ix->null_ptr, st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(al->ev[1], st));
   {
@@ -1250,6 +1421,7 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd) {
   al->acc.n_records += nrec;
   al->acc.g0_kept += sv[ST_G0_KEPT]; al->acc.g0_hits += sv[ST_G0_HITS]; al->acc.g0_chains += sv[ST_G0_CHAINS];
   al->acc.l0_hits += sv[ST_L0_HITS]; al->acc.l0_strands += sv[ST_L0_STRANDS];
+  al->acc.fit_chains += sv[ST_FIT_CHAINS]; al->acc.fit_points += sv[ST_FIT_POINTS];
   if (al->fine) {
     al->acc.n_fine_hits += sv[ST_FINE_HITS];
     al->acc.n_fine_windows += nrec;
@@ -1288,6 +1460,8 @@ pbgpu_status pbgpu_download(pbgpu_aligner* al, pbgpu_coords_batch** out) {
   h->recs.resize(nr);
   static_assert(sizeof(pbgpu_record) == sizeof(Rec), "record layout");
   if (nr) HIPCHK(hipMemcpy(h->recs.data(), al->recs_sorted.p, nr * sizeof(Rec), hipMemcpyDeviceToHost));
+  if (al->ix->sr_begin)  // a shard's device super-read ids are local
+    for (auto& r : h->recs) r.sr_index += (uint32_t)al->ix->sr_begin;
   if (al->last_info) {
     h->km.resize(al->last_info); h->kb.resize(al->last_info);
     HIPCHK(hipMemcpy(h->km.data(), al->info_m.p, al->last_info * 4, hipMemcpyDeviceToHost));
@@ -1306,8 +1480,59 @@ pbgpu_status pbgpu_coords_free(pbgpu_coords_batch* c) {
   return PBGPU_OK;
 }
 
+// Per read, the shards' record runs (each sorted) merged by the per-read sort
+// key of the whole index: (rs, re, ql) (jf_aligner.cc:148-154, coords_info::
+// operator<) with the (sr_index, emit) tie-break; kmers_info copied along.
+pbgpu_status pbgpu_coords_merge(const pbgpu_coords_batch* const* parts, uint64_t n_parts, pbgpu_coords_batch** out) {
+  if (!parts || !out || !n_parts) return fail(PBGPU_ERR_INVALID, "null argument");
+  for (uint64_t p = 0; p < n_parts; ++p) {
+    if (!parts[p]) return fail(PBGPU_ERR_INVALID, "null part");
+    if (parts[p]->n_reads != parts[0]->n_reads) return fail(PBGPU_ERR_INVALID, "parts cover different read batches");
+  }
+  API_TRY
+  std::unique_ptr<coords_holder> h(new coords_holder);
+  const uint64_t n = parts[0]->n_reads;
+  uint64_t nr = 0, ni = 0;
+  for (uint64_t p = 0; p < n_parts; ++p) { nr += parts[p]->n_records; ni += parts[p]->n_info; }
+  h->off.assign(n + 1, 0);
+  h->recs.reserve(nr);
+  h->km.reserve(ni); h->kb.reserve(ni);
+  auto before = [](const pbgpu_record& a, const pbgpu_record& b) {
+    if (a.rs != b.rs) return a.rs < b.rs;
+    if (a.re != b.re) return a.re < b.re;
+    if (a.ql != b.ql) return a.ql < b.ql;
+    if (a.sr_index != b.sr_index) return a.sr_index < b.sr_index;
+    return a.emit < b.emit;
+  };
+  std::vector<std::pair<uint64_t, uint64_t>> run;  // (part, record)
+  for (uint64_t r = 0; r < n; ++r) {
+    run.clear();
+    for (uint64_t p = 0; p < n_parts; ++p)
+      for (uint64_t i = parts[p]->read_offsets[r]; i < parts[p]->read_offsets[r + 1]; ++i) run.emplace_back(p, i);
+    std::sort(run.begin(), run.end(), [&](const std::pair<uint64_t, uint64_t>& a, const std::pair<uint64_t, uint64_t>& b) {
+      return before(parts[a.first]->records[a.second], parts[b.first]->records[b.second]);
+    });
+    for (const auto& q : run) {
+      const pbgpu_coords_batch* c = parts[q.first];
+      pbgpu_record R = c->records[q.second];
+      const uint64_t io = h->km.size();
+      h->km.insert(h->km.end(), c->kmers_info + R.info_offset, c->kmers_info + R.info_offset + R.n_info);
+      h->kb.insert(h->kb.end(), c->bases_info + R.info_offset, c->bases_info + R.info_offset + R.n_info);
+      R.info_offset = io;
+      h->recs.push_back(R);
+    }
+    h->off[r + 1] = h->recs.size();
+  }
+  h->c.n_reads = n; h->c.n_records = h->recs.size(); h->c.read_offsets = h->off.data(); h->c.records = h->recs.data();
+  h->c.n_info = h->km.size(); h->c.kmers_info = h->km.data(); h->c.bases_info = h->kb.data();
+  *out = &h.release()->c;
+  return PBGPU_OK;
+  API_CATCH
+}
+
 pbgpu_status pbgpu_aligner_set_details(pbgpu_aligner* al, int enable) {
   if (!al) return fail(PBGPU_ERR_INVALID, "null argument");
+  if (enable && al->ix->n_shards > 1) return fail(PBGPU_ERR_UNSUPPORTED, "--details runs on a whole index only");
   al->details = enable != 0;
   return PBGPU_OK;
 }

@@ -101,6 +101,7 @@ enum StatSlot {
   ST_G0_KEPT, ST_G0_HITS, ST_G0_CHAINS,  // work completed by first-tier (4-wave LDS) k_group launches
   ST_L0_HITS, ST_L0_STRANDS,             // work of the tier-0 (n <= 255) k_lis_w launches
   ST_FINE_HITS,                          // fine aligner: windowed hits
+  ST_FIT_CHAINS, ST_FIT_POINTS,          // coarse k_coords work: chains, lis points (counted by the chain order pass)
   ST_N
 };
 

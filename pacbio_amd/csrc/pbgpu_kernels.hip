@@ -217,12 +217,25 @@ __global__ void k_headers(const uint64_t* keys, const uint64_t* kpos, const uint
 
 // ================================================================== seed
 // One workgroup per read.  fetch_super_reads (coarse_aligner.cc:81-125).
-template <int BLOCK, int PER>
+// MODE (index sharded by super-read range):
+//   SEED_WHOLE   the index holds every super-read: counts come from the table;
+//   SEED_COUNTS  this shard's count of every looked-up k-mer, saturated at
+//                max_count + 1, goes to gcount[read offset + position] (then
+//                summed over the shards by the caller: RCCL all-reduce) -- a sum
+//                of per-shard counts saturated at max_count + 1 decides every
+//                use of the count (skip, histogram, threshold) exactly;
+//   SEED_FINISH  the summed counts drive the filter and the 99% threshold, so
+//                every shard keeps the same k-mers; hits come from this shard's
+//                occurrence lists (a k-mer absent here points at the index's
+//                empty header).
+enum { SEED_WHOLE = 0, SEED_COUNTS = 1, SEED_FINISH = 2 };
+template <int BLOCK, int PER, int MODE>
 __global__ __launch_bounds__(BLOCK) void k_seed(IndexView ix, const uint8_t* __restrict__ seq,
                                                 const uint64_t* __restrict__ roff, uint32_t n_reads,
                                                 AlignParamsDev P, KRec* __restrict__ krec,
                                                 uint32_t* __restrict__ n_kept_out, uint32_t* __restrict__ thr_out,
-                                                uint64_t* __restrict__ nhits_out, unsigned long long* stats) {
+                                                uint64_t* __restrict__ nhits_out, unsigned long long* stats,
+                                                uint32_t* __restrict__ gcount, uint64_t null_ptr) {
   constexpr int TILE = BLOCK * PER;
   constexpr int LOOK = 32;
   __shared__ uint8_t s_seq[TILE + LOOK];
@@ -300,11 +313,20 @@ __global__ __launch_bounds__(BLOCK) void k_seed(IndexView ix, const uint8_t* __r
         uint64_t payload; uint32_t pr = 0;
         const bool found = table_lookup(ix, canon, payload, pr);
         my_probes += pr;
+        uint32_t cnt = 0;
+        uint64_t ptr = null_ptr;
         if (found) {
-          uint32_t cnt = (uint32_t)(payload & SAT_COUNT);
-          const uint64_t ptr = payload >> 24;
+          cnt = (uint32_t)(payload & SAT_COUNT);
+          ptr = payload >> 24;
           if (cnt == SAT_COUNT) cnt = (uint32_t)(ix.occ[ptr] & 0xFFFFFFFFull);
-          if (cnt < (uint32_t)P.max_count) {  // count >= 1 here
+        }
+        const uint64_t gi = base + (uint64_t)(p0 + q);
+        if (MODE == SEED_COUNTS) {
+          const uint32_t sat = (uint32_t)P.max_count + 1u;
+          gcount[gi] = cnt < sat ? cnt : sat;
+        } else {
+          if (MODE == SEED_FINISH) cnt = gcount[gi];
+          if (cnt != 0 && cnt < (uint32_t)P.max_count) {
             fl[q] = 1; ++nkept;
             kp_ptr[q] = ptr | ((mm[q] < rr[q]) ? (1ull << 63) : 0ull);
             kp_cnt[q] = cnt;
@@ -330,6 +352,15 @@ __global__ __launch_bounds__(BLOCK) void k_seed(IndexView ix, const uint8_t* __r
     __syncthreads();
   }
 
+  if (MODE == SEED_COUNTS) {
+    const uint64_t kmers = block_sum_u64<BLOCK>(my_kmers, s_tmp64);
+    const uint64_t probes = block_sum_u64<BLOCK>(my_probes, s_tmp64);
+    if (tid == 0) {
+      atomicAdd(&stats[ST_KMERS], (unsigned long long)kmers);
+      atomicAdd(&stats[ST_PROBES], (unsigned long long)probes);
+    }
+    return;
+  }
   // ---- 99% threshold (coarse_aligner.cc:117-125) via block radix select
   const uint32_t n_kept = kept_carry;
   const uint32_t sum_thresh = (uint32_t)round((double)n_kept * 0.99);
@@ -397,6 +428,10 @@ __global__ __launch_bounds__(BLOCK) void k_seed(IndexView ix, const uint8_t* __r
 // 4 waves share one read's table; reads touching many super-reads use a
 // 16-wave block over the largest LDS table.
 constexpr uint32_t GROUP_BLOCK = 256, GROUP_BLOCK_BIG = 1024;
+#ifndef PBGPU_GROUP_PF
+#define PBGPU_GROUP_PF 1
+#endif
+constexpr int GROUP_PF = PBGPU_GROUP_PF;  // 256-hit steps whose occurrence loads are in flight at once
 
 template <bool GLOBAL_TABLE, uint32_t B>
 __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restrict__ krec,
@@ -486,20 +521,30 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
         pb = s_pb[lo];
         return fwd ? s_pf[lo] + local : s_pbk[lo] + (local - s_nf[lo]);
       };
-      uint64_t e_nx = 0;
-      uint32_t rec_nx = 0xFFFFFFFFu;
-      bool fwd_nx = true;
-      int32_t pb_nx = 0;
-      if (tid < total) e_nx = ix.occ[locate(tid, rec_nx, fwd_nx, pb_nx)];
-      for (uint32_t h0 = 0; h0 < total; h0 += B) {
+      // GROUP_PF steps of occurrence loads in flight per thread (a ring of
+      // statically indexed registers): the enumeration is latency-bound otherwise
+      uint64_t e_q[GROUP_PF];
+      uint32_t rec_q[GROUP_PF];
+      bool fwd_q[GROUP_PF];
+      int32_t pb_q[GROUP_PF];
+#pragma unroll
+      for (int d = 0; d < GROUP_PF; ++d) {
+        e_q[d] = 0; rec_q[d] = 0xFFFFFFFFu; fwd_q[d] = true; pb_q[d] = 0;
+        if (d * B + tid < total) e_q[d] = ix.occ[locate(d * B + tid, rec_q[d], fwd_q[d], pb_q[d])];
+      }
+      for (uint32_t hq = 0; hq < total; hq += GROUP_PF * B) {
+#pragma unroll
+      for (int d = 0; d < GROUP_PF; ++d) {
+        const uint32_t h0 = hq + d * B;
+        if (h0 >= total) break;  // block-uniform
         const uint32_t h = h0 + tid;
         const bool valid = h < total;
         uint32_t sr = 0, slot = 0, rec = 0xFFFFFFFFu;  // rec: the hit's k-mer record (unused after locate)
         int32_t so = 0, pb = 0;
         bool fwd = true;
-        const uint64_t e = e_nx;
-        if (valid) { rec = rec_nx; fwd = fwd_nx; pb = pb_nx; }
-        if (h + B < total) e_nx = ix.occ[locate(h + B, rec_nx, fwd_nx, pb_nx)];
+        const uint64_t e = e_q[d];
+        if (valid) { rec = rec_q[d]; fwd = fwd_q[d]; pb = pb_q[d]; }
+        if (h + GROUP_PF * B < total) e_q[d] = ix.occ[locate(h + GROUP_PF * B, rec_q[d], fwd_q[d], pb_q[d])];
         bool mine = valid;
         if (valid) {
           sr = (uint32_t)(e >> 32);
@@ -541,6 +586,7 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
           }
           if (mine) O.X[hbase + pos] = make_int2(pb, fwd ? so : -so);
         }
+      }
       }
       __syncthreads();
 #ifdef PBGPU_PROF
@@ -635,12 +681,25 @@ struct ChainLisLen {  // item = chain; the longer of its two lis
   const uint32_t* lisl;
   DEV uint32_t operator()(uint32_t c) const { const uint32_t a = lisl[2 * c], b = lisl[2 * c + 1]; return a > b ? a : b; }
 };
+// sums (optional): [0] += number of non-empty items, [1] += their total length
+// (one atomic pair per block: the work counters of the kernel that consumes them)
 template <typename F>
-__global__ __launch_bounds__(256) void k_len_hist(F f, uint32_t n, uint32_t* hist) {
+__global__ __launch_bounds__(256) void k_len_hist(F f, uint32_t n, uint32_t* hist, unsigned long long* sums) {
   __shared__ uint32_t h[NLB];
+  __shared__ uint64_t s_red[4];
   for (uint32_t i = threadIdx.x; i < NLB; i += 256) h[i] = 0;
   __syncthreads();
-  for (uint32_t c = blockIdx.x * 256 + threadIdx.x; c < n; c += gridDim.x * 256) atomicAdd(&h[len_bucket(f(c))], 1u);
+  uint64_t cnt = 0, len = 0;
+  for (uint32_t c = blockIdx.x * 256 + threadIdx.x; c < n; c += gridDim.x * 256) {
+    const uint32_t v = f(c);
+    atomicAdd(&h[len_bucket(v)], 1u);
+    cnt += v != 0; len += v;
+  }
+  if (sums) {
+    cnt = block_sum_u64<256>(cnt, s_red);
+    len = block_sum_u64<256>(len, s_red);
+    if (threadIdx.x == 0 && cnt) { atomicAdd(&sums[0], (unsigned long long)cnt); atomicAdd(&sums[1], (unsigned long long)len); }
+  }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < NLB; i += 256) if (h[i]) atomicAdd(&hist[i], h[i]);
 }
@@ -1854,10 +1913,19 @@ void launch_headers(const uint64_t* keys, const uint64_t* kpos, const uint64_t* 
 }
 
 constexpr int SEED_BLOCK = 256, SEED_PER = 8;
-void launch_seed(IndexView ix, const uint8_t* seq, const uint64_t* roff, uint32_t n_reads, AlignParamsDev P,
-                 KRec* krec, uint32_t* n_kept, uint32_t* thr, uint64_t* nhits, unsigned long long* stats, hipStream_t st) {
-  hipLaunchKernelGGL((k_seed<SEED_BLOCK, SEED_PER>), dim3(n_reads), dim3(SEED_BLOCK), 0, st, ix, seq, roff, n_reads, P,
-                     krec, n_kept, thr, nhits, stats);
+// mode: SEED_WHOLE / SEED_COUNTS / SEED_FINISH (gcount: per read position, indexed like seq)
+void launch_seed(int mode, IndexView ix, const uint8_t* seq, const uint64_t* roff, uint32_t n_reads, AlignParamsDev P,
+                 KRec* krec, uint32_t* n_kept, uint32_t* thr, uint64_t* nhits, unsigned long long* stats,
+                 uint32_t* gcount, uint64_t null_ptr, hipStream_t st) {
+  if (mode == SEED_COUNTS)
+    hipLaunchKernelGGL((k_seed<SEED_BLOCK, SEED_PER, SEED_COUNTS>), dim3(n_reads), dim3(SEED_BLOCK), 0, st, ix, seq, roff,
+                       n_reads, P, krec, n_kept, thr, nhits, stats, gcount, null_ptr);
+  else if (mode == SEED_FINISH)
+    hipLaunchKernelGGL((k_seed<SEED_BLOCK, SEED_PER, SEED_FINISH>), dim3(n_reads), dim3(SEED_BLOCK), 0, st, ix, seq, roff,
+                       n_reads, P, krec, n_kept, thr, nhits, stats, gcount, null_ptr);
+  else
+    hipLaunchKernelGGL((k_seed<SEED_BLOCK, SEED_PER, SEED_WHOLE>), dim3(n_reads), dim3(SEED_BLOCK), 0, st, ix, seq, roff,
+                       n_reads, P, krec, n_kept, thr, nhits, stats, gcount, null_ptr);
 }
 
 void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const uint32_t* n_kept, const uint32_t* thr,
@@ -1899,17 +1967,23 @@ void launch_strand_order(const uint32_t* slen, uint32_t n_items, uint32_t* hist,
                          int phase, hipStream_t st) {
   if (!n_items) return;
   StrandLen f{slen};
-  if (phase == 0) hipLaunchKernelGGL((k_len_hist<StrandLen>), dim3(grid_for(n_items, 256, 2048)), dim3(256), 0, st, f, n_items, hist);
+  if (phase == 0)
+    hipLaunchKernelGGL((k_len_hist<StrandLen>), dim3(grid_for(n_items, 256, 2048)), dim3(256), 0, st, f, n_items, hist,
+                       (unsigned long long*)nullptr);
   else hipLaunchKernelGGL((k_len_perm<StrandLen>), dim3((n_items + 255) / 256), dim3(256), 0, st, f, n_items, cursor, perm);
 }
 void launch_chain_order(const uint32_t* lisl, uint32_t n, uint32_t* hist, uint32_t* cursor, uint32_t* perm, int phase,
-                        hipStream_t st) {
+                        unsigned long long* sums, hipStream_t st) {
   if (!n) return;
   ChainLisLen f{lisl};
-  if (phase == 0) hipLaunchKernelGGL((k_len_hist<ChainLisLen>), dim3(grid_for(n, 256, 2048)), dim3(256), 0, st, f, n, hist);
+  if (phase == 0)
+    hipLaunchKernelGGL((k_len_hist<ChainLisLen>), dim3(grid_for(n, 256, 2048)), dim3(256), 0, st, f, n, hist, sums);
   else hipLaunchKernelGGL((k_len_perm<ChainLisLen>), dim3((n + 255) / 256), dim3(256), 0, st, f, n, cursor, perm);
 }
-constexpr int LIS_CH16 = 8, LIS_CH32 = 8, FIT_CH = 8;
+#ifndef PBGPU_FIT_CH
+#define PBGPU_FIT_CH 8
+#endif
+constexpr int LIS_CH16 = 8, LIS_CH32 = 8, FIT_CH = PBGPU_FIT_CH;
 void launch_lis(bool big_nodes, const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen,
                 const int2* X, void* N, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx,
                 unsigned long long* stats, hipStream_t st) {

@@ -34,6 +34,9 @@ EXPORTS = [
     "pbgpu_aligner_get_stats", "pbgpu_aligner_reset_stats", "pbgpu_aligner_set_hit_budget",
     "pbgpu_format_coords", "pbgpu_free_text",
     "pbgpu_aligner_set_details", "pbgpu_download_details", "pbgpu_details_free", "pbgpu_format_details",
+    "pbgpu_shard_counts", "pbgpu_shard_counts_download", "pbgpu_shard_counts_upload", "pbgpu_rccl_unique_id",
+    "pbgpu_rccl_comm_create", "pbgpu_rccl_comm_free", "pbgpu_shard_counts_allreduce", "pbgpu_align_resident_shard",
+    "pbgpu_coords_merge",
 ]
 
 
@@ -45,13 +48,13 @@ class PbgpuError(RuntimeError):
 
 class IndexParams(C.Structure):
     _fields_ = [("k", C.c_uint32), ("psa_min", C.c_uint32), ("device", C.c_int32), ("threads", C.c_int32),
-                ("fine_k", C.c_uint32)]
+                ("fine_k", C.c_uint32), ("shard", C.c_uint32), ("n_shards", C.c_uint32)]
 
 
 class IndexInfo(C.Structure):
     _fields_ = [("n_sr", C.c_uint64), ("text_len", C.c_uint64), ("n_kmers", C.c_uint64),
                 ("n_occurrences", C.c_uint64), ("table_buckets", C.c_uint64), ("device_bytes", C.c_uint64),
-                ("build_seconds", C.c_double)]
+                ("build_seconds", C.c_double), ("sr_begin", C.c_uint64), ("sr_end", C.c_uint64)]
 
 
 class AlignParams(C.Structure):
@@ -94,7 +97,8 @@ class Stats(C.Structure):
                [(n, C.c_double) for n in ("ms_seed", "ms_group", "ms_lis", "ms_fit", "ms_records")] + \
                [("kernel_ms", C.c_double * 8), ("kernel_launches", C.c_uint64 * 8)] + \
                [(n, C.c_uint64) for n in ("g0_kept", "g0_hits", "g0_chains", "l0_hits", "l0_strands",
-                                          "n_fine_hits", "n_fine_windows")] + [("ms_fine", C.c_double)]
+                                          "n_fine_hits", "n_fine_windows")] + [("ms_fine", C.c_double)] + \
+               [(n, C.c_uint64) for n in ("fit_chains", "fit_points")]
 
     def as_dict(self):
         d = {n: getattr(self, n) for n, _ in self._fields_ if not n.startswith("kernel_")}
@@ -152,6 +156,16 @@ def lib():
         L.pbgpu_details_free.argtypes = [C.POINTER(DetailsBatch)]
         L.pbgpu_format_details.argtypes = [vp, C.POINTER(DetailsBatch), C.POINTER(C.c_char_p), C.c_int,
                                            C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]
+        L.pbgpu_shard_counts.argtypes = [vp, vp]
+        L.pbgpu_shard_counts_download.argtypes = [vp, C.c_void_p, C.c_uint64]
+        L.pbgpu_shard_counts_upload.argtypes = [vp, C.c_void_p, C.c_uint64]
+        L.pbgpu_rccl_unique_id.argtypes = [C.c_void_p]
+        L.pbgpu_rccl_comm_create.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.POINTER(vp)]
+        L.pbgpu_rccl_comm_free.argtypes = [vp]
+        L.pbgpu_shard_counts_allreduce.argtypes = [vp, vp]
+        L.pbgpu_align_resident_shard.argtypes = [vp, vp]
+        L.pbgpu_coords_merge.argtypes = [C.POINTER(C.POINTER(CoordsBatch)), C.c_uint64,
+                                         C.POINTER(C.POINTER(CoordsBatch))]
         L.pbgpu_free_text.argtypes = [C.c_void_p]
         L.pbgpu_free_text.restype = None
         _lib = L
@@ -202,15 +216,15 @@ class Index:
         self.h = handle
 
     @classmethod
-    def from_fasta(cls, paths, k, psa_min=13, device=0, threads=0, fine_k=0):
-        p = IndexParams(k, psa_min, device, threads, fine_k)
+    def from_fasta(cls, paths, k, psa_min=13, device=0, threads=0, fine_k=0, shard=0, n_shards=1):
+        p = IndexParams(k, psa_min, device, threads, fine_k, shard, n_shards)
         h = C.c_void_p()
         _check(lib().pbgpu_index_build_fasta(_cstrs(paths), len(paths), C.byref(p), C.byref(h)))
         return cls(h)
 
     @classmethod
-    def from_records(cls, names, seqs, k, psa_min=13, device=0, threads=0, fine_k=0):
-        p = IndexParams(k, psa_min, device, threads, fine_k)
+    def from_records(cls, names, seqs, k, psa_min=13, device=0, threads=0, fine_k=0, shard=0, n_shards=1):
+        p = IndexParams(k, psa_min, device, threads, fine_k, shard, n_shards)
         bs = [s if isinstance(s, bytes) else s.encode() for s in seqs]
         lens = (C.c_uint64 * max(1, len(bs)))(*[len(b) for b in bs])
         h = C.c_void_p()
@@ -339,6 +353,28 @@ class Aligner:
     def reset_stats(self):
         _check(lib().pbgpu_aligner_reset_stats(self.h))
 
+    def shard_counts(self, reads):
+        """Sharded index, step 1: this shard's saturated k-mer counts of the batch
+        into the aligner's count buffer."""
+        _check(lib().pbgpu_shard_counts(self.h, reads.h))
+
+    def counts_download(self, n_bases):
+        out = np.empty(n_bases, dtype=np.uint32)
+        _check(lib().pbgpu_shard_counts_download(self.h, out.ctypes.data, n_bases))
+        return out
+
+    def counts_upload(self, counts):
+        c = np.ascontiguousarray(counts, dtype=np.uint32)
+        _check(lib().pbgpu_shard_counts_upload(self.h, c.ctypes.data, len(c)))
+
+    def counts_allreduce(self, comm):
+        """Step 2 over RCCL: sum the count buffers of all ranks in place."""
+        _check(lib().pbgpu_shard_counts_allreduce(self.h, comm.h))
+
+    def align_resident_shard(self, reads):
+        """Sharded index, step 3: the rest of the path with the summed counts."""
+        _check(lib().pbgpu_align_resident_shard(self.h, reads.h))
+
     def set_details(self, on=True):
         _check(lib().pbgpu_aligner_set_details(self.h, int(bool(on))))
 
@@ -360,6 +396,41 @@ class Aligner:
             self.close()
         except Exception:
             pass
+
+
+def rccl_unique_id():
+    buf = (C.c_uint8 * 128)()
+    _check(lib().pbgpu_rccl_unique_id(buf))
+    return bytes(buf)
+
+
+class RcclComm:
+    """An RCCL communicator (one per rank) for the sharded-index count exchange."""
+
+    def __init__(self, device, n_ranks, rank, uid):
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        h = C.c_void_p()
+        _check(lib().pbgpu_rccl_comm_create(device, n_ranks, rank, buf, C.byref(h)))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            lib().pbgpu_rccl_comm_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def merge_coords(parts):
+    """pbgpu_coords_merge: the shards' batches of one read batch, merged per read."""
+    arr = (C.POINTER(CoordsBatch) * len(parts))(*[p.ptr for p in parts])
+    out = C.POINTER(CoordsBatch)()
+    _check(lib().pbgpu_coords_merge(arr, len(parts), C.byref(out)))
+    return Coords(out)
 
 
 class Details:
