@@ -1343,7 +1343,7 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_
       HIPCHK(hipEventRecord(al->ev[13], st));
       launch_coords(v, al->P, al->chains.p, al->perm.p, n_fit, rd->off.p, 0, CO, st);
       HIPCHK(hipGetLastError());
-      HIPCHK(hipEventRecord(al->ev[14], st));
+      HIPCHK(hipEventRecord(al->ev[14], st));  // the timed k_coords slot: the first launch alone
       // --max-match rounds: discard the emitted lis, redo the strand's LIS, emit again
       for (uint32_t round = 1, cur = 0; al->P.max_match; ++round) {
         uint32_t nr3[3];
@@ -1371,7 +1371,6 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_
         launch_coords(v, al->P, al->chains.p, al->redo[2].p, nre, rd->off.p, round, CO, st);
         HIPCHK(hipGetLastError());
       }
-      HIPCHK(hipEventRecord(al->ev[14], st));
       HIPCHK(hipEventRecord(al->ev[7], st));
       uint32_t nrec = 0;
       unsigned long long ninfo = 0, ovf = 0;

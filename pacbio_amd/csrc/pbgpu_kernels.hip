@@ -1204,21 +1204,27 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
     while (cur < n) {
       const uint32_t pend = cur + 64 < n ? cur + 64 : n;
       uint32_t m = 0;
-      if (fast && head != NONE) {
+      if (fast) {
+        // The strand's first element (empty list) is clean too: no scan, len 1,
+        // P = NONE, its own root, inserted at the head (what the literal step does).
+        const bool empty = head == NONE;
         const uint32_t i = cur + lane;
         bool clean = false;
         int2 xi = make_int2(0, 0);
         if (i < pend) {
-          const uint32_t hj = lane == 0 ? head : i - 1;
           xi = sx[i];
-          const int2 xj = sx[hj];
-          clean = xi.y > xj.y && affine_ok(lp.a, lp.b, lp.C, (double)(xi.x - xj.x), (double)(xi.y - xj.y));
+          if (lane == 0 && empty) {
+            clean = true;
+          } else {
+            const int2 xj = sx[lane == 0 ? head : i - 1];
+            clean = xi.y > xj.y && affine_ok(lp.a, lp.b, lp.C, (double)(xi.x - xj.x), (double)(xi.y - xj.y));
+          }
         }
         const uint64_t bad = __ballot(i < pend && !clean);
         m = bad ? (uint32_t)__ffsll((unsigned long long)bad) - 1 : pend - cur;
         if (m) {
-          const uint32_t hl = sln[head], hr = sroot[head];
-          const uint32_t rsr = head + 1 == cur ? srs[head] : cur;  // run of P(e) = e-1 links
+          const uint32_t hl = empty ? 0u : sln[head], hr = empty ? cur : sroot[head];
+          const uint32_t rsr = !empty && head + 1 == cur ? srs[head] : cur;  // run of P(e) = e-1 links
           const int2 hrx = sx[hr];
           bool cand = false;
           if ((uint32_t)lane < m) {
@@ -1235,8 +1241,10 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
             longest = hl + 1 + top; longest_ind = cur + top;
           }
           head = cur + m - 1;
-          tests += m;
+          tests += m - (empty ? 1u : 0u);  // the first element tests nothing
           cur += m;
+          PROF_ADD(21, 1);
+          PROF_ADD(22, m);
           lds_fence();
         }
       }
@@ -1245,8 +1253,12 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
         const uint32_t i = cur;
         const int2 xi = sx[i];
         uint32_t prev = NONE, prev_len = 0, prev_nxt = NONE, found = NONE;
+#ifdef PBGPU_PROF
+        PROF_ADD(20, 1);
+#endif
         for (uint32_t it = head; it != NONE;) {
           ++tests;
+          PROF_ADD(23, 1);
           const uint32_t lj = sln[it];
           const int2 xj = sx[it];
           if (xi.y > xj.y) {
@@ -1327,6 +1339,9 @@ struct KmersInfo {
   const int32_t* cl;  // optional cache: length of unitig i at cl[i * stride], UL_INVALID if unusable
   uint32_t cunitig;
   int32_t cend, prev_pos;
+  // pending increments of element 2 * cunitig (mers, bases), kept in registers
+  // while consecutive points stay in one unitig: the common case touches no memory
+  int32_t pm, pb;
   static constexpr int32_t UL_INVALID = INT32_MIN;
   DEV uint32_t uid(uint32_t i) const { return i >= nsz ? INVALID_UNITIG : (rev ? ids[nsz - 1 - i] : ids[i]); }
   DEV int32_t ulen_direct(uint32_t i) const {
@@ -1354,6 +1369,10 @@ struct KmersInfo {
     cunitig = 0;
     cend = l0;
     prev_pos = (int32_t)(0u - (uint32_t)k);
+    pm = 0; pb = 0;
+  }
+  DEV void flush() {
+    if (pm | pb) { M(2 * cunitig) += pm; B(2 * cunitig) += pb; pm = 0; pb = 0; }
   }
   DEV void add(int32_t sr_pos) {
     if (!ok) return;
@@ -1363,14 +1382,15 @@ struct KmersInfo {
         if (cunitig >= nsz - 1) { ok = false; return; }
         const int32_t mx = sr_pos > prev_pos + k ? sr_pos : prev_pos + k;
         const int32_t nbb = cend - mx + 1;
-        B(2 * cunitig) += nbb; B(2 * cunitig + 1) += nbb;
+        pb += nbb; B(2 * cunitig + 1) += nbb;
       }
+      flush();
       const int32_t l = ulen(++cunitig);
       if (l == UL_INVALID) { ok = false; return; }
       cend = (int32_t)((uint32_t)cend + (uint32_t)l - (uint32_t)uk + 1u);
     }
-    ++M(2 * cunitig);
-    B(2 * cunitig) += new_bases;
+    ++pm;
+    pb += new_bases;
     int32_t cendi = cend;
     for (uint32_t i = cunitig; (i < nsz - 1) && ((uint32_t)sr_pos + (uint32_t)k > (uint32_t)cendi - (uint32_t)uk + 1u); ++i) {
       const int32_t full_mer = sr_pos + uk > cendi + 1;
@@ -1543,6 +1563,7 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
       R.info_off = io;
       if (info_lds) {
         if (KI.ok) {
+          KI.flush();
           for (uint32_t q = 0; q < need; ++q) { O.info_m[io + q] = im[q * 64 + lane]; O.info_b[io + q] = ib[q * 64 + lane]; }
           R.n_info = need;
         }
@@ -1558,7 +1579,7 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
   G3.init(base, pass3 ? nl : 0);
   const uint32_t nch3 = wave_max_u32(G3.chunks());
   stream_rows<CH>(O.pts, G3, nch3, ps, [&](const int2 p) { KI.add(info_pos(p.y)); });
-  if (pass3 && KI.ok) R.n_info = 2 * nsz - 1;
+  if (pass3 && KI.ok) { KI.flush(); R.n_info = 2 * nsz - 1; }
   if (keep) {
     const uint32_t ri = atomicAdd(O.rec_count, 1u);
     if (ri < O.rec_cap && info_ok) O.recs[ri] = R;
@@ -1912,7 +1933,10 @@ void launch_headers(const uint64_t* keys, const uint64_t* kpos, const uint64_t* 
   hipLaunchKernelGGL(k_headers, dim3(4096), dim3(256), 0, st, keys, kpos, run_start, U, occ, table, bucket_mask, k, ebits);
 }
 
-constexpr int SEED_BLOCK = 256, SEED_PER = 8;
+#ifndef PBGPU_SEED_PER
+#define PBGPU_SEED_PER 8
+#endif
+constexpr int SEED_BLOCK = 256, SEED_PER = PBGPU_SEED_PER;
 // mode: SEED_WHOLE / SEED_COUNTS / SEED_FINISH (gcount: per read position, indexed like seq)
 void launch_seed(int mode, IndexView ix, const uint8_t* seq, const uint64_t* roff, uint32_t n_reads, AlignParamsDev P,
                  KRec* krec, uint32_t* n_kept, uint32_t* thr, uint64_t* nhits, unsigned long long* stats,

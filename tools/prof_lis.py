@@ -43,6 +43,7 @@ def main():
     for n, x in zip(names[:6], v[:6]):
         print(f"  {n:16s} {x / waves:12.0f} ticks/wave  ({100.0 * x / max(1, v[5]):5.1f}%)")
     g = list(buf)
+    print(f"k_lis_w: literal steps={g[20]} (scan iterations {g[23]}), clean runs={g[21]} covering {g[22]} elements")
     for label, sb in (("k_group 2048-slot tier", 8), ("k_group 8192-slot tier", 14)):
         blocks = max(1, g[sb + 5])
         print(f"{label}: blocks={g[sb + 5]} (ms: tier0 {st['kernel_ms']['k_group']:.2f})")
