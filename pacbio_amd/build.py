@@ -67,19 +67,27 @@ def build_pbgpu(force=False):
     return lib
 
 
-def build_pbgpu_prof():
-    """Phase-profiling variant (-DPBGPU_PROF) for tools/prof_lis.py; never the product library."""
-    objdir = os.path.join(ROOT, "build", "prof")
+def build_pbgpu_variant(name, defines):
+    """Experiment / profiling variant libpbgpu_<name>.so built with extra -D
+    flags (tools/prof_*.py, tools/exp_*.py); never the product library."""
+    objdir = os.path.join(ROOT, "build", name)
     os.makedirs(objdir, exist_ok=True)
-    objs = []
+    jobs, objs = [], []
     for s in ["pbgpu_kernels.hip", "pbgpu_api.hip"]:
         obj = os.path.join(objdir, s + ".o")
-        _run([HIPCC] + HIPFLAGS + ["-DPBGPU_PROF", "-c", os.path.join(CSRC, s), "-o", obj])
+        jobs.append([HIPCC] + HIPFLAGS + list(defines) + ["-c", os.path.join(CSRC, s), "-o", obj])
         objs.append(obj)
-    lib = os.path.join(PKG, "libpbgpu_prof.so")
+    with ThreadPoolExecutor(len(jobs)) as ex:
+        list(ex.map(_run, jobs))
+    lib = os.path.join(PKG, f"libpbgpu_{name}.so")
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + objs +
          ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-lpthread"])
     return lib
+
+
+def build_pbgpu_prof():
+    """Phase-profiling variant (-DPBGPU_PROF) for tools/prof_lis.py; never the product library."""
+    return build_pbgpu_variant("prof", ["-DPBGPU_PROF"])
 
 
 def build_oracle():

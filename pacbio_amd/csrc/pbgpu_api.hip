@@ -709,7 +709,8 @@ static void capture_details(pbgpu_aligner* al, uint32_t nch, uint64_t Hs) {
       const bool mine = (strand == 0) == fa;
       for (uint32_t i = 0; i < n; ++i) {
         D.hits.push_back(L[i].x); D.hits.push_back(L[i].y);
-        const bool in = mine && li < nl && P[li].x == L[i].x && P[li].y == L[i].y;
+        const int2 q = mine && li < nl ? pt_get(P, li) : make_int2(0, 0);
+        const bool in = mine && li < nl && q.x == L[i].x && q.y == L[i].y;
         D.lis.push_back(in ? 1 : 0);
         li += in;
       }

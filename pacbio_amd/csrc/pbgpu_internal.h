@@ -124,6 +124,30 @@ struct LisParams {
   int ordered;           // lists are already in list order (no k_group order restoration)
 };
 
+// Lis points of one strand, written by the LIS kernels into the strand's own
+// region of the per-hit array pts (room for n >= len int2) and read by
+// k_coords and the details capture.  Two layouts:
+//  * compact (len >= 2, every point within 65535 of the last one in x and y):
+//    word 0 = last.x | PT_COMPACT, word 1 = last.y, word 2 + i =
+//    (last.x - x_i) << 16 | (last.y - y_i) -- 4 bytes a point;
+//  * wide: pts[i] = (x_i, y_i), x_i > 0 (a pb offset) so word 0 has no flag.
+constexpr uint32_t PT_COMPACT = 0x80000000u;
+__host__ __device__ inline bool pt_fits(int2 last, int2 p) {
+  return (uint32_t)(last.x - p.x) < 65536u && (uint32_t)(last.y - p.y) < 65536u;
+}
+__host__ __device__ inline uint32_t pt_word(int2 last, int2 p) {
+  return (uint32_t)(last.x - p.x) << 16 | (uint32_t)(last.y - p.y);
+}
+__host__ __device__ inline int2 pt_decode(int2 last, uint32_t w) {
+  return make_int2(last.x - (int32_t)(w >> 16), last.y - (int32_t)(w & 0xFFFFu));
+}
+// point i of the lis stored at region (host side: details)
+__host__ __device__ inline int2 pt_get(const int2* region, uint32_t i) {
+  const uint32_t* w = (const uint32_t*)region;
+  if (w[0] & PT_COMPACT) return pt_decode(make_int2((int32_t)(w[0] & ~PT_COMPACT), (int32_t)w[1]), w[2 + i]);
+  return region[i];
+}
+
 struct ChainOut {
   const int2* pts;
   const uint32_t* lisl;

@@ -24,7 +24,8 @@ namespace pbgpu {
 // Optional phase profiling of k_lis (build with -DPBGPU_PROF; tools/prof_lis.py):
 // per-wave s_memtime deltas summed into g_prof.
 #ifdef PBGPU_PROF
-__device__ unsigned long long g_prof[32];
+constexpr int PROF_SLOTS = 96;
+__device__ unsigned long long g_prof[PROF_SLOTS];
 #define PROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define PROF_ADD(slot, v) do { if (lane_id() == 0) atomicAdd(&g_prof[slot], (unsigned long long)(v)); } while (0)
 #else
@@ -803,8 +804,8 @@ template <int CH>
 struct ChunkGrid;
 // Streams every lane's item through the LDS tile chunk by chunk, the next
 // chunk's rows in flight while f() consumes the current one.
-template <int CH, typename F>
-DEV void stream_rows(const int2* __restrict__ src, const ChunkGrid<CH>& G, uint32_t nch, int2* tile, F&& f);
+template <int CH, typename T, typename F>
+DEV void stream_rows(const T* __restrict__ src, const ChunkGrid<CH>& G, uint32_t nch, T* tile, F&& f);
 
 // A lane's item occupies [b, b + n) of a per-hit array; chunks follow the
 // absolute CH-aligned grid so that every row is one aligned segment.
@@ -824,10 +825,10 @@ struct ChunkGrid {
   }
 };
 
-template <int CH, typename F>
-DEV void stream_rows(const int2* __restrict__ src, const ChunkGrid<CH>& G, uint32_t nch, int2* tile, F&& f) {
+template <int CH, typename T, typename F>
+DEV void stream_rows(const T* __restrict__ src, const ChunkGrid<CH>& G, uint32_t nch, T* tile, F&& f) {
   const int lane = lane_id();
-  RowPipe<CH, int2> pp;
+  RowPipe<CH, T> pp;
   if (nch) pp.issue(src, G.row(0), G.lo(0), G.hi(0));
   for (uint32_t j = 0; j < nch; ++j) {
     const uint32_t lo = G.lo(j), hi = G.hi(j);
@@ -886,6 +887,7 @@ __global__ __launch_bounds__(64) void k_lis(const ChainDesc* __restrict__ chains
   uint64_t tests = 0;
   uint32_t head = NONE, hlen = 0, hnxt = NONE, hroot = 0, longest = 0, longest_ind = 0;
   int2 hx = make_int2(0, 0), hrootx = make_int2(0, 0);
+  int32_t xmn = INT32_MAX, xmx = INT32_MIN, ymn = INT32_MAX, ymx = INT32_MIN;  // hit spans: lis layout
   PROF_T(t_start);
 #ifdef PBGPU_PROF
   uint64_t p_load = 0, p_fetch = 0, p_elem = 0, p_store = 0;
@@ -940,6 +942,7 @@ __global__ __launch_bounds__(64) void k_lis(const ChainDesc* __restrict__ chains
       if ((uint32_t)e < lo || (uint32_t)e >= hi) continue;
       const uint32_t i = c0 + e;
       const int2 xi = xr[e];
+      xmn = min(xmn, xi.x); xmx = max(xmx, xi.x); ymn = min(ymn, xi.y); ymx = max(ymx, xi.y);
       uint32_t prev = NONE, prev_len = 0, prev_nxt = NONE, found = NONE, f_len = 0, f_root = 0;
       int2 f_rootx = hrootx;
       if (head != NONE) {
@@ -1011,6 +1014,10 @@ __global__ __launch_bounds__(64) void k_lis(const ChainDesc* __restrict__ chains
   uint32_t s = longest_ind, t = 0;
   bool need = longest > 0;
   int2* Pl = pts + base;
+  // compact layout when every hit of the strand lies within 65535 of every other
+  uint32_t* Pw = (uint32_t*)Pl + 2;
+  const bool cmp = longest >= 2 && (uint32_t)(xmx - xmn) < 65536u && (uint32_t)(ymx - ymn) < 65536u;
+  const int2 last = cmp ? Xl[longest_ind] : make_int2(0, 0);
   auto sweep_rows = [&](int64_t j, uint32_t& lo, uint32_t& hi) {
     const bool here = need && (uint64_t)base + s >= G.row((uint32_t)j);
     lo = here ? G.lo((uint32_t)j) : 0; hi = here ? G.hi((uint32_t)j) : 0;
@@ -1042,7 +1049,9 @@ __global__ __launch_bounds__(64) void k_lis(const ChainDesc* __restrict__ chains
     if (need && (uint64_t)base + s >= row) {
       while (need && (uint64_t)base + s >= row) {
         const uint32_t o = longest - 1 - t;
-        Pl[o] = xs[(s - c0) * RS + lane];
+        const int2 p = xs[(s - c0) * RS + lane];
+        if (cmp) Pw[o] = pt_word(last, p);
+        else Pl[o] = p;
         const uint32_t ps = wide(ns[(s - c0) * RS + lane].P);
         if (keep_idx) Nl[o].nxt = (I)s;  // nxt is dead after the forward pass; the sweep reads only P
         s = ps;
@@ -1052,6 +1061,7 @@ __global__ __launch_bounds__(64) void k_lis(const ChainDesc* __restrict__ chains
     lds_fence();
   }
   (void)lo_n; (void)hi_n;
+  if (cmp) { Pw[-2] = (uint32_t)last.x | PT_COMPACT; Pw[-1] = (uint32_t)last.y; }
   PROF_T(t_end);
   PROF_ADD(0, p_load); PROF_ADD(1, p_fetch); PROF_ADD(2, p_elem); PROF_ADD(3, p_store);
   PROF_ADD(4, t_end - t_fwd); PROF_ADD(5, t_end - t_start); PROF_ADD(6, nch); PROF_ADD(7, 1);
@@ -1299,17 +1309,30 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
       }
     }
     // ---- backtracking (indices): whole P(e) = e-1 runs at a time, lis points in ascending order
-    uint32_t t = longest, s = longest_ind;
+    // compact layout unless a point lies too far from the last one: then once
+    // more in the wide layout (rare: spans beyond 64 kb)
     int2* Pl = pts + base;
-    while (t > 0) {
-      const uint32_t r = srs[s];
-      const uint32_t run = s - r + 1, cnt = run < t ? run : t;
-      for (uint32_t j = lane; j < cnt; j += 64) {
-        Pl[t - 1 - j] = sx[s - j];
-        if (keep_idx) N16[base + t - 1 - j].nxt = (uint16_t)(s - j);
+    uint32_t* Pw = (uint32_t*)Pl + 2;
+    const int2 last = longest ? sx[longest_ind] : make_int2(0, 0);
+    for (int wide = longest < 2; wide < 2; ++wide) {
+      uint32_t t = longest, s = longest_ind;
+      bool far = false;
+      while (t > 0) {
+        const uint32_t r = srs[s];
+        const uint32_t run = s - r + 1, cnt = run < t ? run : t;
+        for (uint32_t j = lane; j < cnt; j += 64) {
+          const int2 p = sx[s - j];
+          if (wide) Pl[t - 1 - j] = p;
+          else { Pw[t - 1 - j] = pt_word(last, p); far |= !pt_fits(last, p); }
+          if (keep_idx) N16[base + t - 1 - j].nxt = (uint16_t)(s - j);
+        }
+        t -= cnt;
+        if (t) s = cnt == run ? sP[r] : s - cnt;
       }
-      t -= cnt;
-      if (t) s = cnt == run ? sP[r] : s - cnt;
+      if (!wide && !__ballot(far)) {
+        if (lane == 0) { Pw[-2] = (uint32_t)last.x | PT_COMPACT; Pw[-1] = (uint32_t)last.y; }
+        break;
+      }
     }
     if (lane == 0) lisl[item] = longest;
     lds_fence();  // LDS reads of this strand done before the next strand's commit
@@ -1326,6 +1349,11 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
 // compute_kmers_info (pb_aligner.cc:84-143) along one lis, one point at a
 // time.  ids: unitig ids of the fwd name; rev => bwd name (reversed list).
 // Any error leaves n_info == 0 (the reference clears both vectors).
+// T: the arrays' element type, int32_t (global) or lds_i32 (LDS): an LDS
+// array must not be reached through a flat pointer, whose accesses wait for
+// every outstanding global load (the row prefetch).
+typedef __attribute__((address_space(3))) int32_t lds_i32;
+template <typename T>
 struct KmersInfo {
   const uint32_t* ids;
   uint32_t nsz;
@@ -1333,15 +1361,19 @@ struct KmersInfo {
   int32_t k, uk;
   const int32_t* ul;
   uint64_t n_ul;
-  int32_t* mers;    // element i at mers[i * stride]
-  int32_t* bases;
+  T* mers;    // element i at mers[i * stride]
+  T* bases;
   uint32_t stride;
-  const int32_t* cl;  // optional cache: length of unitig i at cl[i * stride], UL_INVALID if unusable
+  T* cl;  // optional cache: length of unitig i at cl[i * stride], UL_INVALID if unusable
   uint32_t cunitig;
   int32_t cend, prev_pos;
-  // pending increments of element 2 * cunitig (mers, bases), kept in registers
-  // while consecutive points stay in one unitig: the common case touches no memory
-  int32_t pm, pb;
+  // Pending increments kept in registers: element 2c (pm, pb: the current
+  // unitig c), 2c+1 (om, ob: its overlap with c+1) and 2c+2 (nm, nb: unitig
+  // c+1), and nlen = ulen(c+1).  Points inside one unitig, and k-mers reaching
+  // into the next one, touch no memory; moving to the next unitig writes 2c
+  // and 2c+1 and makes 2c+2 the current element.  Overlaps reaching further
+  // than the next unitig (unitigs shorter than a k-mer) update memory directly.
+  int32_t pm, pb, om, ob, nm, nb, nlen;
   static constexpr int32_t UL_INVALID = INT32_MIN;
   DEV uint32_t uid(uint32_t i) const { return i >= nsz ? INVALID_UNITIG : (rev ? ids[nsz - 1 - i] : ids[i]); }
   DEV int32_t ulen_direct(uint32_t i) const {
@@ -1352,10 +1384,10 @@ struct KmersInfo {
     if (cl) return i < nsz ? cl[i * stride] : UL_INVALID;
     return ulen_direct(i);
   }
-  DEV int32_t& M(uint32_t i) { return mers[i * stride]; }
-  DEV int32_t& B(uint32_t i) { return bases[i * stride]; }
-  DEV void init(const AlignParamsDev& P, const uint32_t* ids_, uint32_t nsz_, bool rev_, int32_t* m, int32_t* b,
-                uint32_t stride_, int32_t* cache = nullptr) {
+  DEV T& M(uint32_t i) { return mers[i * stride]; }
+  DEV T& B(uint32_t i) { return bases[i * stride]; }
+  DEV void init(const AlignParamsDev& P, const uint32_t* ids_, uint32_t nsz_, bool rev_, T* m, T* b,
+                uint32_t stride_, T* cache = nullptr) {
     ids = ids_; nsz = nsz_; rev = rev_; k = (int32_t)P.k; uk = (int32_t)P.unitigs_k; ul = P.ul; n_ul = P.n_ul;
     mers = m; bases = b; stride = stride_; cl = nullptr;
     if (cache) {
@@ -1369,10 +1401,16 @@ struct KmersInfo {
     cunitig = 0;
     cend = l0;
     prev_pos = (int32_t)(0u - (uint32_t)k);
-    pm = 0; pb = 0;
+    pm = pb = om = ob = nm = nb = 0;
+    nlen = ulen(1);
   }
   DEV void flush() {
-    if (pm | pb) { M(2 * cunitig) += pm; B(2 * cunitig) += pb; pm = 0; pb = 0; }
+    M(2 * cunitig) += pm; B(2 * cunitig) += pb;
+    if (cunitig + 1 < nsz) {
+      M(2 * cunitig + 1) += om; B(2 * cunitig + 1) += ob;
+      M(2 * cunitig + 2) += nm; B(2 * cunitig + 2) += nb;
+    }
+    pm = pb = om = ob = nm = nb = 0;
   }
   DEV void add(int32_t sr_pos) {
     if (!ok) return;
@@ -1382,48 +1420,75 @@ struct KmersInfo {
         if (cunitig >= nsz - 1) { ok = false; return; }
         const int32_t mx = sr_pos > prev_pos + k ? sr_pos : prev_pos + k;
         const int32_t nbb = cend - mx + 1;
-        pb += nbb; B(2 * cunitig + 1) += nbb;
+        pb += nbb; ob += nbb;
       }
-      flush();
-      const int32_t l = ulen(++cunitig);
+      // unitig c is done: write 2c and 2c+1, 2c+2 becomes current
+      M(2 * cunitig) += pm; B(2 * cunitig) += pb;
+      if (cunitig + 1 < nsz) { M(2 * cunitig + 1) += om; B(2 * cunitig + 1) += ob; }
+      pm = nm; pb = nb; om = ob = nm = nb = 0;
+      const int32_t l = nlen;
+      ++cunitig;
       if (l == UL_INVALID) { ok = false; return; }
       cend = (int32_t)((uint32_t)cend + (uint32_t)l - (uint32_t)uk + 1u);
+      nlen = ulen(cunitig + 1);
     }
     ++pm;
     pb += new_bases;
-    int32_t cendi = cend;
-    for (uint32_t i = cunitig; (i < nsz - 1) && ((uint32_t)sr_pos + (uint32_t)k > (uint32_t)cendi - (uint32_t)uk + 1u); ++i) {
-      const int32_t full_mer = sr_pos + uk > cendi + 1;
-      M(2 * i + 1) += full_mer; M(2 * i + 2) += full_mer;
-      const int32_t tt = sr_pos + k - cendi + uk - 2;
-      const int32_t nbb = new_bases < tt ? new_bases : tt;
-      B(2 * i + 1) += nbb; B(2 * i + 2) += nbb;
-      const int32_t l = ulen(i + 1);
-      if (l != UL_INVALID) cendi = (int32_t)((uint32_t)cendi + (uint32_t)l - (uint32_t)uk + 1u);
-      else { ok = false; return; }
+    if ((cunitig < nsz - 1) && ((uint32_t)sr_pos + (uint32_t)k > (uint32_t)cend - (uint32_t)uk + 1u)) {
+      // first overlapping unitig (the loop below at i = cunitig), in registers
+      const int32_t full_mer = sr_pos + uk > cend + 1;
+      om += full_mer; nm += full_mer;
+      const int32_t tt0 = sr_pos + k - cend + uk - 2;
+      const int32_t nbb0 = new_bases < tt0 ? new_bases : tt0;
+      ob += nbb0; nb += nbb0;
+      if (nlen == UL_INVALID) { ok = false; return; }
+      int32_t cendi = (int32_t)((uint32_t)cend + (uint32_t)nlen - (uint32_t)uk + 1u);
+      for (uint32_t i = cunitig + 1; (i < nsz - 1) && ((uint32_t)sr_pos + (uint32_t)k > (uint32_t)cendi - (uint32_t)uk + 1u); ++i) {
+        const int32_t fm = sr_pos + uk > cendi + 1;
+        M(2 * i + 1) += fm; M(2 * i + 2) += fm;
+        const int32_t tt = sr_pos + k - cendi + uk - 2;
+        const int32_t nbb = new_bases < tt ? new_bases : tt;
+        B(2 * i + 1) += nbb; B(2 * i + 2) += nbb;
+        const int32_t l = ulen(i + 1);
+        if (l != UL_INVALID) cendi = (int32_t)((uint32_t)cendi + (uint32_t)l - (uint32_t)uk + 1u);
+        else { ok = false; return; }
+      }
     }
     prev_pos = sr_pos;
   }
 };
 
-// least_square_2d::add (least_square_2d.hpp:47-67), x = sr offset, y = pb offset
+// a / b correctly rounded from y = RN(1 / b): one correction makes q faithful,
+// whose residual is then exact, and Markstein's step rounds it correctly
+// (Handbook of Floating-Point Arithmetic, thm. "Markstein"); no over- or
+// underflow here.  The sign of a zero quotient may differ from a / b, which
+// no sum below can see (the accumulators are never -0).
+DEV double div_rcp(double a, double b, double y) {
+  const double q0 = __dmul_rn(a, y);
+  const double q1 = __fma_rn(__fma_rn(-b, q0, a), y, q0);
+  return __fma_rn(__fma_rn(-b, q1, a), y, q1);
+}
+
+// least_square_2d::add (least_square_2d.hpp:47-67), x = sr offset, y = pb offset;
+// the four divisions by n share one correctly rounded reciprocal
 struct Lsq {
   double EX = 0, EY = 0, EXX = 0, EXY = 0, VX = 0, CXY = 0, NB = 0;
   long n = 0;
   DEV void add(double x, double y) {
     ++n;
     const double dn = (double)n;
+    const double rn = __ddiv_rn(1.0, dn);
     const double deltaX = __dadd_rn(x, -EX);
-    EX = __dadd_rn(EX, __ddiv_rn(deltaX, dn));
+    EX = __dadd_rn(EX, div_rcp(deltaX, dn, rn));
     const double ndeltaX = __dadd_rn(x, -EX);
     VX = __dadd_rn(VX, __dmul_rn(deltaX, ndeltaX));
     const double deltaY = __dadd_rn(y, -EY);
-    EY = __dadd_rn(EY, __ddiv_rn(deltaY, dn));
+    EY = __dadd_rn(EY, div_rcp(deltaY, dn, rn));
     const double ndeltaY = __dadd_rn(y, -EY);
     const double deltaXX = __dadd_rn(__dmul_rn(x, x), -EXX);
-    EXX = __dadd_rn(EXX, __ddiv_rn(deltaXX, dn));
+    EXX = __dadd_rn(EXX, div_rcp(deltaXX, dn, rn));
     const double deltaXY = __dadd_rn(__dmul_rn(x, y), -EXY);
-    EXY = __dadd_rn(EXY, __ddiv_rn(deltaXY, dn));
+    EXY = __dadd_rn(EXY, div_rcp(deltaXY, dn, rn));
     CXY = __dadd_rn(CXY, __dmul_rn(deltaX, ndeltaY));
     NB = __dadd_rn(NB, __dadd_rn(__dmul_rn(deltaXY, ndeltaX), -__dmul_rn(deltaXX, ndeltaY)));
   }
@@ -1474,6 +1539,34 @@ DEV bool coords_finish(const AlignParamsDev& P, uint32_t rl, Rec& R) {
 // written once if the record is kept; longer names use a third pass that
 // updates the arrays in HBM.  With --max-match, kept chains go to the redo list.
 constexpr uint32_t INFO_LDS_UNITIGS = 8, INFO_LDS = 2 * INFO_LDS_UNITIGS - 1;
+// One lane's lis (pt_get's two layouts) streamed in order through the LDS
+// tile: the compact lanes' words in 2*CH-word rows, then the wide lanes'
+// points in CH-point rows (a lane takes part in one of the two loops).
+template <int CH>
+struct LisStream {
+  int2 last;
+  bool cmp;
+  uint64_t base;
+  DEV void init(const int2* pts, uint64_t base_, uint32_t nl) {
+    base = base_; cmp = false; last = make_int2(0, 0);
+    if (nl) {
+      const uint2 h = *(const uint2*)(pts + base);
+      cmp = (h.x & PT_COMPACT) != 0;
+      last = make_int2((int32_t)(h.x & ~PT_COMPACT), (int32_t)h.y);
+    }
+  }
+  template <typename F>
+  DEV void run(const int2* pts, uint32_t n, int2* tile, F&& f) const {
+    ChunkGrid<2 * CH> gc;
+    gc.init(2 * base + 2, cmp ? n : 0);
+    ChunkGrid<CH> gw;
+    gw.init(base, cmp ? 0 : n);
+    const uint32_t ncc = wave_max_u32(gc.chunks()), ncw = wave_max_u32(gw.chunks());
+    const int2 l = last;
+    stream_rows<2 * CH>((const uint32_t*)pts, gc, ncc, (uint32_t*)tile, [&](const uint32_t w) { f(pt_decode(l, w)); });
+    stream_rows<CH>(pts, gw, ncw, tile, f);
+  }
+};
 template <int CH>
 __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, const ChainDesc* __restrict__ chains,
                                                const uint32_t* __restrict__ list, uint32_t n,
@@ -1481,6 +1574,7 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
   __shared__ int2 ps[CH * RS];
   __shared__ int32_t im[INFO_LDS * 64], ib[INFO_LDS * 64], iul[INFO_LDS_UNITIGS * 64];
   const int lane = lane_id();
+  PROF_T(kc_t0);
   const uint32_t w = blockIdx.x * 64 + lane;
   const bool act = w < n;
   uint32_t c = 0, nl = 0;
@@ -1495,9 +1589,8 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
     nl = fwd_align ? lf : lb;
     base = d.hit_base + (fwd_align ? 0 : d.nf);
   }
-  ChunkGrid<CH> G;
-  G.init(base, nl);
-  const uint32_t nch = wave_max_u32(G.chunks());
+  LisStream<CH> LS;
+  LS.init(O.pts, base, act ? nl : 0);
   const uint32_t k = P.k;
   Rec R;
   R.nb_mers = (int32_t)nl; R.pb_cons = 0; R.sr_cons = 0; R.pb_cover = k; R.sr_cover = k;
@@ -1509,8 +1602,10 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
   uint32_t u0 = 0, nsz = 0;
   if (act && nl && P.unitigs_k) { u0 = ix.sr_uoff[d.sr]; nsz = ix.sr_uoff[d.sr + 1] - u0; }
   const bool info_lds = nsz && nsz <= INFO_LDS_UNITIGS;
-  KmersInfo KI;
-  if (info_lds) KI.init(P, ix.sr_uids + u0, nsz, (R.flags & 2u) != 0, im + lane, ib + lane, 64, iul + lane);
+  KmersInfo<lds_i32> KI;
+  if (info_lds)
+    KI.init(P, ix.sr_uids + u0, nsz, (R.flags & 2u) != 0, (lds_i32*)(im + lane), (lds_i32*)(ib + lane), 64,
+            (lds_i32*)(iul + lane));
   auto info_pos = [&](int32_t so) -> int32_t {
     const int32_t pos = fwd_align ? so : (int32_t)(R.ql + (uint32_t)so - k + 2u);
     return pos < 0 ? -pos : pos;
@@ -1518,7 +1613,12 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
   // pass 1: cons / cover, the least-squares fit (pb_aligner.cc:19-47), kmers_info (LDS case)
   Lsq L;
   int2 prev = make_int2(0, 0), first = make_int2(0, 0);
-  stream_rows<CH>(O.pts, G, nch, ps, [&](const int2 p) {
+  PROF_T(kc_t1);
+#ifdef PBGPU_EXP_NO_PASS1
+  LS.run(O.pts, 0, ps, [&](const int2 p) {
+#else
+  LS.run(O.pts, nl, ps, [&](const int2 p) {
+#endif
     if (L.n == 0) {
       first = p;
     } else {
@@ -1529,11 +1629,18 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
       R.sr_cons += sr_diff == 1u;
       R.sr_cover += k < sr_diff ? k : sr_diff;
     }
+#ifndef PBGPU_EXP_NO_LSQ
     L.add((double)p.y, (double)p.x);
+#else
+    ++L.n; L.EX += p.y;
+#endif
+#ifndef PBGPU_EXP_NO_INFO
     if (info_lds) KI.add(info_pos(p.y));
+#endif
     prev = p;
   });
   // pass 2: average error of the fit (least_square_2d.hpp:70-80 + pb_aligner.cc:49-60)
+  PROF_T(kc_t2);
   double a = 0, b = 0;
   if (L.n == 1) {
     R.stretch = 1.0; R.offset = __dadd_rn(L.EY, -L.EX); R.avg_err = 0;
@@ -1541,14 +1648,16 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
     a = __ddiv_rn(L.CXY, L.VX); b = __ddiv_rn(L.NB, L.VX);
     R.stretch = a; R.offset = b;
   }
-  ChunkGrid<CH> G2;
-  G2.init(base, L.n > 1 ? nl : 0);
-  const uint32_t nch2 = wave_max_u32(G2.chunks());
   double err = 0;
-  stream_rows<CH>(O.pts, G2, nch2, ps, [&](const int2 p) {
+#ifdef PBGPU_EXP_NO_PASS2
+  LS.run(O.pts, 0, ps, [&](const int2 p) {
+#else
+  LS.run(O.pts, L.n > 1 ? nl : 0, ps, [&](const int2 p) {
+#endif
     err = __dadd_rn(err, fabs(__dadd_rn(__dadd_rn(__dmul_rn(a, (double)p.y), b), -(double)p.x)));
   });
   if (L.n > 1) R.avg_err = __ddiv_rn(err, (double)L.n);
+  PROF_T(kc_t3);
   R.rs = first.x;
   R.re = (int32_t)((uint32_t)prev.x + k - 1u);
   R.qs = first.y; R.qe = prev.y;
@@ -1556,6 +1665,7 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
   const bool keep = act && nl > 0 && coords_finish(P, rl, R);
   // info arrays: allocate for kept records, copy the LDS case, or run pass 3 in HBM
   bool info_ok = true, pass3 = false;
+  KmersInfo<int32_t> KG;  // pass 3: the arrays in HBM
   if (keep && nsz) {
     const uint32_t need = 2 * nsz - 1;
     const unsigned long long io = atomicAdd(O.info_count, (unsigned long long)need);
@@ -1568,24 +1678,37 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
           R.n_info = need;
         }
       } else {
-        KI.init(P, ix.sr_uids + u0, nsz, (R.flags & 2u) != 0, O.info_m + io, O.info_b + io, 1);
-        pass3 = KI.ok;
+        KG.init(P, ix.sr_uids + u0, nsz, (R.flags & 2u) != 0, O.info_m + io, O.info_b + io, 1);
+        pass3 = KG.ok;
       }
     } else {
       info_ok = false;
     }
   }
-  ChunkGrid<CH> G3;
-  G3.init(base, pass3 ? nl : 0);
-  const uint32_t nch3 = wave_max_u32(G3.chunks());
-  stream_rows<CH>(O.pts, G3, nch3, ps, [&](const int2 p) { KI.add(info_pos(p.y)); });
-  if (pass3 && KI.ok) { KI.flush(); R.n_info = 2 * nsz - 1; }
+  PROF_T(kc_t4);
+  LS.run(O.pts, pass3 ? nl : 0, ps, [&](const int2 p) { KG.add(info_pos(p.y)); });
+  if (pass3 && KG.ok) { KG.flush(); R.n_info = 2 * nsz - 1; }
+  PROF_T(kc_t5);
   if (keep) {
     const uint32_t ri = atomicAdd(O.rec_count, 1u);
     if (ri < O.rec_cap && info_ok) O.recs[ri] = R;
     else atomicAdd(&O.stats[ST_REC_OVERFLOW], 1ull);
     if (P.max_match) O.redo[atomicAdd(O.n_redo, 1u)] = c;
   }
+#ifdef PBGPU_PROF
+  {  // slots 32..: waves, total, prologue, pass 1, pass 2, gap, pass 3, chunks; per-log2(chunks) ticks / waves
+    PROF_T(kc_t6);
+    const uint32_t lane_ch = (nl + CH - 1) / CH;
+    unsigned long long sum_ch = lane_ch;
+    for (int o = 32; o > 0; o >>= 1) sum_ch += __shfl_xor(sum_ch, o, 64);
+    const uint32_t nch = wave_max_u32(lane_ch);
+    const uint32_t bk = nch ? 32 - __builtin_clz(nch) : 0;
+    PROF_ADD(32, 1); PROF_ADD(33, kc_t6 - kc_t0); PROF_ADD(34, kc_t1 - kc_t0); PROF_ADD(35, kc_t2 - kc_t1);
+    PROF_ADD(36, kc_t3 - kc_t2); PROF_ADD(37, kc_t4 - kc_t3); PROF_ADD(38, kc_t5 - kc_t4); PROF_ADD(39, nch);
+    PROF_ADD(40, sum_ch); PROF_ADD(41, __ballot(pass3) ? 1 : 0); PROF_ADD(42, kc_t6 - kc_t5);
+    PROF_ADD(48 + (bk > 15 ? 15 : bk), kc_t6 - kc_t0); PROF_ADD(64 + (bk > 15 ? 15 : bk), 1);
+  }
+#endif
 }
 
 // --max-match: mer_lists::discard_update_LIS (pb_aligner.hpp:86-92) drops the
@@ -2077,10 +2200,10 @@ void launch_strand_order(const ChainDesc* chains, const uint32_t* items, uint32_
 }
 #ifdef PBGPU_PROF
 extern "C" int pbgpu_debug_prof(unsigned long long* out, int n, int reset) {
-  if (n > 32) n = 32;
+  if (n > PROF_SLOTS) n = PROF_SLOTS;
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), n * sizeof(unsigned long long)) != hipSuccess) return -1;
   if (reset) {
-    unsigned long long z[32] = {};
+    unsigned long long z[PROF_SLOTS] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof z) != hipSuccess) return -1;
   }
   return 0;

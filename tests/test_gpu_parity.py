@@ -48,3 +48,18 @@ def test_parity_small(small, name):
     got, exp = _run(small, CONFIGS[name])
     assert exp.count("\n") > 10, "workload produced too few records to be meaningful"
     assert_same_coords(got, exp, name)
+
+
+@pytest.fixture(scope="module")
+def short_unitigs():
+    """Unitigs from 31 bases (= unitigs_k) up: k-mers span several unitigs, the
+    kmers_info paths beyond the next unitig run."""
+    from tools.synth import Dataset
+    return Dataset("small", seed=9, unitig_mean=40, unitig_min=31)
+
+
+@pytest.mark.parametrize("name", ["forward_ul", "max_match"])
+def test_parity_short_unitigs(short_unitigs, name):
+    got, exp = _run(short_unitigs, CONFIGS[name])
+    assert exp.count("\n") > 10, "workload produced too few records to be meaningful"
+    assert_same_coords(got, exp, name)
