@@ -1114,7 +1114,7 @@ static void fine_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
     launch_fine_desc(v, al->recs_sorted.p, ws0, nws, al->lstart.p, al->lend.p, al->PF.unitigs_k != 0, al->chains.p,
                      al->emit_of.p, info_need, st);
     HIPCHK(hipGetLastError());
-    al->pts.ensure(Hs + 1); al->nodes.ensure((Hs + 1) * 8);
+    al->pts.ensure(Hs + 9); al->nodes.ensure((Hs + 1) * 8);  // pts: + one 64-byte row (k_coords row loads)
     const uint32_t n_fit = lis_stage(al, nws, Hs, al->lpf, 0, false, false);
     unsigned long long need = 0;
     HIPCHK(hipMemcpyAsync(&need, info_need, 8, hipMemcpyDeviceToHost, st));
@@ -1213,7 +1213,7 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_
     while (r1 < n && hoff[r1 + 1] - hoff[r0] <= budget) ++r1;
     const uint64_t Hs = hoff[r1] - hoff[r0];
     const uint32_t nr = r1 - r0;
-    al->X.ensure(Hs + 1); al->pts.ensure(Hs + 1); al->nodes.ensure((Hs + 1) * 8);
+    al->X.ensure(Hs + 1); al->pts.ensure(Hs + 9); al->nodes.ensure((Hs + 1) * 8);  // pts: + one 64-byte row (k_coords row loads)
     al->chains.ensure(std::min<uint64_t>(Hs, (uint64_t)nr << 10) + 1);  // grown below if a batch needs more
     GroupOut O;
     O.X = al->X.p; O.chains = al->chains.p;

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <algorithm>
+#include <type_traits>
 #include "pbgpu_internal.h"
 
 namespace pbgpu {
@@ -704,19 +705,29 @@ __global__ __launch_bounds__(256) void k_len_hist(F f, uint32_t n, uint32_t* his
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < NLB; i += 256) if (h[i]) atomicAdd(&hist[i], h[i]);
 }
-// block-aggregated: one global atomic per (block, bucket); zero-length items are dropped
+// block-aggregated over LEN_PERM_ITEMS items a thread: one global atomic per
+// (block, bucket) -- the few hot buckets (the shortest lengths) see one atomic
+// per 4096 items; zero-length items are dropped
+constexpr uint32_t LEN_PERM_ITEMS = 16;
 template <typename F>
 __global__ __launch_bounds__(256) void k_len_perm(F f, uint32_t n, uint32_t* cursor, uint32_t* perm) {
   __shared__ uint32_t cnt[NLB], base[NLB];
   for (uint32_t i = threadIdx.x; i < NLB; i += 256) cnt[i] = 0;
   __syncthreads();
-  const uint32_t c = blockIdx.x * 256 + threadIdx.x;
-  uint32_t b = 0, loc = 0;
-  if (c < n) { b = len_bucket(f(c)); if (b) loc = atomicAdd(&cnt[b], 1u); }
+  const uint32_t c0 = blockIdx.x * 256 * LEN_PERM_ITEMS + threadIdx.x;
+  uint32_t b[LEN_PERM_ITEMS], loc[LEN_PERM_ITEMS];
+#pragma unroll
+  for (uint32_t q = 0; q < LEN_PERM_ITEMS; ++q) {
+    const uint32_t c = c0 + q * 256;
+    b[q] = c < n ? len_bucket(f(c)) : 0u;
+    loc[q] = b[q] ? atomicAdd(&cnt[b[q]], 1u) : 0u;
+  }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < NLB; i += 256) if (cnt[i]) base[i] = atomicAdd(&cursor[i], cnt[i]);
   __syncthreads();
-  if (c < n && b) perm[base[b] + loc] = c;
+#pragma unroll
+  for (uint32_t q = 0; q < LEN_PERM_ITEMS; ++q)
+    if (b[q]) perm[base[b[q]] + loc[q]] = c0 + q * 256;
 }
 
 // ================================================================= lis / fit
@@ -825,9 +836,51 @@ struct ChunkGrid {
   }
 };
 
+// Row pipe for 64-byte rows (CH * sizeof(T) == 64) loaded 16 bytes a lane:
+// 4 lanes per row, 16 rows per load instruction, every lane loading (a lane
+// with no row in the chunk re-reads row 0 of src).  The rows are CH-aligned
+// 64-byte segments: src must be readable up to the next 64-byte boundary.
+template <int CH, typename T>
+struct RowPipe16 {
+  static_assert(CH * sizeof(T) == 64, "64-byte rows");
+  static constexpr int E = 16 / sizeof(T);  // elements per 16-byte piece
+  uint4 v[4];
+  DEV void issue(const T* __restrict__ src, uint64_t row, bool has) {
+    const int lane = lane_id();
+    const uint64_t r = has ? row : 0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const uint64_t rl = shfl_u64(r, g * 16 + lane / 4);
+      v[g] = *(const uint4*)(src + rl + (lane % 4) * E);
+    }
+  }
+  DEV void commit(T* tile) const {
+    const int lane = lane_id();
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const T* p = (const T*)&v[g];
+#pragma unroll
+      for (int q = 0; q < E; ++q) tile[((lane % 4) * E + q) * RS + g * 16 + lane / 4] = p[q];
+    }
+  }
+};
+
 template <int CH, typename T, typename F>
 DEV void stream_rows(const T* __restrict__ src, const ChunkGrid<CH>& G, uint32_t nch, T* tile, F&& f) {
   const int lane = lane_id();
+  if constexpr (CH * sizeof(T) == 64) {
+    RowPipe16<CH, T> pp;
+    if (nch) pp.issue(src, G.row(0), G.hi(0) > G.lo(0));
+    for (uint32_t j = 0; j < nch; ++j) {
+      const uint32_t lo = G.lo(j), hi = G.hi(j);
+      pp.commit(tile);
+      if (j + 1 < nch) pp.issue(src, G.row(j + 1), G.hi(j + 1) > G.lo(j + 1));
+      lds_fence();
+      for (uint32_t e = lo; e < hi; ++e) f(tile[e * RS + lane]);
+      lds_fence();
+    }
+    return;
+  }
   RowPipe<CH, T> pp;
   if (nch) pp.issue(src, G.row(0), G.lo(0), G.hi(0));
   for (uint32_t j = 0; j < nch; ++j) {
@@ -1386,6 +1439,12 @@ struct KmersInfo {
   }
   DEV T& M(uint32_t i) { return mers[i * stride]; }
   DEV T& B(uint32_t i) { return bases[i * stride]; }
+  // x[i] += v; in LDS a no-return atomic add (each lane owns its column): no
+  // read to wait for -- the arrays are read once, after the last point
+  DEV void acc(T* x, uint32_t i, int32_t v) {
+    if constexpr (std::is_same<T, lds_i32>::value) __atomic_fetch_add(x + i * stride, v, __ATOMIC_RELAXED);
+    else x[i * stride] += v;
+  }
   DEV void init(const AlignParamsDev& P, const uint32_t* ids_, uint32_t nsz_, bool rev_, T* m, T* b,
                 uint32_t stride_, T* cache = nullptr) {
     ids = ids_; nsz = nsz_; rev = rev_; k = (int32_t)P.k; uk = (int32_t)P.unitigs_k; ul = P.ul; n_ul = P.n_ul;
@@ -1405,10 +1464,10 @@ struct KmersInfo {
     nlen = ulen(1);
   }
   DEV void flush() {
-    M(2 * cunitig) += pm; B(2 * cunitig) += pb;
+    acc(mers, 2 * cunitig, pm); acc(bases, 2 * cunitig, pb);
     if (cunitig + 1 < nsz) {
-      M(2 * cunitig + 1) += om; B(2 * cunitig + 1) += ob;
-      M(2 * cunitig + 2) += nm; B(2 * cunitig + 2) += nb;
+      acc(mers, 2 * cunitig + 1, om); acc(bases, 2 * cunitig + 1, ob);
+      acc(mers, 2 * cunitig + 2, nm); acc(bases, 2 * cunitig + 2, nb);
     }
     pm = pb = om = ob = nm = nb = 0;
   }
@@ -1423,8 +1482,8 @@ struct KmersInfo {
         pb += nbb; ob += nbb;
       }
       // unitig c is done: write 2c and 2c+1, 2c+2 becomes current
-      M(2 * cunitig) += pm; B(2 * cunitig) += pb;
-      if (cunitig + 1 < nsz) { M(2 * cunitig + 1) += om; B(2 * cunitig + 1) += ob; }
+      acc(mers, 2 * cunitig, pm); acc(bases, 2 * cunitig, pb);
+      if (cunitig + 1 < nsz) { acc(mers, 2 * cunitig + 1, om); acc(bases, 2 * cunitig + 1, ob); }
       pm = nm; pb = nb; om = ob = nm = nb = 0;
       const int32_t l = nlen;
       ++cunitig;
@@ -1445,10 +1504,10 @@ struct KmersInfo {
       int32_t cendi = (int32_t)((uint32_t)cend + (uint32_t)nlen - (uint32_t)uk + 1u);
       for (uint32_t i = cunitig + 1; (i < nsz - 1) && ((uint32_t)sr_pos + (uint32_t)k > (uint32_t)cendi - (uint32_t)uk + 1u); ++i) {
         const int32_t fm = sr_pos + uk > cendi + 1;
-        M(2 * i + 1) += fm; M(2 * i + 2) += fm;
+        acc(mers, 2 * i + 1, fm); acc(mers, 2 * i + 2, fm);
         const int32_t tt = sr_pos + k - cendi + uk - 2;
         const int32_t nbb = new_bases < tt ? new_bases : tt;
-        B(2 * i + 1) += nbb; B(2 * i + 2) += nbb;
+        acc(bases, 2 * i + 1, nbb); acc(bases, 2 * i + 2, nbb);
         const int32_t l = ulen(i + 1);
         if (l != UL_INVALID) cendi = (int32_t)((uint32_t)cendi + (uint32_t)l - (uint32_t)uk + 1u);
         else { ok = false; return; }
@@ -2117,7 +2176,8 @@ void launch_strand_order(const uint32_t* slen, uint32_t n_items, uint32_t* hist,
   if (phase == 0)
     hipLaunchKernelGGL((k_len_hist<StrandLen>), dim3(grid_for(n_items, 256, 2048)), dim3(256), 0, st, f, n_items, hist,
                        (unsigned long long*)nullptr);
-  else hipLaunchKernelGGL((k_len_perm<StrandLen>), dim3((n_items + 255) / 256), dim3(256), 0, st, f, n_items, cursor, perm);
+  else hipLaunchKernelGGL((k_len_perm<StrandLen>), dim3((n_items + 256 * LEN_PERM_ITEMS - 1) / (256 * LEN_PERM_ITEMS)), dim3(256), 0,
+                          st, f, n_items, cursor, perm);
 }
 void launch_chain_order(const uint32_t* lisl, uint32_t n, uint32_t* hist, uint32_t* cursor, uint32_t* perm, int phase,
                         unsigned long long* sums, hipStream_t st) {
@@ -2125,7 +2185,8 @@ void launch_chain_order(const uint32_t* lisl, uint32_t n, uint32_t* hist, uint32
   ChainLisLen f{lisl};
   if (phase == 0)
     hipLaunchKernelGGL((k_len_hist<ChainLisLen>), dim3(grid_for(n, 256, 2048)), dim3(256), 0, st, f, n, hist, sums);
-  else hipLaunchKernelGGL((k_len_perm<ChainLisLen>), dim3((n + 255) / 256), dim3(256), 0, st, f, n, cursor, perm);
+  else hipLaunchKernelGGL((k_len_perm<ChainLisLen>), dim3((n + 256 * LEN_PERM_ITEMS - 1) / (256 * LEN_PERM_ITEMS)), dim3(256), 0,
+                          st, f, n, cursor, perm);
 }
 #ifndef PBGPU_FIT_CH
 #define PBGPU_FIT_CH 8
