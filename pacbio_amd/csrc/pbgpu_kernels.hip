@@ -1201,42 +1201,118 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
   const uint32_t nwaves = gridDim.x * WPB;
   const bool fast = lp.W == 1 && !lp.mer_all;
   uint64_t tests = 0, my_hits = 0, my_strands = 0;
-  auto strand = [&](uint32_t w, uint64_t& base, uint32_t& n, uint32_t& item) {
-    item = items[w];
+  auto desc = [&](uint32_t item, uint64_t& base, uint32_t& n) {
     const ChainDesc d = chains[item >> 1];
     base = d.hit_base + ((item & 1) ? d.nf : 0);
     n = slen[item];
   };
-  // strands are prefetched into registers one strand ahead (small SMAX only)
+  // Software pipeline over this wave's strands w, w + nwaves, ...: while strand
+  // w is processed, the X rows of w + nwaves (small SMAX: into registers), the
+  // descriptor of w + 2 nwaves and the item id of w + 3 nwaves are in flight,
+  // so the dependent item -> descriptor -> rows chain never stalls a strand.
   constexpr bool PREFETCH = PF <= 8;
   uint32_t w = blockIdx.x * WPB + wv;
   int2 pf[PREFETCH ? PF : 1];
-  uint64_t nbase = 0;
-  uint32_t nn = 0, nitem = 0;
+  uint64_t nbase = 0, nbase2 = 0;
+  uint32_t nn = 0, nitem = 0, nn2 = 0, nitem2 = 0, nitem3 = 0;
   if (w < n_items) {
-    strand(w, nbase, nn, nitem);
+    nitem = items[w];
+    desc(nitem, nbase, nn);
     if constexpr (PREFETCH) {
 #pragma unroll
       for (int q = 0; q < PF; ++q) { const uint32_t j = q * 64 + lane; if (j < nn) pf[q] = X[nbase + j]; }
     }
+    if (w + nwaves < n_items) { nitem2 = items[w + nwaves]; desc(nitem2, nbase2, nn2); }
+    if (w + 2 * nwaves < n_items) nitem3 = items[w + 2 * nwaves];
   }
   for (; w < n_items; w += nwaves) {
     const uint64_t base = nbase;
     const uint32_t n = nn, item = nitem;
     my_hits += n; ++my_strands;
+    int2 xv[PREFETCH ? PF : 1];
     if constexpr (PREFETCH) {
 #pragma unroll
-      for (int q = 0; q < PF; ++q) { const uint32_t j = q * 64 + lane; if (j < n) sx[j] = pf[q]; }
-    } else {
-      for (uint32_t j = lane; j < n; j += 64) sx[j] = X[base + j];
+      for (int q = 0; q < PF; ++q) xv[q] = pf[q];
     }
-    // issue the next strand's loads now; they land while this strand is processed
+    // advance the pipeline: rows of w + nwaves, descriptor of w + 2 nwaves, item of w + 3 nwaves
+    nbase = nbase2; nn = nn2; nitem = nitem2;
     if (w + nwaves < n_items) {
-      strand(w + nwaves, nbase, nn, nitem);
       if constexpr (PREFETCH) {
 #pragma unroll
         for (int q = 0; q < PF; ++q) { const uint32_t j = q * 64 + lane; if (j < nn) pf[q] = X[nbase + j]; }
       }
+      if (w + 2 * nwaves < n_items) {
+        nitem2 = nitem3;
+        desc(nitem2, nbase2, nn2);
+        if (w + 3 * nwaves < n_items) nitem3 = items[w + 3 * nwaves];
+      }
+    }
+    if constexpr (PREFETCH) {
+      // Register path: a strand already in list order whose every element is
+      // clean (passes the test against its predecessor, see below) is one run
+      // P(e) = e-1 from element 0; the forward pass then only picks the last
+      // element whose span from element 0 passes `linear`, and the lis is
+      // elements 0..top.  Same result as the LDS path, no LDS traffic.
+#ifdef PBGPU_EXP_NO_LISW_REG
+      if (false) {
+#else
+      if (fast) {
+#endif
+        const int2 x0 = make_int2(__shfl(xv[0].x, 0, 64), __shfl(xv[0].y, 0, 64));
+        bool bad = false;
+        int32_t top = -1;
+#pragma unroll
+        for (int q = 0; q < PF; ++q) {
+          if ((uint32_t)q * 64 >= n) break;  // wave-uniform
+          const uint32_t i = q * 64 + lane;
+          const int src = (lane + 63) & 63;
+          int2 pv = make_int2(__shfl(xv[q].x, src, 64), __shfl(xv[q].y, src, 64));
+          if (q > 0 && lane == 0) pv = make_int2(__shfl(xv[q - 1].x, 63, 64), __shfl(xv[q - 1].y, 63, 64));
+          const int2 xi = xv[q];
+          if (i < n && i > 0) {
+            const bool clean = xi.y > pv.y && affine_ok(lp.a, lp.b, lp.C, (double)(xi.x - pv.x), (double)(xi.y - pv.y));
+            bad |= !clean || (!lp.ordered && hit_after(pv, xi));
+          }
+          const bool lin = i < n && (lp.seq_all || linear_ok(lp.a, (double)(xi.x - x0.x), (double)(xi.y - x0.y)));
+          const uint64_t lb = __ballot(lin);
+          if (lb) top = q * 64 + 63 - (int32_t)__clzll((long long)lb);
+        }
+        if (!__ballot(bad)) {
+          const uint32_t longest = (uint32_t)(top + 1);  // element 0 always passes
+          int2 last = make_int2(0, 0);
+#pragma unroll
+          for (int q = 0; q < PF; ++q)
+            if (top >> 6 == q) last = make_int2(__shfl(xv[q].x, top & 63, 64), __shfl(xv[q].y, top & 63, 64));
+          bool far = false;
+#pragma unroll
+          for (int q = 0; q < PF; ++q) {
+            const int32_t i = q * 64 + lane;
+            if (i <= top) far |= !pt_fits(last, xv[q]);
+          }
+          const bool cmp = longest >= 2 && !__ballot(far);
+          int2* Pl = pts + base;
+          uint32_t* Pw = (uint32_t*)Pl + 2;
+#pragma unroll
+          for (int q = 0; q < PF; ++q) {
+            const int32_t i = q * 64 + lane;
+            if (i <= top) {
+              if (cmp) Pw[i] = pt_word(last, xv[q]);
+              else Pl[i] = xv[q];
+              if (keep_idx) N16[base + i].nxt = (uint16_t)i;
+            }
+          }
+          if (lane == 0) {
+            if (cmp) { Pw[-2] = (uint32_t)last.x | PT_COMPACT; Pw[-1] = (uint32_t)last.y; }
+            lisl[item] = longest;
+          }
+          tests += n - 1;
+          continue;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < PF; ++q) { const uint32_t j = q * 64 + lane; if (j < n) sx[j] = xv[q]; }
+    } else {
+      for (uint32_t j = lane; j < n; j += 64) sx[j] = X[base + j];
     }
     lds_fence();
     // ---- list order: k_group leaves each 256-hit step's run of a list unordered.
