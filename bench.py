@@ -79,8 +79,9 @@ def _kernel_bytes(st):
     kn = st["kernel_launches"]
     per = lambda v, k: v / max(1, kn[k])
     return {
-        # read bases (1 B), one 64-B bucket per probe, kept k-mer records (16 B) written
-        "k_seed": per(st["n_bases"] + st["n_probes"] * 64 + st["n_kept"] * 16, "k_seed"),
+        # read bases (1 B), one presence-filter word (8 B) per lookup, one 64-B bucket per probe
+        # that passes it, kept k-mer records (16 B) written
+        "k_seed": per(st["n_bases"] + st["n_filter"] * 8 + st["n_probes"] * 64 + st["n_kept"] * 16, "k_seed"),
         # first-tier launches only (the timed ones): k-mer records (16 B) + occurrence headers
         # (16 B) read, every occurrence (8 B) read once, every hit (8 B) written, chain
         # descriptors (24 B) written -- counted by the kernel for the reads it completed
@@ -110,6 +111,7 @@ def main():
     ap.add_argument("--no-brand", action="store_true", help="skip the B_rand gather microbenchmark")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
+    ap.add_argument("--hit-budget", type=float, default=0, help="hits per sub-batch (0 = the library default)")
     args = ap.parse_args()
 
     rank, world, local = _dist()
@@ -133,6 +135,8 @@ def main():
     info = index.info()
     al = pbgpu.Aligner(index, k=k, forward=True, unitigs_k=31, unitig_lengths=ds.unitig_lengths,
                        bases_matching=15.0, max_count=5000, stretch_cap=10000.0)
+    if args.hit_budget:
+        al.set_hit_budget(int(args.hit_budget))
     blob, off = ds.pb_blob()
     reads = al.upload(blob=blob, offsets=off)
     bases_rank = int(off[-1])

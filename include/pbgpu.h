@@ -221,11 +221,14 @@ typedef struct {
   double   ms_fine;
   /* work of the timed k_coords slot (coarse): chains fitted, lis points streamed */
   uint64_t fit_chains, fit_points;
+  /* presence-filter words read by k_seed (8 B each) before the bucket probes */
+  uint64_t n_filter;
 } pbgpu_stats;
 pbgpu_status pbgpu_aligner_get_stats(const pbgpu_aligner* al, pbgpu_stats* s);
 pbgpu_status pbgpu_aligner_reset_stats(pbgpu_aligner* al);
 /* Tuning: the maximum number of seed hits grouped and chained per device
- * sub-batch (default 1.2e9, about 38 GB of working buffers).  A read whose
+ * sub-batch (default 4e9, about 128 GB of working buffers at most; a batch is
+ * split into equal sub-batches of at most this many hits).  A read whose
  * hits exceed it forms a sub-batch of its own.  Results do not depend on it. */
 pbgpu_status pbgpu_aligner_set_hit_budget(pbgpu_aligner* al, uint64_t hits);
 

@@ -31,7 +31,8 @@ void launch_runs(const uint64_t* keys, const uint64_t* uidx, uint64_t N, uint32_
 void launch_occ_fill(const uint64_t* vals, const uint64_t* uidx, const uint64_t* kpos, uint64_t N, uint64_t* occ,
                      hipStream_t st);
 void launch_headers(const uint64_t* keys, const uint64_t* kpos, const uint64_t* run_start, uint64_t U, uint64_t* occ,
-                    ulonglong2* table, uint64_t bucket_mask, uint32_t k, uint32_t ebits, hipStream_t st);
+                    ulonglong2* table, uint64_t bucket_mask, uint32_t k, uint32_t ebits, uint64_t* filt,
+                    uint32_t filt_shift, hipStream_t st);
 enum { SEED_WHOLE = 0, SEED_COUNTS = 1, SEED_FINISH = 2 };  // k_seed modes (pbgpu_kernels.hip)
 void launch_seed(int mode, IndexView ix, const uint8_t* seq, const uint64_t* roff, uint32_t n_reads, AlignParamsDev P,
                  KRec* krec, uint32_t* n_kept, uint32_t* thr, uint64_t* nhits, unsigned long long* stats,
@@ -189,6 +190,9 @@ struct pbgpu_index {
   dbuf<uint64_t> text, d_sr_start, occ;
   dbuf<ulonglong2> table;
   dbuf<uint32_t> sr_uoff, sr_uids;
+  // presence filter of the coarse table's k-mers (k_seed), 2^filt_log2 words; none if empty
+  dbuf<uint64_t> filt;
+  uint32_t filt_log2 = 0;
   // index sharded by super-read range: this shard holds super-reads
   // [sr_begin, sr_end) (device arrays use local ids) plus a k-1-base seam
   uint32_t shard = 0, n_shards = 1;
@@ -204,16 +208,18 @@ struct pbgpu_index {
     IndexView v;
     v.text = text.p; v.n = n; v.sr_start = d_sr_start.p; v.n_sr = (uint32_t)(sr_end - sr_begin); v.k = k;
     v.table = table.p; v.bucket_mask = buckets - 1; v.occ = occ.p; v.sr_uoff = sr_uoff.p; v.sr_uids = sr_uids.p;
+    v.filt = filt.n ? filt.p : nullptr; v.filt_shift = 64 - filt_log2;
     return v;
   }
   IndexView fine_view() const {
     IndexView v = view();
     v.k = fk; v.table = f_table.p; v.bucket_mask = f_buckets - 1; v.occ = f_occv.p;
+    v.filt = nullptr;
     return v;
   }
   uint64_t device_bytes() const {
     return text.bytes() + d_sr_start.bytes() + occ.bytes() + table.bytes() + sr_uoff.bytes() + sr_uids.bytes() +
-           f_occv.bytes() + f_table.bytes();
+           f_occv.bytes() + f_table.bytes() + filt.bytes();
   }
 };
 
@@ -277,7 +283,7 @@ static void load_fasta(const char* path, text_builder& tb) {
 // orders each list by the K - km bases that follow (the fine sub-index).
 static void build_kmer_table(pbgpu_index* ix, uint32_t km, uint32_t K, uint32_t ebits, hipStream_t st,
                              dbuf<ulonglong2>& table, dbuf<uint64_t>& occ, uint64_t& n_buckets, uint64_t& n_kmers,
-                             uint64_t& n_occ) {
+                             uint64_t& n_occ, dbuf<uint64_t>* filt = nullptr, uint32_t* filt_log2 = nullptr) {
   const uint64_t N = ix->n >= km ? ix->n - km + 1 : 0;
   IndexView v = ix->view();
   if (N == 0) {
@@ -346,7 +352,22 @@ static void build_kmer_table(pbgpu_index* ix, uint32_t km, uint32_t K, uint32_t 
   table.alloc(4 * buckets);
   HIPCHK(hipMemsetAsync(table.p, 0xFF, table.bytes(), st));
   launch_occ_fill(vals, uidx, kpos.p, N, occ.p, st);
-  launch_headers(keys, kpos.p, run_start, U, occ.p, table.p, buckets - 1, km, ebits, st);
+  // presence filter: PBGPU_FILTER_BITS bits per k-mer (default 16, 0 = none), a power of two of words
+  uint64_t* fp = nullptr;
+  uint32_t flog = 0;
+  if (filt) {
+    const char* e = getenv("PBGPU_FILTER_BITS");
+    const uint64_t bits = e ? strtoull(e, nullptr, 10) : 16;
+    if (bits) {
+      flog = 6;  // >= 64 words
+      while ((1ull << flog) < U * bits / 64) ++flog;
+      filt->alloc(1ull << flog);
+      HIPCHK(hipMemsetAsync(filt->p, 0, filt->bytes(), st));
+      fp = filt->p;
+      *filt_log2 = flog;
+    }
+  }
+  launch_headers(keys, kpos.p, run_start, U, occ.p, table.p, buckets - 1, km, ebits, fp, 64 - flog, st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(st));  // the temporaries above are freed on return
 }
@@ -429,7 +450,8 @@ static void build_device_index(pbgpu_index* ix, text_builder& tb) {
   if (luoff[nloc])
     HIPCHK(hipMemcpy(ix->sr_uids.p, uids.data() + uoff[ix->sr_begin], (size_t)luoff[nloc] * 4, hipMemcpyHostToDevice));
 
-  build_kmer_table(ix, k, k, 0, st, ix->table, ix->occ, ix->buckets, ix->n_kmers, ix->n_occ);
+  build_kmer_table(ix, k, k, 0, st, ix->table, ix->occ, ix->buckets, ix->n_kmers, ix->n_occ, &ix->filt,
+                   &ix->filt_log2);
   ix->null_ptr = 2 * ix->n_kmers + ix->n_occ;
   if (ix->fk)
     build_kmer_table(ix, ix->fk, k, 2 * (k - ix->fk) + 1, st, ix->f_table, ix->f_occv, ix->f_buckets, ix->f_kmers,
@@ -649,7 +671,7 @@ struct pbgpu_aligner {
   // stats
   pbgpu_stats acc{};
   hipEvent_t ev[18]{};
-  uint64_t hit_budget = 1200000000ull, rec_hint = 0, info_per_chain = 32;
+  uint64_t hit_budget = 4000000000ull, rec_hint = 0, info_per_chain = 32;
   double chains_per_hit = 1.0 / 48;  // k_group partition estimate, refined after every batch
   dbuf<uint32_t> ovf_list, read_list;
   dbuf<uint8_t> nparts;
@@ -1076,9 +1098,12 @@ static void fine_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   const uint64_t budget = std::min<uint64_t>(al->hit_budget, 0xFFFFFFF0ull);
   uint64_t rec_done = 0, info_done = 0;
   unsigned long long* info_need = al->stats.p + ST_N;  // scratch slot past the stat slots
+  // sub-batches of about equal hits (ceil(total / budget) of them), each <= budget
+  const uint64_t n_sub = (hoff[n] + budget - 1) / budget;
+  const uint64_t target = n_sub ? (hoff[n] + n_sub - 1) / n_sub : 0;
   for (uint32_t r0 = 0; r0 < n;) {
     uint32_t r1 = r0 + 1;
-    while (r1 < n && hoff[r1 + 1] - hoff[r0] <= budget) ++r1;
+    while (r1 < n && hoff[r1] - hoff[r0] < target && hoff[r1 + 1] - hoff[r0] <= budget) ++r1;
     const uint64_t Hs = hoff[r1] - hoff[r0];
     if (Hs > 0xFFFFFFF0ull) throw unsupported("a single read has more than 2^32 fine hits");
     const uint64_t ws0 = woff[r0];
@@ -1208,9 +1233,12 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_
   double k_ms[PBGPU_KERNEL_N] = {};
   uint64_t k_n[PBGPU_KERNEL_N] = {};
   uint64_t n_chains = 0, n_tests = 0;
+  // sub-batches of about equal hits (ceil(total / budget) of them), each <= budget
+  const uint64_t n_sub = (hoff[n] + budget - 1) / budget;
+  const uint64_t target = n_sub ? (hoff[n] + n_sub - 1) / n_sub : 0;
   for (uint32_t r0 = 0; r0 < n;) {
     uint32_t r1 = r0 + 1;
-    while (r1 < n && hoff[r1 + 1] - hoff[r0] <= budget) ++r1;
+    while (r1 < n && hoff[r1] - hoff[r0] < target && hoff[r1 + 1] - hoff[r0] <= budget) ++r1;
     const uint64_t Hs = hoff[r1] - hoff[r0];
     const uint32_t nr = r1 - r0;
     al->X.ensure(Hs + 1); al->pts.ensure(Hs + 9); al->nodes.ensure((Hs + 1) * 8);  // pts: + one 64-byte row (k_coords row loads)
@@ -1422,6 +1450,7 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_
   al->acc.g0_kept += sv[ST_G0_KEPT]; al->acc.g0_hits += sv[ST_G0_HITS]; al->acc.g0_chains += sv[ST_G0_CHAINS];
   al->acc.l0_hits += sv[ST_L0_HITS]; al->acc.l0_strands += sv[ST_L0_STRANDS];
   al->acc.fit_chains += sv[ST_FIT_CHAINS]; al->acc.fit_points += sv[ST_FIT_POINTS];
+  al->acc.n_filter += sv[ST_FILTER];
   if (al->fine) {
     al->acc.n_fine_hits += sv[ST_FINE_HITS];
     al->acc.n_fine_windows += nrec;

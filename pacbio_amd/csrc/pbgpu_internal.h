@@ -33,6 +33,8 @@ struct IndexView {
   const uint64_t* occ;
   const uint32_t* sr_uoff;    // n_sr + 1 offsets into sr_uids
   const uint32_t* sr_uids;    // unitig ids of the fwd name (super_read_name::unitig_id)
+  const uint64_t* filt;       // presence filter of the table's canonical k-mers (null: none)
+  uint32_t filt_shift;        // word index = filter hash >> filt_shift
 };
 
 struct AlignParamsDev {
@@ -102,6 +104,7 @@ enum StatSlot {
   ST_L0_HITS, ST_L0_STRANDS,             // work of the tier-0 (n <= 255) k_lis_w launches
   ST_FINE_HITS,                          // fine aligner: windowed hits
   ST_FIT_CHAINS, ST_FIT_POINTS,          // coarse k_coords work: chains, lis points (counted by the chain order pass)
+  ST_FILTER,                             // presence-filter words read by k_seed (8 B each)
   ST_N
 };
 

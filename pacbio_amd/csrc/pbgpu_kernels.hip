@@ -141,6 +141,25 @@ DEV bool table_lookup(const IndexView& ix, uint64_t key, uint64_t& payload, uint
   }
 }
 
+// Presence filter in front of the table: one 64-bit word per key, FILT_HASHES
+// bits set in it (a register-blocked Bloom filter, 16 bits per key).  ~90% of
+// a CLR read's k-mers are absent from the index; their 8-byte filter word sits
+// in L2 / MALL (16 MB on C2) instead of a 64-byte HBM bucket probe.  No false
+// negatives, so results do not depend on it.
+constexpr int FILT_HASHES = 5;
+DEV uint64_t filt_hash(uint64_t key) { return fmix64(key * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull); }
+DEV uint64_t filt_bits(uint64_t h) {
+  uint64_t m = 0;
+#pragma unroll
+  for (int i = 0; i < FILT_HASHES; ++i) m |= 1ull << ((h >> (6 * i)) & 63);
+  return m;
+}
+DEV bool filt_test(const IndexView& ix, uint64_t key) {
+  const uint64_t h = filt_hash(key);
+  const uint64_t m = filt_bits(h);
+  return (__ldg(ix.filt + (h >> ix.filt_shift)) & m) == m;
+}
+
 // ============================================================ index build
 // Sort keys, one per text position x in [0, N), N = n - km + 1:
 //   (canonical km-mer << 1 | orientation) << ebits | extension
@@ -189,7 +208,8 @@ __global__ void k_occ_fill(const uint64_t* vals, const uint64_t* uidx, const uin
 }
 
 __global__ void k_headers(const uint64_t* keys, const uint64_t* kpos, const uint64_t* run_start, uint64_t U,
-                          uint64_t* occ, ulonglong2* table, uint64_t bucket_mask, uint32_t k, uint32_t ebits) {
+                          uint64_t* occ, ulonglong2* table, uint64_t bucket_mask, uint32_t k, uint32_t ebits,
+                          unsigned long long* filt, uint32_t filt_shift) {
   for (uint64_t u = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; u < U; u += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t s = run_start[u], e = run_start[u + 1];
     const uint64_t canon = keys[s] >> (ebits + 1);
@@ -203,6 +223,10 @@ __global__ void k_headers(const uint64_t* keys, const uint64_t* kpos, const uint
     occ[hb] = cnt32 | ((uint64_t)pal << 32);
     occ[hb + 1] = nA | (nB << 32);
     const uint64_t payload = (hb << 24) | (count < SAT_COUNT ? count : SAT_COUNT);
+    if (filt) {
+      const uint64_t h = filt_hash(canon);
+      atomicOr(filt + (h >> filt_shift), (unsigned long long)filt_bits(h));
+    }
     uint64_t b = fmix64(canon) & bucket_mask;
     for (;;) {
       bool done = false;
@@ -254,7 +278,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed(IndexView ix, const uint8_t* __r
   const uint64_t mask = mer_mask(k);
   const uint32_t hs = 2 * (k - 1);
   uint32_t cand_carry = 0, kept_carry = 0;
-  uint64_t my_kmers = 0, my_probes = 0;
+  uint64_t my_kmers = 0, my_probes = 0, my_fchecks = 0;
 
   for (int64_t t0 = 0; t0 < L; t0 += TILE) {
     for (int i = tid; i < TILE + LOOK; i += BLOCK) {
@@ -312,8 +336,10 @@ __global__ __launch_bounds__(BLOCK) void k_seed(IndexView ix, const uint8_t* __r
       fl[q] = 0;
       if (go) {
         const uint64_t canon = mm[q] < rr[q] ? mm[q] : rr[q];
-        uint64_t payload; uint32_t pr = 0;
-        const bool found = table_lookup(ix, canon, payload, pr);
+        uint64_t payload = 0; uint32_t pr = 0;
+        bool found = false;
+        if (ix.filt) ++my_fchecks;
+        if (!ix.filt || filt_test(ix, canon)) found = table_lookup(ix, canon, payload, pr);
         my_probes += pr;
         uint32_t cnt = 0;
         uint64_t ptr = null_ptr;
@@ -357,9 +383,11 @@ __global__ __launch_bounds__(BLOCK) void k_seed(IndexView ix, const uint8_t* __r
   if (MODE == SEED_COUNTS) {
     const uint64_t kmers = block_sum_u64<BLOCK>(my_kmers, s_tmp64);
     const uint64_t probes = block_sum_u64<BLOCK>(my_probes, s_tmp64);
+    const uint64_t fchecks = block_sum_u64<BLOCK>(my_fchecks, s_tmp64);
     if (tid == 0) {
       atomicAdd(&stats[ST_KMERS], (unsigned long long)kmers);
       atomicAdd(&stats[ST_PROBES], (unsigned long long)probes);
+      atomicAdd(&stats[ST_FILTER], (unsigned long long)fchecks);
     }
     return;
   }
@@ -407,7 +435,9 @@ __global__ __launch_bounds__(BLOCK) void k_seed(IndexView ix, const uint8_t* __r
   const uint64_t hits = block_sum_u64<BLOCK>(my_hits, s_tmp64);
   const uint64_t kmers = block_sum_u64<BLOCK>(my_kmers, s_tmp64);
   const uint64_t probes = block_sum_u64<BLOCK>(my_probes, s_tmp64);
+  const uint64_t fchecks = block_sum_u64<BLOCK>(my_fchecks, s_tmp64);
   if (tid == 0) {
+    atomicAdd(&stats[ST_FILTER], (unsigned long long)fchecks);
     n_kept_out[r] = n_kept;
     thr_out[r] = thr;
     nhits_out[r] = hits;
@@ -2187,8 +2217,10 @@ void launch_occ_fill(const uint64_t* vals, const uint64_t* uidx, const uint64_t*
   hipLaunchKernelGGL(k_occ_fill, dim3(4096), dim3(256), 0, st, vals, uidx, kpos, N, occ);
 }
 void launch_headers(const uint64_t* keys, const uint64_t* kpos, const uint64_t* run_start, uint64_t U, uint64_t* occ,
-                    ulonglong2* table, uint64_t bucket_mask, uint32_t k, uint32_t ebits, hipStream_t st) {
-  hipLaunchKernelGGL(k_headers, dim3(4096), dim3(256), 0, st, keys, kpos, run_start, U, occ, table, bucket_mask, k, ebits);
+                    ulonglong2* table, uint64_t bucket_mask, uint32_t k, uint32_t ebits, uint64_t* filt,
+                    uint32_t filt_shift, hipStream_t st) {
+  hipLaunchKernelGGL(k_headers, dim3(4096), dim3(256), 0, st, keys, kpos, run_start, U, occ, table, bucket_mask, k, ebits,
+                     (unsigned long long*)filt, filt_shift);
 }
 
 #ifndef PBGPU_SEED_PER
