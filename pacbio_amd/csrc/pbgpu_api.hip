@@ -1263,9 +1263,11 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_
         return hoff[a + 1] - hoff[a] > hoff[b + 1] - hoff[b];
       });
       const double fill_small = 0.95 * (double)((1u << hcap_log2) - (1u << hcap_log2) / 4);
+      // tests: PBGPU_GROUP_PRED_SCALE=0 routes every read to the smallest table (all overflow paths)
+      const double pred_scale = getenv("PBGPU_GROUP_PRED_SCALE") ? atof(getenv("PBGPU_GROUP_PRED_SCALE")) : 1.0;
       const double fill_big = 0.95 * (double)((1u << kGroupLdsMaxLog2) - (1u << kGroupLdsMaxLog2) / 4);
       for (uint32_t r : rl) {
-        const double pred = (double)(hoff[r + 1] - hoff[r]) * al->chains_per_hit;
+        const double pred = (double)(hoff[r + 1] - hoff[r]) * al->chains_per_hit * pred_scale;
         parts[r - r0] = (uint8_t)std::min(255.0, std::max(1.0, std::ceil(pred / fill_big)));
         (pred > fill_small ? rb : rs).push_back(r);
       }

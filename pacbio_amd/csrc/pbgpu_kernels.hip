@@ -459,7 +459,10 @@ __global__ __launch_bounds__(BLOCK) void k_seed(IndexView ix, const uint8_t* __r
 // reference's frags_pos order (coarse_aligner.cc:128-140) -- no sort needed.
 // 4 waves share one read's table; reads touching many super-reads use a
 // 16-wave block over the largest LDS table.
-constexpr uint32_t GROUP_BLOCK = 256, GROUP_BLOCK_BIG = 1024;
+#ifndef PBGPU_GROUP_BLOCK
+#define PBGPU_GROUP_BLOCK 256
+#endif
+constexpr uint32_t GROUP_BLOCK = PBGPU_GROUP_BLOCK, GROUP_BLOCK_BIG = 1024;
 #ifndef PBGPU_GROUP_PF
 #define PBGPU_GROUP_PF 1
 #endif
@@ -586,9 +589,14 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
         }
         if (pass == 0) {
           // order-free: distinct super-reads and per-strand list lengths
+          // Once the table is over its fill limit the read is abandoned (it resumes in
+          // a larger tier), but the rest of this k-mer group still runs and may fill
+          // the table: long probe sequences give up once the flag is set (or after
+          // hcap probes), so a full table can never trap a thread.
           if (mine) {
             bool ok = true;
-            for (;;) {
+            for (uint32_t probe = 0;; ++probe) {
+              if (probe >= 8 && (probe == hcap || *(volatile uint32_t*)&s_flag)) { s_flag = 1; ok = false; break; }
               const uint32_t old = atomicCAS(&tkey[slot], 0u, sr + 1);
               if (old == 0) { if (atomicAdd(&s_used, 1u) >= used_limit) { s_flag = 1; ok = false; } break; }
               if (old == sr + 1) break;
@@ -612,10 +620,14 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
             cur = fwd ? &tcf[slot] : &tcb[slot];
           }
           uint32_t pos = 0;
+#ifdef PBGPU_EXP_GROUP_NOORDER
+          if (mine) pos = atomicAdd(cur, 1u);
+#else
           for (uint32_t w = 0; w < B / 64; ++w) {
             if (wave == w && mine) pos = atomicAdd(cur, 1u);
             __syncthreads();
           }
+#endif
           if (mine) O.X[hbase + pos] = make_int2(pb, fwd ? so : -so);
         }
       }

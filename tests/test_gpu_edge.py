@@ -114,6 +114,20 @@ def test_dense_group_overflow(dense, cfg):
     assert_same_coords(got, exp, f"dense {cfg}")
 
 
+@pytest.mark.parametrize("data", ["dense", "small"])
+def test_group_all_overflow(data, dense, small, monkeypatch):
+    """Every read predicted to fit the smallest (2048-slot) table: reads touching
+    more super-reads abandon it mid k-mer group and resume in the 8192-slot LDS
+    tier and the HBM tables; a full table must never trap a thread."""
+    ds = dense if data == "dense" else small
+    monkeypatch.setenv("PBGPU_GROUP_PRED_SCALE", "0")
+    names, seqs = ds.sr_names(), ds.sr_seqs()
+    pnames, pseqs = ds.pb_names(), ds.pb_seqs()
+    exp = _oracle(names, seqs, pnames, pseqs, ul=ds.unitig_lengths, forward=True, unitigs_k=31)
+    got, _ = _gpu(names, seqs, pnames, pseqs, ul=ds.unitig_lengths, forward=True, unitigs_k=31)
+    assert_same_coords(got, exp, f"all-overflow {data}")
+
+
 def test_repeats_threshold():
     from tools.synth import Dataset
     ds = Dataset("small", seed=3, repeat_frac=0.2, n_pb=30)
