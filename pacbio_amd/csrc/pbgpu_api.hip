@@ -41,6 +41,7 @@ void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const ui
                   const uint64_t* hit_off, uint64_t node_base, uint32_t r0, const uint32_t* read_list, uint32_t n_list,
                   uint32_t hcap_log2, uint32_t* gtable, GroupOut O, unsigned long long* stats, hipStream_t st);
 uint64_t group_table_words(uint32_t hcap_log2);
+void launch_sr_ul(const uint32_t* ids, uint64_t n, const int32_t* ul, uint64_t n_ul, int32_t* out, hipStream_t st);
 constexpr uint32_t kGroupLdsMaxLog2 = 13;  // 8192-slot table, 96 KiB of LDS
 void launch_init_slen(const ChainDesc* chains, uint32_t n_chains, uint32_t* slen, hipStream_t st);
 void launch_strand_order(const uint32_t* slen, uint32_t n_items, uint32_t* hist, uint32_t* cursor, uint32_t* perm,
@@ -647,7 +648,7 @@ struct pbgpu_aligner {
   AlignParamsDev P{};
   LisParams lp{};
   hipStream_t st = nullptr;
-  dbuf<int32_t> ul;
+  dbuf<int32_t> ul, sr_ul;  // unitig lengths; the same resolved along every super-read name (k_sr_ul)
   // per-batch buffers
   dbuf<KRec> krec;
   dbuf<uint32_t> n_kept, thr, rec_per_read, rec_cursor, order, ovf_reads, counters;
@@ -777,6 +778,15 @@ pbgpu_status pbgpu_aligner_create(const pbgpu_index* ix, const pbgpu_align_param
   P.mers_factor = params->mers_matching / 100.0; P.bases_factor = params->bases_matching / 100.0;
   P.unitigs_k = params->unitigs_k && params->n_unitigs ? params->unitigs_k : 0;
   P.ul = al->ul.p; P.n_ul = params->unitigs_k ? params->n_unitigs : 0;
+  P.sr_ul = nullptr;
+  if (P.unitigs_k) {  // lengths along every super-read name, resolved once (k_coords' kmers_info)
+    const uint64_t nu = ix->sr_uids.n;
+    al->sr_ul.alloc(std::max<uint64_t>(nu, 1));
+    launch_sr_ul(ix->sr_uids.p, nu, al->ul.p, P.n_ul, al->sr_ul.p, nullptr);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipDeviceSynchronize());
+    P.sr_ul = al->sr_ul.p;
+  }
   al->lp.W = params->window_size; al->lp.a = params->stretch_factor; al->lp.b = params->stretch_constant;
   al->lp.C = params->stretch_cap; al->lp.mer_all = 0; al->lp.seq_all = 0; al->lp.ordered = 0;
   if (params->fine_k) {  // fine_aligner (fine_aligner.hpp:31-37): align_k = fine_k, compute_coords_info(forward = true)

@@ -48,6 +48,7 @@ struct AlignParamsDev {
   uint32_t unitigs_k;
   const int32_t* ul;
   uint64_t n_ul;
+  const int32_t* sr_ul;    // unitig length of every name entry (index sr_uids order), INT32_MIN if unusable
   int32_t fine;            // fine_aligner pass: every chain emits a record, no filters (fine_aligner.cc:43-48)
 };
 

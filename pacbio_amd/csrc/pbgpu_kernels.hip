@@ -241,6 +241,15 @@ __global__ void k_headers(const uint64_t* keys, const uint64_t* kpos, const uint
   }
 }
 
+// Unitig length of every name entry of the index (sr_uids), for kmers_info:
+// ulen(id) = ul[id], unusable (INT32_MIN) for an invalid id or one past the table
+__global__ void k_sr_ul(const uint32_t* ids, uint64_t n, const int32_t* ul, uint64_t n_ul, int32_t* out) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t id = ids[i];
+    out[i] = (id == INVALID_UNITIG || id >= n_ul) ? INT32_MIN : ul[id];
+  }
+}
+
 // ================================================================== seed
 // One workgroup per read.  fetch_super_reads (coarse_aligner.cc:81-125).
 // MODE (index sharded by super-read range):
@@ -1518,20 +1527,22 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
 }
 
 // compute_kmers_info (pb_aligner.cc:84-143) along one lis, one point at a
-// time.  ids: unitig ids of the fwd name; rev => bwd name (reversed list).
+// time.  lens: unitig lengths along the fwd name (P.sr_ul, resolved once per
+// aligner, so no dependent id -> length gather per chain); rev => bwd name
+// (reversed list).
 // Any error leaves n_info == 0 (the reference clears both vectors).
 // T: the arrays' element type, int32_t (global) or lds_i32 (LDS): an LDS
 // array must not be reached through a flat pointer, whose accesses wait for
 // every outstanding global load (the row prefetch).
 typedef __attribute__((address_space(3))) int32_t lds_i32;
+// kmers_info of names with at most INFO_LDS_UNITIGS unitigs is accumulated in LDS (k_coords)
+constexpr uint32_t INFO_LDS_UNITIGS = 8, INFO_LDS = 2 * INFO_LDS_UNITIGS - 1;
 template <typename T>
 struct KmersInfo {
-  const uint32_t* ids;
+  const int32_t* lens;
   uint32_t nsz;
   bool rev, ok;
   int32_t k, uk;
-  const int32_t* ul;
-  uint64_t n_ul;
   T* mers;    // element i at mers[i * stride]
   T* bases;
   uint32_t stride;
@@ -1546,11 +1557,7 @@ struct KmersInfo {
   // than the next unitig (unitigs shorter than a k-mer) update memory directly.
   int32_t pm, pb, om, ob, nm, nb, nlen;
   static constexpr int32_t UL_INVALID = INT32_MIN;
-  DEV uint32_t uid(uint32_t i) const { return i >= nsz ? INVALID_UNITIG : (rev ? ids[nsz - 1 - i] : ids[i]); }
-  DEV int32_t ulen_direct(uint32_t i) const {
-    const uint32_t id = uid(i);
-    return (id == INVALID_UNITIG || id >= n_ul) ? UL_INVALID : ul[id];
-  }
+  DEV int32_t ulen_direct(uint32_t i) const { return i >= nsz ? UL_INVALID : lens[rev ? nsz - 1 - i : i]; }
   DEV int32_t ulen(uint32_t i) const {
     if (cl) return i < nsz ? cl[i * stride] : UL_INVALID;
     return ulen_direct(i);
@@ -1563,12 +1570,16 @@ struct KmersInfo {
     if constexpr (std::is_same<T, lds_i32>::value) __atomic_fetch_add(x + i * stride, v, __ATOMIC_RELAXED);
     else x[i * stride] += v;
   }
-  DEV void init(const AlignParamsDev& P, const uint32_t* ids_, uint32_t nsz_, bool rev_, T* m, T* b,
+  DEV void init(const AlignParamsDev& P, const int32_t* lens_, uint32_t nsz_, bool rev_, T* m, T* b,
                 uint32_t stride_, T* cache = nullptr) {
-    ids = ids_; nsz = nsz_; rev = rev_; k = (int32_t)P.k; uk = (int32_t)P.unitigs_k; ul = P.ul; n_ul = P.n_ul;
+    lens = lens_; nsz = nsz_; rev = rev_; k = (int32_t)P.k; uk = (int32_t)P.unitigs_k;
     mers = m; bases = b; stride = stride_; cl = nullptr;
-    if (cache) {
-      for (uint32_t i = 0; i < nsz; ++i) cache[i * stride] = ulen_direct(i);
+    if (cache) {  // nsz <= INFO_LDS_UNITIGS: independent loads, issued together
+      int32_t v[INFO_LDS_UNITIGS];
+#pragma unroll
+      for (uint32_t i = 0; i < INFO_LDS_UNITIGS; ++i) v[i] = i < nsz ? ulen_direct(i) : 0;
+#pragma unroll
+      for (uint32_t i = 0; i < INFO_LDS_UNITIGS; ++i) if (i < nsz) cache[i * stride] = v[i];
       cl = cache;
     }
     const int32_t l0 = ulen(0);
@@ -1715,7 +1726,6 @@ DEV bool coords_finish(const AlignParamsDev& P, uint32_t rl, Rec& R) {
 // INFO_LDS_UNITIGS unitigs is accumulated in LDS during the first pass and
 // written once if the record is kept; longer names use a third pass that
 // updates the arrays in HBM.  With --max-match, kept chains go to the redo list.
-constexpr uint32_t INFO_LDS_UNITIGS = 8, INFO_LDS = 2 * INFO_LDS_UNITIGS - 1;
 // One lane's lis (pt_get's two layouts) streamed in order through the LDS
 // tile: the compact lanes' words in 2*CH-word rows, then the wide lanes'
 // points in CH-point rows (a lane takes part in one of the two loops).
@@ -1781,7 +1791,7 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
   const bool info_lds = nsz && nsz <= INFO_LDS_UNITIGS;
   KmersInfo<lds_i32> KI;
   if (info_lds)
-    KI.init(P, ix.sr_uids + u0, nsz, (R.flags & 2u) != 0, (lds_i32*)(im + lane), (lds_i32*)(ib + lane), 64,
+    KI.init(P, P.sr_ul + u0, nsz, (R.flags & 2u) != 0, (lds_i32*)(im + lane), (lds_i32*)(ib + lane), 64,
             (lds_i32*)(iul + lane));
   auto info_pos = [&](int32_t so) -> int32_t {
     const int32_t pos = fwd_align ? so : (int32_t)(R.ql + (uint32_t)so - k + 2u);
@@ -1855,7 +1865,7 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
           R.n_info = need;
         }
       } else {
-        KG.init(P, ix.sr_uids + u0, nsz, (R.flags & 2u) != 0, O.info_m + io, O.info_b + io, 1);
+        KG.init(P, P.sr_ul + u0, nsz, (R.flags & 2u) != 0, O.info_m + io, O.info_b + io, 1);
         pass3 = KG.ok;
       }
     } else {
@@ -2278,6 +2288,9 @@ void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const ui
     hipLaunchKernelGGL((k_group<true, GROUP_BLOCK_BIG>), dim3(n_list), dim3(GROUP_BLOCK_BIG), 0, st, ix, krec, roff,
                        n_kept, thr, hit_off, node_base, r0, read_list, n_list, hcap_log2, gtable, O, stats);
   }
+}
+void launch_sr_ul(const uint32_t* ids, uint64_t n, const int32_t* ul, uint64_t n_ul, int32_t* out, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_sr_ul, dim3(1024), dim3(256), 0, st, ids, n, ul, n_ul, out);
 }
 uint64_t group_table_words(uint32_t hcap_log2) { return (uint64_t)3 << hcap_log2; }
 
