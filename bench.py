@@ -68,7 +68,7 @@ class Comm:
 
 
 # the rocprofv3 kernel each timed slot corresponds to (tools/pmc_summary.py file names)
-ROCPROF_FILE = {"k_seed": "k_seed_256_8", "k_group": "k_group_false_256u", "k_lis": "k_lis_w_255_8",
+ROCPROF_FILE = {"k_seed": "k_seed_256_8_0", "k_group": "k_group_false_256u", "k_lis": "k_lis_w_255_8",
                 "k_coords": "k_coords_8", "k_rec_sort": "k_rec_sort_256_2048"}
 
 

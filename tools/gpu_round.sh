@@ -11,5 +11,4 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun
 cat gpurun_out/smoke_$TAG.log
 timeout -k 10 600 python -u bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { tail -30 gpurun_out/bench_$TAG.err; exit 1; }
 cat gpurun_out/bench_$TAG.json
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof_bench_$TAG.json 2> gpurun_out/prof_$TAG.err || { tail -30 gpurun_out/prof_$TAG.err; exit 1; }
-find gpurun_out/prof_$TAG -name '*stats*'
+bash tools/prof_round.sh $TAG
