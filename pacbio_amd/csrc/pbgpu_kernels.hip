@@ -1622,15 +1622,20 @@ struct KmersInfo {
     }
     ++pm;
     pb += new_bases;
-    if ((cunitig < nsz - 1) && ((uint32_t)sr_pos + (uint32_t)k > (uint32_t)cend - (uint32_t)uk + 1u)) {
-      // first overlapping unitig (the loop below at i = cunitig), in registers
-      const int32_t full_mer = sr_pos + uk > cend + 1;
-      om += full_mer; nm += full_mer;
-      const int32_t tt0 = sr_pos + k - cend + uk - 2;
-      const int32_t nbb0 = new_bases < tt0 ? new_bases : tt0;
-      ob += nbb0; nb += nbb0;
+    // First overlapping unitig (the reference's loop at i = cunitig), branch-free: the
+    // lanes of a wave sit at unrelated places of their super-reads, so a branch here
+    // would run for the whole wave at nearly every point.
+    const bool in_ov = (cunitig < nsz - 1) && ((uint32_t)sr_pos + (uint32_t)k > (uint32_t)cend - (uint32_t)uk + 1u);
+    const int32_t full_mer = (in_ov && sr_pos + uk > cend + 1) ? 1 : 0;
+    const int32_t tt0 = sr_pos + k - cend + uk - 2;
+    const int32_t nbb0 = in_ov ? (new_bases < tt0 ? new_bases : tt0) : 0;
+    om += full_mer; nm += full_mer;
+    ob += nbb0; nb += nbb0;
+    // rare: an unusable next length, or the k-mer also reaches the unitig after it
+    int32_t cendi = (int32_t)((uint32_t)cend + (uint32_t)nlen - (uint32_t)uk + 1u);
+    if (in_ov && (nlen == UL_INVALID ||
+                  (cunitig + 1 < nsz - 1 && (uint32_t)sr_pos + (uint32_t)k > (uint32_t)cendi - (uint32_t)uk + 1u))) {
       if (nlen == UL_INVALID) { ok = false; return; }
-      int32_t cendi = (int32_t)((uint32_t)cend + (uint32_t)nlen - (uint32_t)uk + 1u);
       for (uint32_t i = cunitig + 1; (i < nsz - 1) && ((uint32_t)sr_pos + (uint32_t)k > (uint32_t)cendi - (uint32_t)uk + 1u); ++i) {
         const int32_t fm = sr_pos + uk > cendi + 1;
         acc(mers, 2 * i + 1, fm); acc(mers, 2 * i + 2, fm);
