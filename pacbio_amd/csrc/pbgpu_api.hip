@@ -60,6 +60,10 @@ void launch_lis_wave(int tier, const ChainDesc* chains, const uint32_t* items, u
                      int2* X, void* N16, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx,
                      unsigned long long* stats, hipStream_t st);
 uint32_t lis_class_bounds(int which);
+uint32_t lis_lane_max();
+void launch_lis_lane(const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen, int2* X,
+                     void* N16, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx, unsigned long long* stats,
+                     hipStream_t st);
 uint32_t len_buckets();
 void launch_strand_order(const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen, int2* X,
                          hipStream_t st);
@@ -983,7 +987,7 @@ static uint32_t lis_stage(pbgpu_aligner* al, uint32_t nch, uint64_t Hs, const Li
   al->perm.ensure(2ull * nch + 1);
   al->lisl.ensure(2ull * nch + 1);
   al->slen.ensure(2ull * nch + 1);
-  uint32_t n_big = 0, n_mid = 0, n_w2 = 0, n_w1 = 0;  // items in classes above LIS_U16_MAX / LISW_LARGE / LISW_SMALL / LISW_TINY
+  uint32_t n_big = 0, n_mid = 0, n_w2 = 0, n_w1 = 0, n_w0 = 0;  // items in classes above LIS_U16_MAX / LISW_LARGE / LISW_SMALL / LISW_TINY
   auto order = [&](int which, uint32_t n_in) -> uint32_t {  // returns the number of items placed
     HIPCHK(hipMemsetAsync(al->hist.p, 0, NB * 4, st));
     if (which == 0) launch_strand_order(al->slen.p, n_in, al->hist.p, nullptr, nullptr, 0, st);
@@ -1004,6 +1008,7 @@ static uint32_t lis_stage(pbgpu_aligner* al, uint32_t nch, uint64_t Hs, const Li
       if ((uint32_t)b == lis_class_bounds(1)) n_mid = acc;
       if ((uint32_t)b == lis_class_bounds(0)) n_w2 = acc;
       if ((uint32_t)b == lis_class_bounds(3)) n_w1 = acc;
+      if ((uint32_t)b == lis_lane_max() + 1) n_w0 = acc;  // len_bucket(n) = n below 128
     }
     cur[0] = acc;
     HIPCHK(hipMemcpyAsync(al->hist.p + NB, cur.data(), NB * 4, hipMemcpyHostToDevice, st));
@@ -1031,8 +1036,12 @@ static uint32_t lis_stage(pbgpu_aligner* al, uint32_t nch, uint64_t Hs, const Li
                   al->lisl.p, lp, keep_idx, al->stats.p, st);
   launch_lis_wave(1, al->chains.p, al->perm.p + nw2, nw1 - nw2, al->slen.p, al->X.p, al->nodes.p,
                   al->pts.p, al->lisl.p, lp, keep_idx, al->stats.p, st);
+  // the shortest strands: lane per strand
+  const uint32_t nw0 = std::max(n_w0, nw1);
+  launch_lis_lane(al->chains.p, al->perm.p + nw0, n_strands - nw0, al->slen.p, al->X.p, al->nodes.p, al->pts.p,
+                  al->lisl.p, lp, keep_idx, al->stats.p, st);
   if (timed) HIPCHK(hipEventRecord(al->ev[10], st));  // the timed k_lis slot: tier-0 k_lis_w alone
-  launch_lis_wave(0, al->chains.p, al->perm.p + nw1, n_strands - nw1, al->slen.p, al->X.p, al->nodes.p,
+  launch_lis_wave(0, al->chains.p, al->perm.p + nw1, nw0 - nw1, al->slen.p, al->X.p, al->nodes.p,
                   al->pts.p, al->lisl.p, lp, keep_idx, al->stats.p, st);
   HIPCHK(hipGetLastError());
   if (timed) HIPCHK(hipEventRecord(al->ev[12], st));

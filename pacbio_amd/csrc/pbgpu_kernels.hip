@@ -1233,6 +1233,41 @@ __global__ __launch_bounds__(256) void k_strand_order(const ChainDesc* __restric
   }
 }
 
+// List order of strands of at most NMAX hits, one strand per lane: an odd-even
+// transposition network over registers (NMAX rounds sort any NMAX elements),
+// written back only when something moved.  These strands then go to the
+// lane-per-strand k_lis: a wave-per-strand kernel would spend a whole wave on
+// a handful of hits (on C2 30% of the non-empty strands have <= 8 hits).
+template <int NMAX>
+__global__ __launch_bounds__(256) void k_order_tiny(const ChainDesc* __restrict__ chains,
+                                                    const uint32_t* __restrict__ items, uint32_t n_items,
+                                                    const uint32_t* __restrict__ slen, int2* X) {
+  const uint32_t w = blockIdx.x * 256 + threadIdx.x;
+  if (w >= n_items) return;
+  const uint32_t item = items[w];
+  const ChainDesc d = chains[item >> 1];
+  const uint64_t base = d.hit_base + ((item & 1) ? d.nf : 0);
+  const uint32_t n = slen[item];
+  int2 v[NMAX];
+#pragma unroll
+  for (int j = 0; j < NMAX; ++j) v[j] = (uint32_t)j < n ? X[base + j] : make_int2(0, 0);
+  bool moved = false;
+#pragma unroll
+  for (int r = 0; r < NMAX; ++r) {
+#pragma unroll
+    for (int j = r & 1; j + 1 < NMAX; j += 2) {
+      if ((uint32_t)(j + 1) < n && hit_after(v[j], v[j + 1])) {
+        const int2 t = v[j]; v[j] = v[j + 1]; v[j + 1] = t;
+        moved = true;
+      }
+    }
+  }
+  if (moved) {
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j) if ((uint32_t)j < n) X[base + j] = v[j];
+  }
+}
+
 constexpr int LISW_TINY_N = 255;  // SMAX of the timed tier-0 k_lis_w
 template <int SMAX, int WPB>
 __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict__ chains,
@@ -2343,6 +2378,20 @@ void launch_lis(bool big_nodes, const ChainDesc* chains, const uint32_t* items, 
                        (LNode<uint16_t>*)N, pts, lisl, lp, keep_idx, stats);
 }
 constexpr uint32_t LISW_TINY = LISW_TINY_N, LISW_SMALL = 511, LISW_LARGE = 4095;
+#ifndef PBGPU_LIS_LANE_MAX
+#define PBGPU_LIS_LANE_MAX 8
+#endif
+// strands of <= LIS_LANE_MAX hits: order restored lane-per-strand, then k_lis (lane per strand)
+void launch_lis_lane(const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen, int2* X,
+                     void* N16, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx, unsigned long long* stats,
+                     hipStream_t st) {
+  if (!n_items) return;
+  if (!lp.ordered)
+    hipLaunchKernelGGL((k_order_tiny<PBGPU_LIS_LANE_MAX>), dim3((n_items + 255) / 256), dim3(256), 0, st, chains, items,
+                       n_items, slen, X);
+  launch_lis(false, chains, items, n_items, slen, X, N16, pts, lisl, lp, keep_idx, stats, st);
+}
+uint32_t lis_lane_max() { return PBGPU_LIS_LANE_MAX; }
 static uint32_t resident_blocks(const void* fn, int block) {
   static int cus = 0;
   if (!cus) {
