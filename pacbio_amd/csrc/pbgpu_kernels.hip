@@ -485,7 +485,9 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
                                                        uint32_t n_list, uint32_t hcap_log2, uint32_t* gtable, GroupOut O,
                                                        unsigned long long* stats) {
   extern __shared__ uint32_t s_dyn[];
-  __shared__ uint32_t s_nf[B], s_nb[B], s_off[B + 1], s_scan[B / 64];
+  // static LDS kept under 8 KiB: with the 2048-slot table a 4-wave block then
+  // needs < 32 KiB, and 5 blocks fit a CU instead of 4
+  __shared__ uint32_t s_nf[B], s_off[B], s_scan[B / 64];
   __shared__ int32_t s_pb[B];
   __shared__ uint64_t s_pf[B], s_pbk[B];
   __shared__ uint32_t s_flag, s_used, s_cbase;
@@ -545,10 +547,9 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
           s_pb[tid] = kr.pb_off;
         }
       }
-      s_nf[tid] = nf; s_nb[tid] = nb;
+      s_nf[tid] = nf;
       uint32_t total;
       s_off[tid] = block_excl_scan<B>(nf + nb, s_scan, total);
-      if (tid == 0) s_off[B] = total;
       __syncthreads();
 #ifdef PBGPU_PROF
       const uint64_t pr_b = __builtin_amdgcn_s_memtime();
