@@ -471,7 +471,10 @@ __global__ __launch_bounds__(BLOCK) void k_seed(IndexView ix, const uint8_t* __r
 #ifndef PBGPU_GROUP_BLOCK
 #define PBGPU_GROUP_BLOCK 256
 #endif
-constexpr uint32_t GROUP_BLOCK = PBGPU_GROUP_BLOCK, GROUP_BLOCK_BIG = 1024;
+#ifndef PBGPU_GROUP_BLOCK_BIG
+#define PBGPU_GROUP_BLOCK_BIG 1024
+#endif
+constexpr uint32_t GROUP_BLOCK = PBGPU_GROUP_BLOCK, GROUP_BLOCK_BIG = PBGPU_GROUP_BLOCK_BIG;
 #ifndef PBGPU_GROUP_PF
 #define PBGPU_GROUP_PF 1
 #endif
