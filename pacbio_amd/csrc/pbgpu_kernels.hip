@@ -948,12 +948,15 @@ DEV void stream_rows(const T* __restrict__ src, const ChunkGrid<CH>& G, uint32_t
   }
 }
 
+// The conjunctions are evaluated in full (bitwise &, no short circuit): every
+// operand is a side-effect-free compare, and a short circuit costs a divergent
+// branch (exec-mask save / restore) per operand in the wave-wide scans.
 DEV bool affine_ok(double a, double b, double C, double df, double ds) {
   // (s.first <= b + a*s.second) && (s.second <= b + a*s.first) && s.first <= C && s.second <= C
-  return (df <= __dadd_rn(b, __dmul_rn(a, ds))) && (ds <= __dadd_rn(b, __dmul_rn(a, df))) && df <= C && ds <= C;
+  return (df <= __dadd_rn(b, __dmul_rn(a, ds))) & (ds <= __dadd_rn(b, __dmul_rn(a, df))) & (df <= C) & (ds <= C);
 }
 DEV bool linear_ok(double a, double df, double ds) {
-  return (df <= __dmul_rn(a, ds)) && (ds <= __dmul_rn(a, df));
+  return (df <= __dmul_rn(a, ds)) & (ds <= __dmul_rn(a, df));
 }
 
 // lis_align::compute_L_P (lis_align.hpp:139-182) + indices (:190-204),
@@ -1359,11 +1362,11 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
           int2 pv = make_int2(__shfl(xv[q].x, src, 64), __shfl(xv[q].y, src, 64));
           if (q > 0 && lane == 0) pv = make_int2(__shfl(xv[q - 1].x, 63, 64), __shfl(xv[q - 1].y, 63, 64));
           const int2 xi = xv[q];
-          if (i < n && i > 0) {
-            const bool clean = xi.y > pv.y && affine_ok(lp.a, lp.b, lp.C, (double)(xi.x - pv.x), (double)(xi.y - pv.y));
-            bad |= !clean || (!lp.ordered && hit_after(pv, xi));
+          {  // branch-free: the lanes past n compute on stale values and are masked out
+            const bool clean = (xi.y > pv.y) & affine_ok(lp.a, lp.b, lp.C, (double)(xi.x - pv.x), (double)(xi.y - pv.y));
+            bad |= (i < n) & (i > 0) & (!clean | ((lp.ordered == 0) & hit_after(pv, xi)));
           }
-          const bool lin = i < n && (lp.seq_all || linear_ok(lp.a, (double)(xi.x - x0.x), (double)(xi.y - x0.y)));
+          const bool lin = (i < n) & ((lp.seq_all != 0) | linear_ok(lp.a, (double)(xi.x - x0.x), (double)(xi.y - x0.y)));
           const uint64_t lb = __ballot(lin);
           if (lb) top = q * 64 + 63 - (int32_t)__clzll((long long)lb);
         }
@@ -1446,7 +1449,7 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
             clean = true;
           } else {
             const int2 xj = sx[lane == 0 ? head : i - 1];
-            clean = xi.y > xj.y && affine_ok(lp.a, lp.b, lp.C, (double)(xi.x - xj.x), (double)(xi.y - xj.y));
+            clean = (xi.y > xj.y) & affine_ok(lp.a, lp.b, lp.C, (double)(xi.x - xj.x), (double)(xi.y - xj.y));
           }
         }
         const uint64_t bad = __ballot(i < pend && !clean);
@@ -1461,8 +1464,8 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
             const uint32_t P = lane == 0 ? head : i - 1;
             snxt[i] = (uint16_t)P; sln[i] = (uint16_t)elen; sP[i] = (uint16_t)P; sroot[i] = (uint16_t)hr;
             srs[i] = (uint16_t)(P + 1 == i ? rsr : i);
-            cand = elen > longest &&
-                   (lp.seq_all || linear_ok(lp.a, (double)(xi.x - hrx.x), (double)(xi.y - hrx.y)));
+            cand = (elen > longest) &
+                   ((lp.seq_all != 0) | linear_ok(lp.a, (double)(xi.x - hrx.x), (double)(xi.y - hrx.y)));
           }
           const uint64_t cb = __ballot(cand);
           if (cb) {
