@@ -1646,12 +1646,11 @@ struct KmersInfo {
     if (!ok) return;
     const int32_t new_bases = k < sr_pos - prev_pos ? k : sr_pos - prev_pos;
     while (sr_pos + k > cend + 1) {
-      if (cend >= sr_pos) {
-        if (cunitig >= nsz - 1) { ok = false; return; }
-        const int32_t mx = sr_pos > prev_pos + k ? sr_pos : prev_pos + k;
-        const int32_t nbb = cend - mx + 1;
-        pb += nbb; ob += nbb;
-      }
+      const bool part = cend >= sr_pos;  // the k-mer starts inside unitig c
+      if (part & (cunitig >= nsz - 1)) { ok = false; return; }
+      const int32_t mx = sr_pos > prev_pos + k ? sr_pos : prev_pos + k;
+      const int32_t nbb = part ? cend - mx + 1 : 0;
+      pb += nbb; ob += nbb;
       // unitig c is done: write 2c and 2c+1, 2c+2 becomes current
       acc(mers, 2 * cunitig, pm); acc(bases, 2 * cunitig, pb);
       if (cunitig + 1 < nsz) { acc(mers, 2 * cunitig + 1, om); acc(bases, 2 * cunitig + 1, ob); }
@@ -1667,16 +1666,16 @@ struct KmersInfo {
     // First overlapping unitig (the reference's loop at i = cunitig), branch-free: the
     // lanes of a wave sit at unrelated places of their super-reads, so a branch here
     // would run for the whole wave at nearly every point.
-    const bool in_ov = (cunitig < nsz - 1) && ((uint32_t)sr_pos + (uint32_t)k > (uint32_t)cend - (uint32_t)uk + 1u);
-    const int32_t full_mer = (in_ov && sr_pos + uk > cend + 1) ? 1 : 0;
+    const bool in_ov = (cunitig < nsz - 1) & ((uint32_t)sr_pos + (uint32_t)k > (uint32_t)cend - (uint32_t)uk + 1u);
+    const int32_t full_mer = (in_ov & (sr_pos + uk > cend + 1)) ? 1 : 0;
     const int32_t tt0 = sr_pos + k - cend + uk - 2;
     const int32_t nbb0 = in_ov ? (new_bases < tt0 ? new_bases : tt0) : 0;
     om += full_mer; nm += full_mer;
     ob += nbb0; nb += nbb0;
     // rare: an unusable next length, or the k-mer also reaches the unitig after it
     int32_t cendi = (int32_t)((uint32_t)cend + (uint32_t)nlen - (uint32_t)uk + 1u);
-    if (in_ov && (nlen == UL_INVALID ||
-                  (cunitig + 1 < nsz - 1 && (uint32_t)sr_pos + (uint32_t)k > (uint32_t)cendi - (uint32_t)uk + 1u))) {
+    if (in_ov & ((nlen == UL_INVALID) |
+                 ((cunitig + 1 < nsz - 1) & ((uint32_t)sr_pos + (uint32_t)k > (uint32_t)cendi - (uint32_t)uk + 1u)))) {
       if (nlen == UL_INVALID) { ok = false; return; }
       for (uint32_t i = cunitig + 1; (i < nsz - 1) && ((uint32_t)sr_pos + (uint32_t)k > (uint32_t)cendi - (uint32_t)uk + 1u); ++i) {
         const int32_t fm = sr_pos + uk > cendi + 1;
