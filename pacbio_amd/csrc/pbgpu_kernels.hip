@@ -71,10 +71,17 @@ DEV int base_code(uint8_t c) {
 DEV bool is_ssr(uint64_t m, uint32_t k) {
   const uint32_t hs = 2 * (k - 1);
   uint64_t n1 = (m >> 2) | ((m & 3) << hs);
-  if (n1 == m) return true;
   uint64_t n2 = (n1 >> 2) | ((n1 & 3) << hs);
-  return n2 == m;
+  return (n1 == m) | (n2 == m);
 }
+// Branch-free base decoding for the seeding loops: ACGT/acgt -> 0..3
+// (((c >> 1) ^ (c >> 2)) & 3), and validity by an exact compare of the
+// upper-cased byte (every other byte resets the k-mer, as base_code's -1).
+DEV bool base_valid(uint8_t c) {
+  const uint32_t u = c & 0xDFu;
+  return (u == 'A') | (u == 'C') | (u == 'G') | (u == 'T');
+}
+DEV uint32_t base_code2(uint8_t c) { return ((c >> 1) ^ (c >> 2)) & 3u; }
 DEV int lane_id() { return threadIdx.x & 63; }
 DEV void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -299,38 +306,35 @@ __global__ __launch_bounds__(BLOCK) void k_seed(IndexView ix, const uint8_t* __r
     const int64_t s = p0 - LOOK > 0 ? p0 - LOOK : 0;
     uint64_t m = 0, rm = 0;
     uint32_t rl = s > 0 ? 1000u : 0u;  // unknown history before s counts as a long valid run
-    for (int64_t q = s; q < p0; ++q) {
-      const int c = base_code(s_seq[q - t0 + LOOK]);
-      if (c < 0) { rl = 0; continue; }
-      ++rl;
-      m = ((m << 2) | (uint64_t)c) & mask;
-      rm = (rm >> 2) | ((uint64_t)(3 - c) << hs);
+    for (int64_t q = s; q < p0; ++q) {  // branch-free: an invalid base resets the run
+      const uint8_t ch = s_seq[q - t0 + LOOK];
+      const bool v = base_valid(ch);
+      const uint64_t c = base_code2(ch);
+      rl = v ? rl + 1 : 0u;
+      m = v ? ((m << 2) | c) & mask : m;
+      rm = v ? (rm >> 2) | ((3ull - c) << hs) : rm;
     }
     uint64_t mm[PER], rr[PER];
     uint32_t fl[PER];  // bit0 valid&!ssr (candidate for lookup), bit1 toggle candidate
     uint32_t ncand = 0;
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
+      // branch-free; positions past the read end hold 'N' in the tile
       const int64_t p = p0 + q;
-      fl[q] = 0;
-      mm[q] = 0; rr[q] = 0;
-      if (p < L) {
-        const int c = base_code(s_seq[p - t0 + LOOK]);
-        if (c < 0) rl = 0;
-        else {
-          ++rl;
-          m = ((m << 2) | (uint64_t)c) & mask;
-          rm = (rm >> 2) | ((uint64_t)(3 - c) << hs);
-          if (rl >= k) {
-            ++my_kmers;
-            if (!is_ssr(m, k)) {
-              fl[q] = 1;
-              if (rl <= 17) { fl[q] |= 2; ++ncand; }  // coarse_aligner.cc:96-102
-            }
-            mm[q] = m; rr[q] = rm;
-          }
-        }
-      }
+      const uint8_t ch = s_seq[p - t0 + LOOK];
+      const bool v = base_valid(ch);
+      const uint64_t c = base_code2(ch);
+      rl = v ? rl + 1 : 0u;
+      m = v ? ((m << 2) | c) & mask : m;
+      rm = v ? (rm >> 2) | ((3ull - c) << hs) : rm;
+      const bool km = v & (rl >= k);
+      my_kmers += km ? 1u : 0u;
+      const bool cand = km & !is_ssr(m, k);
+      const bool tog = cand & (rl <= 17u);  // coarse_aligner.cc:96-102
+      fl[q] = (cand ? 1u : 0u) | (tog ? 2u : 0u);
+      ncand += tog ? 1u : 0u;
+      mm[q] = km ? m : 0; rr[q] = km ? rm : 0;
+      (void)p;
     }
     // toggle: candidate number c (1-based, whole read) is processed iff c is odd
     uint32_t ctot;
