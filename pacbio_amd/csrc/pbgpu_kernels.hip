@@ -565,8 +565,9 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
       // hit h -> (record, strand, occurrence address); the occurrence of the next
       // 256-hit step is loaded one step ahead so its latency overlaps the table work
       auto locate = [&](uint32_t h, uint32_t& rec, bool& fwd, int32_t& pb) -> uint64_t {
-        uint32_t lo = 0, hi = B;  // last record with s_off <= h
-        while (hi - lo > 1) { const uint32_t md = (lo + hi) >> 1; if (s_off[md] <= h) lo = md; else hi = md; }
+        uint32_t lo = 0;  // last record with s_off <= h (s_off[0] = 0): fixed-depth, branch-free
+#pragma unroll
+        for (uint32_t stp = B / 2; stp >= 1; stp >>= 1) lo = s_off[lo + stp] <= h ? lo + stp : lo;
         rec = lo;
         const uint32_t local = h - s_off[lo];
         fwd = local < s_nf[lo];
