@@ -1833,6 +1833,9 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
   Rec R;
   R.nb_mers = (int32_t)nl; R.pb_cons = 0; R.sr_cons = 0; R.pb_cover = k; R.sr_cover = k;
   R.ql = act ? (uint32_t)(ix.sr_start[d.sr + 1] - ix.sr_start[d.sr]) : 0;
+  // the read length is needed only by the filters at the end: loaded here, with the other
+  // descriptor-dependent loads, so it does not stall the wave after the passes
+  const uint32_t rl = act ? (uint32_t)(roff[d.read + 1] - roff[d.read]) : 0;
   R.sr = d.sr; R.read = d.read; R.flags = (P.forward && !fwd_align) ? 2u : 0u;
   R.n_info = 0; R.reserved = 0; R.info_off = 0; R.emit = O.emit_of ? (act ? O.emit_of[c] : 0u) : emit;
   R.stretch = 0; R.offset = 0; R.avg_err = 0;
@@ -1899,7 +1902,6 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
   R.rs = first.x;
   R.re = (int32_t)((uint32_t)prev.x + k - 1u);
   R.qs = first.y; R.qe = prev.y;
-  const uint32_t rl = act ? (uint32_t)(roff[d.read + 1] - roff[d.read]) : 0;
   const bool keep = act && nl > 0 && coords_finish(P, rl, R);
   // info arrays: allocate for kept records, copy the LDS case, or run pass 3 in HBM
   bool info_ok = true, pass3 = false;
