@@ -422,10 +422,12 @@ __global__ __launch_bounds__(BLOCK) void k_seed(IndexView ix, const uint8_t* __r
         if ((v & pmask) == prefix) atomicAdd(&s_hist[(v >> shift) & 255], 1u);
       }
       __syncthreads();
-      if (tid == 0) {
-        uint32_t cum = 0, d = 0;
-        for (; d < 256; ++d) { if (cum + s_hist[d] > rank) break; cum += s_hist[d]; }
-        s_sel[0] = d; s_sel[1] = rank - cum;
+      {  // the digit whose bin holds the rank-th count: one block scan, not 256 serial steps
+        static_assert(BLOCK == 256, "one histogram bin per thread");
+        const uint32_t hv = s_hist[tid];
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan<BLOCK>(hv, s_tmp, tot);
+        if (ex <= rank && rank < ex + hv) { s_sel[0] = tid; s_sel[1] = rank - ex; }
       }
       __syncthreads();
       prefix |= s_sel[0] << shift; pmask |= 255u << shift; rank = s_sel[1];
