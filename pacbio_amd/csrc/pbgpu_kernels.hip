@@ -1212,8 +1212,8 @@ __global__ __launch_bounds__(64) void k_lis(const ChainDesc* __restrict__ chains
 // List order of a strand (coarse_aligner.cc:128-140): pb offset
 // ascending, then occurrence order, which within one super-read and strand is
 // |sr offset| descending.  (pb, |so|) pairs are unique within a list.
-DEV bool hit_after(int2 a, int2 b) {
-  return a.x != b.x ? a.x > b.x : abs(a.y) < abs(b.y);
+DEV bool hit_after(int2 a, int2 b) {  // branch-free (a select compiled to an if / else)
+  return (a.x > b.x) | ((a.x == b.x) & (abs(a.y) < abs(b.y)));
 }
 
 // Restores list order for strands too long for k_lis_w's LDS (one block per
@@ -1320,7 +1320,10 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
     desc(nitem, nbase, nn);
     if constexpr (PREFETCH) {
 #pragma unroll
-      for (int q = 0; q < PF; ++q) { const uint32_t j = q * 64 + lane; if (j < nn) pf[q] = X[nbase + j]; }
+      for (int q = 0; q < PF; ++q) {  // clamped, not branched: lanes past the strand reload its last hit
+        const uint32_t j = q * 64 + lane;
+        pf[q] = X[nbase + (j < nn ? j : nn - 1)];
+      }
     }
     if (w + nwaves < n_items) { nitem2 = items[w + nwaves]; desc(nitem2, nbase2, nn2); }
     if (w + 2 * nwaves < n_items) nitem3 = items[w + 2 * nwaves];
@@ -1339,7 +1342,10 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
     if (w + nwaves < n_items) {
       if constexpr (PREFETCH) {
 #pragma unroll
-        for (int q = 0; q < PF; ++q) { const uint32_t j = q * 64 + lane; if (j < nn) pf[q] = X[nbase + j]; }
+        for (int q = 0; q < PF; ++q) {  // clamped, not branched: lanes past the strand reload its last hit
+        const uint32_t j = q * 64 + lane;
+        pf[q] = X[nbase + (j < nn ? j : nn - 1)];
+      }
       }
       if (w + 2 * nwaves < n_items) {
         nitem2 = nitem3;
