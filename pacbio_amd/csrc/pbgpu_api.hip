@@ -79,8 +79,8 @@ void launch_fine_desc(IndexView ix, const Rec* recs, uint64_t w_sub0, uint32_t n
                       unsigned long long* info_need, hipStream_t st);
 void launch_fine_empty(IndexView ix, uint32_t k, const ChainDesc* chains, uint32_t n, const uint32_t* lisl,
                        const uint32_t* emit_of, ChainOut O, hipStream_t st);
-void launch_rec_hist(const Rec* recs, uint32_t n, uint32_t* per_read, hipStream_t st);
-void launch_rec_scatter(const Rec* recs, uint32_t n, const uint64_t* rec_off, uint32_t* cursor, uint32_t* order,
+void launch_rec_hist(const uint32_t* rec_read, uint32_t n, uint32_t* per_read, hipStream_t st);
+void launch_rec_scatter(const uint32_t* rec_read, uint32_t n, const uint64_t* rec_off, uint32_t* cursor, uint32_t* order,
                         hipStream_t st);
 int rec_sort_lcap();
 void launch_rec_sort(const Rec* recs, const uint64_t* rec_off, const uint32_t* order, uint64_t* gscratch,
@@ -666,6 +666,7 @@ struct pbgpu_aligner {
   dbuf<uint32_t> lisl, hist, slen;
   dbuf<uint32_t> redo[3];
   dbuf<Rec> recs, recs_sorted;
+  dbuf<uint32_t> rec_read;  // the read of every record of recs (written with it)
   dbuf<int32_t> info_m, info_b;
   dbuf<uint8_t> tmp;
   dbuf<uint32_t> gtable;
@@ -1057,7 +1058,7 @@ static void records_stage(pbgpu_aligner* al, uint32_t n, uint32_t nrec, bool tim
   al->rec_per_read.ensure(n); al->rec_cursor.ensure(n);
   HIPCHK(hipMemsetAsync(al->rec_per_read.p, 0, n * 4, st));
   HIPCHK(hipMemsetAsync(al->rec_cursor.p, 0, n * 4, st));
-  launch_rec_hist(al->recs.p, nrec, al->rec_per_read.p, st);
+  launch_rec_hist(al->rec_read.p, nrec, al->rec_per_read.p, st);
   {
     struct RecOp {
       const uint32_t* c; uint64_t n;
@@ -1072,7 +1073,7 @@ static void records_stage(pbgpu_aligner* al, uint32_t n, uint32_t nrec, bool tim
   al->order.ensure(nrec + 1);
   al->sort_scratch.ensure(6ull * nrec + 6);
   al->recs_sorted.ensure(nrec + 1);
-  launch_rec_scatter(al->recs.p, nrec, al->rec_off.p, al->rec_cursor.p, al->order.p, st);
+  launch_rec_scatter(al->rec_read.p, nrec, al->rec_off.p, al->rec_cursor.p, al->order.p, st);
   if (timed) HIPCHK(hipEventRecord(al->ev[15], st));
   launch_rec_sort(al->recs.p, al->rec_off.p, al->order.p, al->sort_scratch.p, n, al->recs_sorted.p, st);
   HIPCHK(hipGetLastError());
@@ -1164,6 +1165,7 @@ static void fine_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
     HIPCHK(hipMemcpyAsync(&need, info_need, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     al->recs.grow_keep(rec_done + nws + 1, rec_done, st);
+    al->rec_read.grow_keep(al->recs.n, rec_done, st);
     if (al->PF.unitigs_k) {
       al->info_m.grow_keep(info_done + need + 1, info_done, st);
       al->info_b.grow_keep(info_done + need + 1, info_done, st);
@@ -1178,7 +1180,7 @@ static void fine_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
     ChainOut CO{};
     CO.pts = al->pts.p; CO.lisl = al->lisl.p;
     CO.redo = nullptr; CO.n_redo = al->counters.p + 8;
-    CO.recs = al->recs.p; CO.rec_count = al->counters.p + 4;
+    CO.recs = al->recs.p; CO.rec_read = al->rec_read.p; CO.rec_count = al->counters.p + 4;
     CO.rec_cap = (uint32_t)std::min<uint64_t>(al->recs.n, 0xFFFFFFFFu);
     CO.info_m = al->info_m.p; CO.info_b = al->info_b.p; CO.info_count = al->info_count.p; CO.info_cap = al->info_m.n;
     CO.stats = al->stats.p;
@@ -1367,6 +1369,7 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_
       const uint32_t n_fit = lis_stage(al, nch, Hs, al->lp, al->P.max_match, true, true);
       const uint64_t rec_need = rec_done + (uint64_t)nch * (al->P.max_match ? 2 : 1) + 1024 * (attempt + 1);
       al->recs.grow_keep(std::max<uint64_t>(rec_need, al->rec_hint), rec_done, st);
+      al->rec_read.grow_keep(al->recs.n, rec_done, st);
       if (al->P.unitigs_k) {
         const uint64_t info_need = info_done + (uint64_t)nch * al->info_per_chain + 4096;
         al->info_m.grow_keep(info_need, info_done, st);
@@ -1385,7 +1388,7 @@ static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_
       ChainOut CO{};
       CO.pts = al->pts.p; CO.lisl = al->lisl.p;
       CO.redo = al->P.max_match ? al->redo[0].p : nullptr; CO.n_redo = n_redo;
-      CO.recs = al->recs.p; CO.rec_count = al->counters.p + 4;
+      CO.recs = al->recs.p; CO.rec_read = al->rec_read.p; CO.rec_count = al->counters.p + 4;
       CO.rec_cap = (uint32_t)std::min<uint64_t>(al->recs.n, 0xFFFFFFFFu);
       CO.info_m = al->info_m.p; CO.info_b = al->info_b.p; CO.info_count = al->info_count.p; CO.info_cap = al->info_m.n;
       CO.stats = al->stats.p;

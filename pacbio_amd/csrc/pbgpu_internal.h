@@ -158,6 +158,7 @@ struct ChainOut {
   uint32_t* redo;          // --max-match: chains to discard + redo
   uint32_t* n_redo;
   Rec* recs;
+  uint32_t* rec_read;       // per record its read (records_stage's histogram / scatter read 4 B, not a 96-B record)
   uint32_t* rec_count;
   uint32_t rec_cap;
   int32_t* info_m;

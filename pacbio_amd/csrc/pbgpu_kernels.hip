@@ -1939,7 +1939,7 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
   PROF_T(kc_t5);
   if (keep) {
     const uint32_t ri = atomicAdd(O.rec_count, 1u);
-    if (ri < O.rec_cap && info_ok) O.recs[ri] = R;
+    if (ri < O.rec_cap && info_ok) { O.recs[ri] = R; O.rec_read[ri] = R.read; }
     else atomicAdd(&O.stats[ST_REC_OVERFLOW], 1ull);
     if (P.max_match) O.redo[atomicAdd(O.n_redo, 1u)] = c;
   }
@@ -2191,19 +2191,20 @@ __global__ void k_fine_empty(IndexView ix, uint32_t k, const ChainDesc* __restri
     R.sr = d.sr; R.read = d.read; R.emit = emit_of[c]; R.flags = 0; R.n_info = 0; R.reserved = 0; R.info_off = 0;
     R.stretch = 0; R.offset = 0; R.avg_err = 0;
     const uint32_t ri = atomicAdd(O.rec_count, 1u);
-    if (ri < O.rec_cap) O.recs[ri] = R;
+    if (ri < O.rec_cap) { O.recs[ri] = R; O.rec_read[ri] = R.read; }
     else atomicAdd(&O.stats[ST_REC_OVERFLOW], 1ull);
   }
 }
 
 // =============================================================== records
-__global__ void k_rec_hist(const Rec* recs, uint32_t n, uint32_t* per_read) {
+__global__ void k_rec_hist(const uint32_t* rec_read, uint32_t n, uint32_t* per_read) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-    atomicAdd(&per_read[recs[i].read], 1u);
+    atomicAdd(&per_read[rec_read[i]], 1u);
 }
-__global__ void k_rec_scatter(const Rec* recs, uint32_t n, const uint64_t* rec_off, uint32_t* cursor, uint32_t* order) {
+__global__ void k_rec_scatter(const uint32_t* rec_read, uint32_t n, const uint64_t* rec_off, uint32_t* cursor,
+                              uint32_t* order) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint32_t r = recs[i].read;
+    const uint32_t r = rec_read[i];
     order[rec_off[r] + atomicAdd(&cursor[r], 1u)] = i;
   }
 }
@@ -2483,14 +2484,14 @@ uint32_t big_bucket() {  // first length class whose items all exceed LIS_U16_MA
   return 128u + 16u * (16u - 7u);
 }
 
-void launch_rec_hist(const Rec* recs, uint32_t n, uint32_t* per_read, hipStream_t st) {
+void launch_rec_hist(const uint32_t* rec_read, uint32_t n, uint32_t* per_read, hipStream_t st) {
   if (!n) return;
-  hipLaunchKernelGGL(k_rec_hist, dim3(1024), dim3(256), 0, st, recs, n, per_read);
+  hipLaunchKernelGGL(k_rec_hist, dim3(1024), dim3(256), 0, st, rec_read, n, per_read);
 }
-void launch_rec_scatter(const Rec* recs, uint32_t n, const uint64_t* rec_off, uint32_t* cursor, uint32_t* order,
+void launch_rec_scatter(const uint32_t* rec_read, uint32_t n, const uint64_t* rec_off, uint32_t* cursor, uint32_t* order,
                         hipStream_t st) {
   if (!n) return;
-  hipLaunchKernelGGL(k_rec_scatter, dim3(1024), dim3(256), 0, st, recs, n, rec_off, cursor, order);
+  hipLaunchKernelGGL(k_rec_scatter, dim3(1024), dim3(256), 0, st, rec_read, n, rec_off, cursor, order);
 }
 constexpr int REC_BLOCK = 256, REC_LCAP = 2048;
 int rec_sort_lcap() { return REC_LCAP; }
