@@ -1465,7 +1465,7 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
             clean = (xi.y > xj.y) & affine_ok(lp.a, lp.b, lp.C, (double)(xi.x - xj.x), (double)(xi.y - xj.y));
           }
         }
-        const uint64_t bad = __ballot(i < pend && !clean);
+        const uint64_t bad = __ballot((i < pend) & !clean);
         m = bad ? (uint32_t)__ffsll((unsigned long long)bad) - 1 : pend - cur;
         if (m) {
           const uint32_t hl = empty ? 0u : sln[head], hr = empty ? cur : sroot[head];
@@ -2226,7 +2226,7 @@ DEV void bitonic_keys(uint64_t* hi, uint64_t* lo, EX* ex, uint32_t np2) {
         const uint32_t i = ((p & ~(j - 1)) << 1) | (p & (j - 1)), l = i + j;
         const uint64_t h0 = hi[i], h1 = hi[l], l0 = lo[i], l1 = lo[l];
         const EX e0 = ex[i], e1 = ex[l];
-        const bool gt = h0 != h1 ? h0 > h1 : l0 != l1 ? l0 > l1 : e0 > e1;
+        const bool gt = (h0 > h1) | ((h0 == h1) & ((l0 > l1) | ((l0 == l1) & (e0 > e1))));
         if (gt == ((i & kk) == 0)) { hi[i] = h1; hi[l] = h0; lo[i] = l1; lo[l] = l0; ex[i] = e1; ex[l] = e0; }
       }
       __syncthreads();
