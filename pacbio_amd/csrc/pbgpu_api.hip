@@ -678,7 +678,7 @@ struct pbgpu_aligner {
   pbgpu_stats acc{};
   hipEvent_t ev[18]{};
   uint64_t hit_budget = 4000000000ull, rec_hint = 0, info_per_chain = 32;
-  double chains_per_hit = 1.0 / 48;  // k_group partition estimate, refined after every batch
+  double chains_per_hit = 1.0 / 80;  // k_group tier estimate (C2: 1.1 x 1/90), refined after every batch
   dbuf<uint32_t> ovf_list, read_list;
   dbuf<uint8_t> nparts;
   dbuf<uint2> prog;
