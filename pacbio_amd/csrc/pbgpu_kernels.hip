@@ -496,9 +496,11 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
   extern __shared__ uint32_t s_dyn[];
   // static LDS kept under 8 KiB: with the 2048-slot table a 4-wave block then
   // needs < 32 KiB, and 5 blocks fit a CU instead of 4
-  __shared__ uint32_t s_nf[B], s_off[B], s_scan[B / 64];
-  __shared__ int32_t s_pb[B];
-  __shared__ uint64_t s_pf[B], s_pbk[B];
+  // per k-mer record of the current group: {fwd list count, pb offset} and the
+  // occurrence addresses {fwd list, bwd list - fwd count}, read together by locate()
+  __shared__ uint32_t s_off[B], s_scan[B / 64];
+  __shared__ uint2 s_np[B];
+  __shared__ ulonglong2 s_ptr[B];
   __shared__ uint32_t s_flag, s_used, s_cbase;
   if (blockIdx.x >= n_list) return;
   const uint32_t tid = threadIdx.x;
@@ -541,6 +543,7 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
 #endif
       const uint32_t i = g0 + tid;
       uint32_t nf = 0, nb = 0;
+      int32_t pbv = 0;
       if (i < nk) {
         const KRec kr = krec[kbase + i];
         if (kr.count <= thr) {
@@ -550,13 +553,15 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
           const uint32_t nA = (uint32_t)(h1 & 0xFFFFFFFFull), nB = (uint32_t)(h1 >> 32);
           const uint64_t A = ptr + 2, Bp = ptr + 2 + nA;
           // occ(m) -> fwd list (+off), occ(rm) -> bwd list (-off)    
-          if ((h0 >> 32) & 1) { nf = nb = nA; s_pf[tid] = A; s_pbk[tid] = A; }
-          else if (canon) { nf = nA; s_pf[tid] = A; nb = nB; s_pbk[tid] = Bp; }
-          else { nf = nB; s_pf[tid] = Bp; nb = nA; s_pbk[tid] = A; }
-          s_pb[tid] = kr.pb_off;
+          uint64_t pf, pbk;
+          if ((h0 >> 32) & 1) { nf = nb = nA; pf = A; pbk = A; }
+          else if (canon) { nf = nA; pf = A; nb = nB; pbk = Bp; }
+          else { nf = nB; pf = Bp; nb = nA; pbk = A; }
+          s_ptr[tid] = make_ulonglong2(pf, pbk - nf);
+          pbv = kr.pb_off;
         }
       }
-      s_nf[tid] = nf;
+      s_np[tid] = make_uint2(nf, (uint32_t)pbv);
       uint32_t total;
       s_off[tid] = block_excl_scan<B>(nf + nb, s_scan, total);
       __syncthreads();
@@ -572,9 +577,11 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
         for (uint32_t stp = B / 2; stp >= 1; stp >>= 1) lo = s_off[lo + stp] <= h ? lo + stp : lo;
         rec = lo;
         const uint32_t local = h - s_off[lo];
-        fwd = local < s_nf[lo];
-        pb = s_pb[lo];
-        return fwd ? s_pf[lo] + local : s_pbk[lo] + (local - s_nf[lo]);
+        const uint2 np = s_np[lo];
+        const ulonglong2 pp = s_ptr[lo];
+        fwd = local < np.x;
+        pb = (int32_t)np.y;
+        return (fwd ? pp.x : pp.y) + local;
       };
       // GROUP_PF steps of occurrence loads in flight per thread (a ring of
       // statically indexed registers): the enumeration is latency-bound otherwise
