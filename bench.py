@@ -119,6 +119,11 @@ def main():
     from pacbio_amd import pbgpu
     from tools.synth import Dataset, PRESETS
 
+    # more ranks than visible GPUs (a rehearsal of the N>1 launch on a 1-GPU box): ranks share
+    ndev = pbgpu.lib().pbgpu_device_count()
+    if ndev > 0:
+        local %= ndev
+
     # B_rand: random 64-B sector gathers over a 64 GB buffer, this GPU, this run
     b_rand = pbgpu.measure_gather(local, 64 << 30) if not args.no_brand else None
 
