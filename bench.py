@@ -9,7 +9,10 @@ flags `-m 17 --psa-min 13 -l ul.txt -k 31 -f -B 15 --max-count 5000
 the rank's 50k resident reads: k-mer seeding + hash lookups + 99% threshold ->
 per-(read, super-read) grouping -> order-exact LIS + least squares + filters
 -> coords records sorted per read, left in HBM.  Index build is outside the
-timed region (reported separately).
+timed region (reported separately).  The rank's batch is spread over
+`--streams` aligners (pbgpu.StreamAligner: own HIP stream and host thread
+each, one shared index), so one stream's host waits and kernel tails are
+filled by the other's work; stage and kernel times are summed over streams.
 
 Multi-GPU: one process per GPU (torchrun); every rank builds its own replica
 of the index and aligns its own 50k-read shard (weak scaling, no collective on
@@ -111,6 +114,8 @@ def main():
     ap.add_argument("--no-brand", action="store_true", help="skip the B_rand gather microbenchmark")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="aligners (HIP stream + host thread each) the rank's batch is spread over")
     ap.add_argument("--hit-budget", type=float, default=0, help="hits per sub-batch (0 = the library default)")
     args = ap.parse_args()
 
@@ -138,8 +143,9 @@ def main():
     index = pbgpu.Index.from_records(names, seqs, k, psa_min=13, device=local)
     t_index = time.time() - t0
     info = index.info()
-    al = pbgpu.Aligner(index, k=k, forward=True, unitigs_k=31, unitig_lengths=ds.unitig_lengths,
-                       bases_matching=15.0, max_count=5000, stretch_cap=10000.0)
+    al = pbgpu.StreamAligner(index, streams=args.streams, k=k, forward=True, unitigs_k=31,
+                             unitig_lengths=ds.unitig_lengths, bases_matching=15.0, max_count=5000,
+                             stretch_cap=10000.0)
     if args.hit_budget:
         al.set_hit_budget(int(args.hit_budget))
     blob, off = ds.pb_blob()
@@ -229,6 +235,7 @@ def main():
                 "reads_per_gpu": len(off) - 1,
                 "bases_per_gpu": bases_rank,
                 "parallelism": f"read-sharded x{world}, index replicated per GPU",
+                "streams_per_gpu": args.streams,
                 "index": {"n_sr": info["n_sr"], "text_len": info["text_len"], "n_kmers": info["n_kmers"],
                           "device_bytes": info["device_bytes"], "build_s": round(t_index, 3),
                           "generate_s": round(t_gen, 3)},
@@ -243,11 +250,17 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dom, "rocprof_kernel": ROCPROF_FILE[dom], "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "alg_bytes_per_launch": kb[dom], "avg_launch_ms": avg_ms,
+                         # the S aligners' launches of this kernel run concurrently (the rocprofv3 trace
+                         # shows the per-step union of the S launches ~= one launch's duration): the
+                         # device-level rate is S launches' bytes in one launch's time
+                         "concurrent_launches": args.streams,
+                         "achieved_concurrent": achieved * args.streams,
+                         "frac_concurrent": achieved * args.streams / HBM_PEAK_GBS,
                          "b_rand_gbs": b_rand, "frac_of_b_rand": (achieved / b_rand) if b_rand else None},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    reads.close()
+    al.free(reads)
     al.close()
     index.close()
 
