@@ -15,6 +15,8 @@
 #include <cstring>
 #include <fstream>
 #include <string>
+#include <condition_variable>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -146,7 +148,8 @@ int main(int argc, char** argv) {
   std::vector<const char*> srs, pbs;
   int device = 0;
   uint64_t batch_bases = 256ull << 20;
-  enum { O_PSA = 256, O_SC, O_SF, O_CAP, O_WIN, O_DETAILS, O_COORDS, O_MAXM, O_MAXC, O_COMPACT, O_NOCOMPACT, O_DEV, O_BATCH };
+  uint32_t streams = 2;
+  enum { O_PSA = 256, O_SC, O_SF, O_CAP, O_WIN, O_DETAILS, O_COORDS, O_MAXM, O_MAXC, O_COMPACT, O_NOCOMPACT, O_DEV, O_BATCH, O_STREAMS };
   static struct option lo[] = {
       {"size", 1, 0, 's'}, {"mer", 1, 0, 'm'}, {"fine-mer", 1, 0, 'F'}, {"psa-min", 1, 0, O_PSA},
       {"threads", 1, 0, 't'}, {"stretch-constant", 1, 0, O_SC}, {"stretch-factor", 1, 0, O_SF},
@@ -156,7 +159,8 @@ int main(int argc, char** argv) {
       {"zero-match", 0, 0, '0'}, {"max-count", 1, 0, O_MAXC}, {"unitigs-lengths", 1, 0, 'l'},
       {"unitigs-sequences", 1, 0, 'u'}, {"compact", 0, 0, O_COMPACT}, {"no-compact", 0, 0, O_NOCOMPACT},
       {"k-mer", 1, 0, 'k'}, {"superreads", 1, 0, 'r'}, {"pacbio", 1, 0, 'p'},
-      {"device", 1, 0, O_DEV}, {"batch-bases", 1, 0, O_BATCH}, {0, 0, 0, 0}};
+      {"device", 1, 0, O_DEV}, {"batch-bases", 1, 0, O_BATCH},
+      {"streams", 1, 0, O_STREAMS}, {0, 0, 0, 0}};
   int c;
   while ((c = getopt_long(argc, argv, "s:m:F:t:fB:M:H0l:u:k:r:p:", lo, nullptr)) != -1) {
     switch (c) {
@@ -187,6 +191,7 @@ int main(int argc, char** argv) {
     case 'p': pbs.push_back(optarg); break;
     case O_DEV: device = (int)parse_u32(optarg, "--device"); break;
     case O_BATCH: batch_bases = parse_suffix(optarg); break;
+    case O_STREAMS: streams = std::max(1u, parse_u32(optarg, "--streams")); break;
     default: die("bad option (see jf_aligner_cmdline.yaggo)");
     }
   }
@@ -214,54 +219,78 @@ int main(int argc, char** argv) {
   pbgpu_index_params ip{ap.k, psa_min, device, (int)threads, ap.fine_k};
   pbgpu_index* ix = nullptr;
   check(pbgpu_index_build_fasta(srs.data(), srs.size(), &ip, &ix), "index");
-  pbgpu_aligner* al = nullptr;
-  check(pbgpu_aligner_create(ix, &ap, &al), "aligner");
-  if (dout) check(pbgpu_aligner_set_details(al, 1), "details");
-
   if (!no_header) {
     fputs("Rstart Rend Qstart Qend Nmers Rcons Qcons Rcover Qcover Rlen Qlen Stretch Offset Err", out);
     if (!compact) fputs(" Rname", out);
     fputs(" Qname\n", out);
   }
+  // Batches are pipelined over `streams` aligners (own HIP stream and buffers
+  // each, one shared index), one host thread per aligner: while one batch is
+  // on the GPU the next is read and the previous formatted.  A worker takes
+  // the next batch under the reader lock, aligns and formats it, then waits
+  // for its turn so the files come out in input order.
   read_stream rs;
   rs.files = pbs;
-  std::string h, s;
+  std::mutex rd_mu, wr_mu;
+  std::condition_variable wr_cv;
   bool more = true;
-  while (more) {
-    std::vector<std::string> headers;
-    std::string seq;
-    std::vector<uint64_t> offs{0};
-    while (seq.size() < batch_bases && (more = rs.next(h, s))) {
-      headers.push_back(h);
-      seq += s;
-      offs.push_back(seq.size());
-    }
-    if (headers.empty()) break;
-    pbgpu_read_batch b{headers.size(), seq.data(), offs.data()};
-    pbgpu_coords_batch* cb = nullptr;
-    check(pbgpu_align_batch(al, &b, &cb), "align");
-    std::vector<const char*> hp(headers.size());
-    std::vector<uint64_t> lens(headers.size());
-    for (size_t i = 0; i < headers.size(); ++i) { hp[i] = headers[i].c_str(); lens[i] = offs[i + 1] - offs[i]; }
-    char* text = nullptr;
-    uint64_t tl = 0;
-    check(pbgpu_format_coords(ix, cb, hp.data(), lens.data(), compact ? 1 : 0, 0, zero ? 1 : 0,
-                              (int)std::max(1u, threads), &text, &tl), "format");
-    fwrite(text, 1, tl, out);
-    pbgpu_free_text(text);
-    pbgpu_coords_free(cb);
-    if (dout) {
-      pbgpu_details_batch* db = nullptr;
-      check(pbgpu_download_details(al, &db), "details");
-      check(pbgpu_format_details(ix, db, hp.data(), (int)std::max(1u, threads), &text, &tl), "format details");
-      fwrite(text, 1, tl, dout);
+  uint64_t next_batch = 0, next_write = 0;
+  auto worker = [&]() {
+    pbgpu_aligner* al = nullptr;
+    check(pbgpu_aligner_create(ix, &ap, &al), "aligner");
+    if (dout) check(pbgpu_aligner_set_details(al, 1), "details");
+    std::string h, s;
+    for (;;) {
+      std::vector<std::string> headers;
+      std::string seq;
+      std::vector<uint64_t> offs{0};
+      uint64_t me;
+      {
+        std::lock_guard<std::mutex> lk(rd_mu);
+        while (seq.size() < batch_bases && more && (more = rs.next(h, s))) {
+          headers.push_back(h);
+          seq += s;
+          offs.push_back(seq.size());
+        }
+        if (headers.empty()) break;
+        me = next_batch++;
+      }
+      pbgpu_read_batch b{headers.size(), seq.data(), offs.data()};
+      pbgpu_coords_batch* cb = nullptr;
+      check(pbgpu_align_batch(al, &b, &cb), "align");
+      std::vector<const char*> hp(headers.size());
+      std::vector<uint64_t> lens(headers.size());
+      for (size_t i = 0; i < headers.size(); ++i) { hp[i] = headers[i].c_str(); lens[i] = offs[i + 1] - offs[i]; }
+      char* text = nullptr;
+      uint64_t tl = 0;
+      check(pbgpu_format_coords(ix, cb, hp.data(), lens.data(), compact ? 1 : 0, 0, zero ? 1 : 0,
+                                (int)std::max(1u, threads), &text, &tl), "format");
+      pbgpu_coords_free(cb);
+      char* dtext = nullptr;
+      uint64_t dtl = 0;
+      if (dout) {
+        pbgpu_details_batch* db = nullptr;
+        check(pbgpu_download_details(al, &db), "details");
+        check(pbgpu_format_details(ix, db, hp.data(), (int)std::max(1u, threads), &dtext, &dtl), "format details");
+        pbgpu_details_free(db);
+      }
+      std::unique_lock<std::mutex> lk(wr_mu);
+      wr_cv.wait(lk, [&] { return next_write == me; });
+      fwrite(text, 1, tl, out);
+      if (dout) fwrite(dtext, 1, dtl, dout);
+      ++next_write;
+      lk.unlock();
+      wr_cv.notify_all();
       pbgpu_free_text(text);
-      pbgpu_details_free(db);
+      if (dtext) pbgpu_free_text(dtext);
     }
-  }
+    pbgpu_aligner_free(al);
+  };
+  std::vector<std::thread> pool;
+  for (uint32_t i = 0; i < streams; ++i) pool.emplace_back(worker);
+  for (auto& t : pool) t.join();
   if (coords_path) fclose(out);
   if (dout) fclose(dout);
-  pbgpu_aligner_free(al);
   pbgpu_index_free(ix);
   return 0;
 }

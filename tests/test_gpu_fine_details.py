@@ -114,3 +114,13 @@ def test_gpu_fine_parity(small, name):
     assert exp.count("\n") > 10
     assert st["n_fine_windows"] > 0 and st["n_fine_hits"] > 0
     assert_same_coords(got, exp, name)
+
+
+@pytest.mark.parametrize("streams", ["1", "3"])
+def test_gpu_cli_stream_pipeline_in_order(streams):
+    """Batches pipelined over several aligners (--streams) come out in input
+    order: many small batches give the same coords and details files as one."""
+    one, d_one = _cli(CLI, *FWD, details=True)
+    many, d_many = _cli(CLI, *FWD, "--batch-bases", "2k", "--streams", streams, details=True)
+    assert many == one
+    assert sorted(d_many.splitlines()) == sorted(d_one.splitlines())
