@@ -399,6 +399,18 @@ class Aligner:
             pass
 
 
+def stream_cuts(offsets, S):
+    """Read-range boundaries [c0=0, c1, ..., cS=n] cutting a batch into S contiguous
+    ranges of about equal bases (non-decreasing; an empty range gets no aligner)."""
+    off = np.asarray(offsets, dtype=np.uint64)
+    n = len(off) - 1
+    cuts = [0] + [int(np.searchsorted(off, off[-1] * np.uint64(i) // np.uint64(S), side="left"))
+                  for i in range(1, S)] + [n]
+    for i in range(1, len(cuts)):
+        cuts[i] = min(max(cuts[i], cuts[i - 1]), n)
+    return cuts
+
+
 class StreamAligner:
     """One batch spread over S aligners (own HIP stream and buffers each) that
     share one index, each driven by its own host thread.  A single aligner
@@ -422,12 +434,10 @@ class StreamAligner:
         off = np.ascontiguousarray(offsets, dtype=np.uint64)
         n = len(off) - 1
         S = len(self.aligners)
-        # cut points at about equal bases; empty ranges get no aligner
-        cuts = [0] + [int(np.searchsorted(off, off[-1] * i // S, side="left")) for i in range(1, S)] + [n]
+        cuts = stream_cuts(off, S)
         raw = memoryview(blob if isinstance(blob, (bytes, bytearray)) else bytes(blob))
         parts = []
         for j, (lo, hi) in enumerate(zip(cuts[:-1], cuts[1:])):
-            hi = max(hi, lo)
             if hi > lo:
                 sub_off = off[lo:hi + 1] - off[lo]
                 parts.append((j, lo, hi, self.aligners[j].upload(blob=bytes(raw[int(off[lo]):int(off[hi])]),
