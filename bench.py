@@ -1,28 +1,34 @@
 #!/usr/bin/env python3
-"""bench.py -- PacBio bases aligned/s of the MI355X jf_aligner path.
+"""bench.py -- PacBio bases aligned/s of the MI355X jf_aligner path, coords out.
 
 Workload (BASELINE.json configs[1], the largest single-GPU config): E. coli
 scale, 50k synthetic PacBio CLR reads (lognormal, mean 12 kb, 13% errors) per
 GPU against 200k synthetic super-reads (~250 Mbp), k=17, with the production
 flags `-m 17 --psa-min 13 -l ul.txt -k 31 -f -B 15 --max-count 5000
---stretch-cap 10000`.  One step = the whole GPU hot path over
-the rank's 50k resident reads: k-mer seeding + hash lookups + 99% threshold ->
-per-(read, super-read) grouping -> order-exact LIS + least squares + filters
--> coords records sorted per read, left in HBM.  Index build is outside the
-timed region (reported separately).  The rank's batch is spread over
-`--streams` aligners (pbgpu.StreamAligner: own HIP stream and host thread
-each, one shared index), so one stream's host waits and kernel tails are
-filled by the other's work; stage and kernel times are summed over streams.
+--stretch-cap 10000`.
 
-Multi-GPU: one process per GPU (torchrun); every rank builds its own replica
-of the index and aligns its own 50k-read shard (weak scaling, no collective on
-the data path).  Timing: barrier + device sync on both sides of exactly
-`--steps` steps, max over ranks.
+`value` is the metric as SURVEY 8(d) defines it: one step = one pass of
+pbgpu_run (the jf_aligner CLI's driver) over the rank's PacBio FASTA -- parse,
+upload, the whole device path, device-side coords formatting, D2H into
+pinned memory, write() of the coords file -- timed from the first batch read
+to the closed coords file.  The index is built once before the timed region
+(reported as config.index.build_s).
+
+`value_device` keeps round 1's device-only figure: the same reads resident
+in HBM, the device path from seeding to per-read sorted records in HBM, no
+formatting or output.  The `roofline` object is for its dominant kernel.
+
+Multi-GPU: one process per GPU (torchrun); every rank builds its own index
+replica and aligns its own 50k-read shard into its own coords file (weak
+scaling, no collective on the data path).  Timing: barrier + device sync on
+both sides of exactly `--steps` steps, max over ranks.
 """
 import argparse
 import json
 import os
+import shutil
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -39,8 +45,8 @@ def _dist():
 
 
 class Comm:
-    """Barrier + max-reduction over ranks.  gloo on the host: the path itself
-    has no exchange step (read sharding), so no RCCL traffic is needed."""
+    """Barrier + max/sum over ranks.  gloo on the host: the path itself has no
+    exchange step (read sharding), so no RCCL traffic is needed."""
 
     def __init__(self, world):
         self.world = world
@@ -53,21 +59,19 @@ class Comm:
         if self.world > 1:
             self.dist.barrier()
 
-    def max(self, x):
+    def _red(self, x, op):
         if self.world == 1:
             return x
         import torch
         t = torch.tensor([float(x)], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        self.dist.all_reduce(t, op=op)
         return float(t.item())
 
+    def max(self, x):
+        return self._red(x, self.dist.ReduceOp.MAX if self.world > 1 else None)
+
     def sum(self, x):
-        if self.world == 1:
-            return x
-        import torch
-        t = torch.tensor([float(x)], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
-        return float(t.item())
+        return self._red(x, self.dist.ReduceOp.SUM if self.world > 1 else None)
 
 
 # the rocprofv3 kernel each timed slot corresponds to (tools/pmc_summary.py file names)
@@ -77,8 +81,8 @@ ROCPROF_FILE = {"k_seed": "k_seed_256_8_0", "k_group": "k_group_false_256u", "k_
 
 def _kernel_bytes(st):
     """Algorithmic HBM bytes per launch of each individually timed kernel
-    (DESIGN.md "Roofline"): every byte the algorithm must move at least once,
-    from the kernels' own counters, divided by that kernel's launch count."""
+    (DESIGN.md s.3): every byte the algorithm must move at least once, from the
+    kernels' own counters, divided by that kernel's launch count."""
     kn = st["kernel_launches"]
     per = lambda v, k: v / max(1, kn[k])
     return {
@@ -93,13 +97,38 @@ def _kernel_bytes(st):
         # and its lis point written (<= 8 B); per strand its item, chain descriptor (24 B),
         # length and lis length (12 B)
         "k_lis": per(st["l0_hits"] * 16 + st["l0_strands"] * 36, "k_lis"),
-        # counted by the kernel: per chain its list entry (4 B), descriptor (24 B), both lis
-        # lengths (8 B), super-read length + unitig range (16 B) and read range (16 B); every lis
-        # point (8 B) read once; every record (96 B) written (kmers_info pairs not counted)
+        # per chain its list entry (4 B), descriptor (24 B), both lis lengths (8 B), super-read
+        # length + unitig range (16 B) and read range (16 B); every lis point (8 B) read once;
+        # every record (96 B) written (kmers_info pairs not counted)
         "k_coords": per(st["fit_chains"] * 68 + st["fit_points"] * 8 + st["n_records"] * 96, "k_coords"),
         # records read + written
         "k_rec_sort": per(st["n_records"] * 96 * 2, "k_rec_sort"),
     }
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _cpu_share():
+    """This job's CPU share of the box.  On the GPU box os.cpu_count() and the
+    affinity mask show the whole 256-thread machine, but a one-GPU job's share is
+    16 (OMP_NUM_THREADS / MAX_JOBS are set to it there, and `nproc` honours it)."""
+    for var in ("OMP_NUM_THREADS", "MAX_JOBS"):
+        v = os.environ.get(var, "")
+        if v.isdigit() and int(v) > 0:
+            return int(v)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
 
 
 def main():
@@ -112,11 +141,13 @@ def main():
     ap.add_argument("--cpu-sample-reads", type=int, default=0, help="CPU baseline sample (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-brand", action="store_true", help="skip the B_rand gather microbenchmark")
-    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this process's CPU share")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
-    ap.add_argument("--streams", type=int, default=2,
-                    help="aligners (HIP stream + host thread each) the rank's batch is spread over")
-    ap.add_argument("--hit-budget", type=float, default=0, help="hits per sub-batch (0 = the library default)")
+    ap.add_argument("--streams", type=int, default=2, help="aligners (HIP stream + host thread each) per GPU")
+    ap.add_argument("--batch-bases", type=float, default=64e6, help="pbgpu_run batch size in bases")
+    ap.add_argument("--device-steps", type=int, default=3, help="steps of the device-only leg (value_device)")
+    ap.add_argument("--workdir", default=os.environ.get("PBGPU_BENCH_DIR", "/tmp"),
+                    help="where the input FASTA and the coords output are written")
     args = ap.parse_args()
 
     rank, world, local = _dist()
@@ -134,44 +165,81 @@ def main():
 
     k = 21 if args.workload == "C3" else 17
     n_pb = args.reads or PRESETS[args.workload]["n_pb"]
-    threads = min(16, os.cpu_count() or 1)
+    threads = _cpu_share()
     t0 = time.time()
-    ds = Dataset(args.workload, seed=42, threads=threads, n_pb=n_pb, pb_index_base=rank * n_pb)
+    ds = Dataset(args.workload, seed=42, threads=min(threads, 16), n_pb=n_pb, pb_index_base=rank * n_pb)
+    wd = tempfile.mkdtemp(prefix=f"pbgpu_bench_r{rank}_", dir=args.workdir)
+    ds.write(wd)
     t_gen = time.time() - t0
-    names, seqs = ds.sr_names(), ds.sr_seqs()
+    sr_fa, pb_fa, ul_txt = (os.path.join(wd, f) for f in ("sr.fa", "pb.fa", "ul.txt"))
     t0 = time.time()
-    index = pbgpu.Index.from_records(names, seqs, k, psa_min=13, device=local)
+    index = pbgpu.Index.from_fasta([sr_fa], k, psa_min=13, device=local)
     t_index = time.time() - t0
     info = index.info()
-    al = pbgpu.StreamAligner(index, streams=args.streams, k=k, forward=True, unitigs_k=31,
-                             unitig_lengths=ds.unitig_lengths, bases_matching=15.0, max_count=5000,
-                             stretch_cap=10000.0)
-    if args.hit_budget:
-        al.set_hit_budget(int(args.hit_budget))
+    akw = dict(k=k, forward=True, unitigs_k=31, unitig_lengths=ds.unitig_lengths, bases_matching=15.0,
+               max_count=5000, stretch_cap=10000.0)
     blob, off = ds.pb_blob()
-    reads = al.upload(blob=blob, offsets=off)
     bases_rank = int(off[-1])
 
-    for _ in range(args.warmup):
-        al.align_resident(reads)
+    # ---- device-only leg (value_device): reads resident in HBM, records left in HBM
+    al = pbgpu.StreamAligner(index, streams=args.streams, **akw)
+    reads = al.upload(blob=blob, offsets=off)
+    al.align_resident(reads)
     al.reset_stats()
     pbgpu.device_synchronize(local)
     comm.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
+    td = time.perf_counter()
+    for _ in range(args.device_steps):
         al.align_resident(reads)
     pbgpu.device_synchronize(local)
     comm.barrier()
-    elapsed = comm.max(time.perf_counter() - t0)
+    el_dev = comm.max(time.perf_counter() - td)
     st = al.stats()
+    al.free(reads)
+    al.close()
+
+    # ---- end to end (value): PacBio FASTA -> coords file, pbgpu_run
+    # (a pbgpu_runner keeps its aligners and pinned buffers across steps: a service
+    # aligning file after file; the CLI's single run pays their setup once).  Every
+    # step writes a new coords file, as the CLI does; the previous step's file is
+    # removed by a background thread while the next step runs (unlinking 4 GB of
+    # page cache is not part of the path, and truncating it in place would be).
+    import threading
+    runner = pbgpu.Runner([index], aligners_per_device=args.streams, batch_bases=int(args.batch_bases), **akw)
+    outs = [os.path.join(wd, f"out{i}.coords") for i in range(args.warmup + args.steps)]
+    cleaners = []
+
+    def _step(i):
+        st_ = runner.run([pb_fa], outs[i])
+        if i > 0:
+            th = threading.Thread(target=os.unlink, args=(outs[i - 1],))
+            th.start()
+            cleaners.append(th)
+        return st_
+    for i in range(args.warmup):
+        _step(i)
+    for th in cleaners:
+        th.join()
+    pbgpu.device_synchronize(local)
+    comm.barrier()
+    t0 = time.perf_counter()
+    rstats = []
+    for i in range(args.warmup, args.warmup + args.steps):
+        rstats.append(_step(i))
+    pbgpu.device_synchronize(local)
+    comm.barrier()
+    elapsed = comm.max(time.perf_counter() - t0)
+    for th in cleaners:
+        th.join()
+    coords_bytes = rstats[-1]["coords_bytes"]
+    runner.close()
 
     total_bases = comm.sum(bases_rank) * args.steps
     value = total_bases / elapsed
-    stage_ms = {"seed": st["ms_seed"], "group": st["ms_group"], "lis": st["ms_lis"], "fit": st["ms_fit"],
-                "records": st["ms_records"]}
+    value_device = comm.sum(bases_rank) * args.device_steps / el_dev
     kb = _kernel_bytes(st)
     kms, kn = st["kernel_ms"], st["kernel_launches"]
-    dom = max(kb, key=lambda k: kms[k])
+    dom = max(kb, key=lambda kk: kms[kk])
     avg_ms = kms[dom] / max(1, kn[dom])
     achieved = kb[dom] / (avg_ms * 1e-3) / 1e9
     traffic = None
@@ -186,34 +254,53 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle.oracle import OracleIndex, params
+        from tests._compare import split_reads
         cthreads = args.cpu_threads or threads
-        oix = OracleIndex.from_records(names, seqs, k, threads=cthreads)
-        p = params(k=k, forward=True, unitigs_k=31, unitig_lengths=ds.unitig_lengths, bases_matching=15.0,
-                   max_count=5000, stretch_cap=10000.0)
-        allp = ds.pb_seqs()
+        oix = OracleIndex.from_fasta([sr_fa], k, threads=cthreads)
+        p = params(**akw)
+        allp, alln = ds.pb_seqs(), ds.pb_names()
         if args.cpu_sample_reads:
             nsamp = min(len(allp), args.cpu_sample_reads)
         else:
-            # bounded sample: a pilot sizes it to about --cpu-seconds of oracle work
-            pilot = allp[:max(1, min(len(allp), 4 * cthreads))]
-            psec, _ = oix.align_timed(p, pilot, threads=cthreads)
-            rate = sum(len(x) for x in pilot) / max(psec, 1e-6)
+            # bounded sample: a pilot sizes it to about --cpu-seconds of oracle work (align + format)
+            npil = max(1, min(len(allp), 4 * cthreads))
+            tp = time.perf_counter()
+            oix.align_format(p, alln[:npil], allp[:npil], threads=cthreads)
+            psec = time.perf_counter() - tp
+            rate = sum(len(x) for x in allp[:npil]) / max(psec, 1e-6)
             want = rate * args.cpu_seconds
             nsamp, acc = 0, 0
             while nsamp < len(allp) and acc < want:
                 acc += len(allp[nsamp])
                 nsamp += 1
-            nsamp = max(nsamp, len(pilot))
-        pseqs = allp[:nsamp]
-        sec, nrec = oix.align_timed(p, pseqs, threads=cthreads)
+            nsamp = max(nsamp, npil)
+        pseqs, pnames = allp[:nsamp], alln[:nsamp]
+        tc = time.perf_counter()
+        exp = oix.align_format(p, pnames, pseqs, threads=cthreads)
+        sec = time.perf_counter() - tc
         sbases = sum(len(x) for x in pseqs)
-        cpu = {"value": sbases / sec, "unit": "bases/s", "cores": cthreads, "kind": "port",
-               "sample": f"first {nsamp} reads of the rank-0 shard ({sbases} bases, {nrec} records) against the full "
-                         f"{args.workload} index; oracle/ C restatement (bit-identical output), {cthreads} threads, "
-                         f"{sec:.2f} s"}
         oix.close()
+        # the same sample through the GPU path (device formatting): parity of the baseline's output
+        g = pbgpu.Aligner(index, **akw)
+        rr = g.upload(pseqs, names=pnames)
+        g.align_resident(rr)
+        got = g.format_device(rr)
+        rr.close()
+        g.close()
+        og, rg = split_reads(got)
+        oe, re_ = split_reads(exp)
+        mism = sum(1 for h in set(og) | set(oe) if sorted(rg.get(h, [])) != sorted(re_.get(h, [])))
+        cpu = {"value": sbases / sec, "unit": "bases/s", "cores": cthreads, "kind": "port",
+               "cpu_model": _cpu_model(),
+               "sample": f"first {nsamp} reads of the rank-0 shard ({sbases} bases, {exp.count(chr(10))} text lines) "
+                         f"against the full {args.workload} index; oracle/ C restatement, align + coords text "
+                         f"formatting, {cthreads} threads (the job's CPU share of the box), {sec:.2f} s",
+               "gpu_parity_reads_checked": len(oe), "gpu_parity_reads_differing": mism}
 
     if rank == 0:
+        stage = {n: round(sum(r[n] for r in rstats) / args.steps * 1e3, 3) for n in
+                 ("read_seconds", "upload_seconds", "align_seconds", "format_seconds", "d2h_seconds",
+                  "write_seconds", "writer_idle_seconds", "open_seconds", "close_seconds", "wall_seconds")}
         out = {
             "metric": "PacBio bases aligned/sec (coords out)",
             "value": value,
@@ -226,43 +313,47 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int32",
-            "data": "synthetic (tools/pbsynth.cc, seed 42; SURVEY.md §8d generator)",
+            "data": "synthetic (tools/pbsynth.cc, seed 42; SURVEY.md §8d generator), written as FASTA",
+            "value_device": value_device,
+            "value_device_note": "reads resident in HBM, device path to sorted records in HBM, no formatting / "
+                                 "output (round-1 definition)",
             "config": {
                 "workload": {"C1": "C1: 100 PB x 10 kb vs 1k SRs, k=17",
                              "C2": "C2 E. coli-scale: 50k PB (lognormal mean 12 kb, CLR 13%) per GPU vs 200k SRs, k=17",
                              "C3": "C3 yeast-scale: PB (mean 12 kb) vs 1M SRs, k=21"}[args.workload],
                 "flags": f"-m {k} --psa-min 13 -l ul.txt -k 31 -f -B 15 --max-count 5000 --stretch-cap 10000",
+                "step": "pbgpu_run: pb.fa -> coords file (parse, upload, align, device format, D2H, write)",
                 "reads_per_gpu": len(off) - 1,
                 "bases_per_gpu": bases_rank,
+                "coords_bytes_per_step": coords_bytes,
+                "records_per_step": rstats[-1]["n_records"],
+                "batches_per_step": rstats[-1]["n_batches"],
+                "batch_bases": int(args.batch_bases),
                 "parallelism": f"read-sharded x{world}, index replicated per GPU",
                 "streams_per_gpu": args.streams,
                 "index": {"n_sr": info["n_sr"], "text_len": info["text_len"], "n_kmers": info["n_kmers"],
                           "device_bytes": info["device_bytes"], "build_s": round(t_index, 3),
-                          "generate_s": round(t_gen, 3)},
-                "stage_ms_per_step": {s: round(v / args.steps, 3) for s, v in stage_ms.items()},
-                "kernel_ms_per_launch": {k: round(kms[k] / max(1, kn[k]), 3) for k in kms},
-                "kernel_launches": dict(kn),
-                "counters_per_step": {n: st[n] // args.steps for n in
-                                      ("n_kmers", "n_probes", "n_kept", "n_hits", "n_chains", "n_lis_tests",
-                                       "n_records")},
+                          "generate_and_write_s": round(t_gen, 3)},
+                "stage_ms_per_step": stage,
+                "device_leg": {"ms_per_step": el_dev / args.device_steps * 1e3,
+                               "stage_ms_per_step": {s: round(st["ms_" + s] / args.device_steps, 3) for s in
+                                                     ("seed", "group", "lis", "fit", "records")},
+                               "kernel_ms_per_launch": {kk: round(kms[kk] / max(1, kn[kk]), 3) for kk in kms},
+                               "kernel_launches": dict(kn),
+                               "counters_per_step": {n: st[n] // args.device_steps for n in
+                                                     ("n_kmers", "n_probes", "n_kept", "n_hits", "n_chains",
+                                                      "n_lis_tests", "n_records")}},
                 "fit_dtype": "f64",
             },
-            "roofline": {"bound": "hbm", "kernel": dom, "rocprof_kernel": ROCPROF_FILE[dom], "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "roofline": {"bound": "hbm", "kernel": dom, "rocprof_kernel": ROCPROF_FILE[dom], "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "alg_bytes_per_launch": kb[dom], "avg_launch_ms": avg_ms,
-                         # the S aligners' launches of this kernel run concurrently (the rocprofv3 trace
-                         # shows the per-step union of the S launches ~= one launch's duration): the
-                         # device-level rate is S launches' bytes in one launch's time
-                         "concurrent_launches": args.streams,
-                         "achieved_concurrent": achieved * args.streams,
-                         "frac_concurrent": achieved * args.streams / HBM_PEAK_GBS,
                          "b_rand_gbs": b_rand, "frac_of_b_rand": (achieved / b_rand) if b_rand else None},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    al.free(reads)
-    al.close()
     index.close()
+    shutil.rmtree(wd, ignore_errors=True)
 
 
 if __name__ == "__main__":

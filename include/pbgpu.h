@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PBGPU_ABI_VERSION 2
+#define PBGPU_ABI_VERSION 3
 
 typedef enum pbgpu_status {
   PBGPU_OK = 0,
@@ -142,6 +142,11 @@ typedef struct {
   uint64_t    n_reads;
   const char* seq;            /* concatenated ASCII bases (any bytes; non-ACGT reset k-mers) */
   const uint64_t* offsets;    /* n_reads + 1 offsets into seq */
+  /* optional (NULL = none): read names -- the header up to its first
+     whitespace (jf_aligner.cc:133-134) -- concatenated, for the device coords
+     text (pbgpu_format_device) */
+  const char* names;
+  const uint64_t* name_offsets; /* n_reads + 1 offsets into names */
 } pbgpu_read_batch;
 
 /* ---------------------------------------------------------------- records
@@ -305,6 +310,76 @@ pbgpu_status pbgpu_format_details(const pbgpu_index* ix, const pbgpu_details_bat
                                   const char* const* read_headers, int threads,
                                   char** text, uint64_t* len);
 void         pbgpu_free_text(char* text);
+
+/* print_coords on the device: the last alignment's records (reads uploaded
+ * with names) as the coords text -- byte-identical to pbgpu_format_coords
+ * with header = 0 -- into a device buffer owned by the aligner; *text_len =
+ * its length.  pbgpu_text_download copies its first len bytes to dst (pinned
+ * host memory from pbgpu_host_alloc is copied at full PCIe rate). */
+pbgpu_status pbgpu_format_device(pbgpu_aligner* al, const pbgpu_reads* reads, int compact, int zero_match,
+                                 uint64_t* text_len);
+pbgpu_status pbgpu_text_download(pbgpu_aligner* al, void* dst, uint64_t len);
+pbgpu_status pbgpu_host_alloc(uint64_t bytes, void** out);   /* pinned host memory */
+pbgpu_status pbgpu_host_free(void* p);
+/* Test aid (no reference counterpart): the device formatter's rendering of
+ * one double, run on the host -- std::ostream << v at precision 6, i.e.
+ * printf("%.6g", v).  out needs 32 bytes; returns the length. */
+int          pbgpu_format_double(double v, char* out);
+
+/* A replica of an index on another device (device-to-device copies of the
+ * resident arrays; no rebuild).  SURVEY 8(e): read-sharded multi-GPU runs
+ * keep one replica per GPU. */
+pbgpu_status pbgpu_index_replicate(const pbgpu_index* src, int device, pbgpu_index** out);
+
+/* ---------------------------------------------------------------- driver
+ * The jf_aligner main loop (jf_aligner.cc:205-230, print_alignments :110-159)
+ * as one call: PacBio FASTA / FASTQ files (plain or gzip) are parsed in
+ * batches; every entry of `indexes` gets `aligners_per_device` aligners (own
+ * HIP stream and host thread each; the same index may be listed twice);
+ * batches go to whichever aligner is free (dynamic assignment absorbs read
+ * length skew); each is aligned and formatted on its device, copied to pinned
+ * host memory and written in input order -- the output is the reference's
+ * with -t 1 (per-read records sorted, reads in input order). */
+typedef struct {
+  const char* const* pb_paths;    /* -p, --pacbio (FASTA/FASTQ, plain or gzip) */
+  size_t n_pb_paths;
+  const char* coords_path;        /* --coords; NULL = stdout */
+  const char* details_path;       /* --details; NULL = none */
+  int32_t compact;                /* --compact (default on) */
+  int32_t header;                 /* print_coords_header unless -H */
+  int32_t zero_match;             /* -0 */
+  uint32_t aligners_per_device;   /* 0 = 2 */
+  uint64_t batch_bases;           /* bases per batch; 0 = 64 M */
+  int32_t host_threads;           /* --details formatting threads; 0 = all */
+} pbgpu_run_params;
+
+typedef struct {
+  double   wall_seconds;          /* first batch read -> coords file closed */
+  uint64_t n_batches, n_reads, n_bases, n_records, coords_bytes, details_bytes;
+  /* busy seconds per stage, summed over the threads doing it */
+  double   read_seconds;          /* reader: parse input into batches */
+  double   upload_seconds;        /* workers: host -> device read copies */
+  double   align_seconds;         /* workers: the device pipeline (host wall) */
+  double   format_seconds;        /* workers: device text formatting */
+  double   d2h_seconds;           /* workers: text -> pinned host memory */
+  double   write_seconds;         /* writer: write() calls */
+  double   writer_idle_seconds;   /* writer: waiting for the next batch in order */
+  double   open_seconds;          /* opening (creating / truncating) the output files */
+  double   close_seconds;         /* closing the coords file after the last write */
+} pbgpu_run_stats;
+
+pbgpu_status pbgpu_run(pbgpu_index* const* indexes, size_t n_indexes, const pbgpu_align_params* params,
+                       const pbgpu_run_params* run, pbgpu_run_stats* stats);
+/* The same as a long-lived object (pbgpu_run = create + run + free): the
+ * aligners, their device buffers and the pinned batch / text buffers are kept
+ * between runs, so a service aligning many files pays their setup once.
+ * create uses run->aligners_per_device, batch_bases and whether
+ * details_path is set; every run must agree on details. */
+typedef struct pbgpu_runner pbgpu_runner;
+pbgpu_status pbgpu_runner_create(pbgpu_index* const* indexes, size_t n_indexes, const pbgpu_align_params* params,
+                                 const pbgpu_run_params* run, pbgpu_runner** out);
+pbgpu_status pbgpu_runner_run(pbgpu_runner* runner, const pbgpu_run_params* run, pbgpu_run_stats* stats);
+pbgpu_status pbgpu_runner_free(pbgpu_runner* runner);
 
 #ifdef __cplusplus
 }

@@ -41,8 +41,9 @@ def _newer(out, srcs):
 def build_pbgpu(force=False):
     objdir = os.path.join(ROOT, "build")
     os.makedirs(objdir, exist_ok=True)
-    hdrs = [os.path.join(CSRC, "pbgpu_internal.h"), os.path.join(ROOT, "include", "pbgpu.h")]
-    srcs = ["pbgpu_kernels.hip", "pbgpu_api.hip"]
+    hdrs = [os.path.join(CSRC, h) for h in ("pbgpu_internal.h", "pbgpu_host.h", "pbgpu_fmt.h")] + \
+        [os.path.join(ROOT, "include", "pbgpu.h")]
+    srcs = ["pbgpu_kernels.hip", "pbgpu_api.hip", "pbgpu_format.hip", "pbgpu_run.hip"]
     objs = []
     jobs = []
     for s in srcs:
@@ -56,7 +57,7 @@ def build_pbgpu(force=False):
     lib = os.path.join(PKG, "libpbgpu.so")
     if force or jobs or _newer(lib, objs):
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + objs +
-             ["-Wl,-soname,libpbgpu.so", "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-lpthread"])
+             ["-Wl,-soname,libpbgpu.so", "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-lz", "-lpthread"])
     bindir = os.path.join(PKG, "bin")
     os.makedirs(bindir, exist_ok=True)
     cli = os.path.join(bindir, "jf_aligner")

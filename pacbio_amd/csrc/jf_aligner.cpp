@@ -1,10 +1,16 @@
 // jf_aligner -- drop-in CLI for the reference's jf_aligner
 // (src_jf_aligner/jf_aligner.cc:161-233, options jf_aligner_cmdline.yaggo:1-77)
-// running the coarse aligner on an MI355X through the pbgpu C ABI.
+// running the coarse aligner on MI355X GPUs through the pbgpu C ABI.
 //
-// Same flags, same coords (and --details) text.  Reads are processed in
-// batches; output is written in input order (what the reference prints with
-// -t 1).  -F runs the fine aligner on the device after the coarse one.
+// Same flags, same coords (and --details) text.  The super-read index is
+// built once on the first device and replicated to the others; pbgpu_run
+// then streams the PacBio files (plain or gzip) in batches over
+// --streams aligners per device, formats the coords on the devices and
+// writes them in input order (what the reference prints with -t 1).
+// -F runs the fine aligner on the device after the coarse one.
+// GPU-only options: --devices 0,1,.. (default 0; a device may repeat),
+// --streams (aligners per device), --batch-bases, --timing (stage times on
+// stderr as one JSON line).
 #include <getopt.h>
 
 #include <algorithm>
@@ -15,9 +21,6 @@
 #include <cstring>
 #include <fstream>
 #include <string>
-#include <condition_variable>
-#include <mutex>
-#include <thread>
 #include <vector>
 
 #include "../../include/pbgpu.h"
@@ -85,57 +88,6 @@ static std::vector<int32_t> read_unitigs_sequences(const char* path) {
   return v;
 }
 
-// FASTA/FASTQ streaming reader: header = line after '>'/'@', sequence =
-// concatenated lines (whole_sequence_parser semantics).
-struct read_stream {
-  std::vector<const char*> files;
-  size_t fi = 0;
-  FILE* f = nullptr;
-  char* line = nullptr;
-  size_t cap = 0;
-  bool have_pending = false;
-  std::string pending;
-  ~read_stream() { if (f) fclose(f); free(line); }
-  bool getl(std::string& out) {
-    for (;;) {
-      if (!f) {
-        if (fi >= files.size()) return false;
-        f = fopen(files[fi++], "r");
-        if (!f) die(std::string("Can't open PacBio file '") + files[fi - 1] + "'");
-      }
-      ssize_t l = getline(&line, &cap, f);
-      if (l < 0) { fclose(f); f = nullptr; continue; }
-      if (l > 0 && line[l - 1] == '\n') --l;
-      out.assign(line, (size_t)l);
-      return true;
-    }
-  }
-  // next record; false at end
-  bool next(std::string& header, std::string& seq) {
-    std::string l;
-    if (have_pending) { l.swap(pending); have_pending = false; }
-    else {
-      do { if (!getl(l)) return false; } while (l.empty());
-    }
-    if (l[0] == '@') {
-      header = l.substr(1);
-      seq.clear();
-      getl(seq);
-      std::string plus, qual;
-      getl(plus); getl(qual);
-      return true;
-    }
-    if (l[0] != '>') die("PacBio input is neither FASTA nor FASTQ");
-    header = l.substr(1);
-    seq.clear();
-    while (getl(l)) {
-      if (!l.empty() && l[0] == '>') { pending.swap(l); have_pending = true; break; }
-      seq += l;
-    }
-    return true;
-  }
-};
-
 int main(int argc, char** argv) {
   pbgpu_align_params ap;
   pbgpu_align_params_default(&ap);
@@ -146,10 +98,12 @@ int main(int argc, char** argv) {
   const char* ul_path = nullptr;
   const char* us_path = nullptr;
   std::vector<const char*> srs, pbs;
-  int device = 0;
-  uint64_t batch_bases = 256ull << 20;
+  std::vector<int> devices;
+  uint64_t batch_bases = 64ull << 20;
   uint32_t streams = 2;
-  enum { O_PSA = 256, O_SC, O_SF, O_CAP, O_WIN, O_DETAILS, O_COORDS, O_MAXM, O_MAXC, O_COMPACT, O_NOCOMPACT, O_DEV, O_BATCH, O_STREAMS };
+  bool timing = false;
+  enum { O_PSA = 256, O_SC, O_SF, O_CAP, O_WIN, O_DETAILS, O_COORDS, O_MAXM, O_MAXC, O_COMPACT, O_NOCOMPACT, O_DEV, O_BATCH,
+         O_STREAMS, O_DEVS, O_TIMING };
   static struct option lo[] = {
       {"size", 1, 0, 's'}, {"mer", 1, 0, 'm'}, {"fine-mer", 1, 0, 'F'}, {"psa-min", 1, 0, O_PSA},
       {"threads", 1, 0, 't'}, {"stretch-constant", 1, 0, O_SC}, {"stretch-factor", 1, 0, O_SF},
@@ -159,8 +113,8 @@ int main(int argc, char** argv) {
       {"zero-match", 0, 0, '0'}, {"max-count", 1, 0, O_MAXC}, {"unitigs-lengths", 1, 0, 'l'},
       {"unitigs-sequences", 1, 0, 'u'}, {"compact", 0, 0, O_COMPACT}, {"no-compact", 0, 0, O_NOCOMPACT},
       {"k-mer", 1, 0, 'k'}, {"superreads", 1, 0, 'r'}, {"pacbio", 1, 0, 'p'},
-      {"device", 1, 0, O_DEV}, {"batch-bases", 1, 0, O_BATCH},
-      {"streams", 1, 0, O_STREAMS}, {0, 0, 0, 0}};
+      {"device", 1, 0, O_DEV}, {"devices", 1, 0, O_DEVS}, {"batch-bases", 1, 0, O_BATCH},
+      {"streams", 1, 0, O_STREAMS}, {"timing", 0, 0, O_TIMING}, {0, 0, 0, 0}};
   int c;
   while ((c = getopt_long(argc, argv, "s:m:F:t:fB:M:H0l:u:k:r:p:", lo, nullptr)) != -1) {
     switch (c) {
@@ -189,7 +143,19 @@ int main(int argc, char** argv) {
     case 'k': ap.unitigs_k = parse_u32(optarg, "-k"); k_given = true; break;
     case 'r': srs.push_back(optarg); break;
     case 'p': pbs.push_back(optarg); break;
-    case O_DEV: device = (int)parse_u32(optarg, "--device"); break;
+    case O_DEV: devices.assign(1, (int)parse_u32(optarg, "--device")); break;
+    case O_DEVS: {
+      devices.clear();
+      std::string l = optarg;
+      for (size_t a = 0; a <= l.size();) {
+        size_t e = l.find(',', a);
+        if (e == std::string::npos) e = l.size();
+        devices.push_back((int)parse_u32(l.substr(a, e - a).c_str(), "--devices"));
+        a = e + 1;
+      }
+      break;
+    }
+    case O_TIMING: timing = true; break;
     case O_BATCH: batch_bases = parse_suffix(optarg); break;
     case O_STREAMS: streams = std::max(1u, parse_u32(optarg, "--streams")); break;
     default: die("bad option (see jf_aligner_cmdline.yaggo)");
@@ -211,86 +177,47 @@ int main(int argc, char** argv) {
   } else {
     ap.unitigs_k = 0;
   }
-  FILE* out = coords_path ? fopen(coords_path, "w") : stdout;
-  if (!out) die(std::string("Failed to open coords file '") + coords_path + "'");
-  FILE* dout = details_path ? fopen(details_path, "w") : nullptr;
-  if (details_path && !dout) die(std::string("Failed to open details file '") + details_path + "'");
+  if (devices.empty()) devices.push_back(0);
 
-  pbgpu_index_params ip{ap.k, psa_min, device, (int)threads, ap.fine_k};
-  pbgpu_index* ix = nullptr;
-  check(pbgpu_index_build_fasta(srs.data(), srs.size(), &ip, &ix), "index");
-  if (!no_header) {
-    fputs("Rstart Rend Qstart Qend Nmers Rcons Qcons Rcover Qcover Rlen Qlen Stretch Offset Err", out);
-    if (!compact) fputs(" Rname", out);
-    fputs(" Qname\n", out);
-  }
-  // Batches are pipelined over `streams` aligners (own HIP stream and buffers
-  // each, one shared index), one host thread per aligner: while one batch is
-  // on the GPU the next is read and the previous formatted.  A worker takes
-  // the next batch under the reader lock, aligns and formats it, then waits
-  // for its turn so the files come out in input order.
-  read_stream rs;
-  rs.files = pbs;
-  std::mutex rd_mu, wr_mu;
-  std::condition_variable wr_cv;
-  bool more = true;
-  uint64_t next_batch = 0, next_write = 0;
-  auto worker = [&]() {
-    pbgpu_aligner* al = nullptr;
-    check(pbgpu_aligner_create(ix, &ap, &al), "aligner");
-    if (dout) check(pbgpu_aligner_set_details(al, 1), "details");
-    std::string h, s;
-    for (;;) {
-      std::vector<std::string> headers;
-      std::string seq;
-      std::vector<uint64_t> offs{0};
-      uint64_t me;
-      {
-        std::lock_guard<std::mutex> lk(rd_mu);
-        while (seq.size() < batch_bases && more && (more = rs.next(h, s))) {
-          headers.push_back(h);
-          seq += s;
-          offs.push_back(seq.size());
-        }
-        if (headers.empty()) break;
-        me = next_batch++;
-      }
-      pbgpu_read_batch b{headers.size(), seq.data(), offs.data()};
-      pbgpu_coords_batch* cb = nullptr;
-      check(pbgpu_align_batch(al, &b, &cb), "align");
-      std::vector<const char*> hp(headers.size());
-      std::vector<uint64_t> lens(headers.size());
-      for (size_t i = 0; i < headers.size(); ++i) { hp[i] = headers[i].c_str(); lens[i] = offs[i + 1] - offs[i]; }
-      char* text = nullptr;
-      uint64_t tl = 0;
-      check(pbgpu_format_coords(ix, cb, hp.data(), lens.data(), compact ? 1 : 0, 0, zero ? 1 : 0,
-                                (int)std::max(1u, threads), &text, &tl), "format");
-      pbgpu_coords_free(cb);
-      char* dtext = nullptr;
-      uint64_t dtl = 0;
-      if (dout) {
-        pbgpu_details_batch* db = nullptr;
-        check(pbgpu_download_details(al, &db), "details");
-        check(pbgpu_format_details(ix, db, hp.data(), (int)std::max(1u, threads), &dtext, &dtl), "format details");
-        pbgpu_details_free(db);
-      }
-      std::unique_lock<std::mutex> lk(wr_mu);
-      wr_cv.wait(lk, [&] { return next_write == me; });
-      fwrite(text, 1, tl, out);
-      if (dout) fwrite(dtext, 1, dtl, dout);
-      ++next_write;
-      lk.unlock();
-      wr_cv.notify_all();
-      pbgpu_free_text(text);
-      if (dtext) pbgpu_free_text(dtext);
-    }
-    pbgpu_aligner_free(al);
+  // one index per distinct device: built on the first, replicated to the rest
+  // (jf_aligner.cc:202-203 builds it once and shares it between threads)
+  pbgpu_index_params ip{ap.k, psa_min, devices[0], (int)threads, ap.fine_k, 0, 1};
+  std::vector<std::pair<int, pbgpu_index*>> built;
+  auto index_on = [&](int dev) -> pbgpu_index* {
+    for (auto& b : built) if (b.first == dev) return b.second;
+    pbgpu_index* ix = nullptr;
+    if (built.empty()) check(pbgpu_index_build_fasta(srs.data(), srs.size(), &ip, &ix), "index");
+    else check(pbgpu_index_replicate(built[0].second, dev, &ix), "index replica");
+    built.emplace_back(dev, ix);
+    return ix;
   };
-  std::vector<std::thread> pool;
-  for (uint32_t i = 0; i < streams; ++i) pool.emplace_back(worker);
-  for (auto& t : pool) t.join();
-  if (coords_path) fclose(out);
-  if (dout) fclose(dout);
-  pbgpu_index_free(ix);
+  std::vector<pbgpu_index*> per_entry;
+  for (int d : devices) per_entry.push_back(index_on(d));
+
+  pbgpu_run_params rp{};
+  rp.pb_paths = pbs.data();
+  rp.n_pb_paths = pbs.size();
+  rp.coords_path = coords_path;
+  rp.details_path = details_path;
+  rp.compact = compact ? 1 : 0;
+  rp.header = no_header ? 0 : 1;
+  rp.zero_match = zero ? 1 : 0;
+  rp.aligners_per_device = streams;
+  rp.batch_bases = batch_bases;
+  rp.host_threads = (int)threads;
+  pbgpu_run_stats st{};
+  const pbgpu_status rs = pbgpu_run(per_entry.data(), per_entry.size(), &ap, &rp, &st);
+  const std::string err = rs == PBGPU_OK ? "" : pbgpu_last_error();
+  for (auto& b : built) pbgpu_index_free(b.second);
+  if (rs != PBGPU_OK) die("align: " + err);
+  if (timing)
+    fprintf(stderr,
+            "{\"wall_s\": %.6f, \"batches\": %llu, \"reads\": %llu, \"bases\": %llu, \"records\": %llu, "
+            "\"coords_bytes\": %llu, \"read_s\": %.6f, \"upload_s\": %.6f, \"align_s\": %.6f, \"format_s\": %.6f, "
+            "\"d2h_s\": %.6f, \"write_s\": %.6f, \"writer_idle_s\": %.6f}\n",
+            st.wall_seconds, (unsigned long long)st.n_batches, (unsigned long long)st.n_reads,
+            (unsigned long long)st.n_bases, (unsigned long long)st.n_records, (unsigned long long)st.coords_bytes,
+            st.read_seconds, st.upload_seconds, st.align_seconds, st.format_seconds, st.d2h_seconds, st.write_seconds,
+            st.writer_idle_seconds);
   return 0;
 }

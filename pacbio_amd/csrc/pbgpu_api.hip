@@ -22,6 +22,7 @@
 
 #include "../../include/pbgpu.h"
 #include "pbgpu_internal.h"
+#include "pbgpu_host.h"
 
 namespace pbgpu {
 // kernels (pbgpu_kernels.hip)
@@ -89,80 +90,8 @@ void launch_rec_sort(const Rec* recs, const uint64_t* rec_off, const uint32_t* o
 
 using namespace pbgpu;
 
-// ------------------------------------------------------------ error state
-static thread_local std::string g_err;
-static pbgpu_status fail(pbgpu_status s, const char* fmt, ...) {
-  char buf[1024];
-  va_list ap;
-  va_start(ap, fmt);
-  vsnprintf(buf, sizeof buf, fmt, ap);
-  va_end(ap);
-  g_err = buf;
-  return s;
-}
-struct hip_error : std::runtime_error {
-  hipError_t e;
-  hip_error(hipError_t e_, const char* what) : std::runtime_error(what), e(e_) {}
-};
-#define HIPCHK(x)                                                                                      \
-  do {                                                                                                 \
-    hipError_t _e = (x);                                                                               \
-    if (_e != hipSuccess) {                                                                            \
-      char _b[512];                                                                                    \
-      snprintf(_b, sizeof _b, "%s failed at %s:%d: %s", #x, __FILE__, __LINE__, hipGetErrorString(_e)); \
-      throw hip_error(_e, _b);                                                                         \
-    }                                                                                                  \
-  } while (0)
-struct bad_input : std::runtime_error { using std::runtime_error::runtime_error; };
-struct pbgpu_comm {  // an RCCL communicator of the sharded-index count exchange
-  ncclComm_t comm = nullptr;
-  int device = 0;
-};
-struct unsupported : std::runtime_error { using std::runtime_error::runtime_error; };
-
-#define API_TRY try { (void)hipGetLastError();  /* launch checks below see only this call's errors */
-#define API_CATCH                                                                 \
-  }                                                                               \
-  catch (const hip_error& e) {                                                    \
-    return fail(e.e == hipErrorOutOfMemory ? PBGPU_ERR_NOMEM : PBGPU_ERR_DEVICE, "%s", e.what()); \
-  }                                                                               \
-  catch (const bad_input& e) { return fail(PBGPU_ERR_IO, "%s", e.what()); }       \
-  catch (const unsupported& e) { return fail(PBGPU_ERR_UNSUPPORTED, "%s", e.what()); } \
-  catch (const std::bad_alloc&) { return fail(PBGPU_ERR_NOMEM, "host allocation failed"); } \
-  catch (const std::exception& e) { return fail(PBGPU_ERR_INTERNAL, "%s", e.what()); }
-
-// --------------------------------------------------------- device buffer
-template <typename T>
-struct dbuf {
-  T* p = nullptr;
-  size_t n = 0;
-  dbuf() = default;
-  dbuf(const dbuf&) = delete;
-  dbuf& operator=(const dbuf&) = delete;
-  ~dbuf() { release(); }
-  void release() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
-  void alloc(size_t cnt) { release(); if (cnt) { HIPCHK(hipMalloc((void**)&p, cnt * sizeof(T))); n = cnt; } }
-  void ensure(size_t cnt) { if (cnt > n) alloc(std::max(cnt, n + n / 4)); }
-  // grow keeping the first `keep` elements (stream-ordered copy)
-  void grow_keep(size_t cnt, size_t keep, hipStream_t st) {
-    if (cnt <= n) return;
-    T* q = nullptr;
-    const size_t nn = std::max(cnt, n + n / 2);
-    HIPCHK(hipMalloc((void**)&q, nn * sizeof(T)));
-    if (p && keep) HIPCHK(hipMemcpyAsync(q, p, keep * sizeof(T), hipMemcpyDeviceToDevice, st));
-    HIPCHK(hipStreamSynchronize(st));
-    release();
-    p = q; n = nn;
-  }
-  size_t bytes() const { return n * sizeof(T); }
-  void swap(dbuf& o) { std::swap(p, o.p); std::swap(n, o.n); }
-};
-
-static void* temp_storage(dbuf<uint8_t>& t, size_t bytes) {
-  t.ensure(bytes ? bytes : 1);
-  return t.p;
-}
-
+// error state, dbuf, temp_storage: pbgpu_host.h
+thread_local std::string g_err;
 // ------------------------------------------------------------------ names
 // super_read_name::parse (super_read_name.cc:74-90) -> unitig ids + oris
 static void parse_unitigs(const std::string& name, std::vector<uint32_t>& id, std::vector<uint8_t>& ori) {
@@ -184,49 +113,6 @@ static void parse_unitigs(const std::string& name, std::vector<uint32_t>& id, st
   }
 }
 
-// ------------------------------------------------------------------ index
-struct pbgpu_index {
-  int device = 0;
-  uint32_t k = 0, psa_min = 0;
-  uint64_t n = 0, n_sr = 0, n_kmers = 0, n_occ = 0, buckets = 0;
-  double build_seconds = 0;
-  std::vector<std::string> name_fwd, name_bwd;
-  std::vector<uint64_t> sr_start;            // host copy
-  dbuf<uint64_t> text, d_sr_start, occ;
-  dbuf<ulonglong2> table;
-  dbuf<uint32_t> sr_uoff, sr_uids;
-  // presence filter of the coarse table's k-mers (k_seed), 2^filt_log2 words; none if empty
-  dbuf<uint64_t> filt;
-  uint32_t filt_log2 = 0;
-  // index sharded by super-read range: this shard holds super-reads
-  // [sr_begin, sr_end) (device arrays use local ids) plus a k-1-base seam
-  uint32_t shard = 0, n_shards = 1;
-  uint64_t sr_begin = 0, sr_end = 0, n_total = 0;
-  std::vector<uint64_t> gstart;   // global text offsets of all super-reads (host)
-  uint64_t null_ptr = 0;          // empty occurrence header: k-mers absent from this shard
-  // fine (-F) sub-index: same table / occurrence layout over fine_k-mers
-  uint32_t fk = 0;
-  uint64_t f_buckets = 0, f_kmers = 0, f_occ = 0;
-  dbuf<uint64_t> f_occv;
-  dbuf<ulonglong2> f_table;
-  IndexView view() const {
-    IndexView v;
-    v.text = text.p; v.n = n; v.sr_start = d_sr_start.p; v.n_sr = (uint32_t)(sr_end - sr_begin); v.k = k;
-    v.table = table.p; v.bucket_mask = buckets - 1; v.occ = occ.p; v.sr_uoff = sr_uoff.p; v.sr_uids = sr_uids.p;
-    v.filt = filt.n ? filt.p : nullptr; v.filt_shift = 64 - filt_log2;
-    return v;
-  }
-  IndexView fine_view() const {
-    IndexView v = view();
-    v.k = fk; v.table = f_table.p; v.bucket_mask = f_buckets - 1; v.occ = f_occv.p;
-    v.filt = nullptr;
-    return v;
-  }
-  uint64_t device_bytes() const {
-    return text.bytes() + d_sr_start.bytes() + occ.bytes() + table.bytes() + sr_uoff.bytes() + sr_uids.bytes() +
-           f_occv.bytes() + f_table.bytes() + filt.bytes();
-  }
-};
 
 // host-side text accumulation with compact_dna line encoding
 struct text_builder {
@@ -611,6 +497,39 @@ pbgpu_status pbgpu_index_free(pbgpu_index* ix) {
   return PBGPU_OK;
 }
 
+pbgpu_status pbgpu_index_replicate(const pbgpu_index* src, int device, pbgpu_index** out) {
+  if (!src || !out) return fail(PBGPU_ERR_INVALID, "null argument");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+    return fail(PBGPU_ERR_INVALID, "device %d out of range", device);
+  API_TRY
+  HIPCHK(hipSetDevice(device));
+  std::unique_ptr<pbgpu_index> ix(new pbgpu_index);
+  ix->device = device;
+  ix->k = src->k; ix->psa_min = src->psa_min;
+  ix->n = src->n; ix->n_sr = src->n_sr; ix->n_kmers = src->n_kmers; ix->n_occ = src->n_occ; ix->buckets = src->buckets;
+  ix->build_seconds = src->build_seconds;
+  ix->name_fwd = src->name_fwd; ix->name_bwd = src->name_bwd; ix->sr_start = src->sr_start;
+  ix->filt_log2 = src->filt_log2;
+  ix->shard = src->shard; ix->n_shards = src->n_shards;
+  ix->sr_begin = src->sr_begin; ix->sr_end = src->sr_end; ix->n_total = src->n_total;
+  ix->gstart = src->gstart; ix->null_ptr = src->null_ptr;
+  ix->fk = src->fk; ix->f_buckets = src->f_buckets; ix->f_kmers = src->f_kmers; ix->f_occ = src->f_occ;
+  auto cp = [&](auto& dst, const auto& s) {  // device-to-device (peer when the devices differ)
+    dst.alloc(s.n);
+    if (!s.n) return;
+    if (device == src->device) HIPCHK(hipMemcpy(dst.p, s.p, s.bytes(), hipMemcpyDeviceToDevice));
+    else HIPCHK(hipMemcpyPeer(dst.p, device, s.p, src->device, s.bytes()));
+  };
+  cp(ix->text, src->text); cp(ix->d_sr_start, src->d_sr_start); cp(ix->occ, src->occ); cp(ix->table, src->table);
+  cp(ix->sr_uoff, src->sr_uoff); cp(ix->sr_uids, src->sr_uids); cp(ix->filt, src->filt);
+  cp(ix->f_occv, src->f_occv); cp(ix->f_table, src->f_table);
+  HIPCHK(hipDeviceSynchronize());
+  *out = ix.release();
+  return PBGPU_OK;
+  API_CATCH
+}
+
 pbgpu_status pbgpu_index_get_info(const pbgpu_index* ix, pbgpu_index_info* info) {
   if (!ix || !info) return fail(PBGPU_ERR_INVALID, "null argument");
   info->n_sr = ix->n_sr; info->text_len = ix->n; info->n_kmers = ix->n_kmers; info->n_occurrences = ix->n_occ;
@@ -635,74 +554,6 @@ void pbgpu_align_params_default(pbgpu_align_params* p) {
 
 }  // extern "C"
 
-// ---------------------------------------------------------------- aligner
-struct pbgpu_reads {
-  pbgpu_aligner* owner = nullptr;
-  int device = 0;  // kept here: the owner may be freed first
-  uint64_t n_reads = 0, n_bases = 0;
-  std::vector<uint64_t> h_off;
-  dbuf<uint8_t> seq;
-  dbuf<uint64_t> off;
-};
-
-struct pbgpu_aligner {
-  const pbgpu_index* ix = nullptr;
-  int device = 0;
-  pbgpu_align_params prm{};
-  AlignParamsDev P{};
-  LisParams lp{};
-  hipStream_t st = nullptr;
-  dbuf<int32_t> ul, sr_ul;  // unitig lengths; the same resolved along every super-read name (k_sr_ul)
-  // per-batch buffers
-  dbuf<KRec> krec;
-  dbuf<uint32_t> n_kept, thr, rec_per_read, rec_cursor, order, ovf_reads, counters;
-  dbuf<uint64_t> sort_scratch;  // k_rec_sort keys of reads above its LDS capacity: 6 words per record
-  dbuf<uint64_t> nhits, hit_off, rec_off, huge_elems;
-  dbuf<int2> hits;
-  dbuf<ChainDesc> chains;
-  dbuf<uint32_t> perm;
-  dbuf<int2> X, pts;
-  dbuf<uint8_t> nodes, nodes32;  // LNode<uint16_t> / LNode<uint32_t> per hit
-  dbuf<uint32_t> lisl, hist, slen;
-  dbuf<uint32_t> redo[3];
-  dbuf<Rec> recs, recs_sorted;
-  dbuf<uint32_t> rec_read;  // the read of every record of recs (written with it)
-  dbuf<int32_t> info_m, info_b;
-  dbuf<uint8_t> tmp;
-  dbuf<uint32_t> gtable;
-  dbuf<unsigned long long> stats, info_count;
-  // last result
-  uint64_t last_reads = 0, last_records = 0, last_info = 0;
-  bool have_result = false;
-  // stats
-  pbgpu_stats acc{};
-  hipEvent_t ev[18]{};
-  uint64_t hit_budget = 4000000000ull, rec_hint = 0, info_per_chain = 32;
-  double chains_per_hit = 1.0 / 80;  // k_group tier estimate (C2: 1.1 x 1/90), refined after every batch
-  dbuf<uint32_t> ovf_list, read_list;
-  dbuf<uint8_t> nparts;
-  dbuf<uint2> prog;
-  // sharded index: per-base k-mer counts of the current batch (SEED_COUNTS, then summed)
-  dbuf<uint32_t> gcount;
-  uint64_t gcount_n = ~0ull;
-  // -F: fine aligner pass (params of k_coords with align_k = fine_k, forward, unfiltered)
-  bool fine = false;
-  AlignParamsDev PF{};
-  LisParams lpf{};
-  dbuf<FineWin> fwin;
-  dbuf<uint64_t> fwk[2], fread_hits;
-  dbuf<uint32_t> fwi[2], fkeys[2], lstart, lend, emit_of;
-  dbuf<int2> X2;
-  // --details: final coarse lists of the last alignment, in sub-batch chain order
-  bool details = false;
-  struct {
-    std::vector<uint32_t> read, sr, nf;
-    std::vector<uint64_t> hoff{0};
-    std::vector<int32_t> hits;
-    std::vector<uint8_t> lis;
-    void clear() { read.clear(); sr.clear(); nf.clear(); hoff.assign(1, 0); hits.clear(); lis.clear(); }
-  } det;
-};
 
 // print_details input (jf_aligner.cc:72-108) of one sub-batch: every (read,
 // super-read) chain's final fwd / bwd lists and the printed lis, marked by
@@ -748,8 +599,43 @@ static void capture_details(pbgpu_aligner* al, uint32_t nch, uint64_t Hs) {
   }
 }
 
-static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode = SEED_WHOLE,
-                             uint32_t* gcount = nullptr);
+// Fills r from a host batch on the aligner's stream.  Device buffers only grow
+// (a reused pbgpu_reads allocates nothing once it is large enough: hipFree
+// would synchronize the device and stall the other aligners' streams).
+void upload_reads_into(pbgpu_aligner* al, const pbgpu_read_batch* b, pbgpu_reads* r) {
+  hipStream_t st = al->st;
+  r->owner = al;
+  r->device = al->device;
+  r->n_reads = b->n_reads;
+  r->h_off.resize(b->n_reads + 1);
+  const uint64_t o0 = b->n_reads ? b->offsets[0] : 0;
+  for (uint64_t i = 0; i <= b->n_reads; ++i) {
+    r->h_off[i] = b->n_reads ? b->offsets[i] - o0 : 0;
+    if (i && r->h_off[i] < r->h_off[i - 1]) throw std::invalid_argument("offsets must be non-decreasing");
+  }
+  r->n_bases = r->h_off[b->n_reads];
+  if (r->n_bases > 0xFFFFFFFFull * 8) throw unsupported("batch too large");
+  r->seq.ensure(r->n_bases + 1);
+  if (r->n_bases) HIPCHK(hipMemcpyAsync(r->seq.p, b->seq + o0, r->n_bases, hipMemcpyHostToDevice, st));
+  r->off.ensure(b->n_reads + 1);
+  HIPCHK(hipMemcpyAsync(r->off.p, r->h_off.data(), (b->n_reads + 1) * 8, hipMemcpyHostToDevice, st));
+  r->has_names = b->names != nullptr && b->name_offsets != nullptr;
+  if (r->has_names) {
+    std::vector<uint64_t>& no = r->h_name_off;
+    no.resize(b->n_reads + 1);
+    const uint64_t n0 = b->n_reads ? b->name_offsets[0] : 0;
+    for (uint64_t i = 0; i <= b->n_reads; ++i) {
+      no[i] = b->n_reads ? b->name_offsets[i] - n0 : 0;
+      if (i && no[i] < no[i - 1]) throw std::invalid_argument("name offsets must be non-decreasing");
+    }
+    r->names.ensure(no[b->n_reads] + 1);
+    if (no[b->n_reads]) HIPCHK(hipMemcpyAsync(r->names.p, b->names + n0, no[b->n_reads], hipMemcpyHostToDevice, st));
+    r->name_off.ensure(b->n_reads + 1);
+    HIPCHK(hipMemcpyAsync(r->name_off.p, no.data(), (b->n_reads + 1) * 8, hipMemcpyHostToDevice, st));
+  }
+  HIPCHK(hipStreamSynchronize(st));  // the host vectors above are the copies' sources
+}
+
 
 extern "C" {
 
@@ -825,21 +711,7 @@ pbgpu_status pbgpu_reads_upload(pbgpu_aligner* al, const pbgpu_read_batch* b, pb
   API_TRY
   HIPCHK(hipSetDevice(al->ix->device));
   std::unique_ptr<pbgpu_reads> r(new pbgpu_reads);
-  r->owner = al;
-  r->device = al->device;
-  r->n_reads = b->n_reads;
-  r->h_off.resize(b->n_reads + 1);
-  const uint64_t o0 = b->n_reads ? b->offsets[0] : 0;
-  for (uint64_t i = 0; i <= b->n_reads; ++i) {
-    r->h_off[i] = b->n_reads ? b->offsets[i] - o0 : 0;
-    if (i && r->h_off[i] < r->h_off[i - 1]) throw std::invalid_argument("offsets must be non-decreasing");
-  }
-  r->n_bases = r->h_off[b->n_reads];
-  if (r->n_bases > 0xFFFFFFFFull * 8) throw unsupported("batch too large");
-  r->seq.alloc(r->n_bases + 1);
-  if (r->n_bases) HIPCHK(hipMemcpy(r->seq.p, b->seq + o0, r->n_bases, hipMemcpyHostToDevice));
-  r->off.alloc(b->n_reads + 1);
-  HIPCHK(hipMemcpy(r->off.p, r->h_off.data(), (b->n_reads + 1) * 8, hipMemcpyHostToDevice));
+  upload_reads_into(al, b, r.get());
   *out = r.release();
   return PBGPU_OK;
   API_CATCH
@@ -1204,7 +1076,7 @@ static void fine_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   records_stage(al, n, (uint32_t)rec_done, false);
 }
 
-static void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, uint32_t* gcount) {
+void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, uint32_t* gcount) {
   const pbgpu_index* ix = al->ix;
   const IndexView v = ix->view();
   hipStream_t st = al->st;

@@ -1,0 +1,229 @@
+// pbgpu_host.h -- host-side objects behind the C ABI (include/pbgpu.h),
+// shared by pbgpu_api.hip (index, aligner, batch pipeline), pbgpu_format.hip
+// (device coords text) and pbgpu_run.hip (the file-to-file driver).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/pbgpu.h"
+#include "pbgpu_internal.h"
+
+using namespace pbgpu;
+
+// ------------------------------------------------------------ error state
+extern thread_local std::string g_err;  // pbgpu_api.hip
+inline pbgpu_status fail(pbgpu_status s, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return s;
+}
+struct hip_error : std::runtime_error {
+  hipError_t e;
+  hip_error(hipError_t e_, const char* what) : std::runtime_error(what), e(e_) {}
+};
+#define HIPCHK(x)                                                                                      \
+  do {                                                                                                 \
+    hipError_t _e = (x);                                                                               \
+    if (_e != hipSuccess) {                                                                            \
+      char _b[512];                                                                                    \
+      snprintf(_b, sizeof _b, "%s failed at %s:%d: %s", #x, __FILE__, __LINE__, hipGetErrorString(_e)); \
+      throw hip_error(_e, _b);                                                                         \
+    }                                                                                                  \
+  } while (0)
+struct bad_input : std::runtime_error { using std::runtime_error::runtime_error; };
+struct pbgpu_comm {  // an RCCL communicator of the sharded-index count exchange
+  ncclComm_t comm = nullptr;
+  int device = 0;
+};
+struct unsupported : std::runtime_error { using std::runtime_error::runtime_error; };
+
+#define API_TRY try { (void)hipGetLastError();  /* launch checks below see only this call's errors */
+#define API_CATCH                                                                 \
+  }                                                                               \
+  catch (const hip_error& e) {                                                    \
+    return fail(e.e == hipErrorOutOfMemory ? PBGPU_ERR_NOMEM : PBGPU_ERR_DEVICE, "%s", e.what()); \
+  }                                                                               \
+  catch (const bad_input& e) { return fail(PBGPU_ERR_IO, "%s", e.what()); }       \
+  catch (const unsupported& e) { return fail(PBGPU_ERR_UNSUPPORTED, "%s", e.what()); } \
+  catch (const std::bad_alloc&) { return fail(PBGPU_ERR_NOMEM, "host allocation failed"); } \
+  catch (const std::exception& e) { return fail(PBGPU_ERR_INTERNAL, "%s", e.what()); }
+
+// --------------------------------------------------------- device buffer
+template <typename T>
+struct dbuf {
+  T* p = nullptr;
+  size_t n = 0;
+  dbuf() = default;
+  dbuf(const dbuf&) = delete;
+  dbuf& operator=(const dbuf&) = delete;
+  ~dbuf() { release(); }
+  void release() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
+  void alloc(size_t cnt) { release(); if (cnt) { HIPCHK(hipMalloc((void**)&p, cnt * sizeof(T))); n = cnt; } }
+  void ensure(size_t cnt) { if (cnt > n) alloc(std::max(cnt, n + n / 4)); }
+  // grow keeping the first `keep` elements (stream-ordered copy)
+  void grow_keep(size_t cnt, size_t keep, hipStream_t st) {
+    if (cnt <= n) return;
+    T* q = nullptr;
+    const size_t nn = std::max(cnt, n + n / 2);
+    HIPCHK(hipMalloc((void**)&q, nn * sizeof(T)));
+    if (p && keep) HIPCHK(hipMemcpyAsync(q, p, keep * sizeof(T), hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
+    release();
+    p = q; n = nn;
+  }
+  size_t bytes() const { return n * sizeof(T); }
+  void swap(dbuf& o) { std::swap(p, o.p); std::swap(n, o.n); }
+};
+
+inline void* temp_storage(dbuf<uint8_t>& t, size_t bytes) {
+  t.ensure(bytes ? bytes : 1);
+  return t.p;
+}
+
+
+// ------------------------------------------------------------------ index
+struct pbgpu_index {
+  int device = 0;
+  uint32_t k = 0, psa_min = 0;
+  uint64_t n = 0, n_sr = 0, n_kmers = 0, n_occ = 0, buckets = 0;
+  double build_seconds = 0;
+  std::vector<std::string> name_fwd, name_bwd;
+  std::vector<uint64_t> sr_start;            // host copy
+  dbuf<uint64_t> text, d_sr_start, occ;
+  dbuf<ulonglong2> table;
+  dbuf<uint32_t> sr_uoff, sr_uids;
+  // presence filter of the coarse table's k-mers (k_seed), 2^filt_log2 words; none if empty
+  dbuf<uint64_t> filt;
+  uint32_t filt_log2 = 0;
+  // index sharded by super-read range: this shard holds super-reads
+  // [sr_begin, sr_end) (device arrays use local ids) plus a k-1-base seam
+  uint32_t shard = 0, n_shards = 1;
+  uint64_t sr_begin = 0, sr_end = 0, n_total = 0;
+  std::vector<uint64_t> gstart;   // global text offsets of all super-reads (host)
+  uint64_t null_ptr = 0;          // empty occurrence header: k-mers absent from this shard
+  // fine (-F) sub-index: same table / occurrence layout over fine_k-mers
+  uint32_t fk = 0;
+  uint64_t f_buckets = 0, f_kmers = 0, f_occ = 0;
+  dbuf<uint64_t> f_occv;
+  dbuf<ulonglong2> f_table;
+  // super-read names on the device (device coords text, pbgpu_format.hip), built on first use
+  std::mutex names_mu;
+  bool names_ready = false;
+  dbuf<char> d_name_fwd, d_name_bwd;
+  dbuf<uint64_t> d_name_fwd_off, d_name_bwd_off;
+  IndexView view() const {
+    IndexView v;
+    v.text = text.p; v.n = n; v.sr_start = d_sr_start.p; v.n_sr = (uint32_t)(sr_end - sr_begin); v.k = k;
+    v.table = table.p; v.bucket_mask = buckets - 1; v.occ = occ.p; v.sr_uoff = sr_uoff.p; v.sr_uids = sr_uids.p;
+    v.filt = filt.n ? filt.p : nullptr; v.filt_shift = 64 - filt_log2;
+    return v;
+  }
+  IndexView fine_view() const {
+    IndexView v = view();
+    v.k = fk; v.table = f_table.p; v.bucket_mask = f_buckets - 1; v.occ = f_occv.p;
+    v.filt = nullptr;
+    return v;
+  }
+  uint64_t device_bytes() const {
+    return text.bytes() + d_sr_start.bytes() + occ.bytes() + table.bytes() + sr_uoff.bytes() + sr_uids.bytes() +
+           f_occv.bytes() + f_table.bytes() + filt.bytes();
+  }
+};
+
+// ---------------------------------------------------------------- aligner
+struct pbgpu_reads {
+  pbgpu_aligner* owner = nullptr;
+  int device = 0;  // kept here: the owner may be freed first
+  uint64_t n_reads = 0, n_bases = 0;
+  std::vector<uint64_t> h_off;
+  dbuf<uint8_t> seq;
+  dbuf<uint64_t> off;
+  // read names (up to the first whitespace) for the device coords text
+  bool has_names = false;
+  dbuf<char> names;
+  dbuf<uint64_t> name_off;
+  std::vector<uint64_t> h_name_off;
+};
+
+struct pbgpu_aligner {
+  const pbgpu_index* ix = nullptr;
+  int device = 0;
+  pbgpu_align_params prm{};
+  AlignParamsDev P{};
+  LisParams lp{};
+  hipStream_t st = nullptr;
+  dbuf<int32_t> ul, sr_ul;  // unitig lengths; the same resolved along every super-read name (k_sr_ul)
+  // per-batch buffers
+  dbuf<KRec> krec;
+  dbuf<uint32_t> n_kept, thr, rec_per_read, rec_cursor, order, ovf_reads, counters;
+  dbuf<uint64_t> sort_scratch;  // k_rec_sort keys of reads above its LDS capacity: 6 words per record
+  dbuf<uint64_t> nhits, hit_off, rec_off, huge_elems;
+  dbuf<int2> hits;
+  dbuf<ChainDesc> chains;
+  dbuf<uint32_t> perm;
+  dbuf<int2> X, pts;
+  dbuf<uint8_t> nodes, nodes32;  // LNode<uint16_t> / LNode<uint32_t> per hit
+  dbuf<uint32_t> lisl, hist, slen;
+  dbuf<uint32_t> redo[3];
+  dbuf<Rec> recs, recs_sorted;
+  dbuf<uint32_t> rec_read;  // the read of every record of recs (written with it)
+  dbuf<int32_t> info_m, info_b;
+  dbuf<uint8_t> tmp;
+  dbuf<uint32_t> gtable;
+  dbuf<unsigned long long> stats, info_count;
+  // last result
+  uint64_t last_reads = 0, last_records = 0, last_info = 0;
+  bool have_result = false;
+  // stats
+  pbgpu_stats acc{};
+  hipEvent_t ev[18]{};
+  uint64_t hit_budget = 4000000000ull, rec_hint = 0, info_per_chain = 32;
+  double chains_per_hit = 1.0 / 80;  // k_group tier estimate (C2: 1.1 x 1/90), refined after every batch
+  dbuf<uint32_t> ovf_list, read_list;
+  dbuf<uint8_t> nparts;
+  dbuf<uint2> prog;
+  // sharded index: per-base k-mer counts of the current batch (SEED_COUNTS, then summed)
+  dbuf<uint32_t> gcount;
+  uint64_t gcount_n = ~0ull;
+  // -F: fine aligner pass (params of k_coords with align_k = fine_k, forward, unfiltered)
+  bool fine = false;
+  AlignParamsDev PF{};
+  LisParams lpf{};
+  dbuf<FineWin> fwin;
+  dbuf<uint64_t> fwk[2], fread_hits;
+  dbuf<uint32_t> fwi[2], fkeys[2], lstart, lend, emit_of;
+  dbuf<int2> X2;
+  // --details: final coarse lists of the last alignment, in sub-batch chain order
+  bool details = false;
+  struct {
+    std::vector<uint32_t> read, sr, nf;
+    std::vector<uint64_t> hoff{0};
+    std::vector<int32_t> hits;
+    std::vector<uint8_t> lis;
+    void clear() { read.clear(); sr.clear(); nf.clear(); hoff.assign(1, 0); hits.clear(); lis.clear(); }
+  } det;
+  // device coords text of the last alignment (pbgpu_format.hip)
+  dbuf<uint32_t> fmt_len;
+  dbuf<uint64_t> fmt_pos;
+  dbuf<char> text;
+  uint64_t text_len = 0;
+};
+
+// the whole device path on a resident batch (seed_mode: SEED_WHOLE = 0; the
+// sharded-index modes pass SEED_FINISH and the summed counts)
+void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode = 0, uint32_t* gcount = nullptr);
+void upload_reads_into(pbgpu_aligner* al, const pbgpu_read_batch* b, pbgpu_reads* r);
+uint64_t format_device_text(pbgpu_aligner* al, const pbgpu_reads* rd, int compact, int zero_match);

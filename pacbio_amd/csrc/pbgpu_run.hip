@@ -1,0 +1,664 @@
+// pbgpu_run.hip -- the file-to-file driver behind pbgpu_run (include/pbgpu.h):
+// the reference's jf_aligner main loop (jf_aligner.cc:205-230) and worker
+// (print_alignments, :110-159) re-laid out for GPUs.
+//
+//   reader thread   PacBio FASTA/FASTQ (plain or gzip, zlib) -> batches of
+//                   ~batch_bases bases: bases, offsets, read names
+//   worker threads  one per aligner (aligners_per_device per listed index):
+//                   take the next batch (dynamic assignment), upload into
+//                   grow-only device buffers, run the device path, format the
+//                   coords text on the device (pbgpu_format.hip), copy it into
+//                   a pinned host buffer
+//   writer thread   writes the texts in batch order (one write() stream: on
+//                   the GPU box one stream writes the page cache at ~10 GB/s
+//                   and parallel pwrite()s do not go faster, the inode lock
+//                   serializes them -- profiles/r02_probe_io.txt)
+// Backpressure: the pinned pool holds workers + 2 buffers, so a slow writer
+// stalls the workers instead of growing memory.  The first error of any
+// thread stops all of them and is returned (no exit() from a worker).
+#include <fcntl.h>
+#include <unistd.h>
+#include <zlib.h>
+
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <map>
+#include <memory>
+#include <thread>
+
+#include "pbgpu_host.h"
+
+namespace {
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// ------------------------------------------------------------ run state
+struct RunState {
+  std::mutex mu;
+  bool stop = false;
+  pbgpu_status status = PBGPU_OK;
+  std::string msg;
+  std::condition_variable* cvs[4] = {};
+  void fail(pbgpu_status s, const std::string& m) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      if (status == PBGPU_OK) { status = s; msg = m; }
+      stop = true;
+    }
+    for (auto* cv : cvs) if (cv) cv->notify_all();
+  }
+  bool stopped() {
+    std::lock_guard<std::mutex> lk(mu);
+    return stop;
+  }
+};
+
+// condition waits re-check every 50 ms: RunState::fail notifies without the
+// waiters' mutexes, so a notification can slip between a check and the wait
+template <class L, class P>
+void wait_until(std::condition_variable& cv, L& lk, P pred) {
+  while (!cv.wait_for(lk, std::chrono::milliseconds(50), pred)) {
+  }
+}
+
+// the API_CATCH classification, for a thread's exception
+void record_exception(RunState& rs) {
+  try {
+    throw;
+  } catch (const hip_error& e) {
+    rs.fail(e.e == hipErrorOutOfMemory ? PBGPU_ERR_NOMEM : PBGPU_ERR_DEVICE, e.what());
+  } catch (const bad_input& e) {
+    rs.fail(PBGPU_ERR_IO, e.what());
+  } catch (const unsupported& e) {
+    rs.fail(PBGPU_ERR_UNSUPPORTED, e.what());
+  } catch (const std::bad_alloc&) {
+    rs.fail(PBGPU_ERR_NOMEM, "host allocation failed");
+  } catch (const std::exception& e) {
+    rs.fail(PBGPU_ERR_INTERNAL, e.what());
+  }
+}
+
+// ------------------------------------------------------------ pinned memory
+struct PinnedVec {  // growable pinned byte buffer (H2D at full PCIe rate, no staging)
+  char* p = nullptr;
+  size_t cap = 0, n = 0;
+  PinnedVec() = default;
+  PinnedVec(const PinnedVec&) = delete;
+  PinnedVec& operator=(const PinnedVec&) = delete;
+  ~PinnedVec() { if (p) (void)hipHostFree(p); }
+  void reserve(size_t c) {
+    if (c <= cap) return;
+    const size_t nc = std::max(c, cap + cap / 2);
+    char* q = nullptr;
+    HIPCHK(hipHostMalloc((void**)&q, nc, hipHostMallocDefault));
+    if (n) memcpy(q, p, n);
+    if (p) (void)hipHostFree(p);
+    p = q;
+    cap = nc;
+  }
+  void append(const char* s, size_t len) {
+    if (n + len > cap) reserve(n + len);
+    memcpy(p + n, s, len);
+    n += len;
+  }
+};
+
+// ------------------------------------------------------------ input
+// Lines of a sequence of files: plain files by read(), gzip (magic 1f 8b) by zlib.
+class LineSource {
+ public:
+  explicit LineSource(const std::vector<std::string>& paths) : paths_(paths) { buf_.resize(1 << 24); }
+  ~LineSource() { close_cur(); }
+  // next line without its '\n' (pointer valid until the next call); false at
+  // the end of the current file -- next_file() then opens the next one
+  bool line(const char*& p, size_t& len) {
+    for (;;) {
+      if (pos_ < end_) {
+        const char* s = buf_.data() + pos_;
+        const char* nl = (const char*)memchr(s, '\n', end_ - pos_);
+        if (nl) {
+          p = s; len = (size_t)(nl - s);
+          pos_ += len + 1;
+          return true;
+        }
+        if (eof_) {  // last line without a newline
+          p = s; len = end_ - pos_;
+          pos_ = end_;
+          return true;
+        }
+      } else if (eof_) {
+        return false;
+      }
+      fill();
+    }
+  }
+  bool next_file() {
+    close_cur();
+    if (fi_ >= paths_.size()) return false;
+    const std::string& path = paths_[fi_++];
+    fd_ = open(path.c_str(), O_RDONLY);
+    if (fd_ < 0) throw bad_input("Can't open PacBio file '" + path + "'");
+    unsigned char mg[2] = {0, 0};
+    const ssize_t m = pread(fd_, mg, 2, 0);
+    if (m == 2 && mg[0] == 0x1f && mg[1] == 0x8b) {
+      gz_ = gzdopen(fd_, "rb");
+      if (!gz_) throw bad_input("Can't open gzip PacBio file '" + path + "'");
+      fd_ = -1;  // owned by gz_
+      gzbuffer(gz_, 1 << 20);
+    }
+    pos_ = end_ = 0;
+    eof_ = false;
+    return true;
+  }
+
+ private:
+  void close_cur() {
+    if (gz_) { gzclose(gz_); gz_ = nullptr; }
+    if (fd_ >= 0) { close(fd_); fd_ = -1; }
+  }
+  void fill() {
+    if (pos_ > 0) {  // keep the partial line at the front
+      memmove(buf_.data(), buf_.data() + pos_, end_ - pos_);
+      end_ -= pos_;
+      pos_ = 0;
+    }
+    if (end_ == buf_.size()) buf_.resize(buf_.size() * 2);  // a line longer than the buffer
+    const size_t want = std::min<size_t>(buf_.size() - end_, 1u << 30);
+    ssize_t got;
+    if (gz_) {
+      got = gzread(gz_, buf_.data() + end_, (unsigned)want);
+      if (got < 0) {
+        int e;
+        throw bad_input(std::string("read error in PacBio file: ") + gzerror(gz_, &e));
+      }
+    } else {
+      do { got = read(fd_, buf_.data() + end_, want); } while (got < 0 && errno == EINTR);
+      if (got < 0) throw bad_input(std::string("read error in PacBio file: ") + strerror(errno));
+    }
+    if (got == 0) eof_ = true;
+    end_ += (size_t)got;
+  }
+  std::vector<std::string> paths_;
+  size_t fi_ = 0;
+  int fd_ = -1;
+  gzFile gz_ = nullptr;
+  std::vector<char> buf_;
+  size_t pos_ = 0, end_ = 0;
+  bool eof_ = true;
+};
+
+struct Batch {
+  uint64_t id = 0;
+  PinnedVec seq;
+  std::string names;
+  std::vector<uint64_t> off{0}, name_off{0};
+  std::vector<std::string> headers;  // full header lines (--details only)
+  uint64_t n() const { return off.size() - 1; }
+  void clear() {
+    seq.n = 0;
+    names.clear();
+    off.assign(1, 0);
+    name_off.assign(1, 0);
+    headers.clear();
+  }
+};
+
+// whole_sequence_parser semantics (jellyfish 2.x, as used at jf_aligner.cc:206-207):
+// FASTA header = line after '>', sequence = the following lines concatenated;
+// FASTQ '@' header, one sequence line, '+' line, quality line.
+class ReadParser {
+ public:
+  ReadParser(const std::vector<std::string>& paths, bool keep_headers) : src_(paths), keep_(keep_headers) {
+    open_ = src_.next_file();
+  }
+  // appends up to ~batch_bases bases worth of reads; false when nothing was added
+  bool fill(Batch& b, uint64_t batch_bases) {
+    while (open_ && b.seq.n < batch_bases) {
+      if (!one(b)) open_ = src_.next_file();
+    }
+    return b.n() > 0;
+  }
+
+ private:
+  bool one(Batch& b) {
+    const char* p;
+    size_t len;
+    if (have_pending_) {
+      have_pending_ = false;
+      hdr_.swap(pending_);
+    } else {
+      do {
+        if (!src_.line(p, len)) return false;
+      } while (len == 0);
+      hdr_.assign(p, len);
+    }
+    const char c0 = hdr_[0];
+    if (c0 != '>' && c0 != '@') throw bad_input("PacBio input is neither FASTA nor FASTQ");
+    if (c0 == '@') {
+      if (src_.line(p, len)) b.seq.append(p, len);
+      src_.line(p, len);  // '+'
+      src_.line(p, len);  // quality
+    } else {
+      while (src_.line(p, len)) {
+        if (len && p[0] == '>') { pending_.assign(p, len); have_pending_ = true; break; }
+        b.seq.append(p, len);
+      }
+    }
+    // name = header up to the first whitespace (jf_aligner.cc:133-134)
+    const size_t nl = strcspn(hdr_.c_str() + 1, " \t\n\v\f\r");
+    b.names.append(hdr_, 1, nl);
+    b.name_off.push_back(b.names.size());
+    b.off.push_back(b.seq.n);
+    if (keep_) b.headers.emplace_back(hdr_, 1);
+    return true;
+  }
+  LineSource src_;
+  bool keep_;
+  bool open_ = false;
+  bool have_pending_ = false;
+  std::string hdr_, pending_;
+};
+
+// ------------------------------------------------------------ plumbing
+template <class T>
+class Queue {  // bounded, closable, stops with the run
+ public:
+  Queue(size_t cap, RunState& rs, int slot) : cap_(cap), rs_(rs) { rs.cvs[slot] = &cv_; }
+  bool push(T v) {
+    std::unique_lock<std::mutex> lk(mu_);
+    wait_until(cv_, lk, [&] { return q_.size() < cap_ || rs_.stopped(); });
+    if (rs_.stopped()) return false;
+    q_.push_back(std::move(v));
+    cv_.notify_all();
+    return true;
+  }
+  bool pop(T& v) {
+    std::unique_lock<std::mutex> lk(mu_);
+    wait_until(cv_, lk, [&] { return !q_.empty() || closed_ || rs_.stopped(); });
+    if (rs_.stopped() || q_.empty()) return false;
+    v = std::move(q_.front());
+    q_.pop_front();
+    cv_.notify_all();
+    return true;
+  }
+  void close() {
+    std::lock_guard<std::mutex> lk(mu_);
+    closed_ = true;
+    cv_.notify_all();
+  }
+
+ private:
+  size_t cap_;
+  RunState& rs_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<T> q_;
+  bool closed_ = false;
+};
+
+struct Pinned {
+  char* p = nullptr;
+  size_t cap = 0;
+};
+
+// Text buffers: they grow to the largest text seen and live as long as the
+// runner.  Batch id may take one only while id < written + n (written =
+// batches the writer has finished): the batch the writer waits for can then
+// always get a buffer, however far the other workers run ahead.
+class TextPool {
+ public:
+  explicit TextPool(size_t n) : n_(n) { free_.resize(n); }
+  ~TextPool() { for (auto& b : free_) if (b.p) (void)hipHostFree(b.p); }
+  void start(RunState* rs) {  // a new run: batch ids restart at 0
+    std::lock_guard<std::mutex> lk(mu_);
+    rs_ = rs;
+    written_ = 0;
+    rs->cvs[1] = &cv_;
+  }
+  bool get(uint64_t id, size_t need, Pinned& out) {
+    std::unique_lock<std::mutex> lk(mu_);
+    wait_until(cv_, lk, [&] { return (!free_.empty() && id < written_ + n_) || rs_->stopped(); });
+    if (rs_->stopped()) return false;
+    out = free_.back();
+    free_.pop_back();
+    lk.unlock();
+    if (out.cap < need) {
+      if (out.p) (void)hipHostFree(out.p);
+      out.p = nullptr;
+      out.cap = 0;
+      const size_t cap = need + need / 4;
+      const hipError_t e = hipHostMalloc((void**)&out.p, cap, hipHostMallocDefault);
+      if (e != hipSuccess) { put(Pinned{}, false); HIPCHK(e); }
+      out.cap = cap;
+    }
+    return true;
+  }
+  void put(Pinned b, bool written) {
+    std::lock_guard<std::mutex> lk(mu_);
+    free_.push_back(b);
+    if (written) ++written_;
+    cv_.notify_all();
+  }
+
+ private:
+  size_t n_;
+  uint64_t written_ = 0;
+  RunState* rs_ = nullptr;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<Pinned> free_;
+};
+
+struct Done {  // a batch's formatted output, waiting for its turn
+  Pinned text;
+  uint64_t len = 0;
+  std::string details;
+};
+
+void write_all(int fd, const char* p, uint64_t n, const char* what) {
+  while (n) {
+    const ssize_t w = write(fd, p, (size_t)std::min<uint64_t>(n, 1ull << 30));
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      throw bad_input(std::string("write to ") + what + " failed: " + strerror(errno));
+    }
+    p += w;
+    n -= (uint64_t)w;
+  }
+}
+
+}  // namespace
+
+// Long-lived resources of the driver: aligners, their resident read buffers,
+// the pinned batch and text buffers.  A server-style caller (bench.py) runs
+// many files through one runner; the CLI runs one.
+struct pbgpu_runner {
+  std::vector<pbgpu_aligner*> al;
+  std::vector<std::unique_ptr<pbgpu_reads>> rd;
+  bool details = false;
+  uint64_t batch_bases = 0;
+  std::vector<std::unique_ptr<Batch>> batches;  // W + 2, recycled
+  std::unique_ptr<TextPool> texts;              // W + 2
+  std::mutex run_mu;                            // one run at a time
+  ~pbgpu_runner() {
+    rd.clear();
+    for (auto* a : al) pbgpu_aligner_free(a);
+  }
+};
+
+static void runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_stats* stats) {
+  std::lock_guard<std::mutex> run_lock(R->run_mu);
+  const double t_start = now_s();
+  pbgpu_run_stats S{};
+  const bool details = R->details;
+  const uint64_t batch_bases = R->batch_bases;
+  const int hthreads = run->host_threads > 0 ? run->host_threads
+                                             : (int)std::max(1u, std::thread::hardware_concurrency());
+  // outputs first (early error reporting, jf_aligner.cc:170-178)
+  int cfd = 1, dfd = -1;
+  if (run->coords_path) {
+    cfd = open(run->coords_path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (cfd < 0) throw bad_input(std::string("Failed to open coords file '") + run->coords_path + "': " + strerror(errno));
+  }
+  struct fd_guard { int& fd; ~fd_guard() { if (fd > 2) close(fd); } } cg{cfd};
+  if (details) {
+    dfd = open(run->details_path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (dfd < 0) throw bad_input(std::string("Failed to open details file '") + run->details_path + "': " + strerror(errno));
+  }
+  struct fd_guard2 { int& fd; ~fd_guard2() { if (fd > 2) close(fd); } } dg{dfd};
+  S.open_seconds = now_s() - t_start;
+  std::vector<std::string> paths;
+  for (size_t i = 0; i < run->n_pb_paths; ++i) paths.emplace_back(run->pb_paths[i]);
+  const size_t W = R->al.size();
+
+  RunState rs;
+  Queue<Batch*> inq(W + 1, rs, 0);
+  Queue<Batch*> freeq(R->batches.size() + 1, rs, 3);
+  for (auto& b : R->batches) freeq.push(b.get());
+  R->texts->start(&rs);
+  std::mutex dmu;
+  std::condition_variable dcv;
+  rs.cvs[2] = &dcv;
+  std::map<uint64_t, Done> done;
+  uint64_t n_batches_total = ~0ull;  // set by the reader when it finishes
+  std::mutex smu;                    // stats
+
+  auto reader = [&]() {
+    try {
+      ReadParser rp(paths, details);
+      for (uint64_t id = 0;; ++id) {
+        Batch* b = nullptr;
+        if (!freeq.pop(b)) break;
+        const double t0 = now_s();
+        b->clear();
+        b->id = id;
+        const bool any = rp.fill(*b, batch_bases);
+        {
+          std::lock_guard<std::mutex> lk(smu);
+          S.read_seconds += now_s() - t0;
+        }
+        if (!any) {
+          std::lock_guard<std::mutex> lk(dmu);
+          n_batches_total = id;
+          dcv.notify_all();
+          break;
+        }
+        if (!inq.push(b)) break;
+      }
+    } catch (...) {
+      record_exception(rs);
+    }
+    inq.close();
+  };
+
+  auto worker = [&](size_t wi) {
+    pbgpu_aligner* al = R->al[wi];
+    pbgpu_reads* rd = R->rd[wi].get();
+    try {
+      HIPCHK(hipSetDevice(al->device));
+      Batch* b = nullptr;
+      while (inq.pop(b)) {
+        pbgpu_read_batch rb{b->n(), b->seq.p, b->off.data(), b->names.data(), b->name_off.data()};
+        const double t0 = now_s();
+        upload_reads_into(al, &rb, rd);
+        const double t1 = now_s();
+        aligner_pipeline(al, rd);
+        const double t2 = now_s();
+        const uint64_t len = format_device_text(al, rd, run->compact, run->zero_match);
+        HIPCHK(hipStreamSynchronize(al->st));
+        const double t3 = now_s();
+        Done d;
+        if (!R->texts->get(b->id, len + 1, d.text)) break;
+        const double t4 = now_s();
+        if (len) HIPCHK(hipMemcpyAsync(d.text.p, al->text.p, len, hipMemcpyDeviceToHost, al->st));
+        HIPCHK(hipStreamSynchronize(al->st));
+        const double t5 = now_s();
+        d.len = len;
+        if (details) {
+          pbgpu_details_batch* db = nullptr;
+          if (pbgpu_download_details(al, &db) != PBGPU_OK) throw std::runtime_error(pbgpu_last_error());
+          std::vector<const char*> hp(b->n());
+          for (size_t i = 0; i < hp.size(); ++i) hp[i] = b->headers[i].c_str();
+          char* txt = nullptr;
+          uint64_t tl = 0;
+          const pbgpu_status s = pbgpu_format_details(al->ix, db, hp.data(), hthreads, &txt, &tl);
+          pbgpu_details_free(db);
+          if (s != PBGPU_OK) throw std::runtime_error(pbgpu_last_error());
+          d.details.assign(txt, tl);
+          pbgpu_free_text(txt);
+        }
+        const uint64_t id = b->id, nreads = b->n(), nbases = b->seq.n;
+        freeq.push(b);  // the batch's host buffers are free again
+        {
+          std::lock_guard<std::mutex> lk(smu);
+          S.upload_seconds += t1 - t0;
+          S.align_seconds += t2 - t1;
+          S.format_seconds += t3 - t2;
+          S.d2h_seconds += t5 - t4;
+          S.n_batches++;
+          S.n_reads += nreads;
+          S.n_bases += nbases;
+          S.n_records += al->last_records;
+        }
+        {
+          std::lock_guard<std::mutex> lk(dmu);
+          done.emplace(id, std::move(d));
+          dcv.notify_all();
+        }
+      }
+    } catch (...) {
+      record_exception(rs);
+    }
+  };
+
+  auto writer = [&]() {
+    try {
+      if (run->header) {
+        std::string h = std::string("Rstart Rend Qstart Qend Nmers Rcons Qcons Rcover Qcover Rlen Qlen Stretch Offset Err") +
+                        (run->compact ? "" : " Rname") + " Qname\n";
+        write_all(cfd, h.data(), h.size(), "coords");
+        S.coords_bytes += h.size();
+      }
+      for (uint64_t next = 0;; ++next) {
+        Done d;
+        {
+          const double t0 = now_s();
+          std::unique_lock<std::mutex> lk(dmu);
+          wait_until(dcv, lk, [&] { return done.count(next) || next >= n_batches_total || rs.stopped(); });
+          if (rs.stopped() || !done.count(next)) break;
+          d = std::move(done[next]);
+          done.erase(next);
+          lk.unlock();
+          std::lock_guard<std::mutex> sl(smu);
+          S.writer_idle_seconds += now_s() - t0;
+        }
+        const double t1 = now_s();
+        write_all(cfd, d.text.p, d.len, "coords");
+        if (dfd >= 0) write_all(dfd, d.details.data(), d.details.size(), "details");
+        {
+          std::lock_guard<std::mutex> sl(smu);
+          S.write_seconds += now_s() - t1;
+          S.coords_bytes += d.len;
+          S.details_bytes += d.details.size();
+        }
+        R->texts->put(d.text, true);
+      }
+    } catch (...) {
+      record_exception(rs);
+    }
+  };
+
+  std::thread rt(reader), wt(writer);
+  std::vector<std::thread> ws;
+  for (size_t i = 0; i < W; ++i) ws.emplace_back(worker, i);
+  for (auto& t : ws) t.join();
+  {  // workers are gone: nothing more can arrive (stops the writer if the run failed mid-way)
+    std::unique_lock<std::mutex> lk(dmu);
+    const bool early = n_batches_total == ~0ull;
+    lk.unlock();
+    if (early && !rs.stopped()) rs.fail(PBGPU_ERR_INTERNAL, "the workers ended before the input did");
+    dcv.notify_all();
+  }
+  rt.join();
+  wt.join();
+  {
+    std::lock_guard<std::mutex> lk(dmu);
+    for (auto& kv : done) R->texts->put(kv.second.text, false);
+    done.clear();
+  }
+  if (rs.status != PBGPU_OK) {
+    switch (rs.status) {
+      case PBGPU_ERR_IO: throw bad_input(rs.msg);
+      case PBGPU_ERR_UNSUPPORTED: throw unsupported(rs.msg);
+      case PBGPU_ERR_NOMEM: throw std::bad_alloc();
+      default: throw std::runtime_error(rs.msg);
+    }
+  }
+  if (cfd > 2) {
+    const double tc = now_s();
+    const int fd = cfd;
+    cfd = -1;
+    if (close(fd)) throw bad_input(std::string("closing the coords file failed: ") + strerror(errno));
+    S.close_seconds = now_s() - tc;
+  }
+  S.wall_seconds = now_s() - t_start;
+  if (stats) *stats = S;
+}
+
+extern "C" {
+
+pbgpu_status pbgpu_host_alloc(uint64_t bytes, void** out) {
+  if (!out) return fail(PBGPU_ERR_INVALID, "null argument");
+  API_TRY
+  *out = nullptr;
+  HIPCHK(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+  return PBGPU_OK;
+  API_CATCH
+}
+
+pbgpu_status pbgpu_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+  return PBGPU_OK;
+}
+
+pbgpu_status pbgpu_runner_create(pbgpu_index* const* indexes, size_t n_indexes, const pbgpu_align_params* params,
+                                 const pbgpu_run_params* run, pbgpu_runner** out) {
+  if (!indexes || !n_indexes || !params || !run || !out) return fail(PBGPU_ERR_INVALID, "null argument");
+  for (size_t i = 0; i < n_indexes; ++i) {
+    if (!indexes[i]) return fail(PBGPU_ERR_INVALID, "null index");
+    if (indexes[i]->n_shards > 1) return fail(PBGPU_ERR_UNSUPPORTED, "the driver needs whole (unsharded) indexes");
+  }
+  API_TRY
+  std::unique_ptr<pbgpu_runner> R(new pbgpu_runner);
+  const uint32_t per_dev = run->aligners_per_device ? run->aligners_per_device : 2;
+  R->batch_bases = run->batch_bases ? run->batch_bases : (64ull << 20);
+  R->details = run->details_path != nullptr;
+  for (size_t i = 0; i < n_indexes; ++i)
+    for (uint32_t j = 0; j < per_dev; ++j) {
+      pbgpu_aligner* a = nullptr;
+      const pbgpu_status s = pbgpu_aligner_create(indexes[i], params, &a);
+      if (s != PBGPU_OK) return s;
+      R->al.push_back(a);
+      R->rd.emplace_back(new pbgpu_reads);
+      if (R->details) pbgpu_aligner_set_details(a, 1);
+    }
+  const size_t W = R->al.size();
+  for (size_t i = 0; i < W + 2; ++i) {
+    R->batches.emplace_back(new Batch);
+    R->batches.back()->seq.reserve(R->batch_bases + (R->batch_bases >> 2));
+  }
+  R->texts.reset(new TextPool(W + 2));
+  *out = R.release();
+  return PBGPU_OK;
+  API_CATCH
+}
+
+pbgpu_status pbgpu_runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_stats* stats) {
+  if (!R || !run || (!run->pb_paths && run->n_pb_paths)) return fail(PBGPU_ERR_INVALID, "null argument");
+  if ((run->details_path != nullptr) != R->details)
+    return fail(PBGPU_ERR_INVALID, "--details must be given to pbgpu_runner_create and every run alike");
+  API_TRY
+  runner_run(R, run, stats);
+  return PBGPU_OK;
+  API_CATCH
+}
+
+pbgpu_status pbgpu_runner_free(pbgpu_runner* R) {
+  delete R;
+  return PBGPU_OK;
+}
+
+pbgpu_status pbgpu_run(pbgpu_index* const* indexes, size_t n_indexes, const pbgpu_align_params* params,
+                       const pbgpu_run_params* run, pbgpu_run_stats* stats) {
+  pbgpu_runner* R = nullptr;
+  pbgpu_status s = pbgpu_runner_create(indexes, n_indexes, params, run, &R);
+  if (s != PBGPU_OK) return s;
+  s = pbgpu_runner_run(R, run, stats);
+  pbgpu_runner_free(R);
+  return s;
+}
+
+}  // extern "C"

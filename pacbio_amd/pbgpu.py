@@ -38,6 +38,8 @@ EXPORTS = [
     "pbgpu_shard_counts", "pbgpu_shard_counts_download", "pbgpu_shard_counts_upload", "pbgpu_rccl_unique_id",
     "pbgpu_rccl_comm_create", "pbgpu_rccl_comm_free", "pbgpu_shard_counts_allreduce", "pbgpu_align_resident_shard",
     "pbgpu_coords_merge",
+    "pbgpu_format_device", "pbgpu_text_download", "pbgpu_host_alloc", "pbgpu_host_free", "pbgpu_format_double",
+    "pbgpu_index_replicate", "pbgpu_run", "pbgpu_runner_create", "pbgpu_runner_run", "pbgpu_runner_free",
 ]
 
 
@@ -67,7 +69,27 @@ class AlignParams(C.Structure):
 
 
 class ReadBatch(C.Structure):
-    _fields_ = [("n_reads", C.c_uint64), ("seq", C.c_void_p), ("offsets", C.POINTER(C.c_uint64))]
+    _fields_ = [("n_reads", C.c_uint64), ("seq", C.c_void_p), ("offsets", C.POINTER(C.c_uint64)),
+                ("names", C.c_void_p), ("name_offsets", C.POINTER(C.c_uint64))]
+
+
+class RunParams(C.Structure):
+    _fields_ = [("pb_paths", C.POINTER(C.c_char_p)), ("n_pb_paths", C.c_size_t), ("coords_path", C.c_char_p),
+                ("details_path", C.c_char_p), ("compact", C.c_int32), ("header", C.c_int32),
+                ("zero_match", C.c_int32), ("aligners_per_device", C.c_uint32), ("batch_bases", C.c_uint64),
+                ("host_threads", C.c_int32)]
+
+
+class RunStats(C.Structure):
+    _fields_ = [("wall_seconds", C.c_double)] + \
+               [(n, C.c_uint64) for n in ("n_batches", "n_reads", "n_bases", "n_records", "coords_bytes",
+                                          "details_bytes")] + \
+               [(n, C.c_double) for n in ("read_seconds", "upload_seconds", "align_seconds", "format_seconds",
+                                          "d2h_seconds", "write_seconds", "writer_idle_seconds", "open_seconds",
+                                          "close_seconds")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
 
 
 RECORD_DTYPE = np.dtype([
@@ -169,6 +191,19 @@ def lib():
                                          C.POINTER(C.POINTER(CoordsBatch))]
         L.pbgpu_free_text.argtypes = [C.c_void_p]
         L.pbgpu_free_text.restype = None
+        L.pbgpu_format_device.argtypes = [vp, vp, C.c_int, C.c_int, C.POINTER(C.c_uint64)]
+        L.pbgpu_text_download.argtypes = [vp, C.c_void_p, C.c_uint64]
+        L.pbgpu_host_alloc.argtypes = [C.c_uint64, C.POINTER(C.c_void_p)]
+        L.pbgpu_host_free.argtypes = [C.c_void_p]
+        L.pbgpu_format_double.argtypes = [C.c_double, C.c_char_p]
+        L.pbgpu_format_double.restype = C.c_int
+        L.pbgpu_index_replicate.argtypes = [vp, C.c_int, C.POINTER(vp)]
+        L.pbgpu_run.argtypes = [C.POINTER(vp), C.c_size_t, C.POINTER(AlignParams), C.POINTER(RunParams),
+                                C.POINTER(RunStats)]
+        L.pbgpu_runner_create.argtypes = [C.POINTER(vp), C.c_size_t, C.POINTER(AlignParams), C.POINTER(RunParams),
+                                          C.POINTER(vp)]
+        L.pbgpu_runner_run.argtypes = [vp, C.POINTER(RunParams), C.POINTER(RunStats)]
+        L.pbgpu_runner_free.argtypes = [vp]
         _lib = L
     return _lib
 
@@ -231,6 +266,12 @@ class Index:
         h = C.c_void_p()
         _check(lib().pbgpu_index_build(_cstrs(names), _cstrs(bs), lens, len(bs), C.byref(p), C.byref(h)))
         return cls(h)
+
+    def replicate(self, device):
+        """pbgpu_index_replicate: the same index on another device (or a second copy on this one)"""
+        h = C.c_void_p()
+        _check(lib().pbgpu_index_replicate(self.h, device, C.byref(h)))
+        return Index(h)
 
     def info(self):
         i = IndexInfo()
@@ -324,19 +365,33 @@ class Aligner:
 
     def align(self, seqs):
         blob, off = _pack_reads(seqs)
-        b = ReadBatch(len(seqs), _addr(blob), off.ctypes.data_as(C.POINTER(C.c_uint64)))
+        b = ReadBatch(len(seqs), _addr(blob), off.ctypes.data_as(C.POINTER(C.c_uint64)), None, None)
         out = C.POINTER(CoordsBatch)()
         _check(lib().pbgpu_align_batch(self.h, C.byref(b), C.byref(out)))
         return Coords(out)
 
-    def upload(self, seqs=None, blob=None, offsets=None):
+    def upload(self, seqs=None, blob=None, offsets=None, names=None):
+        """names: read names (header up to the first whitespace) for format_device"""
         if seqs is not None:
             blob, offsets = _pack_reads(seqs)
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
-        b = ReadBatch(len(offsets) - 1, _addr(blob), offsets.ctypes.data_as(C.POINTER(C.c_uint64)))
+        b = ReadBatch(len(offsets) - 1, _addr(blob), offsets.ctypes.data_as(C.POINTER(C.c_uint64)), None, None)
+        if names is not None:
+            nblob, noff = _pack_reads(names)
+            b.names = _addr(nblob)
+            b.name_offsets = noff.ctypes.data_as(C.POINTER(C.c_uint64))
         r = C.c_void_p()
         _check(lib().pbgpu_reads_upload(self.h, C.byref(b), C.byref(r)))
         return ResidentReads(r)
+
+    def format_device(self, reads, compact=True, zero_match=False):
+        """pbgpu_format_device + pbgpu_text_download: the last alignment's coords text,
+        formatted on the device"""
+        n = C.c_uint64()
+        _check(lib().pbgpu_format_device(self.h, reads.h, int(compact), int(zero_match), C.byref(n)))
+        buf = C.create_string_buffer(n.value + 1)
+        _check(lib().pbgpu_text_download(self.h, buf, n.value))
+        return buf.raw[:n.value].decode()
 
     def align_resident(self, reads):
         _check(lib().pbgpu_align_resident(self.h, reads.h))
@@ -498,6 +553,69 @@ class StreamAligner:
     def close(self):
         for al in self.aligners:
             al.close()
+
+
+def _run_params(pb_paths, coords_path, details_path=None, compact=True, header=True, zero_match=False,
+                aligners_per_device=2, batch_bases=0, host_threads=0):
+    paths = _cstrs([p if isinstance(p, bytes) else str(p).encode() for p in pb_paths])
+    rp = RunParams(paths, len(pb_paths), coords_path.encode() if coords_path else None,
+                   details_path.encode() if details_path else None, int(compact), int(header), int(zero_match),
+                   aligners_per_device, int(batch_bases), host_threads)
+    return rp, paths
+
+
+def _index_handles(indexes):
+    if isinstance(indexes, Index):
+        indexes = [indexes]
+    return (C.c_void_p * len(indexes))(*[ix.h.value if isinstance(ix.h, C.c_void_p) else ix.h for ix in indexes])
+
+
+_RUN_KEYS = ("details_path", "compact", "header", "zero_match", "aligners_per_device", "batch_bases", "host_threads")
+
+
+def run(indexes, pb_paths, coords_path, **kw):
+    """pbgpu_run: PacBio files -> coords file, on every listed index (one per device, repeats allowed).
+    Returns the run's stage statistics."""
+    rkw = {k: kw.pop(k) for k in list(kw) if k in _RUN_KEYS}
+    p, keep = align_params(**kw)
+    rp, paths = _run_params(pb_paths, coords_path, **rkw)
+    st = RunStats()
+    hs = _index_handles(indexes)
+    _check(lib().pbgpu_run(hs, len(hs), C.byref(p), C.byref(rp), C.byref(st)))
+    del keep
+    return st.as_dict()
+
+
+class Runner:
+    """pbgpu_runner: the driver's aligners and pinned buffers kept across runs."""
+
+    def __init__(self, indexes, aligners_per_device=2, batch_bases=0, details=False, **align_kw):
+        self._p, self._keep = align_params(**align_kw)
+        self.details = details
+        rp, _ = _run_params([], None, details_path="-" if details else None, aligners_per_device=aligners_per_device,
+                            batch_bases=batch_bases)
+        hs = _index_handles(indexes)
+        h = C.c_void_p()
+        _check(lib().pbgpu_runner_create(hs, len(hs), C.byref(self._p), C.byref(rp), C.byref(h)))
+        self.h = h
+
+    def run(self, pb_paths, coords_path, details_path=None, compact=True, header=True, zero_match=False,
+            host_threads=0):
+        rp, paths = _run_params(pb_paths, coords_path, details_path, compact, header, zero_match, 0, 0, host_threads)
+        st = RunStats()
+        _check(lib().pbgpu_runner_run(self.h, C.byref(rp), C.byref(st)))
+        return st.as_dict()
+
+    def close(self):
+        if self.h:
+            lib().pbgpu_runner_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def rccl_unique_id():

@@ -1,0 +1,145 @@
+"""Device coords text (pbgpu_format_device) and the file-to-file driver
+(pbgpu_run, the jf_aligner CLI): byte-identical to the host formatter and,
+per read, to the CPU restatement (oracle/), for every parity configuration,
+multi-batch / multi-aligner / two-index ("--devices 0,0") runs, gzip input,
+and the worker error path."""
+import gzip
+import os
+import shutil
+import subprocess
+import tempfile
+
+import pytest
+
+from tests._compare import assert_same_coords
+from tests.test_gpu_parity import CONFIGS
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(ROOT, "pacbio_amd", "bin", "jf_aligner")
+
+
+@pytest.fixture(scope="module")
+def small():
+    from tools.synth import Dataset
+    return Dataset("small", seed=7)
+
+
+@pytest.fixture(scope="module")
+def small_dir(small):
+    d = tempfile.mkdtemp(prefix="pbgpu_fmt_")
+    small.write(d)
+    yield d
+    shutil.rmtree(d, ignore_errors=True)
+
+
+def _split(cfg):
+    cfg = dict(cfg)
+    k = cfg.pop("k", 17)
+    use_ul = cfg.pop("use_ul", False)
+    return k, use_ul, cfg
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_device_text_matches_host_and_oracle(small, name):
+    from oracle.oracle import OracleIndex, params
+    from pacbio_amd import pbgpu
+    k, use_ul, cfg = _split(CONFIGS[name])
+    ul = small.unitig_lengths if use_ul else None
+    names, seqs = small.sr_names(), small.sr_seqs()
+    pnames, pseqs = small.pb_names(), small.pb_seqs()
+    gix = pbgpu.Index.from_records(names, seqs, k)
+    al = pbgpu.Aligner(gix, k=k, unitig_lengths=ul, **cfg)
+    rd = al.upload(pseqs, names=pnames)
+    al.align_resident(rd)
+    dev = al.format_device(rd)
+    host = al.download().format(gix, pnames, [len(s) for s in pseqs])
+    assert dev == host
+    exp = OracleIndex.from_records(names, seqs, k).align_format(params(k=k, unitig_lengths=ul, **cfg), pnames, pseqs,
+                                                                threads=8)
+    assert_same_coords(dev, exp, name)
+    # non-compact lines and -0 headers
+    assert al.format_device(rd, compact=False, zero_match=True) == \
+        al.download().format(gix, pnames, [len(s) for s in pseqs], compact=False, zero_match=True)
+    rd.close()
+
+
+def _oracle_file_text(ds, k=17, **cfg):
+    from oracle.oracle import OracleIndex, params
+    oix = OracleIndex.from_records(ds.sr_names(), ds.sr_seqs(), k)
+    return oix.align_format(params(k=k, **cfg), ds.pb_names(), ds.pb_seqs(), threads=8, header=True)
+
+
+def test_run_many_batches_two_indexes(small, small_dir):
+    """pbgpu_run: tiny batches over 2 x 3 aligners on two index entries of
+    device 0 (--devices 0,0) give the one-batch bytes, which match the oracle."""
+    from pacbio_amd import pbgpu
+    kw = dict(forward=True, unitigs_k=31, unitig_lengths=small.unitig_lengths, bases_matching=15.0)
+    gix = pbgpu.Index.from_fasta([os.path.join(small_dir, "sr.fa")], 17)
+    rep = gix.replicate(0)
+    pb = [os.path.join(small_dir, "pb.fa")]
+    out1, out2 = os.path.join(small_dir, "one.coords"), os.path.join(small_dir, "many.coords")
+    st1 = pbgpu.run([gix], pb, out1, aligners_per_device=1, **kw)
+    st2 = pbgpu.run([gix, rep], pb, out2, aligners_per_device=3, batch_bases=20_000, **kw)
+    one, many = open(out1).read(), open(out2).read()
+    assert st1["n_batches"] == 1 and st2["n_batches"] > 8
+    assert st2["n_bases"] == st1["n_bases"] and st2["coords_bytes"] == len(many.encode())
+    assert many == one
+    assert_same_coords(one, _oracle_file_text(small, **kw), "run")
+    rep.close()
+    gix.close()
+
+
+def test_run_gzip_input(small, small_dir):
+    from pacbio_amd import pbgpu
+    pb = os.path.join(small_dir, "pb.fa")
+    gz = os.path.join(small_dir, "pb.fa.gz")
+    with open(pb, "rb") as f, gzip.open(gz, "wb") as g:
+        g.write(f.read())
+    gix = pbgpu.Index.from_fasta([os.path.join(small_dir, "sr.fa")], 17)
+    a, b = os.path.join(small_dir, "plain.coords"), os.path.join(small_dir, "gz.coords")
+    pbgpu.run([gix], [pb], a, batch_bases=50_000)
+    pbgpu.run([gix], [gz], b, batch_bases=50_000)
+    assert open(a).read() == open(b).read()
+    assert open(a).read().count("\n") > 100
+    gix.close()
+
+
+def test_run_error_is_returned(small_dir):
+    """a missing PacBio file fails the run with PBGPU_ERR_IO (reader thread error, no exit, no hang)"""
+    from pacbio_amd import pbgpu
+    gix = pbgpu.Index.from_fasta([os.path.join(small_dir, "sr.fa")], 17)
+    with pytest.raises(pbgpu.PbgpuError) as e:
+        pbgpu.run([gix], [os.path.join(small_dir, "pb.fa"), os.path.join(small_dir, "missing.fa")],
+                  os.path.join(small_dir, "err.coords"), batch_bases=20_000)
+    assert e.value.status == 2
+    gix.close()
+
+
+def test_cli_devices_and_gzip(small, small_dir):
+    """jf_aligner --devices 0,0 and gzip input: the same bytes as one device and plain FASTA."""
+    gz = os.path.join(small_dir, "pb2.fa.gz")
+    with open(os.path.join(small_dir, "pb.fa"), "rb") as f, gzip.open(gz, "wb") as g:
+        g.write(f.read())
+    base = [CLI, "-s", "1", "-m", "17", "-r", os.path.join(small_dir, "sr.fa"), "-l", os.path.join(small_dir, "ul.txt"),
+            "-k", "31", "-f", "-B", "15", "--coords", "/dev/stdout"]
+    r1 = subprocess.run(base + ["-p", os.path.join(small_dir, "pb.fa")], capture_output=True, text=True, timeout=300)
+    r2 = subprocess.run(base + ["-p", gz, "--devices", "0,0", "--batch-bases", "30k", "--timing"], capture_output=True,
+                        text=True, timeout=300)
+    assert r1.returncode == 0, r1.stderr
+    assert r2.returncode == 0, r2.stderr
+    assert r1.stdout == r2.stdout
+    assert '"wall_s"' in r2.stderr
+    assert_same_coords(r1.stdout, _oracle_file_text(small, forward=True, unitigs_k=31,
+                                                     unitig_lengths=small.unitig_lengths, bases_matching=15.0), "cli")
+
+
+def test_cli_bad_input_exits_1(small_dir):
+    bad = os.path.join(small_dir, "bad.fa")
+    with open(bad, "w") as f:
+        f.write("not a fasta\nACGT\n")
+    r = subprocess.run([CLI, "-s", "1", "-m", "17", "-r", os.path.join(small_dir, "sr.fa"), "-p", bad, "--coords",
+                        "/dev/null"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 1
+    assert "neither FASTA nor FASTQ" in r.stderr

@@ -1,0 +1,64 @@
+// Page-cache write bandwidth probe: one file of `gib` GiB written from a
+// host buffer by (a) one write() stream, (b) T threads pwrite()ing disjoint
+// ranges, (c) T threads memcpy()ing into a shared mmap of the file.
+// usage: probe_write <path> <gib> <threads...>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+static double now() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int main(int argc, char** argv) {
+  if (argc < 4) { fprintf(stderr, "usage: probe_write path gib threads...\n"); return 1; }
+  const char* path = argv[1];
+  const size_t N = (size_t)(atof(argv[2]) * (1ull << 30));
+  std::vector<char> src(N);
+  for (size_t i = 0; i < N; ++i) src[i] = "ACGT 0123456789\n"[i & 15];
+  for (int a = 3; a < argc; ++a) {
+    const int T = atoi(argv[a]);
+    for (int mode = 0; mode < 3; ++mode) {
+      if (mode == 0 && T != 1) continue;
+      unlink(path);
+      int fd = open(path, O_CREAT | O_RDWR | O_TRUNC, 0644);
+      if (fd < 0) { perror("open"); return 1; }
+      const double t0 = now();
+      if (mode == 0) {
+        size_t o = 0;
+        while (o < N) { ssize_t w = write(fd, src.data() + o, std::min<size_t>(N - o, 64 << 20)); if (w <= 0) { perror("write"); return 1; } o += (size_t)w; }
+      } else if (mode == 1) {
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; ++t)
+          th.emplace_back([&, t] {
+            size_t a0 = N * t / T, a1 = N * (t + 1) / T;
+            while (a0 < a1) { ssize_t w = pwrite(fd, src.data() + a0, std::min<size_t>(a1 - a0, 64 << 20), (off_t)a0); if (w <= 0) { perror("pwrite"); exit(1); } a0 += (size_t)w; }
+          });
+        for (auto& x : th) x.join();
+      } else {
+        if (ftruncate(fd, (off_t)N)) { perror("ftruncate"); return 1; }
+        char* m = (char*)mmap(nullptr, N, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        if (m == MAP_FAILED) { perror("mmap"); return 1; }
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; ++t)
+          th.emplace_back([&, t] { size_t a0 = N * t / T, a1 = N * (t + 1) / T; memcpy(m + a0, src.data() + a0, a1 - a0); });
+        for (auto& x : th) x.join();
+        munmap(m, N);
+      }
+      close(fd);
+      const double dt = now() - t0;
+      printf("%s threads=%d %.2f GB/s (%.3f s)\n", mode == 0 ? "write" : mode == 1 ? "pwrite" : "mmap", T, N / dt / 1e9, dt);
+      fflush(stdout);
+    }
+  }
+  unlink(path);
+  return 0;
+}
