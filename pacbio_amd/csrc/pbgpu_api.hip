@@ -26,14 +26,18 @@
 
 namespace pbgpu {
 // kernels (pbgpu_kernels.hip)
-void launch_build_keys(IndexView ix, uint32_t km, uint32_t K, uint32_t ebits, uint64_t N, uint64_t* keys, uint64_t* vals,
-                       hipStream_t st);
+void launch_build_keys(IndexView ix, uint32_t km, uint32_t K, uint32_t ebits, uint64_t N, const uint64_t* sel,
+                       uint64_t Nsel, uint64_t* keys, uint64_t* vals, hipStream_t st);
+void launch_part_ids(IndexView ix, uint32_t km, uint64_t N, uint32_t P, uint8_t* pid, unsigned long long* hist,
+                     hipStream_t st);
+void launch_table_insert(const ulonglong2* kh, uint64_t U, uint64_t base, ulonglong2* table, uint64_t bucket_mask,
+                         uint64_t* filt, uint32_t filt_shift, hipStream_t st);
 void launch_runs(const uint64_t* keys, const uint64_t* uidx, uint64_t N, uint32_t sh, uint64_t* run_start, hipStream_t st);
 void launch_occ_fill(const uint64_t* vals, const uint64_t* uidx, const uint64_t* kpos, uint64_t N, uint64_t* occ,
                      hipStream_t st);
 void launch_headers(const uint64_t* keys, const uint64_t* kpos, const uint64_t* run_start, uint64_t U, uint64_t* occ,
                     ulonglong2* table, uint64_t bucket_mask, uint32_t k, uint32_t ebits, uint64_t* filt,
-                    uint32_t filt_shift, hipStream_t st);
+                    uint32_t filt_shift, ulonglong2* kh, hipStream_t st);
 enum { SEED_WHOLE = 0, SEED_COUNTS = 1, SEED_FINISH = 2 };  // k_seed modes (pbgpu_kernels.hip)
 void launch_seed(int mode, IndexView ix, const uint8_t* seq, const uint64_t* roff, uint32_t n_reads, AlignParamsDev P,
                  KRec* krec, uint32_t* n_kept, uint32_t* thr, uint64_t* nhits, unsigned long long* stats,
@@ -168,10 +172,94 @@ static void load_fasta(const char* path, text_builder& tb) {
   }
 }
 
+// One sorted run of (key, value) pairs -> occurrence lists.  keys/vals hold
+// M sorted pairs (spare_k / spare_v: scratch of M entries each); writes the
+// lists and headers into `occ` (block-local header indices) and either inserts
+// the k-mers into `table` or, with kh, returns {canon, payload} per k-mer.
+struct RunsOut { uint64_t U = 0, kept = 0; };
+static RunsOut lists_from_sorted(uint64_t* keys, uint64_t* vals, uint64_t* spare_k, uint64_t* spare_v, uint64_t M,
+                                 uint32_t km, uint32_t ebits, hipStream_t st, dbuf<uint8_t>& tmp, dbuf<uint64_t>& occ,
+                                 dbuf<ulonglong2>* table, uint64_t* n_buckets, dbuf<uint64_t>* filt, uint32_t* filt_log2,
+                                 dbuf<ulonglong2>* kh) {
+  const uint32_t sh = ebits + 1;  // keys >> sh = canonical km-mer
+  // uidx = inclusive scan of run heads (into spare_k), kpos = exclusive scan of keep (M+1, into a new buffer)
+  struct HeadOp {
+    const uint64_t* keys; uint32_t sh;
+    __host__ __device__ uint64_t operator()(const uint64_t& i) const {
+      return (i == 0 || (keys[i] >> sh) != (keys[i - 1] >> sh)) ? 1ull : 0ull;
+    }
+  };
+  struct KeepOp {
+    const uint64_t* vals; uint64_t N;
+    __host__ __device__ uint64_t operator()(const uint64_t& i) const { return (i < N && vals[i] != ~0ull) ? 1ull : 0ull; }
+  };
+  hipcub::CountingInputIterator<uint64_t> cnt(0);
+  hipcub::TransformInputIterator<uint64_t, HeadOp, hipcub::CountingInputIterator<uint64_t>> heads(cnt, HeadOp{keys, sh});
+  uint64_t* uidx = spare_k;
+  size_t tbytes = 0;
+  HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tbytes, heads, uidx, M, st));
+  HIPCHK(hipcub::DeviceScan::InclusiveSum(temp_storage(tmp, tbytes), tbytes, heads, uidx, M, st));
+  dbuf<uint64_t> kpos;
+  kpos.alloc(M + 1);
+  hipcub::TransformInputIterator<uint64_t, KeepOp, hipcub::CountingInputIterator<uint64_t>> keeps(cnt, KeepOp{vals, M});
+  tbytes = 0;
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tbytes, keeps, kpos.p, M + 1, st));
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(temp_storage(tmp, tbytes), tbytes, keeps, kpos.p, M + 1, st));
+  RunsOut o;
+  HIPCHK(hipMemcpyAsync(&o.U, uidx + M - 1, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&o.kept, kpos.p + M, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const uint64_t U = o.U, kept = o.kept;
+  uint64_t* run_start = spare_v;  // U + 1 <= M + 1 ... spare_v has M entries; U < M unless all distinct
+  dbuf<uint64_t> rs_extra;
+  if (U + 1 > M) { rs_extra.alloc(U + 1); run_start = rs_extra.p; }
+  launch_runs(keys, uidx, M, sh, run_start, st);
+  HIPCHK(hipMemcpyAsync(run_start + U, &M, 8, hipMemcpyHostToDevice, st));
+  occ.alloc(2 * U + kept + 2);  // + an empty header {0, 0} at 2U + kept (the whole index's null_ptr)
+  HIPCHK(hipMemsetAsync(occ.p + 2 * U + kept, 0, 16, st));
+  launch_occ_fill(vals, uidx, kpos.p, M, occ.p, st);
+  ulonglong2* tp = nullptr;
+  uint64_t buckets = 1;
+  uint64_t* fp = nullptr;
+  uint32_t flog = 0;
+  if (table) {
+    while (buckets * 2 < U) buckets <<= 1;  // slots = 4*buckets >= 2U: load <= 0.5
+    *n_buckets = buckets;
+    table->alloc(4 * buckets);
+    HIPCHK(hipMemsetAsync(table->p, 0xFF, table->bytes(), st));
+    tp = table->p;
+    // presence filter: PBGPU_FILTER_BITS bits per k-mer (default 16, 0 = none), a power of two of words
+    if (filt) {
+      const char* e = getenv("PBGPU_FILTER_BITS");
+      const uint64_t bits = e ? strtoull(e, nullptr, 10) : 16;
+      if (bits) {
+        flog = 6;  // >= 64 words
+        while ((1ull << flog) < U * bits / 64) ++flog;
+        filt->alloc(1ull << flog);
+        HIPCHK(hipMemsetAsync(filt->p, 0, filt->bytes(), st));
+        fp = filt->p;
+        *filt_log2 = flog;
+      }
+    }
+  } else {
+    kh->alloc(U + 1);
+  }
+  launch_headers(keys, kpos.p, run_start, U, occ.p, tp, buckets - 1, km, ebits, fp, 64 - flog, kh ? kh->p : nullptr, st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(st));  // the temporaries above are freed on return
+  return o;
+}
+
 // Hash table + occurrence lists of the km-mers of the text (layout in
 // pbgpu_internal.h): sort keys (k_build_keys) -> radix sort -> runs of equal
 // canonical km-mer -> occurrence lists and headers -> table.  ebits > 0
 // orders each list by the K - km bases that follow (the fine sub-index).
+// A text whose sort buffers (~48 B a position) do not fit beside the index is
+// built in P partitions by hash of the canonical km-mer (all occurrences of a
+// km-mer in one partition): each partition is selected in enumeration order
+// (stable), sorted and turned into its own occurrence block and k-mer list;
+// the blocks are then laid end to end and the k-mers inserted into one table.
+// PBGPU_BUILD_PARTS forces P (tests).
 static void build_kmer_table(pbgpu_index* ix, uint32_t km, uint32_t K, uint32_t ebits, hipStream_t st,
                              dbuf<ulonglong2>& table, dbuf<uint64_t>& occ, uint64_t& n_buckets, uint64_t& n_kmers,
                              uint64_t& n_occ, dbuf<uint64_t>* filt = nullptr, uint32_t* filt_log2 = nullptr) {
@@ -187,70 +275,120 @@ static void build_kmer_table(pbgpu_index* ix, uint32_t km, uint32_t K, uint32_t 
     return;
   }
   const int key_bits = (int)(2 * km + 1 + ebits);
-  dbuf<uint64_t> k0, k1, v0, v1;
-  k0.alloc(N); k1.alloc(N); v0.alloc(N); v1.alloc(N);
-  launch_build_keys(v, km, K, ebits, N, k0.p, v0.p, st);
-  HIPCHK(hipGetLastError());
-  dbuf<uint8_t> tmp;
-  size_t tbytes = 0;
-  hipcub::DoubleBuffer<uint64_t> dk(k0.p, k1.p), dv(v0.p, v1.p);
-  HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tbytes, dk, dv, N, 0, key_bits, st));
-  HIPCHK(hipcub::DeviceRadixSort::SortPairs(temp_storage(tmp, tbytes), tbytes, dk, dv, N, 0, key_bits, st));
-  uint64_t* keys = dk.Current();
-  uint64_t* vals = dv.Current();
-  uint64_t* spare_k = dk.Alternate();
-  uint64_t* spare_v = dv.Alternate();
-  const uint32_t sh = ebits + 1;  // keys >> sh = canonical km-mer
-  // uidx = inclusive scan of run heads (into spare_k), kpos = exclusive scan of keep (N+1, into a new buffer)
-  struct HeadOp {
-    const uint64_t* keys; uint32_t sh;
-    __host__ __device__ uint64_t operator()(const uint64_t& i) const {
-      return (i == 0 || (keys[i] >> sh) != (keys[i - 1] >> sh)) ? 1ull : 0ull;
+  uint32_t P = 1;
+  if (const char* e = getenv("PBGPU_BUILD_PARTS")) {
+    P = (uint32_t)std::max(1l, std::min(255l, strtol(e, nullptr, 10)));
+  } else {
+    size_t free_b = 0, total_b = 0;
+    HIPCHK(hipMemGetInfo(&free_b, &total_b));
+    // one pass: 4 sort arrays + scan + lists ~56 B a position; partitioned: ~48 B a
+    // partition position + the finished blocks (~9 B a position) + 1 B of partition ids
+    if (56.0 * N > 0.8 * (double)free_b || N >= (1ull << 31)) {
+      P = 2;
+      while (P < 255 && (48.0 * N / P + 10.0 * N > 0.8 * (double)free_b || N / P >= (1ull << 31))) P *= 2;
+      if (P > 255) P = 255;
     }
-  };
-  struct KeepOp {
-    const uint64_t* vals; uint64_t N;
-    __host__ __device__ uint64_t operator()(const uint64_t& i) const { return (i < N && vals[i] != ~0ull) ? 1ull : 0ull; }
-  };
-  hipcub::CountingInputIterator<uint64_t> cnt(0);
-  hipcub::TransformInputIterator<uint64_t, HeadOp, hipcub::CountingInputIterator<uint64_t>> heads(cnt, HeadOp{keys, sh});
-  uint64_t* uidx = spare_k;
-  tbytes = 0;
-  HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tbytes, heads, uidx, N, st));
-  HIPCHK(hipcub::DeviceScan::InclusiveSum(temp_storage(tmp, tbytes), tbytes, heads, uidx, N, st));
-  dbuf<uint64_t> kpos;
-  kpos.alloc(N + 1);
-  hipcub::TransformInputIterator<uint64_t, KeepOp, hipcub::CountingInputIterator<uint64_t>> keeps(cnt, KeepOp{vals, N});
-  tbytes = 0;
-  HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tbytes, keeps, kpos.p, N + 1, st));
-  HIPCHK(hipcub::DeviceScan::ExclusiveSum(temp_storage(tmp, tbytes), tbytes, keeps, kpos.p, N + 1, st));
+  }
+  if (P == 1) {
+    dbuf<uint64_t> k0, k1, v0, v1;
+    k0.alloc(N); k1.alloc(N); v0.alloc(N); v1.alloc(N);
+    launch_build_keys(v, km, K, ebits, N, nullptr, N, k0.p, v0.p, st);
+    HIPCHK(hipGetLastError());
+    dbuf<uint8_t> tmp;
+    size_t tbytes = 0;
+    hipcub::DoubleBuffer<uint64_t> dk(k0.p, k1.p), dv(v0.p, v1.p);
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tbytes, dk, dv, N, 0, key_bits, st));
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(temp_storage(tmp, tbytes), tbytes, dk, dv, N, 0, key_bits, st));
+    const RunsOut o = lists_from_sorted(dk.Current(), dv.Current(), dk.Alternate(), dv.Alternate(), N, km, ebits, st,
+                                        tmp, occ, &table, &n_buckets, filt, filt_log2, nullptr);
+    n_kmers = o.U;
+    n_occ = o.kept;
+    return;
+  }
+  // ---- partitioned build
+  std::vector<uint64_t> Np(P);
+  dbuf<uint8_t> pid, tmp;
+  pid.alloc(N);
+  {
+    dbuf<unsigned long long> hist;
+    hist.alloc(P);
+    HIPCHK(hipMemsetAsync(hist.p, 0, P * 8, st));
+    launch_part_ids(v, km, N, P, pid.p, hist.p, st);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(Np.data(), hist.p, P * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  const uint64_t maxNp = std::max<uint64_t>(1, *std::max_element(Np.begin(), Np.end()));
+  std::vector<dbuf<uint64_t>> blocks(P);
+  std::vector<dbuf<ulonglong2>> khs(P);
+  std::vector<RunsOut> ro(P);
+  {
+    dbuf<uint64_t> sel, k0, k1, v0, v1, nsel;
+    sel.alloc(maxNp); k0.alloc(maxNp); k1.alloc(maxNp); v0.alloc(maxNp); v1.alloc(maxNp); nsel.alloc(1);
+    struct PidSel {
+      const uint8_t* pid; uint8_t p;
+      __host__ __device__ bool operator()(const uint64_t& i) const { return pid[i] == p; }
+    };
+    for (uint32_t p = 0; p < P; ++p) {
+      // stable selection of the partition's enumeration indices, in chunks of < 2^31 items
+      uint64_t got = 0;
+      for (uint64_t c0 = 0; c0 < N; c0 += (1ull << 30)) {
+        const int cn = (int)std::min<uint64_t>(N - c0, 1ull << 30);
+        hipcub::CountingInputIterator<uint64_t> it(c0);
+        size_t tb = 0;
+        HIPCHK(hipcub::DeviceSelect::If(nullptr, tb, it, sel.p + got, nsel.p, cn, PidSel{pid.p, (uint8_t)p}, st));
+        HIPCHK(hipcub::DeviceSelect::If(temp_storage(tmp, tb), tb, it, sel.p + got, nsel.p, cn,
+                                        PidSel{pid.p, (uint8_t)p}, st));
+        uint64_t ns = 0;
+        HIPCHK(hipMemcpyAsync(&ns, nsel.p, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        got += ns & 0xFFFFFFFFull;  // DeviceSelect writes the count as its offset type (int / uint32)
+      }
+      if (got != Np[p]) throw std::runtime_error("partitioned index build: selection count mismatch");
+      const uint64_t M = Np[p];
+      if (M == 0) {
+        blocks[p].alloc(1);
+        ro[p] = RunsOut{};
+        continue;
+      }
+      launch_build_keys(v, km, K, ebits, N, sel.p, M, k0.p, v0.p, st);
+      HIPCHK(hipGetLastError());
+      size_t tbytes = 0;
+      hipcub::DoubleBuffer<uint64_t> dk(k0.p, k1.p), dv(v0.p, v1.p);
+      HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tbytes, dk, dv, M, 0, key_bits, st));
+      HIPCHK(hipcub::DeviceRadixSort::SortPairs(temp_storage(tmp, tbytes), tbytes, dk, dv, M, 0, key_bits, st));
+      ro[p] = lists_from_sorted(dk.Current(), dv.Current(), dk.Alternate(), dv.Alternate(), M, km, ebits, st, tmp,
+                                blocks[p], nullptr, nullptr, nullptr, nullptr, &khs[p]);
+    }
+  }
+  pid.release();
+  tmp.release();
   uint64_t U = 0, kept = 0;
-  HIPCHK(hipMemcpyAsync(&U, uidx + N - 1, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(&kept, kpos.p + N, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  uint64_t* run_start = spare_v;  // U + 1 <= N + 1 ... spare_v has N entries; U < N unless all distinct
-  dbuf<uint64_t> rs_extra;
-  if (U + 1 > N) { rs_extra.alloc(U + 1); run_start = rs_extra.p; }
-  launch_runs(keys, uidx, N, sh, run_start, st);
-  HIPCHK(hipMemcpyAsync(run_start + U, &N, 8, hipMemcpyHostToDevice, st));
-  n_kmers = U;
-  n_occ = kept;
-  occ.alloc(2 * U + kept + 2);  // + an empty header {0, 0} at 2U + kept (index null_ptr)
-  HIPCHK(hipMemsetAsync(occ.p + 2 * U + kept, 0, 16, st));
+  for (uint32_t p = 0; p < P; ++p) { U += ro[p].U; kept += ro[p].kept; }
+  occ.alloc(2 * U + kept + 2);
+  HIPCHK(hipMemsetAsync(occ.p + 2 * U + kept, 0, 16, st));  // the null header
+  std::vector<uint64_t> base(P);
+  uint64_t b = 0;
+  for (uint32_t p = 0; p < P; ++p) {
+    base[p] = b;
+    const uint64_t len = 2 * ro[p].U + ro[p].kept;
+    if (len) HIPCHK(hipMemcpyAsync(occ.p + b, blocks[p].p, len * 8, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
+    blocks[p].release();
+    b += len;
+  }
   uint64_t buckets = 1;
-  while (buckets * 2 < U) buckets <<= 1;  // slots = 4*buckets >= 2U: load <= 0.5
+  while (buckets * 2 < U) buckets <<= 1;
   n_buckets = buckets;
   table.alloc(4 * buckets);
   HIPCHK(hipMemsetAsync(table.p, 0xFF, table.bytes(), st));
-  launch_occ_fill(vals, uidx, kpos.p, N, occ.p, st);
-  // presence filter: PBGPU_FILTER_BITS bits per k-mer (default 16, 0 = none), a power of two of words
   uint64_t* fp = nullptr;
   uint32_t flog = 0;
   if (filt) {
     const char* e = getenv("PBGPU_FILTER_BITS");
     const uint64_t bits = e ? strtoull(e, nullptr, 10) : 16;
     if (bits) {
-      flog = 6;  // >= 64 words
+      flog = 6;
       while ((1ull << flog) < U * bits / 64) ++flog;
       filt->alloc(1ull << flog);
       HIPCHK(hipMemsetAsync(filt->p, 0, filt->bytes(), st));
@@ -258,9 +396,13 @@ static void build_kmer_table(pbgpu_index* ix, uint32_t km, uint32_t K, uint32_t 
       *filt_log2 = flog;
     }
   }
-  launch_headers(keys, kpos.p, run_start, U, occ.p, table.p, buckets - 1, km, ebits, fp, 64 - flog, st);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(st));  // the temporaries above are freed on return
+  for (uint32_t p = 0; p < P; ++p) {
+    if (ro[p].U) launch_table_insert(khs[p].p, ro[p].U, base[p], table.p, buckets - 1, fp, 64 - flog, st);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  n_kmers = U;
+  n_occ = kept;
 }
 
 static void build_device_index(pbgpu_index* ix, text_builder& tb) {

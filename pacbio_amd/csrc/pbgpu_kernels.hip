@@ -177,9 +177,14 @@ DEV bool filt_test(const IndexView& ix, uint64_t key) {
 // (sort_one_mer, mer_sa_imp.hpp:351-364: extension lexicographic, a truncated
 // one first, then x descending).  Positions are enumerated in descending
 // order so the stable radix sort keeps x descending among equal keys.
-__global__ void k_build_keys(IndexView ix, uint32_t km, uint32_t K, uint32_t ebits, uint64_t N, uint64_t* keys,
-                             uint64_t* vals) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < N; i += (uint64_t)gridDim.x * blockDim.x) {
+// Partitioned build (indexes too large to sort at once, e.g. C4's 10 Gbp):
+// sel lists the enumeration indices i of one partition (ascending, so the
+// order among equal keys is still x descending); key j of the output is
+// position N - 1 - sel[j].  sel == nullptr: every position, Nsel == N.
+__global__ void k_build_keys(IndexView ix, uint32_t km, uint32_t K, uint32_t ebits, uint64_t N, const uint64_t* sel,
+                             uint64_t Nsel, uint64_t* keys, uint64_t* vals) {
+  for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < Nsel; j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = sel ? sel[j] : j;
     const uint64_t x = N - 1 - i;
     const uint64_t f = text_kmer(ix.text, x, km);
     const uint64_t r = revcomp(f, km);
@@ -195,10 +200,35 @@ __global__ void k_build_keys(IndexView ix, uint32_t km, uint32_t K, uint32_t ebi
       const uint64_t ext = K > km ? text_kmer(ix.text, x + km, K - km) : 0;  // text is zero past n
       key = (key << ebits) | (ext << 1) | (x + K <= ix.n ? 1u : 0u);
     }
-    keys[i] = key;
-    vals[i] = cross ? ~0ull : (((uint64_t)s << 32) | (uint32_t)(x - ix.sr_start[s] + 1));
+    keys[j] = key;
+    vals[j] = cross ? ~0ull : (((uint64_t)s << 32) | (uint32_t)(x - ix.sr_start[s] + 1));
   }
 }
+
+// partition of the canonical km-mer at enumeration index i (x = N - 1 - i): all
+// occurrences of a km-mer fall in one partition, so its list stays contiguous
+DEV uint32_t kmer_part(uint64_t canon, uint32_t P) { return (uint32_t)(((fmix64(canon) >> 32) * P) >> 32); }
+__global__ void k_part_ids(IndexView ix, uint32_t km, uint64_t N, uint32_t P, uint8_t* pid,
+                           unsigned long long* hist) {
+  __shared__ unsigned long long s_h[256];
+  for (uint32_t t = threadIdx.x; t < P; t += blockDim.x) s_h[t] = 0;
+  __syncthreads();
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < N; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t x = N - 1 - i;
+    const uint64_t f = text_kmer(ix.text, x, km);
+    const uint64_t r = revcomp(f, km);
+    const uint32_t p = kmer_part(f < r ? f : r, P);
+    pid[i] = (uint8_t)p;
+    atomicAdd(&s_h[p], 1ull);
+  }
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < P; t += blockDim.x) if (s_h[t]) atomicAdd(&hist[t], s_h[t]);
+}
+
+// the table entries of a partition's k-mers (k_headers with kh != null), moved to
+// the final occurrence array at base: payload += base << 24
+__global__ void k_table_insert(const ulonglong2* kh, uint64_t U, uint64_t base, ulonglong2* table, uint64_t bucket_mask,
+                               unsigned long long* filt, uint32_t filt_shift);
 
 __global__ void k_runs(const uint64_t* keys, const uint64_t* uidx, uint64_t N, uint32_t sh, uint64_t* run_start) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < N; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -214,9 +244,35 @@ __global__ void k_occ_fill(const uint64_t* vals, const uint64_t* uidx, const uin
   }
 }
 
+DEV void table_put(ulonglong2* table, uint64_t bucket_mask, uint64_t canon, uint64_t payload, unsigned long long* filt,
+                   uint32_t filt_shift) {
+  if (filt) {
+    const uint64_t h = filt_hash(canon);
+    atomicOr(filt + (h >> filt_shift), (unsigned long long)filt_bits(h));
+  }
+  uint64_t b = fmix64(canon) & bucket_mask;
+  for (;;) {
+    for (int sl = 0; sl < 4; ++sl) {
+      unsigned long long* kp = (unsigned long long*)&table[4 * b + sl].x;
+      const unsigned long long old = atomicCAS(kp, (unsigned long long)EMPTY_KEY, (unsigned long long)canon);
+      if (old == EMPTY_KEY) { table[4 * b + sl].y = payload; return; }
+    }
+    b = (b + 1) & bucket_mask;
+  }
+}
+
+__global__ void k_table_insert(const ulonglong2* kh, uint64_t U, uint64_t base, ulonglong2* table, uint64_t bucket_mask,
+                               unsigned long long* filt, uint32_t filt_shift) {
+  for (uint64_t u = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; u < U; u += (uint64_t)gridDim.x * blockDim.x) {
+    const ulonglong2 e = kh[u];
+    table_put(table, bucket_mask, e.x, e.y + (base << 24), filt, filt_shift);
+  }
+}
+
+// kh != null (partitioned build): {canon, payload} per k-mer instead of the table insert
 __global__ void k_headers(const uint64_t* keys, const uint64_t* kpos, const uint64_t* run_start, uint64_t U,
                           uint64_t* occ, ulonglong2* table, uint64_t bucket_mask, uint32_t k, uint32_t ebits,
-                          unsigned long long* filt, uint32_t filt_shift) {
+                          unsigned long long* filt, uint32_t filt_shift, ulonglong2* kh) {
   for (uint64_t u = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; u < U; u += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t s = run_start[u], e = run_start[u + 1];
     const uint64_t canon = keys[s] >> (ebits + 1);
@@ -230,21 +286,8 @@ __global__ void k_headers(const uint64_t* keys, const uint64_t* kpos, const uint
     occ[hb] = cnt32 | ((uint64_t)pal << 32);
     occ[hb + 1] = nA | (nB << 32);
     const uint64_t payload = (hb << 24) | (count < SAT_COUNT ? count : SAT_COUNT);
-    if (filt) {
-      const uint64_t h = filt_hash(canon);
-      atomicOr(filt + (h >> filt_shift), (unsigned long long)filt_bits(h));
-    }
-    uint64_t b = fmix64(canon) & bucket_mask;
-    for (;;) {
-      bool done = false;
-      for (int sl = 0; sl < 4; ++sl) {
-        unsigned long long* kp = (unsigned long long*)&table[4 * b + sl].x;
-        unsigned long long old = atomicCAS(kp, (unsigned long long)EMPTY_KEY, (unsigned long long)canon);
-        if (old == EMPTY_KEY) { table[4 * b + sl].y = payload; done = true; break; }
-      }
-      if (done) break;
-      b = (b + 1) & bucket_mask;
-    }
+    if (kh) kh[u] = make_ulonglong2(canon, payload);
+    else table_put(table, bucket_mask, canon, payload, filt, filt_shift);
   }
 }
 
@@ -1380,7 +1423,12 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
           const uint32_t i = q * 64 + lane;
           const int src = (lane + 63) & 63;
           int2 pv = make_int2(__shfl(xv[q].x, src, 64), __shfl(xv[q].y, src, 64));
-          if (q > 0 && lane == 0) pv = make_int2(__shfl(xv[q - 1].x, 63, 64), __shfl(xv[q - 1].y, 63, 64));
+          // the previous chunk's last element, shuffled by every lane: a shuffle in
+          // lane-0-only code reads the other lanes' registers as 0 (ds_bpermute
+          // takes nothing from inactive lanes), which once made element 64 look clean
+          const int qp = q > 0 ? q - 1 : 0;
+          const int2 plast = make_int2(__shfl(xv[qp].x, 63, 64), __shfl(xv[qp].y, 63, 64));
+          if (q > 0 && lane == 0) pv = plast;
           const int2 xi = xv[q];
           {  // branch-free: the lanes past n compute on stale values and are masked out
             const bool clean = (xi.y > pv.y) & affine_ok(lp.a, lp.b, lp.C, (double)(xi.x - pv.x), (double)(xi.y - pv.y));
@@ -2296,9 +2344,18 @@ __global__ __launch_bounds__(BLOCK) void k_rec_sort(const Rec* __restrict__ recs
 // ====================================================== launch wrappers
 namespace pbgpu {
 
-void launch_build_keys(IndexView ix, uint32_t km, uint32_t K, uint32_t ebits, uint64_t N, uint64_t* keys, uint64_t* vals,
-                       hipStream_t st) {
-  hipLaunchKernelGGL(k_build_keys, dim3(4096), dim3(256), 0, st, ix, km, K, ebits, N, keys, vals);
+void launch_build_keys(IndexView ix, uint32_t km, uint32_t K, uint32_t ebits, uint64_t N, const uint64_t* sel,
+                       uint64_t Nsel, uint64_t* keys, uint64_t* vals, hipStream_t st) {
+  hipLaunchKernelGGL(k_build_keys, dim3(4096), dim3(256), 0, st, ix, km, K, ebits, N, sel, Nsel, keys, vals);
+}
+void launch_part_ids(IndexView ix, uint32_t km, uint64_t N, uint32_t P, uint8_t* pid, unsigned long long* hist,
+                     hipStream_t st) {
+  hipLaunchKernelGGL(k_part_ids, dim3(4096), dim3(256), 0, st, ix, km, N, P, pid, hist);
+}
+void launch_table_insert(const ulonglong2* kh, uint64_t U, uint64_t base, ulonglong2* table, uint64_t bucket_mask,
+                         uint64_t* filt, uint32_t filt_shift, hipStream_t st) {
+  hipLaunchKernelGGL(k_table_insert, dim3(4096), dim3(256), 0, st, kh, U, base, table, bucket_mask,
+                     (unsigned long long*)filt, filt_shift);
 }
 void launch_runs(const uint64_t* keys, const uint64_t* uidx, uint64_t N, uint32_t sh, uint64_t* run_start, hipStream_t st) {
   hipLaunchKernelGGL(k_runs, dim3(4096), dim3(256), 0, st, keys, uidx, N, sh, run_start);
@@ -2309,9 +2366,9 @@ void launch_occ_fill(const uint64_t* vals, const uint64_t* uidx, const uint64_t*
 }
 void launch_headers(const uint64_t* keys, const uint64_t* kpos, const uint64_t* run_start, uint64_t U, uint64_t* occ,
                     ulonglong2* table, uint64_t bucket_mask, uint32_t k, uint32_t ebits, uint64_t* filt,
-                    uint32_t filt_shift, hipStream_t st) {
+                    uint32_t filt_shift, ulonglong2* kh, hipStream_t st) {
   hipLaunchKernelGGL(k_headers, dim3(4096), dim3(256), 0, st, keys, kpos, run_start, U, occ, table, bucket_mask, k, ebits,
-                     (unsigned long long*)filt, filt_shift);
+                     (unsigned long long*)filt, filt_shift, kh);
 }
 
 #ifndef PBGPU_SEED_PER

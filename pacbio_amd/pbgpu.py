@@ -267,6 +267,14 @@ class Index:
         _check(lib().pbgpu_index_build(_cstrs(names), _cstrs(bs), lens, len(bs), C.byref(p), C.byref(h)))
         return cls(h)
 
+    @classmethod
+    def from_pointers(cls, names, seqs, lens, n, k, psa_min=13, device=0, threads=0, fine_k=0, shard=0, n_shards=1):
+        """pbgpu_index_build on caller-owned C arrays (names / seqs: char* arrays, lens: uint64)"""
+        p = IndexParams(k, psa_min, device, threads, fine_k, shard, n_shards)
+        h = C.c_void_p()
+        _check(lib().pbgpu_index_build(names, seqs, lens, n, C.byref(p), C.byref(h)))
+        return cls(h)
+
     def replicate(self, device):
         """pbgpu_index_replicate: the same index on another device (or a second copy on this one)"""
         h = C.c_void_p()

@@ -30,6 +30,10 @@ PRESETS = {
     "C2": dict(genome_len=4_600_000, n_sr=200_000, n_pb=50_000, pb_len_mean=12000, pb_len_sigma=0.5),
     # configs[2]: yeast-scale, 300k PB vs 1M SRs, k=21
     "C3": dict(genome_len=12_000_000, n_sr=1_000_000, n_pb=300_000, pb_len_mean=12000, pb_len_sigma=0.5),
+    # configs[3] (property tests only; the oracle cannot hold its index): chr1-scale, 10M SRs over a
+    # 250 Mbp genome with 2% 5-50-copy repeats, PB reads of 15 kb N50 (lognormal mean 12.5 kb, sigma 0.6)
+    "C4": dict(genome_len=250_000_000, n_sr=10_000_000, n_pb=2_000_000, pb_len_mean=12500, pb_len_sigma=0.6,
+               repeat_frac=0.02),
     "tiny": dict(genome_len=20_000, n_sr=60, n_pb=8, pb_len_mean=2000, pb_len_sigma=0.0),
     "small": dict(genome_len=200_000, n_sr=1500, n_pb=40, pb_len_mean=6000, pb_len_sigma=0.4),
 }
@@ -76,6 +80,20 @@ class Dataset:
         n = s.n
         off = np.ctypeslib.as_array(s.off, shape=(n + 1,))
         return (C.c_char * int(off[n])).from_address(s.seq), off
+
+    def sr_pointers(self):
+        """(names, seqs, lens) as ctypes arrays pointing into the generator's buffers
+        (no Python copies: C4 holds 10 Gbp of super-reads)"""
+        s = self.sr
+        n = s.n
+        off = np.ctypeslib.as_array(s.off, shape=(n + 1,))
+        noff = np.ctypeslib.as_array(s.name_off, shape=(n,))
+        seqp = (off[:-1] + np.uint64(s.seq)).astype(np.uint64)
+        namep = (noff + np.uint64(s.names)).astype(np.uint64)
+        lens = np.diff(off).astype(np.uint64)
+        self._keep_ptrs = (seqp, namep, lens)
+        P = C.POINTER(C.c_char_p)
+        return (namep.ctypes.data_as(P), seqp.ctypes.data_as(P), lens.ctypes.data_as(C.POINTER(C.c_uint64)), n)
 
     def pb_blob(self):
         """(bytes-like buffer, offsets) of the concatenated PB reads"""
