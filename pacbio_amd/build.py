@@ -74,7 +74,7 @@ def build_pbgpu_variant(name, defines):
     objdir = os.path.join(ROOT, "build", name)
     os.makedirs(objdir, exist_ok=True)
     jobs, objs = [], []
-    for s in ["pbgpu_kernels.hip", "pbgpu_api.hip"]:
+    for s in ["pbgpu_kernels.hip", "pbgpu_api.hip", "pbgpu_format.hip", "pbgpu_run.hip"]:
         obj = os.path.join(objdir, s + ".o")
         jobs.append([HIPCC] + HIPFLAGS + list(defines) + ["-c", os.path.join(CSRC, s), "-o", obj])
         objs.append(obj)
@@ -82,7 +82,7 @@ def build_pbgpu_variant(name, defines):
         list(ex.map(_run, jobs))
     lib = os.path.join(PKG, f"libpbgpu_{name}.so")
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + objs +
-         ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-lpthread"])
+         ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-lz", "-lpthread"])
     return lib
 
 

@@ -13,6 +13,8 @@
 // the file is compiled with -ffp-contract=off and the critical expressions
 // use explicit __dadd_rn / __dmul_rn so that no FMA is ever formed.
 #include <hip/hip_runtime.h>
+
+#include <atomic>
 #include <stdint.h>
 #include <algorithm>
 #include <type_traits>
@@ -2396,13 +2398,17 @@ void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const ui
   if (!n_list) return;
   if (!gtable) {  // LDS table: hcap_log2 <= 13; the 8192-slot table gets a 16-wave block
     const size_t lds = ((size_t)3 << hcap_log2) * sizeof(uint32_t);
-    static bool attr = false;
-    if (!attr) {
+    // the 96 KiB dynamic-LDS attribute, set once per device (function attributes are per device)
+    static std::atomic<uint64_t> attr_done(0);
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const uint64_t bit = 1ull << (dev & 63);
+    if (!(attr_done.load(std::memory_order_acquire) & bit)) {
       (void)hipFuncSetAttribute((const void*)k_group<false, GROUP_BLOCK>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 120 * 1024);
       (void)hipFuncSetAttribute((const void*)k_group<false, GROUP_BLOCK_BIG>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
-      attr = true;
+      attr_done.fetch_or(bit, std::memory_order_acq_rel);
     }
     if (hcap_log2 >= 13)
       hipLaunchKernelGGL((k_group<false, GROUP_BLOCK_BIG>), dim3(n_list), dim3(GROUP_BLOCK_BIG), lds, st, ix, krec, roff,
@@ -2478,14 +2484,23 @@ void launch_lis_lane(const ChainDesc* chains, const uint32_t* items, uint32_t n_
   launch_lis(false, chains, items, n_items, slen, X, N16, pts, lisl, lp, keep_idx, stats, st);
 }
 uint32_t lis_lane_max() { return PBGPU_LIS_LANE_MAX; }
-static uint32_t resident_blocks(const void* fn, int block) {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
+// CU count of the current device, cached per device (aligners on several
+// devices and host threads call this concurrently: atomics, no lock)
+static int device_cus() {
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) dev = 0;
+  int c = cache[dev].load(std::memory_order_relaxed);
+  if (!c) {
     hipDeviceProp_t pr;
-    cus = hipGetDeviceProperties(&pr, dev) == hipSuccess ? pr.multiProcessorCount : 256;
+    c = hipGetDeviceProperties(&pr, dev) == hipSuccess ? pr.multiProcessorCount : 256;
+    cache[dev].store(c, std::memory_order_relaxed);
   }
+  return c;
+}
+static uint32_t resident_blocks(const void* fn, int block) {
+  const int cus = device_cus();
   int per = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, block, 0) != hipSuccess || per < 1) per = 1;
   return (uint32_t)(per * cus);

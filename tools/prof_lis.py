@@ -26,9 +26,16 @@ def main():
     rr = al.upload(blob=blob, offsets=off)
     al.align_resident(rr)
     L = pbgpu.lib()
-    f = L.pbgpu_debug_prof
-    f.argtypes = [C.POINTER(C.c_ulonglong), C.c_int, C.c_int]
     buf = (C.c_ulonglong * 32)()
+    f = getattr(L, "pbgpu_debug_prof", None)  # -DPBGPU_PROF builds only
+    if f is None:
+        al.reset_stats()
+        al.align_resident(rr)
+        pbgpu.device_synchronize(0)
+        st = al.stats()
+        print(f"k_group tier0: {st['kernel_ms']['k_group']:.2f} ms, k_lis: {st['kernel_ms']['k_lis']:.2f} ms")
+        return
+    f.argtypes = [C.POINTER(C.c_ulonglong), C.c_int, C.c_int]
     f(buf, 32, 1)
     al.reset_stats()
     al.align_resident(rr)
