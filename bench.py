@@ -16,7 +16,9 @@ to the closed coords file.  The index is built once before the timed region
 
 `value_device` keeps round 1's device-only figure: the same reads resident
 in HBM, the device path from seeding to per-read sorted records in HBM, no
-formatting or output.  The `roofline` object is for its dominant kernel.
+formatting or output -- run with one aligner (--device-streams 1), so every
+kernel launch runs alone and its HIP-event time is the kernel's own.  The
+`roofline` object is for the dominant kernel of that leg.
 
 Multi-GPU: one process per GPU (torchrun); every rank builds its own index
 replica and aligns its own 50k-read shard into its own coords file (weak
@@ -146,6 +148,9 @@ def main():
     ap.add_argument("--streams", type=int, default=2, help="aligners (HIP stream + host thread each) per GPU")
     ap.add_argument("--batch-bases", type=float, default=64e6, help="pbgpu_run batch size in bases")
     ap.add_argument("--device-steps", type=int, default=3, help="steps of the device-only leg (value_device)")
+    ap.add_argument("--device-streams", type=int, default=1,
+                    help="aligners of the device-only leg: 1 = every launch runs alone, so the per-launch event times "
+                         "(the roofline) measure the kernel, not two overlapping launches")
     ap.add_argument("--workdir", default=os.environ.get("PBGPU_BENCH_DIR", "/tmp"),
                     help="where the input FASTA and the coords output are written")
     args = ap.parse_args()
@@ -162,6 +167,8 @@ def main():
 
     # B_rand: random 64-B sector gathers over a 64 GB buffer, this GPU, this run
     b_rand = pbgpu.measure_gather(local, 64 << 30) if not args.no_brand else None
+    # the same for random 512-B runs of 8-B words: the shape of k_group's occurrence-list reads
+    b_run = pbgpu.measure_gather(local, 64 << 30, unit_bytes=512) if not args.no_brand else None
 
     k = 21 if args.workload == "C3" else 17
     n_pb = args.reads or PRESETS[args.workload]["n_pb"]
@@ -182,7 +189,7 @@ def main():
     bases_rank = int(off[-1])
 
     # ---- device-only leg (value_device): reads resident in HBM, records left in HBM
-    al = pbgpu.StreamAligner(index, streams=args.streams, **akw)
+    al = pbgpu.StreamAligner(index, streams=args.device_streams, **akw)
     reads = al.upload(blob=blob, offsets=off)
     al.align_resident(reads)
     al.reset_stats()
@@ -242,15 +249,19 @@ def main():
     dom = max(kb, key=lambda kk: kms[kk])
     avg_ms = kms[dom] / max(1, kn[dom])
     achieved = kb[dom] / (avg_ms * 1e-3) / 1e9
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{ROCPROF_FILE[dom]}.json")
-    if os.path.exists(pmc_path):
+    # HBM traffic per launch of the dominant kernel from the committed rocprofv3 PMC
+    # summary (tools/prof_r02.sh): FETCH_SIZE calibrated on the 512-B-run gather
+    # microbenchmark (bytes moved / FETCH_SIZE), + WRITE_SIZE
+    traffic, traffic_note = None, None
+    summ = os.path.join(ROOT, "profiles", "r02_rocprof_summary.json")
+    if dom == "k_group" and os.path.exists(summ):
         try:
-            with open(pmc_path) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+            with open(summ) as f:
+                t = json.load(f).get("k_group_traffic_bytes", {})
+            traffic = t.get("calibrated_runs")
+            traffic_note = {k: t.get(k) for k in ("raw_fetch_plus_write", "guide_2x_fetch_plus_write")}
         except Exception:
             traffic = None
-
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle.oracle import OracleIndex, params
@@ -335,7 +346,7 @@ def main():
                           "device_bytes": info["device_bytes"], "build_s": round(t_index, 3),
                           "generate_and_write_s": round(t_gen, 3)},
                 "stage_ms_per_step": stage,
-                "device_leg": {"ms_per_step": el_dev / args.device_steps * 1e3,
+                "device_leg": {"ms_per_step": el_dev / args.device_steps * 1e3, "streams": args.device_streams,
                                "stage_ms_per_step": {s: round(st["ms_" + s] / args.device_steps, 3) for s in
                                                      ("seed", "group", "lis", "fit", "records")},
                                "kernel_ms_per_launch": {kk: round(kms[kk] / max(1, kn[kk]), 3) for kk in kms},
@@ -348,7 +359,11 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dom, "rocprof_kernel": ROCPROF_FILE[dom], "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "alg_bytes_per_launch": kb[dom], "avg_launch_ms": avg_ms,
-                         "b_rand_gbs": b_rand, "frac_of_b_rand": (achieved / b_rand) if b_rand else None},
+                         "traffic_source": "profiles/r02_rocprof_summary.json (FETCH_SIZE x run-shape calibration + "
+                                           "WRITE_SIZE, per device-leg launch)" if traffic else None,
+                         "traffic_alternatives": traffic_note,
+                         "b_rand_gbs": b_rand, "frac_of_b_rand": (achieved / b_rand) if b_rand else None,
+                         "b_run512_gbs": b_run, "frac_of_b_run512": (achieved / b_run) if b_run else None},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -59,6 +59,10 @@ pbgpu_status pbgpu_device_synchronize(int device);
  * 64-byte sector loads over a fresh device buffer of buffer_bytes, all CUs
  * (SURVEY 8(d) B_rand, the random-access roofline).  Frees the buffer. */
 pbgpu_status pbgpu_measure_gather(int device, uint64_t buffer_bytes, double* gbps);
+/* The same for another access shape: unit_bytes 64 (random 64-B sectors, as
+ * pbgpu_measure_gather) or 512 (random 512-B runs read as 64 consecutive 8-B
+ * words, the shape of k_group's occurrence-list reads). */
+pbgpu_status pbgpu_measure_gather_shape(int device, uint64_t buffer_bytes, uint32_t unit_bytes, double* gbps);
 
 /* ------------------------------------------------------------------ index
  * Replaces superread_parse() + sequence_psa (superread_parser.hpp:53-224):

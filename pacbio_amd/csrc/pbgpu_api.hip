@@ -555,15 +555,43 @@ __global__ __launch_bounds__(256) void k_gather_sectors(const uint4* __restrict_
   }
   if ((acc.x & 0xFFFFF) == 0x12345) sink[gid & 1023] = acc;  // keeps the loads live, practically never stores
 }
+// Runs of 64 x 8 B (one 512-B contiguous run per wave-instruction, 8-B-aligned
+// words, 64-B-aligned runs): the access shape of k_group's occurrence-list reads
+// (a k-mer's occurrences are consecutive 8-B entries).  Calibrates FETCH_SIZE
+// for that shape and gives its achievable rate.
+__global__ __launch_bounds__(256) void k_gather_runs(const uint2* __restrict__ buf, uint64_t n_runs, uint32_t iters,
+                                                     uint32_t seed, uint2* __restrict__ sink) {
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t wv = gid >> 6;
+  const uint32_t lane = threadIdx.x & 63;
+  uint2 acc = make_uint2(0, 0);
+  for (uint32_t it = 0; it < iters; ++it) {
+    uint2 v[GATHER_UNR];
+#pragma unroll
+    for (int u = 0; u < GATHER_UNR; ++u) {
+      uint64_t h = (wv * GATHER_UNR + u) * 0x9E3779B97F4A7C15ull + ((uint64_t)(it + 1) * seed);
+      h ^= h >> 31; h *= 0xD6E8FEB86659FD93ull; h ^= h >> 32;
+      v[u] = buf[(h % n_runs) * 64 + lane];
+    }
+#pragma unroll
+    for (int u = 0; u < GATHER_UNR; ++u) { acc.x ^= v[u].x; acc.y ^= v[u].y; }
+  }
+  if ((acc.x & 0xFFFFF) == 0x12345) sink[gid & 1023] = acc;
+}
 }  // namespace
 
 pbgpu_status pbgpu_measure_gather(int device, uint64_t buffer_bytes, double* gbps) {
-  if (!gbps || buffer_bytes < (1u << 20)) return fail(PBGPU_ERR_INVALID, "bad argument");
+  return pbgpu_measure_gather_shape(device, buffer_bytes, 64, gbps);
+}
+
+pbgpu_status pbgpu_measure_gather_shape(int device, uint64_t buffer_bytes, uint32_t unit_bytes, double* gbps) {
+  if (!gbps || buffer_bytes < (1u << 20) || (unit_bytes != 64 && unit_bytes != 512))
+    return fail(PBGPU_ERR_INVALID, "bad argument");
   API_TRY
   HIPCHK(hipSetDevice(device));
   dbuf<uint4> buf, sink;
-  const uint64_t n_sectors = buffer_bytes / 64;
-  buf.ensure(n_sectors * 4);
+  const uint64_t n_units = buffer_bytes / unit_bytes;
+  buf.ensure(n_units * unit_bytes / 16);
   sink.ensure(1024);
   hipDeviceProp_t pr;
   HIPCHK(hipGetDeviceProperties(&pr, device));
@@ -572,18 +600,27 @@ pbgpu_status pbgpu_measure_gather(int device, uint64_t buffer_bytes, double* gbp
   HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
   hipEvent_t e0, e1;
   HIPCHK(hipEventCreate(&e0)); HIPCHK(hipEventCreate(&e1));
-  hipLaunchKernelGGL(k_gather_sectors, dim3(blocks), dim3(256), 0, st, buf.p, n_sectors, iters, 7u, sink.p);
+  auto launch = [&](uint32_t seed) {
+    if (unit_bytes == 64)
+      hipLaunchKernelGGL(k_gather_sectors, dim3(blocks), dim3(256), 0, st, buf.p, n_units, iters, seed, sink.p);
+    else
+      hipLaunchKernelGGL(k_gather_runs, dim3(blocks), dim3(256), 0, st, (const uint2*)buf.p, n_units, iters, seed,
+                         (uint2*)sink.p);
+  };
+  launch(7u);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(e0, st));
   const int reps = 3;
-  for (int r = 0; r < reps; ++r)
-    hipLaunchKernelGGL(k_gather_sectors, dim3(blocks), dim3(256), 0, st, buf.p, n_sectors, iters, 11u + 2u * r, sink.p);
+  for (int r = 0; r < reps; ++r) launch(11u + 2u * r);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(e1, st));
   HIPCHK(hipEventSynchronize(e1));
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, e0, e1));
-  const double bytes = (double)reps * blocks * 256 / 4 * GATHER_UNR * iters * 64.0;
+  // bytes moved: sectors: 4 lanes x 16 B per 64-B sector; runs: 64 lanes x 8 B per 512-B run
+  const double units_per_launch = unit_bytes == 64 ? (double)blocks * 256 / 4 * GATHER_UNR * iters
+                                                   : (double)blocks * 256 / 64 * GATHER_UNR * iters;
+  const double bytes = (double)reps * units_per_launch * unit_bytes;
   *gbps = bytes / (ms * 1e-3) / 1e9;
   (void)hipEventDestroy(e0); (void)hipEventDestroy(e1); (void)hipStreamDestroy(st);
   return PBGPU_OK;

@@ -426,6 +426,11 @@ static void runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_s
   uint64_t n_batches_total = ~0ull;  // set by the reader when it finishes
   std::mutex smu;                    // stats
 
+  // PBGPU_RAMP: the first batch holds batch_bases >> ramp bases, doubling up to batch_bases
+  const uint32_t ramp = getenv("PBGPU_RAMP") ? (uint32_t)atoi(getenv("PBGPU_RAMP")) : 3u;
+  // PBGPU_WRITE_CHUNK: bytes per write() call
+  const uint64_t wchunk = getenv("PBGPU_WRITE_CHUNK") ? strtoull(getenv("PBGPU_WRITE_CHUNK"), nullptr, 10)
+                                                      : (64ull << 20);
   auto reader = [&]() {
     try {
       ReadParser rp(paths, details);
@@ -435,7 +440,10 @@ static void runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_s
         const double t0 = now_s();
         b->clear();
         b->id = id;
-        const bool any = rp.fill(*b, batch_bases);
+        // ramp: the first batches are small so the writer (the slowest stage) starts
+        // after a short pipeline fill; then full batches (GPU efficiency)
+        const uint64_t want = std::min<uint64_t>(batch_bases, std::max<uint64_t>(1, (batch_bases >> ramp) << id));
+        const bool any = rp.fill(*b, want);
         {
           std::lock_guard<std::mutex> lk(smu);
           S.read_seconds += now_s() - t0;
@@ -536,7 +544,8 @@ static void runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_s
           S.writer_idle_seconds += now_s() - t0;
         }
         const double t1 = now_s();
-        write_all(cfd, d.text.p, d.len, "coords");
+        for (uint64_t o = 0; o < d.len; o += wchunk)
+          write_all(cfd, d.text.p + o, std::min<uint64_t>(wchunk, d.len - o), "coords");
         if (dfd >= 0) write_all(dfd, d.details.data(), d.details.size(), "details");
         {
           std::lock_guard<std::mutex> sl(smu);

@@ -26,7 +26,7 @@ STATUS = {0: "OK", 1: "INVALID", 2: "IO", 3: "NOMEM", 4: "DEVICE", 5: "UNSUPPORT
 # every symbol include/pbgpu.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "pbgpu_abi_version", "pbgpu_last_error", "pbgpu_device_count", "pbgpu_device_synchronize",
-    "pbgpu_measure_gather",
+    "pbgpu_measure_gather", "pbgpu_measure_gather_shape",
     "pbgpu_index_build_fasta", "pbgpu_index_build", "pbgpu_index_free", "pbgpu_index_get_info",
     "pbgpu_index_sr_name", "pbgpu_index_sr_len",
     "pbgpu_align_params_default", "pbgpu_aligner_create", "pbgpu_aligner_free",
@@ -149,6 +149,7 @@ def lib():
         L.pbgpu_device_count.restype = C.c_int
         L.pbgpu_device_synchronize.argtypes = [C.c_int]
         L.pbgpu_measure_gather.argtypes = [C.c_int, C.c_uint64, C.POINTER(C.c_double)]
+        L.pbgpu_measure_gather_shape.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.POINTER(C.c_double)]
         L.pbgpu_index_build_fasta.argtypes = [C.POINTER(C.c_char_p), C.c_size_t, C.POINTER(IndexParams), C.POINTER(vp)]
         L.pbgpu_index_build.argtypes = [C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.POINTER(C.c_uint64),
                                         C.c_size_t, C.POINTER(IndexParams), C.POINTER(vp)]
@@ -217,10 +218,11 @@ def device_synchronize(device=0):
     _check(lib().pbgpu_device_synchronize(device))
 
 
-def measure_gather(device=0, buffer_bytes=64 << 30):
-    """GB/s of uniformly random 64-B sector loads over a buffer of buffer_bytes (B_rand)."""
+def measure_gather(device=0, buffer_bytes=64 << 30, unit_bytes=64):
+    """GB/s of uniformly random 64-B sector loads (B_rand), or of random 512-B runs
+    read as 64 consecutive 8-B words (unit_bytes=512), over a buffer of buffer_bytes."""
     g = C.c_double()
-    _check(lib().pbgpu_measure_gather(device, buffer_bytes, C.byref(g)))
+    _check(lib().pbgpu_measure_gather_shape(device, buffer_bytes, unit_bytes, C.byref(g)))
     return g.value
 
 

@@ -1,0 +1,108 @@
+#!/usr/bin/env python3
+"""Summaries of a tools/prof_r02.sh collection.
+
+kernel stats: per kernel (and, for k_group<false, 256u>, the device-leg launches
+-- the largest grids, one per device step -- apart from the e2e ones), mean
+launch time from the kernel trace.
+PMC: per-launch FETCH_SIZE / WRITE_SIZE of the device-leg k_group launches, and
+the calibration of FETCH_SIZE on the two gather microbenchmarks (known bytes):
+traffic = FETCH_SIZE x (bytes moved / FETCH_SIZE of the 512-B run shape) + WRITE_SIZE.
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import re
+import sys
+
+
+def short(name):
+    m = re.match(r"(?:void )?(?:pbgpu::)?(?:\(anonymous namespace\)::)?([A-Za-z_0-9]+)(<[^(]*>)?", name)
+    return (m.group(1) + (m.group(2) or "")) if m else name
+
+
+def grid(r):
+    for k in ("Grid_Size", "Grid_Size_X", "grid_size"):
+        if k in r and r[k]:
+            return int(r[k])
+    return 0
+
+
+def trace(path):
+    rows = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            rows.append((short(r["Kernel_Name"]), grid(r), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6))
+    return rows
+
+
+def counters(d):
+    acc = collections.defaultdict(lambda: collections.defaultdict(float))  # (kernel, dispatch) -> counter -> value
+    meta = {}
+    for p in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(p) as f:
+            for r in csv.DictReader(f):
+                key = (short(r["Kernel_Name"]), r["Dispatch_Id"], os.path.dirname(p))
+                acc[key][r["Counter_Name"]] += float(r["Counter_Value"])
+                meta[key] = grid(r)
+    return acc, meta
+
+
+def main(d, out):
+    res = {}
+    rows = trace(glob.glob(os.path.join(d, "kt", "**", "*kernel_trace.csv"), recursive=True)[0])
+    stats = collections.defaultdict(list)
+    for k, g, ms in rows:
+        stats[k].append((g, ms))
+    lines = []
+    for k, v in sorted(stats.items(), key=lambda kv: -sum(x[1] for x in kv[1])):
+        lines.append(f"{k:44s} n={len(v):5d} total={sum(x[1] for x in v):10.3f} ms mean={sum(x[1] for x in v) / len(v):8.3f} ms")
+    kg = stats.get("k_group<false, 256u>", [])
+    if kg:
+        gmax = max(g for g, _ in kg)
+        dev = [ms for g, ms in kg if g >= 0.5 * gmax]
+        res["k_group_device_leg"] = {"launches": len(dev), "mean_ms": sum(dev) / len(dev), "grid": gmax,
+                                     "all_launches_mean_ms": sum(x[1] for x in kg) / len(kg)}
+        lines.append(f"k_group<false, 256u> device-leg launches (grid >= {gmax // 2}): n={len(dev)} "
+                     f"mean={sum(dev) / len(dev):.3f} ms")
+    # PMC
+    acc, meta = counters(d)
+    per = collections.defaultdict(lambda: collections.defaultdict(list))
+    for (k, disp, src), c in acc.items():
+        for n, v in c.items():
+            per[k][n].append((meta[(k, disp, src)], v))
+    cal = {}
+    # blocks = 8 x CUs (256), 256 threads, GATHER_UNR 8, iters 64
+    moved = {"k_gather_sectors": 2048 * 256 / 4 * 8 * 64 * 64, "k_gather_runs": 2048 * 256 / 64 * 8 * 64 * 512}
+    for k, b in moved.items():
+        if k in per and per[k].get("FETCH_SIZE"):
+            f = [v for _, v in per[k]["FETCH_SIZE"]]
+            fb = sum(f) / len(f) * 1024.0
+            cal[k] = {"bytes_moved": b, "fetch_size_bytes": fb, "ratio_moved_over_fetch": b / fb}
+    res["fetch_calibration"] = cal
+    if "k_group<false, 256u>" in per:
+        c = per["k_group<false, 256u>"]
+        out_c = {}
+        for n in ("FETCH_SIZE", "WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"):
+            if c.get(n):
+                gmax = max(g for g, _ in c[n])
+                vals = [v for g, v in c[n] if g >= 0.5 * gmax]
+                out_c[n] = sum(vals) / len(vals)
+        res["k_group_pmc_device_leg"] = out_c
+        if "FETCH_SIZE" in out_c and "WRITE_SIZE" in out_c:
+            f = out_c["FETCH_SIZE"] * 1024.0
+            w = out_c["WRITE_SIZE"] * 1024.0
+            r = cal.get("k_gather_runs", {}).get("ratio_moved_over_fetch")
+            res["k_group_traffic_bytes"] = {"raw_fetch_plus_write": f + w, "guide_2x_fetch_plus_write": 2 * f + w,
+                                            "calibrated_runs": (f * r + w) if r else None}
+    with open(os.path.join(out, "r02_rocprof_summary.json"), "w") as fo:
+        json.dump(res, fo, indent=1)
+    with open(os.path.join(out, "r02_kernel_stats.txt"), "w") as fo:
+        fo.write("\n".join(lines) + "\n")
+    print("\n".join(lines[:25]))
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else ".")
