@@ -355,6 +355,16 @@ typedef struct {
   uint32_t aligners_per_device;   /* 0 = 2 */
   uint64_t batch_bases;           /* bases per batch; 0 = 64 M */
   int32_t host_threads;           /* --details formatting threads; 0 = all */
+  /* Optional consumer of the records (create_mega_reads, create_mega_reads.cc:
+   * 25-93): when set, each batch's records are downloaded and handed to it on
+   * the worker thread instead of being formatted as coords; the text it returns
+   * (malloc'd, freed by the driver; NULL = none) is written to coords_path and
+   * its side text (*side_text, e.g. the --dot graph) to details_path, both in
+   * batch order.  Nonzero *status from it stops the run (PBGPU_ERR_INTERNAL). */
+  char* (*records_fn)(void* user, const pbgpu_index* ix, const pbgpu_coords_batch* coords,
+                      const char* const* read_names, const uint64_t* read_lens, uint64_t* text_len,
+                      char** side_text, uint64_t* side_len, int* status);
+  void* records_user;
 } pbgpu_run_params;
 
 typedef struct {

@@ -65,6 +65,13 @@ def build_pbgpu(force=False):
     if force or _newer(cli, [cli_src, lib] + hdrs):
         _run(["g++", "-O2", "-std=c++17", "-o", cli, cli_src, "-I" + os.path.join(ROOT, "include"),
               "-L" + PKG, "-lpbgpu", "-Wl,-rpath,$ORIGIN/..", "-lpthread"])
+    # create_mega_reads: the same library + the host overlap graph (no FMA contraction:
+    # its double arithmetic follows overlap_graph.cc's operation order)
+    cmr = os.path.join(bindir, "create_mega_reads")
+    cmr_src = [os.path.join(CSRC, f) for f in ("create_mega_reads.cpp", "overlap_graph.cpp")]
+    if force or _newer(cmr, cmr_src + [os.path.join(CSRC, "overlap_graph.hpp"), lib] + hdrs):
+        _run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-o", cmr] + cmr_src +
+             ["-I" + os.path.join(ROOT, "include"), "-L" + PKG, "-lpbgpu", "-Wl,-rpath,$ORIGIN/..", "-lpthread"])
     return lib
 
 

@@ -336,6 +336,11 @@ class TextPool {
     }
     return true;
   }
+  void advance() {  // a batch written without a pinned buffer (records consumer)
+    std::lock_guard<std::mutex> lk(mu_);
+    ++written_;
+    cv_.notify_all();
+  }
   void put(Pinned b, bool written) {
     std::lock_guard<std::mutex> lk(mu_);
     free_.push_back(b);
@@ -353,8 +358,9 @@ class TextPool {
 };
 
 struct Done {  // a batch's formatted output, waiting for its turn
-  Pinned text;
+  Pinned text;       // device-formatted coords (pinned)
   uint64_t len = 0;
+  char* mtext = nullptr;  // or: host text from the records consumer (malloc'd)
   std::string details;
 };
 
@@ -379,6 +385,7 @@ struct pbgpu_runner {
   std::vector<pbgpu_aligner*> al;
   std::vector<std::unique_ptr<pbgpu_reads>> rd;
   bool details = false;
+  bool side = false;  // a second output file (details, or the records consumer's side text)
   uint64_t batch_bases = 0;
   std::vector<std::unique_ptr<Batch>> batches;  // W + 2, recycled
   std::unique_ptr<TextPool> texts;              // W + 2
@@ -404,7 +411,7 @@ static void runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_s
     if (cfd < 0) throw bad_input(std::string("Failed to open coords file '") + run->coords_path + "': " + strerror(errno));
   }
   struct fd_guard { int& fd; ~fd_guard() { if (fd > 2) close(fd); } } cg{cfd};
-  if (details) {
+  if (R->side) {
     dfd = open(run->details_path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
     if (dfd < 0) throw bad_input(std::string("Failed to open details file '") + run->details_path + "': " + strerror(errno));
   }
@@ -475,16 +482,40 @@ static void runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_s
         const double t1 = now_s();
         aligner_pipeline(al, rd);
         const double t2 = now_s();
-        const uint64_t len = format_device_text(al, rd, run->compact, run->zero_match);
-        HIPCHK(hipStreamSynchronize(al->st));
-        const double t3 = now_s();
         Done d;
-        if (!R->texts->get(b->id, len + 1, d.text)) break;
-        const double t4 = now_s();
-        if (len) HIPCHK(hipMemcpyAsync(d.text.p, al->text.p, len, hipMemcpyDeviceToHost, al->st));
-        HIPCHK(hipStreamSynchronize(al->st));
-        const double t5 = now_s();
-        d.len = len;
+        double t3, t4, t5;
+        if (run->records_fn) {  // records to the host consumer (create_mega_reads)
+          pbgpu_coords_batch* cb = nullptr;
+          if (pbgpu_download(al, &cb) != PBGPU_OK) throw std::runtime_error(pbgpu_last_error());
+          t3 = t4 = now_s();
+          std::vector<std::string> nm(b->n());
+          std::vector<const char*> np(b->n());
+          std::vector<uint64_t> lens(b->n());
+          for (uint64_t i = 0; i < b->n(); ++i) {
+            nm[i].assign(b->names.data() + b->name_off[i], b->name_off[i + 1] - b->name_off[i]);
+            np[i] = nm[i].c_str();
+            lens[i] = b->off[i + 1] - b->off[i];
+          }
+          uint64_t tl = 0, sl = 0;
+          char* side = nullptr;
+          int fst = 0;
+          d.mtext = run->records_fn(run->records_user, al->ix, cb, np.data(), lens.data(), &tl, &side, &sl, &fst);
+          pbgpu_coords_free(cb);
+          if (side) { d.details.assign(side, sl); free(side); }
+          if (fst) { free(d.mtext); throw std::runtime_error("the records consumer failed"); }
+          d.len = d.mtext ? tl : 0;
+          t5 = now_s();
+        } else {
+          const uint64_t len = format_device_text(al, rd, run->compact, run->zero_match);
+          HIPCHK(hipStreamSynchronize(al->st));
+          t3 = now_s();
+          if (!R->texts->get(b->id, len + 1, d.text)) break;
+          t4 = now_s();
+          if (len) HIPCHK(hipMemcpyAsync(d.text.p, al->text.p, len, hipMemcpyDeviceToHost, al->st));
+          HIPCHK(hipStreamSynchronize(al->st));
+          t5 = now_s();
+          d.len = len;
+        }
         if (details) {
           pbgpu_details_batch* db = nullptr;
           if (pbgpu_download_details(al, &db) != PBGPU_OK) throw std::runtime_error(pbgpu_last_error());
@@ -524,7 +555,7 @@ static void runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_s
 
   auto writer = [&]() {
     try {
-      if (run->header) {
+      if (run->header && !run->records_fn) {
         std::string h = std::string("Rstart Rend Qstart Qend Nmers Rcons Qcons Rcover Qcover Rlen Qlen Stretch Offset Err") +
                         (run->compact ? "" : " Rname") + " Qname\n";
         write_all(cfd, h.data(), h.size(), "coords");
@@ -544,8 +575,9 @@ static void runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_s
           S.writer_idle_seconds += now_s() - t0;
         }
         const double t1 = now_s();
+        const char* src = d.mtext ? d.mtext : d.text.p;
         for (uint64_t o = 0; o < d.len; o += wchunk)
-          write_all(cfd, d.text.p + o, std::min<uint64_t>(wchunk, d.len - o), "coords");
+          write_all(cfd, src + o, std::min<uint64_t>(wchunk, d.len - o), "coords");
         if (dfd >= 0) write_all(dfd, d.details.data(), d.details.size(), "details");
         {
           std::lock_guard<std::mutex> sl(smu);
@@ -553,7 +585,12 @@ static void runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_s
           S.coords_bytes += d.len;
           S.details_bytes += d.details.size();
         }
-        R->texts->put(d.text, true);
+        if (d.mtext) {
+          free(d.mtext);
+          R->texts->advance();
+        } else {
+          R->texts->put(d.text, true);
+        }
       }
     } catch (...) {
       record_exception(rs);
@@ -575,7 +612,10 @@ static void runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_s
   wt.join();
   {
     std::lock_guard<std::mutex> lk(dmu);
-    for (auto& kv : done) R->texts->put(kv.second.text, false);
+    for (auto& kv : done) {
+      if (kv.second.mtext) free(kv.second.mtext);
+      else R->texts->put(kv.second.text, false);
+    }
     done.clear();
   }
   if (rs.status != PBGPU_OK) {
@@ -624,7 +664,8 @@ pbgpu_status pbgpu_runner_create(pbgpu_index* const* indexes, size_t n_indexes, 
   std::unique_ptr<pbgpu_runner> R(new pbgpu_runner);
   const uint32_t per_dev = run->aligners_per_device ? run->aligners_per_device : 2;
   R->batch_bases = run->batch_bases ? run->batch_bases : (64ull << 20);
-  R->details = run->details_path != nullptr;
+  R->details = run->details_path != nullptr && run->records_fn == nullptr;  // --details coords output
+  R->side = run->details_path != nullptr;
   for (size_t i = 0; i < n_indexes; ++i)
     for (uint32_t j = 0; j < per_dev; ++j) {
       pbgpu_aligner* a = nullptr;
@@ -647,7 +688,7 @@ pbgpu_status pbgpu_runner_create(pbgpu_index* const* indexes, size_t n_indexes, 
 
 pbgpu_status pbgpu_runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_stats* stats) {
   if (!R || !run || (!run->pb_paths && run->n_pb_paths)) return fail(PBGPU_ERR_INVALID, "null argument");
-  if ((run->details_path != nullptr) != R->details)
+  if ((run->details_path != nullptr) != R->side)
     return fail(PBGPU_ERR_INVALID, "--details must be given to pbgpu_runner_create and every run alike");
   API_TRY
   runner_run(R, run, stats);

@@ -77,7 +77,7 @@ class RunParams(C.Structure):
     _fields_ = [("pb_paths", C.POINTER(C.c_char_p)), ("n_pb_paths", C.c_size_t), ("coords_path", C.c_char_p),
                 ("details_path", C.c_char_p), ("compact", C.c_int32), ("header", C.c_int32),
                 ("zero_match", C.c_int32), ("aligners_per_device", C.c_uint32), ("batch_bases", C.c_uint64),
-                ("host_threads", C.c_int32)]
+                ("host_threads", C.c_int32), ("records_fn", C.c_void_p), ("records_user", C.c_void_p)]
 
 
 class RunStats(C.Structure):
@@ -570,7 +570,7 @@ def _run_params(pb_paths, coords_path, details_path=None, compact=True, header=T
     paths = _cstrs([p if isinstance(p, bytes) else str(p).encode() for p in pb_paths])
     rp = RunParams(paths, len(pb_paths), coords_path.encode() if coords_path else None,
                    details_path.encode() if details_path else None, int(compact), int(header), int(zero_match),
-                   aligners_per_device, int(batch_bases), host_threads)
+                   aligners_per_device, int(batch_bases), host_threads, None, None)
     return rp, paths
 
 

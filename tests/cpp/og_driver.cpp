@@ -1,0 +1,183 @@
+// Test driver for pacbio_amd/csrc/overlap_graph.cpp (no GPU): built and run by
+// tests/test_mega_reads.py.
+//   og_driver graph PARAMS RECORDS   mega-reads of the records (one read after another)
+//   og_driver tiling SEED N          tests/test_tiling.cc's properties on N random instances
+//   og_driver names                  super_read_name / union_find checks (test_super_read_name.cc,
+//                                    test_union_find.cc restated)
+// PARAMS: k play errors bases density min_len tiling trim ul_path [useqs_path | -]
+// RECORDS: "R name n" then n lines: rs re qs qe nb_mers sr_cover rl ql stretch offset avg_err
+//          (hex floats) name n_info kmers... bases...
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <limits>
+#include <map>
+#include <random>
+#include <sstream>
+
+#include "../../pacbio_amd/csrc/overlap_graph.hpp"
+
+namespace megareads {
+struct ReadGraphTest {
+  static inline int le_violations = 0;
+  // tests/test_tiling.cc:35-75 (Tiling.Uniform): random candidate intervals
+  static int run(unsigned seed, int iters) {
+    std::mt19937_64 rng(seed);
+    std::uniform_real_distribution<double> pos(0, 1000), dens(0.02, 0.2);
+    std::vector<int> no_lengths;
+    Params p;
+    p.overlap_play = 1.2; p.k_len = 70; p.unitig_lengths = &no_lengths;
+    int fails = 0;
+    le_violations = 0;
+    for (int it = 0; it < iters; ++it) {
+      const int n = 100;
+      ReadGraph g(p);
+      std::vector<MegaRead> data(n);
+      g.nodes_.assign(n, Node{});
+      g.mega_reads_.clear();
+      for (int i = 0; i < n; ++i) {
+        double a = pos(rng), b = pos(rng);
+        if (b < a) std::swap(a, b);
+        MegaRead& m = data[i];
+        m.tiling_start = a; m.tiling_end = b; m.density = dens(rng);
+        m.start_node = m.end_node = i;
+        g.nodes_[i].imp_s = a; g.nodes_[i].imp_e = b; g.nodes_[i].lstart = -1;
+        g.nodes_[i].lpath = (int)(m.density * (b - a));
+      }
+      for (auto& m : data) g.mega_reads_.push_back(&m);
+      std::vector<int> sg(n), sm(n), rg, rm;
+      for (int i = 0; i < n; ++i) sg[i] = sm[i] = i;
+      std::sort(sg.begin(), sg.end(), [&](int i, int j) { return g.nodes_[i].lpath < g.nodes_[j].lpath; });
+      std::sort(sm.begin(), sm.end(), [&](int i, int j) { return g.nodes_[i].imp_e < g.nodes_[j].imp_e; });
+      const int s_g = g.tile_greedy(sg, rg), s_m = g.tile_maximal(sm, rm);
+      auto score = [&](const std::vector<int>& t) { int s = 0; for (int i : t) s += g.nodes_[i].lpath; return s; };
+      // EXPECT_LE(greedy, maximal): greedy tolerates longer overlaps than maximal (see
+      // below), so the reference's time-seeded test fails on a fraction of seeds; counted
+      if (!(s_g <= s_m)) ++le_violations;
+      if (score(rg) != s_g || score(rm) != s_m) { ++fails; if (getenv("OG_VERBOSE")) fprintf(stderr, "score\n"); }
+      // check_no_overlap (test_tiling.cc:17-28): no piece of (covered & pos) is as long as
+      // min(play * k, |pos|); covered = union of the earlier intervals, touching ones joined
+      for (const auto* t : {&rg, &rm}) {
+        std::vector<std::pair<double, double>> cov;  // disjoint, sorted
+        for (int i : *t) {
+          const double a = g.nodes_[i].imp_s, b = g.nodes_[i].imp_e;
+          // maximal: the test's bound.  greedy: the bound overlap_graph.cc:177 applies,
+          // max(play * k, |pos| * (play - 0.9)); test_tiling.cc checks min(play * k, |pos|)
+          // for both, which the reference's own greedy does not guarantee
+          const double mx = t == &rm ? std::min(1.2 * 70, b - a) : std::max(1.2 * 70, (b - a) * (1.2 - 0.9));
+          for (auto& c : cov) {
+            const double lo = std::max(a, c.first), hi = std::min(b, c.second);
+            if (lo < hi && hi - lo >= mx) { ++fails; if (getenv("OG_VERBOSE")) fprintf(stderr, "ovl %s %g %g\n", t == &rg ? "greedy" : "maximal", a, b); break; }
+          }
+          if (a < b) {
+            double lo = a, hi = b;
+            std::vector<std::pair<double, double>> nc;
+            for (auto& c : cov) {
+              if (c.second < lo || c.first > hi) nc.push_back(c);
+              else { lo = std::min(lo, c.first); hi = std::max(hi, c.second); }
+            }
+            nc.emplace_back(lo, hi);
+            std::sort(nc.begin(), nc.end());
+            cov.swap(nc);
+          }
+        }
+      }
+    }
+    return fails;
+  }
+};
+}  // namespace megareads
+
+using namespace megareads;
+
+static int names_checks() {
+  int f = 0;
+  auto eq = [&](bool c, const char* what) { if (!c) { fprintf(stderr, "FAIL %s\n", what); ++f; } };
+  const unitig_list a = parse_name("1234F_10R_56F");
+  eq(a.size() == 3 && unitig_id(a[0]) == 1234 && !unitig_rev(a[0]) && unitig_rev(a[1]), "parse");
+  std::ostringstream os;
+  print_name(os, reverse_name(a));
+  eq(os.str() == "56R_10F_1234R", "reverse");               // test_super_read_name.cc: reverse
+  eq(parse_name("junk").empty() && parse_name("").empty(), "parse invalid");
+  eq(parse_name("17").size() == 1 && !unitig_rev(parse_name("17")[0]), "plain number = F");
+  // overlap: last m of a == first m of b (dovetail), m < size
+  eq(name_overlap(parse_name("1F_2F_3F"), parse_name("2F_3F_4F")) == 2, "overlap 2");
+  eq(name_overlap(parse_name("1F_2F_3F"), parse_name("3F_4F")) == 1, "overlap 1");
+  eq(name_overlap(parse_name("1F_2F_3F"), parse_name("4F_5F")) == 0, "no overlap");
+  eq(name_overlap(parse_name("1F"), parse_name("1F_2F")) == 0, "short names");
+  eq(name_overlap(parse_name("1F_2F_3F"), parse_name("1F_2F_3F")) == 0, "self: proper suffix only");
+  eq(name_overlap(parse_name("1F_1F_1F"), parse_name("1F_1F_1F")) == 2, "repeat overlap");
+  // union_find (test_union_find.cc): union by rank, roots shared after unions
+  UnionFind u;
+  u.reset(6);
+  u.unite(0, 1); u.unite(2, 3); u.unite(1, 3);
+  eq(u.root(0) == u.root(3) && u.root(4) != u.root(0) && u.root(5) == 5, "union find");
+  return f;
+}
+
+int main(int argc, char** argv) {
+  if (argc >= 2 && !strcmp(argv[1], "names")) return names_checks() ? 1 : 0;
+  if (argc >= 4 && !strcmp(argv[1], "tiling")) {
+    const int f = ReadGraphTest::run((unsigned)atoi(argv[2]), atoi(argv[3]));
+    printf("tiling property failures: %d greedy>maximal: %d\n", f, ReadGraphTest::le_violations);
+    return f ? 1 : 0;
+  }
+  if (argc < 4 || strcmp(argv[1], "graph")) { fprintf(stderr, "usage: og_driver graph|tiling|names ...\n"); return 2; }
+  std::ifstream pf(argv[2]);
+  Params p;
+  int bases;
+  std::string tiling, trim, ul_path, us_path = "-";
+  pf >> p.k_len >> p.overlap_play >> p.nb_errors >> bases >> p.min_density >> p.min_len >> tiling >> trim >> ul_path >> us_path;
+  p.maximize_bases = bases != 0;
+  p.tiling = tiling == "none" ? Tiling::NONE : tiling == "maximal" ? Tiling::MAXIMAL
+           : tiling == "weighted" ? Tiling::WEIGHTED : Tiling::GREEDY;
+  p.trim = trim == "match" ? Trim::MATCH : trim == "branch" ? Trim::BRANCH : Trim::NONE;
+  std::vector<int> ul;
+  std::vector<std::string> useqs;
+  if (us_path != "-") {  // -u (create_mega_reads.cpp read_unitigs_sequences)
+    std::ifstream is(us_path);
+    while (is.ignore(std::numeric_limits<std::streamsize>::max(), '\n')) {
+      useqs.push_back("");
+      std::getline(is, useqs.back());
+      ul.push_back((int)useqs.back().size());
+    }
+    p.unitig_sequences = &useqs;
+  } else {
+    std::ifstream is(ul_path);
+    std::string nm;
+    unsigned len;
+    is >> nm >> len;
+    while (is.good()) { ul.push_back((int)len); is >> nm >> len; }
+  }
+  p.unitig_lengths = &ul;
+  std::ifstream rf(argv[3]);
+  std::string tag, name;
+  size_t n;
+  std::map<std::string, unitig_list> names;
+  std::vector<std::vector<int32_t>> infos;
+  ReadGraph g(p);
+  while (rf >> tag >> name >> n) {
+    std::vector<Coord> coords(n);
+    std::vector<std::string> qn(n);
+    std::vector<std::vector<int32_t>> km(n), kb(n);
+    for (size_t i = 0; i < n; ++i) {
+      Coord& c = coords[i];
+      std::string st, of, er;
+      uint32_t ni;
+      rf >> c.rs >> c.re >> c.qs >> c.qe >> c.nb_mers >> c.sr_cover >> c.rl >> c.ql >> st >> of >> er >> qn[i] >> ni;
+      c.stretch = strtod(st.c_str(), nullptr); c.offset = strtod(of.c_str(), nullptr); c.avg_err = strtod(er.c_str(), nullptr);
+      km[i].resize(ni); kb[i].resize(ni);
+      for (auto& x : km[i]) rf >> x;
+      for (auto& x : kb[i]) rf >> x;
+      if (!names.count(qn[i])) names[qn[i]] = parse_name(qn[i]);
+      c.name = &names[qn[i]];
+      c.kmers_info = km[i].data(); c.bases_info = kb[i].data(); c.n_info = ni;
+    }
+    g.process(coords, name, std::cout, nullptr);
+  }
+  return 0;
+}

@@ -211,6 +211,18 @@ def main():
                "coords_forward_expected", "details_normal_expected", "details_forward_expected"]:
         shutil.copyfile(os.path.join(REFSRC, "tests", "aligner_output", fn), os.path.join(dst, fn))
     print("aligner_output ok")
+    copy_mega_reads_output()
+
+
+def copy_mega_reads_output():
+    """Inputs of the reference's tests/mega_reads_output (its Tupfile runs create_mega_reads on
+    them; no expected mega-reads are held, and expect_coords is from an older aligner: the
+    Tupfile's diff against it is commented out) -- data files, copied verbatim."""
+    dst = os.path.join(HERE, "mega_reads_output")
+    os.makedirs(dst, exist_ok=True)
+    for fn in ["sr.fa", "pb.fa", "kUnitigLengths.txt"]:
+        shutil.copyfile(os.path.join(REFSRC, "tests", "mega_reads_output", fn), os.path.join(dst, fn))
+    print("mega_reads_output ok")
 
 
 if __name__ == "__main__":

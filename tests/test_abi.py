@@ -84,3 +84,23 @@ CLI = os.path.join(ROOT, "pacbio_amd", "bin", "jf_aligner")
 def test_cli_argument_errors(args, msg):
     r = subprocess.run([CLI] + args, capture_output=True, text=True)
     assert r.returncode != 0 and msg in r.stderr, r.stderr
+
+
+CMR = os.path.join(ROOT, "pacbio_amd", "bin", "create_mega_reads")
+
+
+@pytest.mark.parametrize("args,msg", [
+    ([], "-s, --size is required"),
+    (["-s", "1"], "-m, --mer is required"),
+    (["-s", "1", "-m", "17"], "-k, --k-mer is required"),
+    (["-s", "1", "-m", "17", "-k", "31"], "unitig lengths (-l) or sequences (-u) are required"),
+    (["-s", "1", "-m", "17", "-k", "31", "-l", "x", "-u", "y"], "conflicts"),
+    (["-s", "1", "-m", "17", "-k", "31", "-l", "x", "--max-count", "0"], "undefined behaviour"),
+    (["-s", "1", "-m", "17", "-k", "31", "-l", "x", "-T", "best"], "invalid --tiling"),
+    (["-s", "1", "-m", "17", "-k", "31", "-l", "x", "--trim", "all"], "invalid --trim"),
+    (["-s", "1", "-m", "17", "-k", "31", "-l", "/nonexistent/ul.txt"], "Failed to open unitig lengths"),
+])
+def test_create_mega_reads_argument_errors(args, msg):
+    """create_mega_reads_cmdline.yaggo's required / conflicting options, checked before any GPU call"""
+    r = subprocess.run([CMR] + args, capture_output=True, text=True)
+    assert r.returncode != 0 and msg in r.stderr, r.stderr

@@ -1,0 +1,142 @@
+"""create_mega_reads on the GPU (pacbio_amd/bin/create_mega_reads: pbgpu_run's
+records consumer -> overlap_graph.cpp) against the CPU restatements: records
+from oracle/pb_oracle.c, mega-reads from oracle/mega_reads.py.  Byte-identical
+output for the reference's tests/mega_reads_output inputs with its Tupfile's
+create_mega_reads flags, and for a synthetic dataset over the tiling / trim /
+-b / -u options; multi-batch and two-index ("--devices 0,0") runs and gzip
+input give the same bytes; --dot writes one graph per read with mega-reads.
+
+Parity is pinned to the restatements only (see tests/test_mega_reads.py)."""
+import gzip
+import os
+import shutil
+import subprocess
+import tempfile
+
+import pytest
+
+from oracle import mega_reads as MR
+from oracle import oracle as O
+from tests.test_mega_reads import MRO, read_fasta, read_ul, write_unitig_sequences
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CMR = os.path.join(ROOT, "pacbio_amd", "bin", "create_mega_reads")
+BIG = str(1 << 30)  # --max-count: the Tupfile's 0 means INT_MAX upstream (undefined behaviour there)
+
+
+def _run(args, timeout=120):
+    r = subprocess.run([CMR, *args], capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr
+    return r
+
+
+def _expect(reads, ul, k, useqs=None, **opt):
+    o = dict(play=1.3, errors=3.0, bases=False, density=0.029, min_len=100.0, tiling="greedy", trim="none")
+    o.update(opt)
+    return "".join(MR.mega_reads(n, recs, ul, k, useqs=useqs, **o) for n, recs in reads)
+
+
+@pytest.fixture(scope="module")
+def mro():
+    names, seqs = read_fasta(os.path.join(MRO, "sr.fa"))
+    ul = read_ul(os.path.join(MRO, "kUnitigLengths.txt"))
+    oix = O.OracleIndex.from_records(names, seqs, 15)
+    p = O.params(k=15, forward=True, max_count=1 << 30, bases_matching=10.0, stretch_cap=400.0, unitigs_k=70,
+                 unitig_lengths=ul)
+    pn, ps = read_fasta(os.path.join(MRO, "pb.fa"))
+    reads = [(n, MR.records_of(oix, p, s)) for n, s in zip(pn, ps)]
+    oix.close()
+    return reads, ul
+
+
+@pytest.mark.parametrize("threads", ["1", "4"])
+def test_reference_inputs_tupfile_flags(mro, tmp_path, threads):
+    """tests/mega_reads_output/Tupfile:16 (create_mega_reads -s 20k -m 15 -B 10 -L 0 -k 70
+    --stretch-cap 400 --dot ...)"""
+    reads, ul = mro
+    out, dot = str(tmp_path / "crm_mega_reads"), str(tmp_path / "crm_mega_reads.dot")
+    _run(["-s", "20k", "-m", "15", "-B", "10", "-L", "0", "--max-count", BIG, "-l",
+          os.path.join(MRO, "kUnitigLengths.txt"), "-o", out, "-k", "70", "--stretch-cap", "400", "--dot", dot,
+          "-t", threads, "-r", os.path.join(MRO, "sr.fa"), "-p", os.path.join(MRO, "pb.fa")])
+    want = _expect(reads, ul, 70, min_len=0.0)
+    assert want.count(">") == 2
+    assert open(out).read() == want
+    d = open(dot).read()
+    assert d.count("digraph") == 2 and d.count("{") == d.count("}") and "[color=\"red\"]" in d
+
+
+@pytest.fixture(scope="module")
+def synth():
+    from tools.synth import Dataset
+    d = tempfile.mkdtemp(prefix="pbgpu_cmr_")
+    ds = Dataset("small", seed=11)
+    ds.write(d)
+    ul = [int(x) for x in ds.unitig_lengths]
+    names, seqs = [n.decode() for n in ds.sr_names()], ds.sr_seqs()
+    pn, ps = [n.decode() for n in ds.pb_names()], ds.pb_seqs()
+    ds.close()
+    oix = O.OracleIndex.from_records(names, seqs, 17)
+    cache = {}
+
+    def reads_for(**pk):
+        key = tuple((k, tuple(v) if isinstance(v, list) else v) for k, v in sorted(pk.items()))
+        if key not in cache:
+            p = O.params(k=17, forward=True, unitigs_k=31, unitig_lengths=pk.pop("ul", ul), **pk)
+            cache[key] = [(n, MR.records_of(oix, p, s)) for n, s in zip(pn, ps)]
+        return cache[key]
+    yield d, ul, reads_for
+    oix.close()
+    shutil.rmtree(d, ignore_errors=True)
+
+
+CASES = [
+    ([], {}, {}),
+    (["-T", "maximal", "-L", "0"], {}, dict(tiling="maximal", min_len=0.0)),
+    (["-T", "weighted", "--trim", "match"], {}, dict(tiling="weighted", trim="match")),
+    (["-T", "none", "-b", "-d", "0.05"], {}, dict(tiling="none", bases=True, density=0.05)),
+    (["-O", "1.5", "-e", "2", "--trim", "branch", "-L", "50"], {}, dict(play=1.5, errors=2.0, trim="branch",
+                                                                         min_len=50.0)),
+    (["--max-match", "-B", "10", "--stretch-cap", "500"], dict(max_match=True, bases_matching=10.0, stretch_cap=500.0),
+     {}),
+]
+
+
+@pytest.mark.parametrize("cli,aopt,gopt", CASES, ids=[" ".join(c[0]) or "defaults" for c in CASES])
+def test_synthetic_options(synth, tmp_path, cli, aopt, gopt):
+    d, ul, reads_for = synth
+    out = str(tmp_path / "mr")
+    _run(["-s", "1M", "-m", "17", "-k", "31", "-l", os.path.join(d, "ul.txt"), "-t", "4", "-o", out, *cli,
+          "-r", os.path.join(d, "sr.fa"), "-p", os.path.join(d, "pb.fa")])
+    want = _expect(reads_for(**aopt), ul, 31, **gopt)
+    assert want.count(">") >= 10
+    assert open(out).read() == want
+
+
+def test_synthetic_unitig_sequences(synth, tmp_path):
+    """-u: unitig lengths from the sequences, each mega-read followed by its sequence"""
+    d, ul, reads_for = synth
+    up = str(tmp_path / "useqs.fa")
+    useqs = write_unitig_sequences(up, ul)
+    uls = [len(s) for s in useqs]
+    out = str(tmp_path / "mr")
+    _run(["-s", "1M", "-m", "17", "-k", "31", "-u", up, "-o", out, "-r", os.path.join(d, "sr.fa"), "-p",
+          os.path.join(d, "pb.fa")])
+    want = _expect(reads_for(ul=uls), uls, 31, useqs=useqs)
+    assert open(out).read() == want
+
+
+def test_batches_devices_gzip_identical(synth, tmp_path):
+    """many small batches over two aligners on two indexes of device 0, gzip input: same bytes"""
+    d, ul, _ = synth
+    base = ["-s", "1M", "-m", "17", "-k", "31", "-l", os.path.join(d, "ul.txt"), "-T", "maximal",
+            "-r", os.path.join(d, "sr.fa")]
+    a, b = str(tmp_path / "a"), str(tmp_path / "b")
+    _run([*base, "-o", a, "-p", os.path.join(d, "pb.fa")])
+    gz = str(tmp_path / "pb.fa.gz")
+    with open(os.path.join(d, "pb.fa"), "rb") as f, gzip.open(gz, "wb") as g:
+        g.write(f.read())
+    _run([*base, "-o", b, "-p", gz, "--devices", "0,0", "--streams", "2", "--batch-bases", "20k", "-t", "3"])
+    ta = open(a).read()
+    assert ta.count(">") >= 10 and open(b).read() == ta
