@@ -1,5 +1,5 @@
 #!/bin/bash
-# k_group tier-0 ms per library variant (tools/prof_lis.py, non-PROF path): bash tools/ab_group_ms.sh v1 v2 ...
+# k_group tier-0 ms per library variant (tools/prof_lis.py, non-PROF path): bash tools/exp/ab_group_ms.sh v1 v2 ...
 # ("base" = the product libpbgpu.so)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1

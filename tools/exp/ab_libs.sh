@@ -1,5 +1,5 @@
 #!/bin/bash
-# phase profile (tools/prof_lis.py) under several library variants: bash tools/ab_libs.sh prof prof_x ...
+# phase profile (tools/prof_lis.py) under several library variants: bash tools/exp/ab_libs.sh prof prof_x ...
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out

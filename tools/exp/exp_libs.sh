@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU suite on the product library, then the C2 bench (3 steps) for it and each
 # experiment variant libpbgpu_<name>.so given as arguments.
-# Usage (via gpurun): bash tools/exp_libs.sh [variant ...]
+# Usage (via gpurun): bash tools/exp/exp_libs.sh [variant ...]
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out

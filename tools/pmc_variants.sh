@@ -1,5 +1,5 @@
 #!/bin/bash
-# TCC hit/miss per k_coords launch for library variants (tools/exp_coords.py).
+# TCC hit/miss per k_coords launch for library variants (tools/exp/exp_coords.py).
 # Usage (via gpurun): bash tools/pmc_variants.sh v1 v2 ...   (libpbgpu_<v>.so)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
@@ -7,7 +7,7 @@ for v in "$@"; do
   D=gpurun_out/pmcv_$v
   mkdir -p $D
   PBGPU_LIB=pacbio_amd/libpbgpu_$v.so timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex k_coords \
-    --output-format csv -d $D -o run -- python3 tools/exp_coords.py --reps 1 > $D/log 2>&1 || { tail -20 $D/log; exit 1; }
+    --output-format csv -d $D -o run -- python3 tools/exp/exp_coords.py --reps 1 > $D/log 2>&1 || { tail -20 $D/log; exit 1; }
   python3 - "$D" "$v" <<'PY'
 import csv, glob, sys, collections
 acc = collections.defaultdict(float); disp = collections.defaultdict(set)
