@@ -374,8 +374,8 @@ typedef struct {
   double   read_seconds;          /* reader: parse input into batches */
   double   upload_seconds;        /* workers: host -> device read copies */
   double   align_seconds;         /* workers: the device pipeline (host wall) */
-  double   format_seconds;        /* workers: device text formatting */
-  double   d2h_seconds;           /* workers: text -> pinned host memory */
+  double   format_seconds;        /* workers: device text formatting (records_fn: record download) */
+  double   d2h_seconds;           /* workers: text -> pinned host memory (records_fn: the consumer) */
   double   write_seconds;         /* writer: write() calls */
   double   writer_idle_seconds;   /* writer: waiting for the next batch in order */
   double   open_seconds;          /* opening (creating / truncating) the output files */

@@ -9,7 +9,8 @@
 // the host and the per-read overlap graph, longest path, tiling and mega-read
 // printing (overlap_graph.cpp) run on a pool of host threads; the mega-reads of
 // each batch are written in input order (the reference's output with -t 1).
-// GPU options as in jf_aligner: --devices, --streams, --batch-bases.
+// GPU options as in jf_aligner: --devices, --streams, --batch-bases, --timing
+// (stage times as JSON on stderr).
 #include <getopt.h>
 
 #include <algorithm>
@@ -170,12 +171,13 @@ int main(int argc, char** argv) {
   ap.forward = 1;  // create_mega_reads.cc:142
   Ctx C;
   uint32_t psa_min = 13, threads = 1, streams = 2;
+  bool timing = false;
   bool s_given = false, m_given = false, k_given = false;
   const char *out_path = nullptr, *dot_path = nullptr, *ul_path = nullptr, *us_path = nullptr;
   std::vector<const char*> srs, pbs;
   std::vector<int> devices;
   uint64_t batch_bases = 64ull << 20;
-  enum { O_PSA = 256, O_DOT, O_SC, O_SF, O_CAP, O_WIN, O_MAXM, O_MAXC, O_TRIM, O_DEVS, O_BATCH, O_STREAMS };
+  enum { O_PSA = 256, O_DOT, O_SC, O_SF, O_CAP, O_WIN, O_MAXM, O_MAXC, O_TRIM, O_DEVS, O_BATCH, O_STREAMS, O_TIMING };
   static struct option lo[] = {
       {"size", 1, 0, 's'}, {"mer", 1, 0, 'm'}, {"fine-mer", 1, 0, 'F'}, {"psa-min", 1, 0, O_PSA},
       {"unitigs-lengths", 1, 0, 'l'}, {"unitigs-sequences", 1, 0, 'u'}, {"k-mer", 1, 0, 'k'},
@@ -185,7 +187,7 @@ int main(int argc, char** argv) {
       {"mers-matching", 1, 0, 'M'}, {"max-match", 0, 0, O_MAXM}, {"max-count", 1, 0, O_MAXC}, {"bases", 0, 0, 'b'},
       {"density", 1, 0, 'd'}, {"min-length", 1, 0, 'L'}, {"tiling", 1, 0, 'T'}, {"trim", 1, 0, O_TRIM},
       {"superreads", 1, 0, 'r'}, {"pacbio", 1, 0, 'p'}, {"devices", 1, 0, O_DEVS}, {"batch-bases", 1, 0, O_BATCH},
-      {"streams", 1, 0, O_STREAMS}, {0, 0, 0, 0}};
+      {"streams", 1, 0, O_STREAMS}, {"timing", 0, 0, O_TIMING}, {0, 0, 0, 0}};
   int c;
   while ((c = getopt_long(argc, argv, "s:m:F:l:u:k:t:o:O:e:B:M:bd:L:T:r:p:", lo, nullptr)) != -1) {
     switch (c) {
@@ -243,6 +245,7 @@ int main(int argc, char** argv) {
     }
     case O_BATCH: batch_bases = parse_suffix(optarg); break;
     case O_STREAMS: streams = std::max(1u, parse_u32(optarg, "--streams")); break;
+    case O_TIMING: timing = true; break;
     default: die("bad option (see create_mega_reads_cmdline.yaggo)");
     }
   }
@@ -314,5 +317,14 @@ int main(int argc, char** argv) {
   const std::string err = rs == PBGPU_OK ? "" : pbgpu_last_error();
   for (auto& b : built) pbgpu_index_free(b.second);
   if (rs != PBGPU_OK) die("align: " + err);
+  if (timing)
+    fprintf(stderr,
+            "{\"wall_s\": %.6f, \"batches\": %llu, \"reads\": %llu, \"bases\": %llu, \"records\": %llu, "
+            "\"output_bytes\": %llu, \"read_s\": %.6f, \"upload_s\": %.6f, \"align_s\": %.6f, "
+            "\"download_s\": %.6f, \"graph_s\": %.6f, \"write_s\": %.6f, \"writer_idle_s\": %.6f}\n",
+            st.wall_seconds, (unsigned long long)st.n_batches, (unsigned long long)st.n_reads,
+            (unsigned long long)st.n_bases, (unsigned long long)st.n_records, (unsigned long long)st.coords_bytes,
+            st.read_seconds, st.upload_seconds, st.align_seconds, st.format_seconds, st.d2h_seconds, st.write_seconds,
+            st.writer_idle_seconds);
   return 0;
 }

@@ -381,8 +381,35 @@ void write_all(int fd, const char* p, uint64_t n, const char* what) {
 // Long-lived resources of the driver: aligners, their resident read buffers,
 // the pinned batch and text buffers.  A server-style caller (bench.py) runs
 // many files through one runner; the CLI runs one.
+// The records of an aligner's last batch in pinned host memory, as a
+// pbgpu_coords_batch view (the records consumer's input): no zero-filled
+// vectors, no pageable staging copies; valid until the next download.
+struct RecordsView {
+  PinnedVec off, recs, km, kb;
+  pbgpu_coords_batch c{};
+  void download(pbgpu_aligner* al) {
+    const uint64_t n = al->last_reads, nr = al->last_records, ni = al->last_info;
+    static_assert(sizeof(pbgpu_record) == sizeof(Rec), "record layout");
+    off.reserve((n + 1) * 8); recs.reserve(std::max<uint64_t>(nr, 1) * sizeof(Rec));
+    km.reserve(std::max<uint64_t>(ni, 1) * 4); kb.reserve(std::max<uint64_t>(ni, 1) * 4);
+    HIPCHK(hipMemcpyAsync(off.p, al->rec_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, al->st));
+    if (nr) HIPCHK(hipMemcpyAsync(recs.p, al->recs_sorted.p, nr * sizeof(Rec), hipMemcpyDeviceToHost, al->st));
+    if (ni) {
+      HIPCHK(hipMemcpyAsync(km.p, al->info_m.p, ni * 4, hipMemcpyDeviceToHost, al->st));
+      HIPCHK(hipMemcpyAsync(kb.p, al->info_b.p, ni * 4, hipMemcpyDeviceToHost, al->st));
+    }
+    HIPCHK(hipStreamSynchronize(al->st));
+    pbgpu_record* r = (pbgpu_record*)recs.p;
+    if (al->ix->sr_begin)  // a shard's device super-read ids are local
+      for (uint64_t i = 0; i < nr; ++i) r[i].sr_index += (uint32_t)al->ix->sr_begin;
+    c.n_reads = n; c.n_records = nr; c.read_offsets = (const uint64_t*)off.p; c.records = r;
+    c.n_info = ni; c.kmers_info = (const int32_t*)km.p; c.bases_info = (const int32_t*)kb.p;
+  }
+};
+
 struct pbgpu_runner {
   std::vector<pbgpu_aligner*> al;
+  std::vector<std::unique_ptr<RecordsView>> views;  // per aligner (records consumer runs)
   std::vector<std::unique_ptr<pbgpu_reads>> rd;
   bool details = false;
   bool side = false;  // a second output file (details, or the records consumer's side text)
@@ -485,8 +512,9 @@ static void runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_s
         Done d;
         double t3, t4, t5;
         if (run->records_fn) {  // records to the host consumer (create_mega_reads)
-          pbgpu_coords_batch* cb = nullptr;
-          if (pbgpu_download(al, &cb) != PBGPU_OK) throw std::runtime_error(pbgpu_last_error());
+          RecordsView& V = *R->views[wi];
+          V.download(al);
+          const pbgpu_coords_batch* cb = &V.c;
           t3 = t4 = now_s();
           std::vector<std::string> nm(b->n());
           std::vector<const char*> np(b->n());
@@ -500,7 +528,6 @@ static void runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_s
           char* side = nullptr;
           int fst = 0;
           d.mtext = run->records_fn(run->records_user, al->ix, cb, np.data(), lens.data(), &tl, &side, &sl, &fst);
-          pbgpu_coords_free(cb);
           if (side) { d.details.assign(side, sl); free(side); }
           if (fst) { free(d.mtext); throw std::runtime_error("the records consumer failed"); }
           d.len = d.mtext ? tl : 0;
@@ -673,6 +700,7 @@ pbgpu_status pbgpu_runner_create(pbgpu_index* const* indexes, size_t n_indexes, 
       if (s != PBGPU_OK) return s;
       R->al.push_back(a);
       R->rd.emplace_back(new pbgpu_reads);
+      R->views.emplace_back(new RecordsView);
       if (R->details) pbgpu_aligner_set_details(a, 1);
     }
   const size_t W = R->al.size();

@@ -8,6 +8,7 @@
 // RECORDS: "R name n" then n lines: rs re qs qe nb_mers sr_cover rl ql stretch offset avg_err
 //          (hex floats) name n_info kmers... bases...
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -160,6 +161,7 @@ int main(int argc, char** argv) {
   std::map<std::string, unitig_list> names;
   std::vector<std::vector<int32_t>> infos;
   ReadGraph g(p);
+  double graph_s = 0;
   while (rf >> tag >> name >> n) {
     std::vector<Coord> coords(n);
     std::vector<std::string> qn(n);
@@ -177,7 +179,10 @@ int main(int argc, char** argv) {
       c.name = &names[qn[i]];
       c.kmers_info = km[i].data(); c.bases_info = kb[i].data(); c.n_info = ni;
     }
+    const auto t0 = std::chrono::steady_clock::now();
     g.process(coords, name, std::cout, nullptr);
+    graph_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
+  if (getenv("OG_TIME")) fprintf(stderr, "graph seconds %.6f\n", graph_s);
   return 0;
 }
