@@ -308,6 +308,17 @@ def main():
                          f"formatting, {cthreads} threads (the job's CPU share of the box), {sec:.2f} s",
                "gpu_parity_reads_checked": len(oe), "gpu_parity_reads_differing": mism}
 
+    # SURVEY 8(d)'s whole-path algorithmic bytes of the device leg: 2-bit read stream,
+    # 64-B index probes, occurrences enumerated (8 B), hits grouped (write + read, 16 B),
+    # LIS predecessor tests (16 B), records out (96 B)
+    dsteps = max(1, args.device_steps)
+    path_bytes = (0.25 * st["n_bases"] + 64 * st["n_probes"] + 8 * st["n_hits"] + 16 * st["n_hits"] +
+                  16 * st["n_lis_tests"] + 96 * st["n_records"]) / dsteps
+    path_gbs = path_bytes / (el_dev / dsteps) / 1e9
+    path_roof = {"bytes_alg_per_step": path_bytes, "achieved": path_gbs, "unit": "GB/s",
+                 "frac": path_gbs / HBM_PEAK_GBS, "frac_of_b_rand": (path_gbs / b_rand) if b_rand else None,
+                 "formula": "0.25*bases + 64*probes + 8*occurrences + 16*hits + 16*lis_tests + 96*records (SURVEY 8d)"}
+
     if rank == 0:
         stage = {n: round(sum(r[n] for r in rstats) / args.steps * 1e3, 3) for n in
                  ("read_seconds", "upload_seconds", "align_seconds", "format_seconds", "d2h_seconds",
@@ -353,7 +364,9 @@ def main():
                                "kernel_launches": dict(kn),
                                "counters_per_step": {n: st[n] // args.device_steps for n in
                                                      ("n_kmers", "n_probes", "n_kept", "n_hits", "n_chains",
-                                                      "n_lis_tests", "n_records")}},
+                                                      "n_lis_tests", "n_records")},
+                               "path_roofline": path_roof},
+                "end_to_end_including_build_s": round(t_index + elapsed / args.steps, 3),
                 "fit_dtype": "f64",
             },
             "roofline": {"bound": "hbm", "kernel": dom, "rocprof_kernel": ROCPROF_FILE[dom], "achieved": achieved,
