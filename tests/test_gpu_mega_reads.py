@@ -82,6 +82,9 @@ def synth():
 
     def reads_for(**pk):
         key = tuple((k, tuple(v) if isinstance(v, list) else v) for k, v in sorted(pk.items()))
+        if pk.get("fine_k") and "fine" not in cache:
+            oix.build_fine(pk["fine_k"])
+            cache["fine"] = pk["fine_k"]
         if key not in cache:
             p = O.params(k=17, forward=True, unitigs_k=31, unitig_lengths=pk.pop("ul", ul), **pk)
             cache[key] = [(n, MR.records_of(oix, p, s)) for n, s in zip(pn, ps)]
@@ -100,6 +103,8 @@ CASES = [
                                                                          min_len=50.0)),
     (["--max-match", "-B", "10", "--stretch-cap", "500"], dict(max_match=True, bases_matching=10.0, stretch_cap=500.0),
      {}),
+    # -F: the records are the fine aligner's (create_mega_reads.cc:64-68)
+    (["-F", "13", "-L", "0"], dict(fine_k=13), dict(min_len=0.0)),
 ]
 
 
