@@ -1408,7 +1408,12 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
         HIPCHK(hipStreamSynchronize(st));
         n_ovf = cnt[3];
       }
+#ifndef PBGPU_EXP_GROUP_ONLY
       const uint32_t nch = cnt[0];
+#else  // experiment: time the group stage alone (no chains go further; tier routing as usual)
+      const uint32_t nch = 0;
+      if (Hs) al->chains_per_hit = std::max(1e-4, 1.1 * (double)cnt[0] / (double)Hs);
+#endif
       if (nch > O.chain_cap) {  // descriptor buffer too small: grow, redo this sub-batch's grouping
         if (attempt > 8) throw std::runtime_error("chain descriptor capacity did not converge");
         al->chains.ensure((uint64_t)nch + nch / 8 + 1);
@@ -1495,7 +1500,9 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
         if (al->details) capture_details(al, nch, Hs);
         rec_done = nrec; info_done = ninfo;
         n_chains += sub[0]; n_tests += sub[1];
+#ifndef PBGPU_EXP_GROUP_ONLY
         if (Hs) al->chains_per_hit = std::max(1e-4, 1.1 * (double)nch / (double)Hs);
+#endif
         break;
       }
       if (attempt > 8) throw std::runtime_error("record buffer growth did not converge");

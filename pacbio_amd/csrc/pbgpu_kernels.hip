@@ -700,7 +700,11 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
             __syncthreads();
           }
 #endif
+#ifndef PBGPU_EXP_GROUP_NOSTORE  // experiment (with PBGPU_EXP_GROUP_ONLY): no list store
           if (mine) O.X[hbase + pos] = make_int2(pb, fwd ? so : -so);
+#else
+          if (mine && pos == 0xFFFFFFFFu) O.X[hbase] = make_int2(pb, so);
+#endif
         }
       }
       }
