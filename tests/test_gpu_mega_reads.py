@@ -145,3 +145,21 @@ def test_batches_devices_gzip_identical(synth, tmp_path):
     _run([*base, "-o", b, "-p", gz, "--devices", "0,0", "--streams", "2", "--batch-bases", "20k", "-t", "3"])
     ta = open(a).read()
     assert ta.count(">") >= 10 and open(b).read() == ta
+
+
+def test_reads_without_records_and_empty_input(synth, tmp_path):
+    """reads with no alignment print nothing (print_mega_reads prints only reads with
+    mega-reads, overlap_graph.hpp:253-262); an empty PacBio file gives an empty output"""
+    import random
+    d, _, _ = synth
+    rng = random.Random(3)
+    pb = tmp_path / "pb.fa"
+    pb.write_text(">empty\n\n>random\n" + "".join(rng.choice("ACGT") for _ in range(3000)) + "\n>short\nACGT\n")
+    out = str(tmp_path / "mr")
+    base = ["-s", "1M", "-m", "17", "-k", "31", "-l", os.path.join(d, "ul.txt"), "-r", os.path.join(d, "sr.fa")]
+    _run([*base, "-o", out, "-p", str(pb)])
+    assert open(out).read() == ""
+    empty = tmp_path / "none.fa"
+    empty.write_text("")
+    _run([*base, "-o", out, "-p", str(empty)])
+    assert open(out).read() == ""
