@@ -108,6 +108,25 @@ def _kernel_bytes(st):
     }
 
 
+def _pick_workdir(want, workload, n_pb):
+    """The work directory must hold, for every rank of this node, its FASTA files
+    (~1.4 B per PacBio base) and a coords file (~6.6 B a base) while the previous one
+    is being removed: ~10 B a base with margin.  /tmp on a GPU box is ~80 GB, which 8
+    ranks of C2 come close to, so fall back to /dev/shm when `want` is too small."""
+    import shutil
+    from tools.synth import PRESETS
+    local_ranks = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+    need = 10.0 * n_pb * PRESETS[workload]["pb_len_mean"] * local_ranks + 2e9
+    for d in (want, "/dev/shm"):
+        try:
+            if shutil.disk_usage(d).free >= need:
+                return d
+        except OSError:
+            pass
+    print(f"bench: warning: no work directory with {need / 1e9:.0f} GB free; using {want}", file=sys.stderr)
+    return want
+
+
 def _cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -175,7 +194,7 @@ def main():
     threads = _cpu_share()
     t0 = time.time()
     ds = Dataset(args.workload, seed=42, threads=min(threads, 16), n_pb=n_pb, pb_index_base=rank * n_pb)
-    wd = tempfile.mkdtemp(prefix=f"pbgpu_bench_r{rank}_", dir=args.workdir)
+    wd = tempfile.mkdtemp(prefix=f"pbgpu_bench_r{rank}_", dir=_pick_workdir(args.workdir, args.workload, n_pb))
     ds.write(wd)
     t_gen = time.time() - t0
     sr_fa, pb_fa, ul_txt = (os.path.join(wd, f) for f in ("sr.fa", "pb.fa", "ul.txt"))
@@ -217,12 +236,11 @@ def main():
     cleaners = []
 
     def _step(i):
-        st_ = runner.run([pb_fa], outs[i])
-        if i > 0:
+        if i > 0:  # the previous step's file goes while this one is written
             th = threading.Thread(target=os.unlink, args=(outs[i - 1],))
             th.start()
             cleaners.append(th)
-        return st_
+        return runner.run([pb_fa], outs[i])
     for i in range(args.warmup):
         _step(i)
     for th in cleaners:
