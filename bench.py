@@ -224,6 +224,22 @@ def main():
     al.free(reads)
     al.close()
 
+    # SURVEY 8(d)'s second flag set: the defaults, without -l / -f (device leg only)
+    al2 = pbgpu.StreamAligner(index, streams=args.device_streams, k=k)
+    reads = al2.upload(blob=blob, offsets=off)
+    al2.align_resident(reads)
+    pbgpu.device_synchronize(local)
+    comm.barrier()
+    td = time.perf_counter()
+    for _ in range(args.device_steps):
+        al2.align_resident(reads)
+    pbgpu.device_synchronize(local)
+    comm.barrier()
+    el_dev2 = comm.max(time.perf_counter() - td)
+    st2 = al2.stats()
+    al2.free(reads)
+    al2.close()
+
     # ---- end to end (value): PacBio FASTA -> coords file, pbgpu_run
     # (a pbgpu_runner keeps its aligners and pinned buffers across steps: a service
     # aligning file after file; the CLI's single run pays their setup once).  Every
@@ -384,6 +400,11 @@ def main():
                                                      ("n_kmers", "n_probes", "n_kept", "n_hits", "n_chains",
                                                       "n_lis_tests", "n_records")},
                                "path_roofline": path_roof},
+                "device_leg_default_flags": {
+                    "flags": f"-m {k} --psa-min 13 (defaults: no -l/-k/-f, -B 17, --max-count 5000)",
+                    "value_device": comm.sum(bases_rank) * args.device_steps / el_dev2,
+                    "ms_per_step": el_dev2 / args.device_steps * 1e3,
+                    "records_per_step": st2["n_records"] // max(1, args.device_steps)},
                 "end_to_end_including_build_s": round(t_index + elapsed / args.steps, 3),
                 "fit_dtype": "f64",
             },
