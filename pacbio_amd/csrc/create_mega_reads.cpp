@@ -21,6 +21,8 @@
 #include <cstring>
 #include <fstream>
 #include <limits>
+#include <mutex>
+#include <stdexcept>
 #include <sstream>
 #include <string>
 #include <thread>
@@ -112,7 +114,10 @@ static char* mega_reads_batch(void* user, const pbgpu_index* ix, const pbgpu_coo
     const uint64_t parts = std::min<uint64_t>(n, (uint64_t)T * 8);
     std::vector<std::string> out(parts), dout(parts);
     std::atomic<uint64_t> next(0);
+    std::mutex err_mu;
+    std::string err;  // the first error of any thread (no exception may leave a std::thread)
     auto work = [&]() {
+      try {
       ReadGraph g(C.gp);
       std::vector<Coord> coords;
       for (;;) {
@@ -139,11 +144,17 @@ static char* mega_reads_batch(void* user, const pbgpu_index* ix, const pbgpu_coo
         out[pi] = os.str();
         if (C.dot) dout[pi] = ds.str();
       }
+      } catch (const std::exception& e) {
+        std::lock_guard<std::mutex> lk(err_mu);
+        if (err.empty()) err = e.what();
+        next.store(parts);  // the other threads stop at their next part
+      }
     };
     std::vector<std::thread> th;
     for (int t = 1; t < T; ++t) th.emplace_back(work);
     work();
     for (auto& t : th) t.join();
+    if (!err.empty()) throw std::runtime_error(err);
     auto join = [](const std::vector<std::string>& v, uint64_t* len) -> char* {
       uint64_t tot = 0;
       for (auto& s : v) tot += s.size();

@@ -163,3 +163,17 @@ def test_reads_without_records_and_empty_input(synth, tmp_path):
     empty.write_text("")
     _run([*base, "-o", out, "-p", str(empty)])
     assert open(out).read() == ""
+
+
+def test_graph_error_exits_cleanly(synth, tmp_path):
+    """a super-read naming a unitig past the -u sequences (super_read_name.cc:133, .at()
+    throws upstream): the error of a graph thread ends the run with a message and exit
+    status 1, not std::terminate"""
+    d, _, _ = synth
+    up = tmp_path / "few.fa"
+    up.write_text(">0\n" + "ACGT" * 20 + "\n>1\n" + "TTGCA" * 20 + "\n")
+    r = subprocess.run([CMR, "-s", "1M", "-m", "17", "-k", "31", "-u", str(up), "-t", "4", "-o",
+                        str(tmp_path / "mr"), "-r", os.path.join(d, "sr.fa"), "-p", os.path.join(d, "pb.fa")],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 1, (r.returncode, r.stderr[-500:])
+    assert "unitig id beyond the unitig sequences" in r.stderr
