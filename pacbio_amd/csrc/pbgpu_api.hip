@@ -1729,10 +1729,7 @@ pbgpu_status pbgpu_format_details(const pbgpu_index* ix, const pbgpu_details_bat
       }
     }
   };
-  std::vector<std::thread> th;
-  for (int t = 1; t < threads; ++t) th.emplace_back(work);
-  work();
-  for (auto& t : th) t.join();
+  run_parallel(threads, work);
   uint64_t total = 0;
   for (auto& p : parts) total += p.size();
   char* t = (char*)malloc(total + 1);
@@ -1817,10 +1814,7 @@ pbgpu_status pbgpu_format_coords(const pbgpu_index* ix, const pbgpu_coords_batch
       }
     }
   };
-  std::vector<std::thread> th;
-  for (int t = 1; t < threads; ++t) th.emplace_back(work);
-  work();
-  for (auto& t : th) t.join();
+  run_parallel(threads, work);
   std::string hdr;
   if (header)
     hdr = std::string("Rstart Rend Qstart Qend Nmers Rcons Qcons Rcover Qcover Rlen Qlen Stretch Offset Err") +

@@ -9,9 +9,11 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <exception>
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/pbgpu.h"
@@ -60,6 +62,27 @@ struct unsupported : std::runtime_error { using std::runtime_error::runtime_erro
   catch (const unsupported& e) { return fail(PBGPU_ERR_UNSUPPORTED, "%s", e.what()); } \
   catch (const std::bad_alloc&) { return fail(PBGPU_ERR_NOMEM, "host allocation failed"); } \
   catch (const std::exception& e) { return fail(PBGPU_ERR_INTERNAL, "%s", e.what()); }
+
+// work() on `threads` host threads (this one included); an exception in any of
+// them is rethrown here after all have joined (none may leave a std::thread)
+template <typename F>
+void run_parallel(int threads, F&& work) {
+  std::mutex mu;
+  std::exception_ptr first;
+  auto guarded = [&]() {
+    try {
+      work();
+    } catch (...) {
+      std::lock_guard<std::mutex> lk(mu);
+      if (!first) first = std::current_exception();
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < threads; ++t) th.emplace_back(guarded);
+  guarded();
+  for (auto& t : th) t.join();
+  if (first) std::rethrow_exception(first);
+}
 
 // --------------------------------------------------------- device buffer
 template <typename T>
