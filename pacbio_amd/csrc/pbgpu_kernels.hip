@@ -509,6 +509,13 @@ __global__ __launch_bounds__(BLOCK) void k_seed(IndexView ix, const uint8_t* __r
 }
 
 // ================================================================= group
+// Workgroup barrier that orders LDS only: outstanding global loads (prefetched
+// occurrences) stay in flight, where __syncthreads() would wait for them.
+DEV void table_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 // One workgroup (4 waves) per read: enumerate the read's hits exactly in the reference's
 // append order (kept k-mers in read order; per k-mer occ(m) then occ(rm),
 // each in descending text position == pos_iterator, superread_parser.hpp:
@@ -526,13 +533,16 @@ __global__ __launch_bounds__(BLOCK) void k_seed(IndexView ix, const uint8_t* __r
 #define PBGPU_GROUP_BLOCK_BIG 1024
 #endif
 constexpr uint32_t GROUP_BLOCK = PBGPU_GROUP_BLOCK, GROUP_BLOCK_BIG = PBGPU_GROUP_BLOCK_BIG;
-#ifndef PBGPU_GROUP_PF
-#define PBGPU_GROUP_PF 1
+#ifndef PBGPU_GROUP_U
+#define PBGPU_GROUP_U 4
 #endif
-constexpr int GROUP_PF = PBGPU_GROUP_PF;  // 256-hit steps whose occurrence loads are in flight at once
+constexpr int GROUP_U = PBGPU_GROUP_U;  // 64-hit windows per wave and step (their occurrence loads are in flight together)
 
+#ifndef PBGPU_GROUP_MINW
+#define PBGPU_GROUP_MINW 1
+#endif
 template <bool GLOBAL_TABLE, uint32_t B>
-__global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restrict__ krec,
+__global__ __launch_bounds__(B, B == 256 ? PBGPU_GROUP_MINW : 1) void k_group(IndexView ix, const KRec* __restrict__ krec,
                                                        const uint64_t* __restrict__ roff, const uint32_t* __restrict__ n_kept,
                                                        const uint32_t* __restrict__ thr_in, const uint64_t* __restrict__ hit_off,
                                                        uint64_t node_base, uint32_t r0, const uint32_t* __restrict__ read_list,
@@ -550,6 +560,7 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
   if (blockIdx.x >= n_list) return;
   const uint32_t tid = threadIdx.x;
   const uint32_t wave = tid >> 6;
+  constexpr uint32_t NW = B / 64;
   const uint32_t r = read_list ? read_list[blockIdx.x] : r0 + blockIdx.x;
   const uint32_t hcap = 1u << hcap_log2;
   // table: key (sr + 1, 0 = empty), fwd count/cursor, bwd count/cursor
@@ -580,7 +591,12 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
   if (GLOBAL_TABLE) __threadfence_block();
   __syncthreads();
 
-  for (int pass = 0; pass < 2; ++pass) {
+#ifdef PBGPU_EXP_SKIP_PASS1  // experiment (with PBGPU_EXP_GROUP_ONLY): pass 0 alone
+  constexpr int n_pass = 1;
+#else
+  constexpr int n_pass = 2;
+#endif
+  for (int pass = 0; pass < n_pass; ++pass) {
     for (uint32_t g0 = 0; g0 < nk; g0 += B) {
       if (s_flag) break;  // uniform (written before the last barrier)
 #ifdef PBGPU_PROF
@@ -614,99 +630,118 @@ __global__ __launch_bounds__(B) void k_group(IndexView ix, const KRec* __restric
       const uint64_t pr_b = __builtin_amdgcn_s_memtime();
       pr_setup[pass] += pr_b - pr_a;
 #endif
-      // hit h -> (record, strand, occurrence address); the occurrence of the next
-      // 256-hit step is loaded one step ahead so its latency overlaps the table work
-      auto locate = [&](uint32_t h, uint32_t& rec, bool& fwd, int32_t& pb) -> uint64_t {
-        uint32_t lo = 0;  // last record with s_off <= h (s_off[0] = 0): fixed-depth, branch-free
+      // ---- the group's hits in 64-hit windows: a wave takes GROUP_U consecutive
+      // windows per step, the waves of a step in order (pass 1 takes its cursors
+      // wave by wave, so the step's hits are placed in enumeration order).  Lane l
+      // of the window at h0 holds hit h0 + l; its k-mer record is the last one
+      // starting at or before it (a fixed-depth search; k-mers without hits tie
+      // with the next start and are skipped, as the reference's enumeration does).
+      // Measured against a ballot walk over record starts held in registers
+      // (one LDS read per 64 records instead of 8 per hit): the walk's readlane
+      // chain was slower (pass 0 7.7 vs 6.9 ms, 25k C2 reads).
+      const uint32_t lane = tid & 63;
+      const uint32_t n_win = (total + 63) >> 6;
+      // locate + load of the wave's GROUP_U windows of step ws, one step ahead of
+      // their use, so the occurrence loads overlap the table work of the step before
+      auto fetch = [&](uint32_t ws, uint64_t (&e_o)[GROUP_U], int32_t (&pb_o)[GROUP_U], bool (&fwd_o)[GROUP_U],
+                       bool (&val_o)[GROUP_U]) {
 #pragma unroll
-        for (uint32_t stp = B / 2; stp >= 1; stp >>= 1) lo = s_off[lo + stp] <= h ? lo + stp : lo;
-        rec = lo;
-        const uint32_t local = h - s_off[lo];
-        const uint2 np = s_np[lo];
-        const ulonglong2 pp = s_ptr[lo];
-        fwd = local < np.x;
-        pb = (int32_t)np.y;
-        return (fwd ? pp.x : pp.y) + local;
+        for (int u = 0; u < GROUP_U; ++u) {
+          const uint32_t h = ((ws + wave * GROUP_U + (uint32_t)u) << 6) + lane;
+          e_o[u] = 0; pb_o[u] = 0; fwd_o[u] = true; val_o[u] = false;
+          if (h < total) {
+            uint32_t lo = 0;  // s_off[0] = 0: fixed depth, branch-free
+#pragma unroll
+            for (uint32_t stp = B / 2; stp >= 1; stp >>= 1) lo = s_off[lo + stp] <= h ? lo + stp : lo;
+            const uint32_t local = h - s_off[lo];
+            const uint2 np = s_np[lo];
+            const ulonglong2 pp = s_ptr[lo];
+            const bool fwd = local < np.x;
+            fwd_o[u] = fwd;
+            pb_o[u] = (int32_t)np.y;
+            val_o[u] = true;
+            e_o[u] = ix.occ[(fwd ? pp.x : pp.y) + local];
+          }
+        }
       };
-      // GROUP_PF steps of occurrence loads in flight per thread (a ring of
-      // statically indexed registers): the enumeration is latency-bound otherwise
-      uint64_t e_q[GROUP_PF];
-      uint32_t rec_q[GROUP_PF];
-      bool fwd_q[GROUP_PF];
-      int32_t pb_q[GROUP_PF];
+      uint64_t e_q[GROUP_U];
+      int32_t pb_q[GROUP_U];
+      bool fwd_q[GROUP_U], val_q[GROUP_U];
+      fetch(0, e_q, pb_q, fwd_q, val_q);
+      for (uint32_t ws = 0; ws < n_win; ws += NW * GROUP_U) {  // block-uniform trip count
+        // this step's hits out of the load registers, then the next step's loads into
+        // them: no register copy that would wait on the loads in flight
+        uint32_t sr_q[GROUP_U], slot_q[GROUP_U];
+        int32_t so_q[GROUP_U], pbx_q[GROUP_U];
+        bool mine_q[GROUP_U], fwdx_q[GROUP_U];
 #pragma unroll
-      for (int d = 0; d < GROUP_PF; ++d) {
-        e_q[d] = 0; rec_q[d] = 0xFFFFFFFFu; fwd_q[d] = true; pb_q[d] = 0;
-        if (d * B + tid < total) e_q[d] = ix.occ[locate(d * B + tid, rec_q[d], fwd_q[d], pb_q[d])];
-      }
-      for (uint32_t hq = 0; hq < total; hq += GROUP_PF * B) {
-#pragma unroll
-      for (int d = 0; d < GROUP_PF; ++d) {
-        const uint32_t h0 = hq + d * B;
-        if (h0 >= total) break;  // block-uniform
-        const uint32_t h = h0 + tid;
-        const bool valid = h < total;
-        uint32_t sr = 0, slot = 0, rec = 0xFFFFFFFFu;  // rec: the hit's k-mer record (unused after locate)
-        int32_t so = 0, pb = 0;
-        bool fwd = true;
-        const uint64_t e = e_q[d];
-        if (valid) { rec = rec_q[d]; fwd = fwd_q[d]; pb = pb_q[d]; }
-        if (h + GROUP_PF * B < total) e_q[d] = ix.occ[locate(h + GROUP_PF * B, rec_q[d], fwd_q[d], pb_q[d])];
-        bool mine = valid;
-        if (valid) {
-          sr = (uint32_t)(e >> 32);
-          so = (int32_t)(uint32_t)(e & 0xFFFFFFFFull);
-          slot = (sr * 0x9E3779B1u) >> (32 - hcap_log2);
-          mine = part_of(sr) == part;
+        for (int u = 0; u < GROUP_U; ++u) {
+          sr_q[u] = (uint32_t)(e_q[u] >> 32);
+          so_q[u] = (int32_t)(uint32_t)(e_q[u] & 0xFFFFFFFFull);
+          slot_q[u] = (sr_q[u] * 0x9E3779B1u) >> (32 - hcap_log2);
+          mine_q[u] = val_q[u] && part_of(sr_q[u]) == part;
+          pbx_q[u] = pb_q[u];
+          fwdx_q[u] = fwd_q[u];
         }
-        if (pass == 0) {
-          // order-free: distinct super-reads and per-strand list lengths
-          // Once the table is over its fill limit the read is abandoned (it resumes in
-          // a larger tier), but the rest of this k-mer group still runs and may fill
-          // the table: long probe sequences give up once the flag is set (or after
-          // hcap probes), so a full table can never trap a thread.
-          if (mine) {
-            bool ok = true;
-            for (uint32_t probe = 0;; ++probe) {
-              if (probe >= 8 && (probe == hcap || *(volatile uint32_t*)&s_flag)) { s_flag = 1; ok = false; break; }
-              const uint32_t old = atomicCAS(&tkey[slot], 0u, sr + 1);
-              if (old == 0) { if (atomicAdd(&s_used, 1u) >= used_limit) { s_flag = 1; ok = false; } break; }
-              if (old == sr + 1) break;
-              slot = (slot + 1) & (hcap - 1);
+        // pin the extracted values here: otherwise the compiler sinks their arithmetic
+        // below the next loads, keeps both register sets alive and waits for the new
+        // loads at the loop's back edge
+#pragma unroll
+        for (int u = 0; u < GROUP_U; ++u) asm volatile("" ::"v"(sr_q[u]), "v"(so_q[u]), "v"(slot_q[u]), "v"(pbx_q[u]));
+        fetch(ws + NW * GROUP_U, e_q, pb_q, fwd_q, val_q);
+#pragma unroll
+        for (int u = 0; u < GROUP_U; ++u) {
+          const uint32_t sr = sr_q[u];
+          if (pass == 0) {
+            // order-free: distinct super-reads and per-strand list lengths
+            // Once the table is over its fill limit the read is abandoned (it resumes in
+            // a larger tier), but the rest of this k-mer group still runs and may fill
+            // the table: long probe sequences give up once the flag is set (or after
+            // hcap probes), so a full table can never trap a thread.
+            if (mine_q[u]) {
+              uint32_t slot = slot_q[u];
+              bool ok = true;
+              for (uint32_t probe = 0;; ++probe) {
+                if (probe >= 8 && (probe == hcap || __hip_atomic_load(&s_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) {
+                  s_flag = 1; ok = false; break;
+                }
+                const uint32_t old = atomicCAS(&tkey[slot], 0u, sr + 1);
+                if (old == 0) { if (atomicAdd(&s_used, 1u) >= used_limit) { s_flag = 1; ok = false; } break; }
+                if (old == sr + 1) break;
+                slot = (slot + 1) & (hcap - 1);
+              }
+              if (ok) atomicAdd(fwdx_q[u] ? &tcf[slot] : &tcb[slot], 1u);
             }
-            if (ok) atomicAdd(fwd ? &tcf[slot] : &tcb[slot], 1u);
-          }
-        } else {
-          // Scatter: each hit takes the next slot of its (super-read, strand) list.  All
-          // hits of one list inside this 256-hit step land in one contiguous run of
-          // slots, in arbitrary order within the run; steps are ordered by the
-          // barriers.  The consumers restore the reference order (pb offset ascending,
-          // then occurrence order = |sr offset| descending) with a transposition pass
-          // that is bounded by the run lengths (k_lis_w, k_strand_order).
-          // The waves take their slots in wave order (one barrier each), so a run is
-          // out of order only where the LDS unit does not serve one wave's same-address
-          // atomics in lane order: usually no consumer work at all.
-          uint32_t* cur = nullptr;
-          if (mine) {
+          } else if (mine_q[u]) {
+            uint32_t slot = slot_q[u];
             while (tkey[slot] != sr + 1) slot = (slot + 1) & (hcap - 1);
-            cur = fwd ? &tcf[slot] : &tcb[slot];
+            slot_q[u] = slot;
           }
-          uint32_t pos = 0;
-#ifdef PBGPU_EXP_GROUP_NOORDER
-          if (mine) pos = atomicAdd(cur, 1u);
-#else
-          for (uint32_t w = 0; w < B / 64; ++w) {
-            if (wave == w && mine) pos = atomicAdd(cur, 1u);
-            __syncthreads();
-          }
-#endif
-#ifndef PBGPU_EXP_GROUP_NOSTORE  // experiment (with PBGPU_EXP_GROUP_ONLY): no list store
-          if (mine) O.X[hbase + pos] = make_int2(pb, fwd ? so : -so);
-#else
-          if (mine && pos == 0xFFFFFFFFu) O.X[hbase] = make_int2(pb, so);
-#endif
         }
-      }
+        if (pass == 1) {
+          // Scatter: each hit takes the next slot of its (super-read, strand) list.  The
+          // waves take their cursors in wave order (one barrier each) and a wave its
+          // windows in order, so a list's run inside this step is out of order only
+          // where the LDS unit does not serve one instruction's same-address atomics in
+          // lane order; the consumers restore the reference order (pb offset ascending,
+          // then |sr offset| descending) with a transposition pass bounded by the run
+          // lengths (k_lis_w, k_strand_order, k_order_tiny).  The turn barriers order
+          // the table's memory only (LDS; the HBM table's atomics return before them),
+          // so the next step's occurrence loads stay in flight across them.
+          uint32_t pos_q[GROUP_U];
+          for (uint32_t w = 0; w < NW; ++w) {
+            if (wave == w) {
+#pragma unroll
+              for (int u = 0; u < GROUP_U; ++u)
+                if (mine_q[u]) pos_q[u] = atomicAdd(fwdx_q[u] ? &tcf[slot_q[u]] : &tcb[slot_q[u]], 1u);
+            }
+            if (GLOBAL_TABLE) __syncthreads();
+            else table_barrier();
+          }
+#pragma unroll
+          for (int u = 0; u < GROUP_U; ++u)
+            if (mine_q[u]) O.X[hbase + pos_q[u]] = make_int2(pbx_q[u], fwdx_q[u] ? so_q[u] : -so_q[u]);
+        }
       }
       __syncthreads();
 #ifdef PBGPU_PROF
