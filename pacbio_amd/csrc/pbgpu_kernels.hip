@@ -689,32 +689,44 @@ __global__ __launch_bounds__(B, B == 256 ? PBGPU_GROUP_MINW : 1) void k_group(In
 #pragma unroll
         for (int u = 0; u < GROUP_U; ++u) asm volatile("" ::"v"(sr_q[u]), "v"(so_q[u]), "v"(slot_q[u]), "v"(pbx_q[u]));
         fetch(ws + NW * GROUP_U, e_q, pb_q, fwd_q, val_q);
+        // The first table probe of every window is issued together (one LDS round trip
+        // for the step), then the rare collisions are walked one window at a time.  A
+        // wave's LDS operations execute in order, so a later window of a lane sees
+        // what an earlier one inserted.
+        uint32_t first[GROUP_U];
 #pragma unroll
         for (int u = 0; u < GROUP_U; ++u) {
-          const uint32_t sr = sr_q[u];
+          first[u] = 0;
+          if (mine_q[u]) first[u] = pass == 0 ? atomicCAS(&tkey[slot_q[u]], 0u, sr_q[u] + 1) : tkey[slot_q[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < GROUP_U; ++u) {
+          if (!mine_q[u]) continue;
+          const uint32_t key = sr_q[u] + 1;
+          uint32_t slot = slot_q[u], old = first[u];
           if (pass == 0) {
             // order-free: distinct super-reads and per-strand list lengths
             // Once the table is over its fill limit the read is abandoned (it resumes in
             // a larger tier), but the rest of this k-mer group still runs and may fill
             // the table: long probe sequences give up once the flag is set (or after
             // hcap probes), so a full table can never trap a thread.
-            if (mine_q[u]) {
-              uint32_t slot = slot_q[u];
-              bool ok = true;
-              for (uint32_t probe = 0;; ++probe) {
+            bool ok = true;
+            if (old == 0) {
+              if (atomicAdd(&s_used, 1u) >= used_limit) { s_flag = 1; ok = false; }
+            } else if (old != key) {
+              for (uint32_t probe = 1;; ++probe) {
+                slot = (slot + 1) & (hcap - 1);
                 if (probe >= 8 && (probe == hcap || __hip_atomic_load(&s_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) {
                   s_flag = 1; ok = false; break;
                 }
-                const uint32_t old = atomicCAS(&tkey[slot], 0u, sr + 1);
+                old = atomicCAS(&tkey[slot], 0u, key);
                 if (old == 0) { if (atomicAdd(&s_used, 1u) >= used_limit) { s_flag = 1; ok = false; } break; }
-                if (old == sr + 1) break;
-                slot = (slot + 1) & (hcap - 1);
+                if (old == key) break;
               }
-              if (ok) atomicAdd(fwdx_q[u] ? &tcf[slot] : &tcb[slot], 1u);
             }
-          } else if (mine_q[u]) {
-            uint32_t slot = slot_q[u];
-            while (tkey[slot] != sr + 1) slot = (slot + 1) & (hcap - 1);
+            if (ok) atomicAdd(fwdx_q[u] ? &tcf[slot] : &tcb[slot], 1u);
+          } else {
+            while (old != key) { slot = (slot + 1) & (hcap - 1); old = tkey[slot]; }
             slot_q[u] = slot;
           }
         }
