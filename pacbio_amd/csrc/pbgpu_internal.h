@@ -111,6 +111,7 @@ enum StatSlot {
 
 struct GroupOut {
   int2* X;
+  int2* sink;              // one entry past the sub-batch's lists: the stores of lanes without a hit
   ChainDesc* chains;
   uint32_t* chain_count;
   uint32_t chain_cap;

@@ -596,7 +596,12 @@ __global__ __launch_bounds__(B, B == 256 ? PBGPU_GROUP_MINW : 1) void k_group(In
 #else
   constexpr int n_pass = 2;
 #endif
-  for (int pass = 0; pass < n_pass; ++pass) {
+  for (int pass_rt = 0; pass_rt < n_pass; ++pass_rt) {
+    // the group loop, compiled once per pass: with a run-time pass the stores of
+    // pass 1 sit behind a branch, and the compiler then cannot count the loads in
+    // flight and waits for all of them
+    auto groups = [&](auto pass_c) {
+    constexpr int pass = decltype(pass_c)::value;
     for (uint32_t g0 = 0; g0 < nk; g0 += B) {
       if (s_flag) break;  // uniform (written before the last barrier)
 #ifdef PBGPU_PROF
@@ -648,29 +653,25 @@ __global__ __launch_bounds__(B, B == 256 ? PBGPU_GROUP_MINW : 1) void k_group(In
 #pragma unroll
         for (int u = 0; u < GROUP_U; ++u) {
           const uint32_t h = ((ws + wave * GROUP_U + (uint32_t)u) << 6) + lane;
-          e_o[u] = 0; pb_o[u] = 0; fwd_o[u] = true; val_o[u] = false;
-          if (h < total) {
-            uint32_t lo = 0;  // s_off[0] = 0: fixed depth, branch-free
+          // no branch around the load (windows past the group's end load occ[0]): the
+          // compiler counts the loads in flight only when every path issues them
+          uint32_t lo = 0;  // s_off[0] = 0: fixed depth, branch-free
 #pragma unroll
-            for (uint32_t stp = B / 2; stp >= 1; stp >>= 1) lo = s_off[lo + stp] <= h ? lo + stp : lo;
-            const uint32_t local = h - s_off[lo];
-            const uint2 np = s_np[lo];
-            const ulonglong2 pp = s_ptr[lo];
-            const bool fwd = local < np.x;
-            fwd_o[u] = fwd;
-            pb_o[u] = (int32_t)np.y;
-            val_o[u] = true;
-            e_o[u] = ix.occ[(fwd ? pp.x : pp.y) + local];
-          }
+          for (uint32_t stp = B / 2; stp >= 1; stp >>= 1) lo = s_off[lo + stp] <= h ? lo + stp : lo;
+          const uint32_t local = h - s_off[lo];
+          const uint2 np = s_np[lo];
+          const ulonglong2 pp = s_ptr[lo];
+          const bool valid = h < total;
+          const bool fwd = local < np.x;
+          fwd_o[u] = fwd;
+          pb_o[u] = (int32_t)np.y;
+          val_o[u] = valid;
+          e_o[u] = ix.occ[valid ? (fwd ? pp.x : pp.y) + local : 0];
         }
       };
-      uint64_t e_q[GROUP_U];
-      int32_t pb_q[GROUP_U];
-      bool fwd_q[GROUP_U], val_q[GROUP_U];
-      fetch(0, e_q, pb_q, fwd_q, val_q);
-      for (uint32_t ws = 0; ws < n_win; ws += NW * GROUP_U) {  // block-uniform trip count
-        // this step's hits out of the load registers, then the next step's loads into
-        // them: no register copy that would wait on the loads in flight
+      // the hits of step ws from register set e_q (loaded one step earlier)
+      auto process = [&](const uint64_t (&e_q)[GROUP_U], const int32_t (&pb_q)[GROUP_U],
+                         const bool (&fwd_q)[GROUP_U], const bool (&val_q)[GROUP_U]) {
         uint32_t sr_q[GROUP_U], slot_q[GROUP_U];
         int32_t so_q[GROUP_U], pbx_q[GROUP_U];
         bool mine_q[GROUP_U], fwdx_q[GROUP_U];
@@ -683,12 +684,6 @@ __global__ __launch_bounds__(B, B == 256 ? PBGPU_GROUP_MINW : 1) void k_group(In
           pbx_q[u] = pb_q[u];
           fwdx_q[u] = fwd_q[u];
         }
-        // pin the extracted values here: otherwise the compiler sinks their arithmetic
-        // below the next loads, keeps both register sets alive and waits for the new
-        // loads at the loop's back edge
-#pragma unroll
-        for (int u = 0; u < GROUP_U; ++u) asm volatile("" ::"v"(sr_q[u]), "v"(so_q[u]), "v"(slot_q[u]), "v"(pbx_q[u]));
-        fetch(ws + NW * GROUP_U, e_q, pb_q, fwd_q, val_q);
         // The first table probe of every window is issued together (one LDS round trip
         // for the step), then the rare collisions are walked one window at a time.  A
         // wave's LDS operations execute in order, so a later window of a lane sees
@@ -730,7 +725,7 @@ __global__ __launch_bounds__(B, B == 256 ? PBGPU_GROUP_MINW : 1) void k_group(In
             slot_q[u] = slot;
           }
         }
-        if (pass == 1) {
+        if constexpr (pass == 1) {
           // Scatter: each hit takes the next slot of its (super-read, strand) list.  The
           // waves take their cursors in wave order (one barrier each) and a wave its
           // windows in order, so a list's run inside this step is out of order only
@@ -741,6 +736,8 @@ __global__ __launch_bounds__(B, B == 256 ? PBGPU_GROUP_MINW : 1) void k_group(In
           // the table's memory only (LDS; the HBM table's atomics return before them),
           // so the next step's occurrence loads stay in flight across them.
           uint32_t pos_q[GROUP_U];
+#pragma unroll
+          for (int u = 0; u < GROUP_U; ++u) pos_q[u] = 0;
           for (uint32_t w = 0; w < NW; ++w) {
             if (wave == w) {
 #pragma unroll
@@ -750,16 +747,36 @@ __global__ __launch_bounds__(B, B == 256 ? PBGPU_GROUP_MINW : 1) void k_group(In
             if (GLOBAL_TABLE) __syncthreads();
             else table_barrier();
           }
+          // every lane stores (lanes without a hit to the sink entry), for the same reason
 #pragma unroll
           for (int u = 0; u < GROUP_U; ++u)
-            if (mine_q[u]) O.X[hbase + pos_q[u]] = make_int2(pbx_q[u], fwdx_q[u] ? so_q[u] : -so_q[u]);
+            (mine_q[u] ? O.X[hbase + pos_q[u]] : *O.sink) = make_int2(pbx_q[u], fwdx_q[u] ? so_q[u] : -so_q[u]);
         }
+      };
+      // Two register sets, each loaded in place one step ahead of its use: with one
+      // set the compiler copies the new loads into it at the loop's back edge and
+      // waits there for them and for the step's stores.
+      uint64_t eA[GROUP_U], eB[GROUP_U];
+      int32_t pbA[GROUP_U], pbB[GROUP_U];
+      bool fwdA[GROUP_U], fwdB[GROUP_U], valA[GROUP_U], valB[GROUP_U];
+      constexpr uint32_t S = NW * GROUP_U;  // windows per block step
+      fetch(0, eA, pbA, fwdA, valA);
+      for (uint32_t ws = 0; ws < n_win; ws += 2 * S) {  // block-uniform trip count
+        fetch(ws + S, eB, pbB, fwdB, valB);
+        process(eA, pbA, fwdA, valA);
+        if (ws + S >= n_win) break;  // block-uniform
+        fetch(ws + 2 * S, eA, pbA, fwdA, valA);
+        process(eB, pbB, fwdB, valB);
       }
       __syncthreads();
 #ifdef PBGPU_PROF
       pr_steps[pass] += __builtin_amdgcn_s_memtime() - pr_b;
 #endif
     }
+    };
+    const int pass = pass_rt;
+    if (pass == 0) groups(std::integral_constant<int, 0>{});
+    else groups(std::integral_constant<int, 1>{});
     if (pass == 0) {
 #ifdef PBGPU_PROF
       const uint64_t pr_c = __builtin_amdgcn_s_memtime();
