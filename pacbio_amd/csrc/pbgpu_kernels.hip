@@ -666,7 +666,12 @@ __global__ __launch_bounds__(B, B == 256 ? PBGPU_GROUP_MINW : 1) void k_group(In
           fwd_o[u] = fwd;
           pb_o[u] = (int32_t)np.y;
           val_o[u] = valid;
-          e_o[u] = ix.occ[valid ? (fwd ? pp.x : pp.y) + local : 0];
+          const uint64_t at = valid ? (fwd ? pp.x : pp.y) + local : 0;
+          // pass 0 needs the super-read id alone: a 4-byte load of the high word (an
+          // 8-byte one leaves a dead half whose register the compiler reuses, which
+          // again drains the loads in flight)
+          if constexpr (pass == 0) e_o[u] = (uint64_t)reinterpret_cast<const uint32_t*>(ix.occ)[2 * at + 1] << 32;
+          else e_o[u] = ix.occ[at];
         }
       };
       // the hits of step ws from register set e_q (loaded one step earlier)
