@@ -79,6 +79,7 @@ class Comm:
 # the rocprofv3 kernel each timed slot corresponds to (tools/pmc_summary.py file names)
 ROCPROF_FILE = {"k_seed": "k_seed_256_8_0", "k_group": "k_group_false_256u", "k_lis": "k_lis_w_255_8",
                 "k_coords": "k_coords_8", "k_rec_sort": "k_rec_sort_256_2048"}
+STAGE_OF = {"k_seed": "seed", "k_group": "group", "k_lis": "lis", "k_coords": "fit", "k_rec_sort": "records"}
 
 
 def _kernel_bytes(st):
@@ -280,19 +281,29 @@ def main():
     value_device = comm.sum(bases_rank) * args.device_steps / el_dev
     kb = _kernel_bytes(st)
     kms, kn = st["kernel_ms"], st["kernel_launches"]
-    dom = max(kb, key=lambda kk: kms[kk])
+    # the dominant kernel: the one whose stage takes the most device time per step
+    # (k_group's stage is both of its tiers; its roofline is taken on the first tier's
+    # launches, the ones its counters describe)
+    dom = max(kb, key=lambda kk: st["ms_" + STAGE_OF[kk]])
     avg_ms = kms[dom] / max(1, kn[dom])
     achieved = kb[dom] / (avg_ms * 1e-3) / 1e9
+    per_kernel = {kk: {"alg_bytes_per_launch": kb[kk], "avg_launch_ms": round(kms[kk] / max(1, kn[kk]), 3),
+                       "achieved_gbs": round(kb[kk] / (kms[kk] / max(1, kn[kk]) * 1e-3) / 1e9, 1),
+                       "frac": round(kb[kk] / (kms[kk] / max(1, kn[kk]) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                       "stage_ms_per_step": round(st["ms_" + STAGE_OF[kk]] / args.device_steps, 3)}
+                  for kk in kb if kn.get(kk)}
     # HBM traffic per launch of the dominant kernel from the committed rocprofv3 PMC
     # summary (tools/prof_r02.sh): FETCH_SIZE calibrated on the 512-B-run gather
     # microbenchmark (bytes moved / FETCH_SIZE), + WRITE_SIZE
     traffic, traffic_note = None, None
-    summ = os.path.join(ROOT, "profiles", "r02b_rocprof_summary.json")
-    if dom == "k_group" and os.path.exists(summ):
+    summ = os.path.join(ROOT, "profiles", "r02c_rocprof_summary.json")
+    if os.path.exists(summ):
         try:
             with open(summ) as f:
-                t = json.load(f).get("k_group_traffic_bytes", {})
-            traffic = t.get("calibrated_runs")
+                t = json.load(f).get(f"{dom}_traffic_bytes", {})
+            # k_group reads occurrence runs (FETCH_SIZE calibrated on that shape); the
+            # other kernels stream rows (the guide's 2x FETCH_SIZE correction)
+            traffic = t.get("calibrated_runs" if dom == "k_group" else "guide_2x_fetch_plus_write")
             traffic_note = {k: t.get(k) for k in ("raw_fetch_plus_write", "guide_2x_fetch_plus_write")}
         except Exception:
             traffic = None
@@ -411,11 +422,14 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dom, "rocprof_kernel": ROCPROF_FILE[dom], "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "alg_bytes_per_launch": kb[dom], "avg_launch_ms": avg_ms,
-                         "traffic_source": "profiles/r02b_rocprof_summary.json (FETCH_SIZE x run-shape calibration + "
-                                           "WRITE_SIZE, per device-leg launch)" if traffic else None,
+                         "traffic_source": ("profiles/r02c_rocprof_summary.json (" +
+                                            ("FETCH_SIZE x run-shape calibration" if dom == "k_group" else
+                                             "2 x FETCH_SIZE") + " + WRITE_SIZE, per device-leg launch)")
+                         if traffic else None,
                          "traffic_alternatives": traffic_note,
                          "b_rand_gbs": b_rand, "frac_of_b_rand": (achieved / b_rand) if b_rand else None,
-                         "b_run512_gbs": b_run, "frac_of_b_run512": (achieved / b_run) if b_run else None},
+                         "b_run512_gbs": b_run, "frac_of_b_run512": (achieved / b_run) if b_run else None,
+                         "by_kernel": per_kernel},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

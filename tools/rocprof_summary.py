@@ -4,7 +4,7 @@
 kernel stats: per kernel (and, for k_group<false, 256u>, the device-leg launches
 -- the largest grids, one per device step -- apart from the e2e ones), mean
 launch time from the kernel trace.
-PMC: per-launch FETCH_SIZE / WRITE_SIZE of the device-leg k_group launches, and
+PMC: per-launch FETCH_SIZE / WRITE_SIZE of the device-leg k_group and k_coords launches, and
 the calibration of FETCH_SIZE on the two gather microbenchmarks (known bytes):
 traffic = FETCH_SIZE x (bytes moved / FETCH_SIZE of the 512-B run shape) + WRITE_SIZE.
 """
@@ -49,6 +49,10 @@ def counters(d):
     return acc, meta
 
 
+# device-leg kernels summarised: (rocprof name, key prefix in the summary)
+KERNELS = [("k_group<false, 256u>", "k_group"), ("k_coords<8>", "k_coords")]
+
+
 def main(d, out):
     res = {}
     rows = trace(glob.glob(os.path.join(d, "kt", "**", "*kernel_trace.csv"), recursive=True)[0])
@@ -58,14 +62,15 @@ def main(d, out):
     lines = []
     for k, v in sorted(stats.items(), key=lambda kv: -sum(x[1] for x in kv[1])):
         lines.append(f"{k:44s} n={len(v):5d} total={sum(x[1] for x in v):10.3f} ms mean={sum(x[1] for x in v) / len(v):8.3f} ms")
-    kg = stats.get("k_group<false, 256u>", [])
-    if kg:
-        gmax = max(g for g, _ in kg)
-        dev = [ms for g, ms in kg if g >= 0.5 * gmax]
-        res["k_group_device_leg"] = {"launches": len(dev), "mean_ms": sum(dev) / len(dev), "grid": gmax,
-                                     "all_launches_mean_ms": sum(x[1] for x in kg) / len(kg)}
-        lines.append(f"k_group<false, 256u> device-leg launches (grid >= {gmax // 2}): n={len(dev)} "
-                     f"mean={sum(dev) / len(dev):.3f} ms")
+    for kname, tag in KERNELS:
+        kg = stats.get(kname, [])
+        if kg:
+            gmax = max(g for g, _ in kg)
+            dev = [ms for g, ms in kg if g >= 0.5 * gmax]
+            res[f"{tag}_device_leg"] = {"launches": len(dev), "mean_ms": sum(dev) / len(dev), "grid": gmax,
+                                        "all_launches_mean_ms": sum(x[1] for x in kg) / len(kg)}
+            lines.append(f"{kname} device-leg launches (grid >= {gmax // 2}): n={len(dev)} "
+                         f"mean={sum(dev) / len(dev):.3f} ms")
     # PMC
     acc, meta = counters(d)
     per = collections.defaultdict(lambda: collections.defaultdict(list))
@@ -81,21 +86,23 @@ def main(d, out):
             fb = sum(f) / len(f) * 1024.0
             cal[k] = {"bytes_moved": b, "fetch_size_bytes": fb, "ratio_moved_over_fetch": b / fb}
     res["fetch_calibration"] = cal
-    if "k_group<false, 256u>" in per:
-        c = per["k_group<false, 256u>"]
+    for kname, tag in KERNELS:
+        if kname not in per:
+            continue
+        c = per[kname]
         out_c = {}
         for n in ("FETCH_SIZE", "WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"):
             if c.get(n):
                 gmax = max(g for g, _ in c[n])
                 vals = [v for g, v in c[n] if g >= 0.5 * gmax]
                 out_c[n] = sum(vals) / len(vals)
-        res["k_group_pmc_device_leg"] = out_c
+        res[f"{tag}_pmc_device_leg"] = out_c
         if "FETCH_SIZE" in out_c and "WRITE_SIZE" in out_c:
             f = out_c["FETCH_SIZE"] * 1024.0
             w = out_c["WRITE_SIZE"] * 1024.0
             r = cal.get("k_gather_runs", {}).get("ratio_moved_over_fetch")
-            res["k_group_traffic_bytes"] = {"raw_fetch_plus_write": f + w, "guide_2x_fetch_plus_write": 2 * f + w,
-                                            "calibrated_runs": (f * r + w) if r else None}
+            res[f"{tag}_traffic_bytes"] = {"raw_fetch_plus_write": f + w, "guide_2x_fetch_plus_write": 2 * f + w,
+                                           "calibrated_runs": (f * r + w) if r else None}
     with open(os.path.join(out, "r02_rocprof_summary.json"), "w") as fo:
         json.dump(res, fo, indent=1)
     with open(os.path.join(out, "r02_kernel_stats.txt"), "w") as fo:
