@@ -1313,7 +1313,7 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
     while (r1 < n && hoff[r1] - hoff[r0] < target && hoff[r1 + 1] - hoff[r0] <= budget) ++r1;
     const uint64_t Hs = hoff[r1] - hoff[r0];
     const uint32_t nr = r1 - r0;
-    al->X.ensure(Hs + 2); al->pts.ensure(Hs + 9); al->nodes.ensure((Hs + 1) * 8);  // pts: + one 64-byte row (k_coords row loads)
+    al->X.ensure(Hs + 1 + GROUP_SINKS); al->pts.ensure(Hs + 9); al->nodes.ensure((Hs + 1) * 8);  // pts: + one 64-byte row (k_coords row loads)
     al->chains.ensure(std::min<uint64_t>(Hs, (uint64_t)nr << 10) + 1);  // grown below if a batch needs more
     GroupOut O;
     O.X = al->X.p; O.chains = al->chains.p;

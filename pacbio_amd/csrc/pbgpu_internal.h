@@ -109,9 +109,10 @@ enum StatSlot {
   ST_N
 };
 
+constexpr uint32_t GROUP_SINKS = 256;  // spread over lines and channels, not one hot address
 struct GroupOut {
   int2* X;
-  int2* sink;              // one entry past the sub-batch's lists: the stores of lanes without a hit
+  int2* sink;              // GROUP_SINKS entries past the sub-batch's lists: the stores of lanes without a hit
   ChainDesc* chains;
   uint32_t* chain_count;
   uint32_t chain_cap;

@@ -755,7 +755,8 @@ __global__ __launch_bounds__(B, B == 256 ? PBGPU_GROUP_MINW : 1) void k_group(In
           // every lane stores (lanes without a hit to the sink entry), for the same reason
 #pragma unroll
           for (int u = 0; u < GROUP_U; ++u)
-            (mine_q[u] ? O.X[hbase + pos_q[u]] : *O.sink) = make_int2(pbx_q[u], fwdx_q[u] ? so_q[u] : -so_q[u]);
+            (mine_q[u] ? O.X[hbase + pos_q[u]] : O.sink[(blockIdx.x + wave) & (GROUP_SINKS - 1)]) =
+                make_int2(pbx_q[u], fwdx_q[u] ? so_q[u] : -so_q[u]);
         }
       };
       // Two register sets, each loaded in place one step ahead of its use: with one
