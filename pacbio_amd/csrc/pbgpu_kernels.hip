@@ -536,7 +536,10 @@ constexpr uint32_t GROUP_BLOCK = PBGPU_GROUP_BLOCK, GROUP_BLOCK_BIG = PBGPU_GROU
 #ifndef PBGPU_GROUP_U
 #define PBGPU_GROUP_U 4
 #endif
-constexpr int GROUP_U = PBGPU_GROUP_U;  // 64-hit windows per wave and step (their occurrence loads are in flight together)
+#ifndef PBGPU_GROUP_U_BIG
+#define PBGPU_GROUP_U_BIG 4
+#endif
+constexpr int GROUP_U = PBGPU_GROUP_U, GROUP_U_BIG = PBGPU_GROUP_U_BIG;  // 64-hit windows per wave and step (their occurrence loads are in flight together)
 
 #ifndef PBGPU_GROUP_MINW
 #define PBGPU_GROUP_MINW 1
@@ -561,6 +564,7 @@ __global__ __launch_bounds__(B, B == 256 ? PBGPU_GROUP_MINW : 1) void k_group(In
   const uint32_t tid = threadIdx.x;
   const uint32_t wave = tid >> 6;
   constexpr uint32_t NW = B / 64;
+  constexpr int GU = B == GROUP_BLOCK ? GROUP_U : GROUP_U_BIG;  // windows per wave and step
   const uint32_t r = read_list ? read_list[blockIdx.x] : r0 + blockIdx.x;
   const uint32_t hcap = 1u << hcap_log2;
   // table: key (sr + 1, 0 = empty), fwd count/cursor, bwd count/cursor
@@ -635,7 +639,7 @@ __global__ __launch_bounds__(B, B == 256 ? PBGPU_GROUP_MINW : 1) void k_group(In
       const uint64_t pr_b = __builtin_amdgcn_s_memtime();
       pr_setup[pass] += pr_b - pr_a;
 #endif
-      // ---- the group's hits in 64-hit windows: a wave takes GROUP_U consecutive
+      // ---- the group's hits in 64-hit windows: a wave takes GU consecutive
       // windows per step, the waves of a step in order (pass 1 takes its cursors
       // wave by wave, so the step's hits are placed in enumeration order).  Lane l
       // of the window at h0 holds hit h0 + l; its k-mer record is the last one
@@ -646,13 +650,13 @@ __global__ __launch_bounds__(B, B == 256 ? PBGPU_GROUP_MINW : 1) void k_group(In
       // chain was slower (pass 0 7.7 vs 6.9 ms, 25k C2 reads).
       const uint32_t lane = tid & 63;
       const uint32_t n_win = (total + 63) >> 6;
-      // locate + load of the wave's GROUP_U windows of step ws, one step ahead of
+      // locate + load of the wave's GU windows of step ws, one step ahead of
       // their use, so the occurrence loads overlap the table work of the step before
-      auto fetch = [&](uint32_t ws, uint64_t (&e_o)[GROUP_U], int32_t (&pb_o)[GROUP_U], bool (&fwd_o)[GROUP_U],
-                       bool (&val_o)[GROUP_U]) {
+      auto fetch = [&](uint32_t ws, uint64_t (&e_o)[GU], int32_t (&pb_o)[GU], bool (&fwd_o)[GU],
+                       bool (&val_o)[GU]) {
 #pragma unroll
-        for (int u = 0; u < GROUP_U; ++u) {
-          const uint32_t h = ((ws + wave * GROUP_U + (uint32_t)u) << 6) + lane;
+        for (int u = 0; u < GU; ++u) {
+          const uint32_t h = ((ws + wave * GU + (uint32_t)u) << 6) + lane;
           // no branch around the load (windows past the group's end load occ[0]): the
           // compiler counts the loads in flight only when every path issues them
           uint32_t lo = 0;  // s_off[0] = 0: fixed depth, branch-free
@@ -675,13 +679,13 @@ __global__ __launch_bounds__(B, B == 256 ? PBGPU_GROUP_MINW : 1) void k_group(In
         }
       };
       // the hits of step ws from register set e_q (loaded one step earlier)
-      auto process = [&](const uint64_t (&e_q)[GROUP_U], const int32_t (&pb_q)[GROUP_U],
-                         const bool (&fwd_q)[GROUP_U], const bool (&val_q)[GROUP_U]) {
-        uint32_t sr_q[GROUP_U], slot_q[GROUP_U];
-        int32_t so_q[GROUP_U], pbx_q[GROUP_U];
-        bool mine_q[GROUP_U], fwdx_q[GROUP_U];
+      auto process = [&](const uint64_t (&e_q)[GU], const int32_t (&pb_q)[GU],
+                         const bool (&fwd_q)[GU], const bool (&val_q)[GU]) {
+        uint32_t sr_q[GU], slot_q[GU];
+        int32_t so_q[GU], pbx_q[GU];
+        bool mine_q[GU], fwdx_q[GU];
 #pragma unroll
-        for (int u = 0; u < GROUP_U; ++u) {
+        for (int u = 0; u < GU; ++u) {
           sr_q[u] = (uint32_t)(e_q[u] >> 32);
           so_q[u] = (int32_t)(uint32_t)(e_q[u] & 0xFFFFFFFFull);
           slot_q[u] = (sr_q[u] * 0x9E3779B1u) >> (32 - hcap_log2);
@@ -693,14 +697,14 @@ __global__ __launch_bounds__(B, B == 256 ? PBGPU_GROUP_MINW : 1) void k_group(In
         // for the step), then the rare collisions are walked one window at a time.  A
         // wave's LDS operations execute in order, so a later window of a lane sees
         // what an earlier one inserted.
-        uint32_t first[GROUP_U];
+        uint32_t first[GU];
 #pragma unroll
-        for (int u = 0; u < GROUP_U; ++u) {
+        for (int u = 0; u < GU; ++u) {
           first[u] = 0;
           if (mine_q[u]) first[u] = pass == 0 ? atomicCAS(&tkey[slot_q[u]], 0u, sr_q[u] + 1) : tkey[slot_q[u]];
         }
 #pragma unroll
-        for (int u = 0; u < GROUP_U; ++u) {
+        for (int u = 0; u < GU; ++u) {
           if (!mine_q[u]) continue;
           const uint32_t key = sr_q[u] + 1;
           uint32_t slot = slot_q[u], old = first[u];
@@ -740,32 +744,42 @@ __global__ __launch_bounds__(B, B == 256 ? PBGPU_GROUP_MINW : 1) void k_group(In
           // lengths (k_lis_w, k_strand_order, k_order_tiny).  The turn barriers order
           // the table's memory only (LDS; the HBM table's atomics return before them),
           // so the next step's occurrence loads stay in flight across them.
-          uint32_t pos_q[GROUP_U];
+          uint32_t pos_q[GU];
 #pragma unroll
-          for (int u = 0; u < GROUP_U; ++u) pos_q[u] = 0;
+          for (int u = 0; u < GU; ++u) pos_q[u] = 0;
+#ifdef PBGPU_EXP_GROUP_NOTURN  // experiment (with PBGPU_EXP_GROUP_ONLY): cursors in any order, no turn barriers
+          for (uint32_t w = wave; w == wave; ++w) {
+#else
           for (uint32_t w = 0; w < NW; ++w) {
+#endif
             if (wave == w) {
 #pragma unroll
-              for (int u = 0; u < GROUP_U; ++u)
+              for (int u = 0; u < GU; ++u)
                 if (mine_q[u]) pos_q[u] = atomicAdd(fwdx_q[u] ? &tcf[slot_q[u]] : &tcb[slot_q[u]], 1u);
             }
+#ifndef PBGPU_EXP_GROUP_NOTURN
             if (GLOBAL_TABLE) __syncthreads();
             else table_barrier();
+#endif
           }
           // every lane stores (lanes without a hit to the sink entry), for the same reason
+#ifndef PBGPU_EXP_GROUP_NOSTORE  // experiment (with PBGPU_EXP_GROUP_ONLY): no list stores
 #pragma unroll
-          for (int u = 0; u < GROUP_U; ++u)
+          for (int u = 0; u < GU; ++u)
             (mine_q[u] ? O.X[hbase + pos_q[u]] : O.sink[(blockIdx.x + wave) & (GROUP_SINKS - 1)]) =
                 make_int2(pbx_q[u], fwdx_q[u] ? so_q[u] : -so_q[u]);
+#else
+          if (pos_q[0] == 0xFFFFFFFFu) O.X[0] = make_int2(pbx_q[0], so_q[0]);
+#endif
         }
       };
       // Two register sets, each loaded in place one step ahead of its use: with one
       // set the compiler copies the new loads into it at the loop's back edge and
       // waits there for them and for the step's stores.
-      uint64_t eA[GROUP_U], eB[GROUP_U];
-      int32_t pbA[GROUP_U], pbB[GROUP_U];
-      bool fwdA[GROUP_U], fwdB[GROUP_U], valA[GROUP_U], valB[GROUP_U];
-      constexpr uint32_t S = NW * GROUP_U;  // windows per block step
+      uint64_t eA[GU], eB[GU];
+      int32_t pbA[GU], pbB[GU];
+      bool fwdA[GU], fwdB[GU], valA[GU], valB[GU];
+      constexpr uint32_t S = NW * GU;  // windows per block step
       fetch(0, eA, pbA, fwdA, valA);
       for (uint32_t ws = 0; ws < n_win; ws += 2 * S) {  // block-uniform trip count
         fetch(ws + S, eB, pbB, fwdB, valB);
