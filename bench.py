@@ -111,13 +111,14 @@ def _kernel_bytes(st):
 
 def _pick_workdir(want, workload, n_pb):
     """The work directory must hold, for every rank of this node, its FASTA files
-    (~1.4 B per PacBio base) and a coords file (~6.6 B a base) while the previous one
-    is being removed: ~10 B a base with margin.  /tmp on a GPU box is ~80 GB, which 8
-    ranks of C2 come close to, so fall back to /dev/shm when `want` is too small."""
+    (~1.4 B per PacBio base) and two coords files (~6.6 B a base each: the step's and
+    the previous one while it is being removed): ~15 B a base with margin.  /tmp on a
+    GPU box is ~80 GB, which 8 ranks of C2 come close to (~74 GB), so fall back to
+    /dev/shm when `want` is too small."""
     import shutil
     from tools.synth import PRESETS
     local_ranks = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
-    need = 10.0 * n_pb * PRESETS[workload]["pb_len_mean"] * local_ranks + 2e9
+    need = 15.0 * n_pb * PRESETS[workload]["pb_len_mean"] * local_ranks + 2e9
     for d in (want, "/dev/shm"):
         try:
             if shutil.disk_usage(d).free >= need:
