@@ -348,7 +348,10 @@ __global__ __launch_bounds__(BLOCK) void k_seed(IndexView ix, const uint8_t* __r
     }
     __syncthreads();
     const int64_t p0 = t0 + (int64_t)tid * PER;
-    const int64_t s = p0 - LOOK > 0 ? p0 - LOOK : 0;
+    // history needed before p0: the k - 1 bases of the first k-mer, and 17 to tell a
+    // run of <= 17 valid bases (the toggle) from a longer one; LOOK (32) bounds both
+    const int64_t lb = k - 1 > 17 ? (int64_t)k - 1 : 17;
+    const int64_t s = p0 - lb > 0 ? p0 - lb : 0;
     uint64_t m = 0, rm = 0;
     uint32_t rl = s > 0 ? 1000u : 0u;  // unknown history before s counts as a long valid run
     for (int64_t q = s; q < p0; ++q) {  // branch-free: an invalid base resets the run
