@@ -297,7 +297,7 @@ def main():
     # summary (tools/prof_r02.sh): FETCH_SIZE calibrated on the 512-B-run gather
     # microbenchmark (bytes moved / FETCH_SIZE), + WRITE_SIZE
     traffic, traffic_note = None, None
-    summ = os.path.join(ROOT, "profiles", "r02d_rocprof_summary.json")
+    summ = os.path.join(ROOT, "profiles", "r02e_rocprof_summary.json")
     if os.path.exists(summ):
         try:
             with open(summ) as f:
@@ -423,7 +423,7 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dom, "rocprof_kernel": ROCPROF_FILE[dom], "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "alg_bytes_per_launch": kb[dom], "avg_launch_ms": avg_ms,
-                         "traffic_source": ("profiles/r02d_rocprof_summary.json (" +
+                         "traffic_source": ("profiles/r02e_rocprof_summary.json (" +
                                             ("FETCH_SIZE x run-shape calibration" if dom == "k_group" else
                                              "2 x FETCH_SIZE") + " + WRITE_SIZE, per device-leg launch)")
                          if traffic else None,
