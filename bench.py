@@ -54,7 +54,18 @@ class Comm:
         self.world = world
         if world > 1:
             import torch.distributed as dist
-            dist.init_process_group("gloo")
+            # gloo prints "[Gloo] Rank r is connected to ..." on stdout while it
+            # connects: send it to stderr, so stdout holds rank 0's JSON line alone
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                dist.init_process_group("gloo")
+                dist.barrier()
+            finally:
+                sys.stdout.flush()
+                os.dup2(saved, 1)
+                os.close(saved)
             self.dist = dist
 
     def barrier(self):
@@ -280,6 +291,8 @@ def main():
     total_bases = comm.sum(bases_rank) * args.steps
     value = total_bases / elapsed
     value_device = comm.sum(bases_rank) * args.device_steps / el_dev
+    # every collective runs on every rank, here, never inside the rank-0 report below
+    value_device2 = comm.sum(bases_rank) * args.device_steps / el_dev2
     kb = _kernel_bytes(st)
     kms, kn = st["kernel_ms"], st["kernel_launches"]
     # the dominant kernel: the one whose stage takes the most device time per step
@@ -414,7 +427,7 @@ def main():
                                "path_roofline": path_roof},
                 "device_leg_default_flags": {
                     "flags": f"-m {k} --psa-min 13 (defaults: no -l/-k/-f, -B 17, --max-count 5000)",
-                    "value_device": comm.sum(bases_rank) * args.device_steps / el_dev2,
+                    "value_device": value_device2,
                     "ms_per_step": el_dev2 / args.device_steps * 1e3,
                     "records_per_step": st2["n_records"] // max(1, args.device_steps)},
                 "end_to_end_including_build_s": round(t_index + elapsed / args.steps, 3),
