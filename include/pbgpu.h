@@ -335,6 +335,16 @@ int          pbgpu_format_double(double v, char* out);
  * keep one replica per GPU. */
 pbgpu_status pbgpu_index_replicate(const pbgpu_index* src, int device, pbgpu_index** out);
 
+/* On-disk index cache ("optionally add an on-disk index
+ * cache"; the reference rebuilds its PSA on every run, superread_parser.hpp:
+ * 219-224).  pbgpu_index_save writes every host and device array of a built
+ * index to `path` with a caller-chosen `tag` (e.g. k, psa_min, fine_k and the
+ * super-read files' sizes and times); pbgpu_index_load rebuilds it on `device`
+ * from the file alone, and fails with PBGPU_ERR_IO when the file is missing,
+ * truncated, of another format version, or saved with another tag. */
+pbgpu_status pbgpu_index_save(const pbgpu_index* ix, const char* path, const char* tag);
+pbgpu_status pbgpu_index_load(const char* path, int device, const char* tag, pbgpu_index** out);
+
 /* ---------------------------------------------------------------- driver
  * The jf_aligner main loop (jf_aligner.cc:205-230, print_alignments :110-159)
  * as one call: PacBio FASTA / FASTQ files (plain or gzip) are parsed in

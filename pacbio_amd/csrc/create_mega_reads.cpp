@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "../../include/pbgpu.h"
+#include "index_cache.h"
 #include "overlap_graph.hpp"
 
 using namespace megareads;
@@ -183,12 +184,13 @@ int main(int argc, char** argv) {
   Ctx C;
   uint32_t psa_min = 13, threads = 1, streams = 2;
   bool timing = false;
+  const char* index_cache = nullptr;  // --index-cache PATH (index_cache.h)
   bool s_given = false, m_given = false, k_given = false;
   const char *out_path = nullptr, *dot_path = nullptr, *ul_path = nullptr, *us_path = nullptr;
   std::vector<const char*> srs, pbs;
   std::vector<int> devices;
   uint64_t batch_bases = 64ull << 20;
-  enum { O_PSA = 256, O_DOT, O_SC, O_SF, O_CAP, O_WIN, O_MAXM, O_MAXC, O_TRIM, O_DEVS, O_BATCH, O_STREAMS, O_TIMING };
+  enum { O_PSA = 256, O_DOT, O_SC, O_SF, O_CAP, O_WIN, O_MAXM, O_MAXC, O_TRIM, O_DEVS, O_BATCH, O_STREAMS, O_TIMING, O_CACHE };
   static struct option lo[] = {
       {"size", 1, 0, 's'}, {"mer", 1, 0, 'm'}, {"fine-mer", 1, 0, 'F'}, {"psa-min", 1, 0, O_PSA},
       {"unitigs-lengths", 1, 0, 'l'}, {"unitigs-sequences", 1, 0, 'u'}, {"k-mer", 1, 0, 'k'},
@@ -198,7 +200,7 @@ int main(int argc, char** argv) {
       {"mers-matching", 1, 0, 'M'}, {"max-match", 0, 0, O_MAXM}, {"max-count", 1, 0, O_MAXC}, {"bases", 0, 0, 'b'},
       {"density", 1, 0, 'd'}, {"min-length", 1, 0, 'L'}, {"tiling", 1, 0, 'T'}, {"trim", 1, 0, O_TRIM},
       {"superreads", 1, 0, 'r'}, {"pacbio", 1, 0, 'p'}, {"devices", 1, 0, O_DEVS}, {"batch-bases", 1, 0, O_BATCH},
-      {"streams", 1, 0, O_STREAMS}, {"timing", 0, 0, O_TIMING}, {0, 0, 0, 0}};
+      {"streams", 1, 0, O_STREAMS}, {"timing", 0, 0, O_TIMING}, {"index-cache", 1, 0, O_CACHE}, {0, 0, 0, 0}};
   int c;
   while ((c = getopt_long(argc, argv, "s:m:F:l:u:k:t:o:O:e:B:M:bd:L:T:r:p:", lo, nullptr)) != -1) {
     switch (c) {
@@ -257,6 +259,7 @@ int main(int argc, char** argv) {
     case O_BATCH: batch_bases = parse_suffix(optarg); break;
     case O_STREAMS: streams = std::max(1u, parse_u32(optarg, "--streams")); break;
     case O_TIMING: timing = true; break;
+    case O_CACHE: index_cache = optarg; break;
     default: die("bad option (see create_mega_reads_cmdline.yaggo)");
     }
   }
@@ -286,7 +289,7 @@ int main(int argc, char** argv) {
   auto index_on = [&](int dev) -> pbgpu_index* {
     for (auto& b : built) if (b.first == dev) return b.second;
     pbgpu_index* ix = nullptr;
-    if (built.empty()) check(pbgpu_index_build_fasta(srs.data(), srs.size(), &ip, &ix), "index");
+    if (built.empty()) check(index_from_cache(index_cache, srs, ip, &ix, timing), "index");
     else check(pbgpu_index_replicate(built[0].second, dev, &ix), "index replica");
     built.emplace_back(dev, ix);
     return ix;

@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "../../include/pbgpu.h"
+#include "index_cache.h"
 
 static void die(const std::string& m) {
   fprintf(stderr, "jf_aligner: %s\n", m.c_str());
@@ -102,8 +103,9 @@ int main(int argc, char** argv) {
   uint64_t batch_bases = 64ull << 20;
   uint32_t streams = 2;
   bool timing = false;
+  const char* index_cache = nullptr;  // --index-cache PATH (index_cache.h)
   enum { O_PSA = 256, O_SC, O_SF, O_CAP, O_WIN, O_DETAILS, O_COORDS, O_MAXM, O_MAXC, O_COMPACT, O_NOCOMPACT, O_DEV, O_BATCH,
-         O_STREAMS, O_DEVS, O_TIMING };
+         O_STREAMS, O_DEVS, O_TIMING, O_CACHE };
   static struct option lo[] = {
       {"size", 1, 0, 's'}, {"mer", 1, 0, 'm'}, {"fine-mer", 1, 0, 'F'}, {"psa-min", 1, 0, O_PSA},
       {"threads", 1, 0, 't'}, {"stretch-constant", 1, 0, O_SC}, {"stretch-factor", 1, 0, O_SF},
@@ -114,7 +116,7 @@ int main(int argc, char** argv) {
       {"unitigs-sequences", 1, 0, 'u'}, {"compact", 0, 0, O_COMPACT}, {"no-compact", 0, 0, O_NOCOMPACT},
       {"k-mer", 1, 0, 'k'}, {"superreads", 1, 0, 'r'}, {"pacbio", 1, 0, 'p'},
       {"device", 1, 0, O_DEV}, {"devices", 1, 0, O_DEVS}, {"batch-bases", 1, 0, O_BATCH},
-      {"streams", 1, 0, O_STREAMS}, {"timing", 0, 0, O_TIMING}, {0, 0, 0, 0}};
+      {"streams", 1, 0, O_STREAMS}, {"timing", 0, 0, O_TIMING}, {"index-cache", 1, 0, O_CACHE}, {0, 0, 0, 0}};
   int c;
   while ((c = getopt_long(argc, argv, "s:m:F:t:fB:M:H0l:u:k:r:p:", lo, nullptr)) != -1) {
     switch (c) {
@@ -156,6 +158,7 @@ int main(int argc, char** argv) {
       break;
     }
     case O_TIMING: timing = true; break;
+    case O_CACHE: index_cache = optarg; break;
     case O_BATCH: batch_bases = parse_suffix(optarg); break;
     case O_STREAMS: streams = std::max(1u, parse_u32(optarg, "--streams")); break;
     default: die("bad option (see jf_aligner_cmdline.yaggo)");
@@ -186,7 +189,7 @@ int main(int argc, char** argv) {
   auto index_on = [&](int dev) -> pbgpu_index* {
     for (auto& b : built) if (b.first == dev) return b.second;
     pbgpu_index* ix = nullptr;
-    if (built.empty()) check(pbgpu_index_build_fasta(srs.data(), srs.size(), &ip, &ix), "index");
+    if (built.empty()) check(index_from_cache(index_cache, srs, ip, &ix, timing), "index");
     else check(pbgpu_index_replicate(built[0].second, dev, &ix), "index replica");
     built.emplace_back(dev, ix);
     return ix;

@@ -709,6 +709,153 @@ pbgpu_status pbgpu_index_replicate(const pbgpu_index* src, int device, pbgpu_ind
   API_CATCH
 }
 
+// ---------------------------------------------------------------- index cache
+// File: magic, version, tag, the scalars, the host vectors, then each device
+// array as (element count, element size, bytes), streamed through one pinned
+// 64 MiB buffer.
+}  // extern "C"
+namespace {
+constexpr char kCacheMagic[8] = {'P', 'B', 'G', 'P', 'U', 'I', 'X', '\0'};
+constexpr uint32_t kCacheVersion = 1;
+struct cache_file {
+  FILE* f = nullptr;
+  const char* path;
+  ~cache_file() { if (f) fclose(f); }
+  void put(const void* p, size_t n) {
+    if (n && fwrite(p, 1, n, f) != n) throw bad_input(std::string("index cache: write failed: ") + path);
+  }
+  void get(void* p, size_t n) {
+    if (n && fread(p, 1, n, f) != n) throw bad_input(std::string("index cache: truncated or unreadable: ") + path);
+  }
+  void put_u64(uint64_t v) { put(&v, 8); }
+  uint64_t get_u64() { uint64_t v; get(&v, 8); return v; }
+  void put_str(const std::string& v) { put_u64(v.size()); put(v.data(), v.size()); }
+  std::string get_str(uint64_t max_len) {
+    const uint64_t n = get_u64();
+    if (n > max_len) throw bad_input(std::string("index cache: corrupt string length: ") + path);
+    std::string v(n, '\0');
+    get(&v[0], n);
+    return v;
+  }
+};
+struct pinned_chunk {
+  static constexpr size_t kBytes = 64ull << 20;
+  char* p = nullptr;
+  pinned_chunk() { HIPCHK(hipHostMalloc((void**)&p, kBytes)); }
+  ~pinned_chunk() { if (p) (void)hipHostFree(p); }
+};
+template <typename T>
+void cache_put_dbuf(cache_file& cf, pinned_chunk& pc, const dbuf<T>& b) {
+  cf.put_u64(b.n);
+  cf.put_u64(sizeof(T));
+  const size_t bytes = b.bytes();
+  for (size_t o = 0; o < bytes; o += pinned_chunk::kBytes) {
+    const size_t m = std::min(pinned_chunk::kBytes, bytes - o);
+    HIPCHK(hipMemcpy(pc.p, (const char*)b.p + o, m, hipMemcpyDeviceToHost));
+    cf.put(pc.p, m);
+  }
+}
+template <typename T>
+void cache_get_dbuf(cache_file& cf, pinned_chunk& pc, dbuf<T>& b) {
+  const uint64_t n = cf.get_u64(), es = cf.get_u64();
+  if (es != sizeof(T) || n > (1ull << 44)) throw bad_input(std::string("index cache: corrupt array header: ") + cf.path);
+  b.alloc(n);
+  const size_t bytes = b.bytes();
+  for (size_t o = 0; o < bytes; o += pinned_chunk::kBytes) {
+    const size_t m = std::min(pinned_chunk::kBytes, bytes - o);
+    cf.get(pc.p, m);
+    HIPCHK(hipMemcpy((char*)b.p + o, pc.p, m, hipMemcpyHostToDevice));
+  }
+}
+}  // namespace
+extern "C" {
+
+pbgpu_status pbgpu_index_save(const pbgpu_index* ix, const char* path, const char* tag) {
+  if (!ix || !path) return fail(PBGPU_ERR_INVALID, "null argument");
+  API_TRY
+  HIPCHK(hipSetDevice(ix->device));
+  const std::string tmp = std::string(path) + ".tmp";
+  {
+    cache_file cf;
+    cf.path = path;
+    cf.f = fopen(tmp.c_str(), "wb");
+    if (!cf.f) return fail(PBGPU_ERR_IO, "cannot write index cache '%s'", tmp.c_str());
+    cf.put(kCacheMagic, 8);
+    cf.put_u64(kCacheVersion);
+    cf.put_str(tag ? tag : "");
+    const uint64_t sc[] = {ix->k, ix->psa_min, ix->n, ix->n_sr, ix->n_kmers, ix->n_occ, ix->buckets, ix->filt_log2,
+                           ix->shard, ix->n_shards, ix->sr_begin, ix->sr_end, ix->n_total, ix->null_ptr, ix->fk,
+                           ix->f_buckets, ix->f_kmers, ix->f_occ};
+    cf.put_u64(sizeof(sc) / 8);
+    cf.put(sc, sizeof(sc));
+    cf.put_u64(ix->name_fwd.size());
+    for (size_t i = 0; i < ix->name_fwd.size(); ++i) { cf.put_str(ix->name_fwd[i]); cf.put_str(ix->name_bwd[i]); }
+    cf.put_u64(ix->sr_start.size()); cf.put(ix->sr_start.data(), ix->sr_start.size() * 8);
+    cf.put_u64(ix->gstart.size()); cf.put(ix->gstart.data(), ix->gstart.size() * 8);
+    pinned_chunk pc;
+    cache_put_dbuf(cf, pc, ix->text); cache_put_dbuf(cf, pc, ix->d_sr_start); cache_put_dbuf(cf, pc, ix->occ);
+    cache_put_dbuf(cf, pc, ix->table); cache_put_dbuf(cf, pc, ix->sr_uoff); cache_put_dbuf(cf, pc, ix->sr_uids);
+    cache_put_dbuf(cf, pc, ix->filt); cache_put_dbuf(cf, pc, ix->f_occv); cache_put_dbuf(cf, pc, ix->f_table);
+    cf.put(kCacheMagic, 8);  // trailer: a file cut short anywhere fails to load
+    if (fflush(cf.f) != 0) return fail(PBGPU_ERR_IO, "cannot write index cache '%s'", tmp.c_str());
+  }
+  if (rename(tmp.c_str(), path) != 0) return fail(PBGPU_ERR_IO, "cannot rename '%s' to '%s'", tmp.c_str(), path);
+  return PBGPU_OK;
+  API_CATCH
+}
+
+pbgpu_status pbgpu_index_load(const char* path, int device, const char* tag, pbgpu_index** out) {
+  if (!path || !out) return fail(PBGPU_ERR_INVALID, "null argument");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+    return fail(PBGPU_ERR_INVALID, "device %d out of range", device);
+  API_TRY
+  const auto t0 = std::chrono::steady_clock::now();
+  cache_file cf;
+  cf.path = path;
+  cf.f = fopen(path, "rb");
+  if (!cf.f) return fail(PBGPU_ERR_IO, "cannot open index cache '%s'", path);
+  char magic[8];
+  cf.get(magic, 8);
+  if (memcmp(magic, kCacheMagic, 8) != 0) return fail(PBGPU_ERR_IO, "'%s' is not an index cache", path);
+  if (cf.get_u64() != kCacheVersion) return fail(PBGPU_ERR_IO, "'%s': index cache of another version", path);
+  if (cf.get_str(1 << 20) != std::string(tag ? tag : ""))
+    return fail(PBGPU_ERR_IO, "'%s': index cache saved for other inputs or parameters (tag differs)", path);
+  uint64_t sc[18];
+  if (cf.get_u64() != 18) return fail(PBGPU_ERR_IO, "'%s': corrupt index cache header", path);
+  cf.get(sc, sizeof(sc));
+  HIPCHK(hipSetDevice(device));
+  std::unique_ptr<pbgpu_index> ix(new pbgpu_index);
+  ix->device = device;
+  ix->k = (uint32_t)sc[0]; ix->psa_min = (uint32_t)sc[1]; ix->n = sc[2]; ix->n_sr = sc[3]; ix->n_kmers = sc[4];
+  ix->n_occ = sc[5]; ix->buckets = sc[6]; ix->filt_log2 = (uint32_t)sc[7]; ix->shard = (uint32_t)sc[8];
+  ix->n_shards = (uint32_t)sc[9]; ix->sr_begin = sc[10]; ix->sr_end = sc[11]; ix->n_total = sc[12];
+  ix->null_ptr = sc[13]; ix->fk = (uint32_t)sc[14]; ix->f_buckets = sc[15]; ix->f_kmers = sc[16]; ix->f_occ = sc[17];
+  const uint64_t nn = cf.get_u64();
+  if (nn > (1ull << 32)) return fail(PBGPU_ERR_IO, "'%s': corrupt index cache (names)", path);
+  ix->name_fwd.resize(nn); ix->name_bwd.resize(nn);
+  for (uint64_t i = 0; i < nn; ++i) { ix->name_fwd[i] = cf.get_str(1 << 24); ix->name_bwd[i] = cf.get_str(1 << 24); }
+  uint64_t m = cf.get_u64();
+  if (m > (1ull << 34)) return fail(PBGPU_ERR_IO, "'%s': corrupt index cache (starts)", path);
+  ix->sr_start.resize(m); cf.get(ix->sr_start.data(), m * 8);
+  m = cf.get_u64();
+  if (m > (1ull << 34)) return fail(PBGPU_ERR_IO, "'%s': corrupt index cache (starts)", path);
+  ix->gstart.resize(m); cf.get(ix->gstart.data(), m * 8);
+  pinned_chunk pc;
+  cache_get_dbuf(cf, pc, ix->text); cache_get_dbuf(cf, pc, ix->d_sr_start); cache_get_dbuf(cf, pc, ix->occ);
+  cache_get_dbuf(cf, pc, ix->table); cache_get_dbuf(cf, pc, ix->sr_uoff); cache_get_dbuf(cf, pc, ix->sr_uids);
+  cache_get_dbuf(cf, pc, ix->filt); cache_get_dbuf(cf, pc, ix->f_occv); cache_get_dbuf(cf, pc, ix->f_table);
+  cf.get(magic, 8);
+  if (memcmp(magic, kCacheMagic, 8) != 0) return fail(PBGPU_ERR_IO, "'%s': index cache trailer missing", path);
+  if (ix->name_fwd.size() != ix->n_sr || ix->sr_start.size() != ix->n_sr + 1)
+    return fail(PBGPU_ERR_IO, "'%s': inconsistent index cache", path);
+  HIPCHK(hipDeviceSynchronize());
+  ix->build_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  *out = ix.release();
+  return PBGPU_OK;
+  API_CATCH
+}
+
 pbgpu_status pbgpu_index_get_info(const pbgpu_index* ix, pbgpu_index_info* info) {
   if (!ix || !info) return fail(PBGPU_ERR_INVALID, "null argument");
   info->n_sr = ix->n_sr; info->text_len = ix->n; info->n_kmers = ix->n_kmers; info->n_occurrences = ix->n_occ;

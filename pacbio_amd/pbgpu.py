@@ -40,6 +40,7 @@ EXPORTS = [
     "pbgpu_coords_merge",
     "pbgpu_format_device", "pbgpu_text_download", "pbgpu_host_alloc", "pbgpu_host_free", "pbgpu_format_double",
     "pbgpu_index_replicate", "pbgpu_run", "pbgpu_runner_create", "pbgpu_runner_run", "pbgpu_runner_free",
+    "pbgpu_index_save", "pbgpu_index_load",
 ]
 
 
@@ -199,6 +200,8 @@ def lib():
         L.pbgpu_format_double.argtypes = [C.c_double, C.c_char_p]
         L.pbgpu_format_double.restype = C.c_int
         L.pbgpu_index_replicate.argtypes = [vp, C.c_int, C.POINTER(vp)]
+        L.pbgpu_index_save.argtypes = [vp, C.c_char_p, C.c_char_p]
+        L.pbgpu_index_load.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.POINTER(vp)]
         L.pbgpu_run.argtypes = [C.POINTER(vp), C.c_size_t, C.POINTER(AlignParams), C.POINTER(RunParams),
                                 C.POINTER(RunStats)]
         L.pbgpu_runner_create.argtypes = [C.POINTER(vp), C.c_size_t, C.POINTER(AlignParams), C.POINTER(RunParams),
@@ -282,6 +285,18 @@ class Index:
         h = C.c_void_p()
         _check(lib().pbgpu_index_replicate(self.h, device, C.byref(h)))
         return Index(h)
+
+    def save(self, path, tag=""):
+        """pbgpu_index_save: the whole index (host and device arrays) to `path`"""
+        _check(lib().pbgpu_index_save(self.h, os.fsencode(path), tag.encode()))
+
+    @classmethod
+    def load(cls, path, device=0, tag=""):
+        """pbgpu_index_load: an index saved by save(), rebuilt on `device` (PBGPU_ERR_IO if
+        the file is missing, truncated or saved with another tag)"""
+        h = C.c_void_p()
+        _check(lib().pbgpu_index_load(os.fsencode(path), device, tag.encode(), C.byref(h)))
+        return cls(h)
 
     def info(self):
         i = IndexInfo()
