@@ -548,7 +548,7 @@ constexpr int GROUP_U = PBGPU_GROUP_U, GROUP_U_BIG = PBGPU_GROUP_U_BIG;  // 64-h
 #define PBGPU_GROUP_MINW 1
 #endif
 template <bool GLOBAL_TABLE, uint32_t B>
-__global__ __launch_bounds__(B, B == 256 ? PBGPU_GROUP_MINW : 1) void k_group(IndexView ix, const KRec* __restrict__ krec,
+__global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_group(IndexView ix, const KRec* __restrict__ krec,
                                                        const uint64_t* __restrict__ roff, const uint32_t* __restrict__ n_kept,
                                                        const uint32_t* __restrict__ thr_in, const uint64_t* __restrict__ hit_off,
                                                        uint64_t node_base, uint32_t r0, const uint32_t* __restrict__ read_list,
@@ -860,7 +860,7 @@ __global__ __launch_bounds__(B, B == 256 ? PBGPU_GROUP_MINW : 1) void k_group(In
   }
 #ifdef PBGPU_PROF
   if (tid == 0 && !GLOBAL_TABLE) {
-    const int sb = B == 256 ? 8 : 14;
+    const int sb = B == GROUP_BLOCK ? 8 : 14;
     atomicAdd(&g_prof[sb + 0], (unsigned long long)pr_setup[0] + pr_setup[1]);
     atomicAdd(&g_prof[sb + 1], (unsigned long long)pr_steps[0]);
     atomicAdd(&g_prof[sb + 2], (unsigned long long)pr_steps[1]);
