@@ -273,6 +273,10 @@ pbgpu_status pbgpu_rccl_unique_id(uint8_t id[128]);
 pbgpu_status pbgpu_rccl_comm_create(int device, int n_ranks, int rank, const uint8_t id[128], pbgpu_comm** out);
 pbgpu_status pbgpu_rccl_comm_free(pbgpu_comm* comm);
 pbgpu_status pbgpu_shard_counts_allreduce(pbgpu_aligner* al, pbgpu_comm* comm);
+/* Bytes each rank contributed to its last count all-reduce: 2 per read base
+ * when n_ranks * (max_count + 1) < 65536 (two saturated 16-bit counts per
+ * ncclUint32), else 4. */
+uint64_t pbgpu_rccl_comm_last_bytes(const pbgpu_comm* comm);
 pbgpu_status pbgpu_align_resident_shard(pbgpu_aligner* al, const pbgpu_reads* reads);
 /* Host-side merge (no device work); the result is freed with pbgpu_coords_free. */
 pbgpu_status pbgpu_coords_merge(const pbgpu_coords_batch* const* parts, uint64_t n_parts, pbgpu_coords_batch** out);

@@ -240,7 +240,10 @@ int main(int argc, char** argv) {
       const std::string t = optarg;
       if (t == "none") C.gp.trim = Trim::NONE;
       else if (t == "match") C.gp.trim = Trim::MATCH;
-      else if (t == "branch") C.gp.trim = Trim::BRANCH;
+      // create_mega_reads.cc:47-49 turns the graph thread's trimming on for "match" only:
+      // "branch" leaves it at NONE (the graph itself would treat BRANCH as MATCH,
+      // overlap_graph.cc:126-127, but the CLI never passes it)
+      else if (t == "branch") C.gp.trim = Trim::NONE;
       else die("invalid --trim '" + t + "' (none, match, branch)");
       break;
     }

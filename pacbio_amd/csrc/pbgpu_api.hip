@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <functional>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -22,6 +23,7 @@
 
 #include "../../include/pbgpu.h"
 #include "pbgpu_internal.h"
+#include "count_pack.h"
 #include "pbgpu_host.h"
 
 namespace pbgpu {
@@ -47,6 +49,7 @@ void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const ui
                   uint32_t hcap_log2, uint32_t* gtable, GroupOut O, unsigned long long* stats, hipStream_t st);
 uint64_t group_table_words(uint32_t hcap_log2);
 void launch_sr_ul(const uint32_t* ids, uint64_t n, const int32_t* ul, uint64_t n_ul, int32_t* out, hipStream_t st);
+void launch_counts_pack16(bool unpack, const uint32_t* src, uint64_t n, uint32_t* dst, hipStream_t st);
 constexpr uint32_t kGroupLdsMaxLog2 = 13;  // 8192-slot table, 96 KiB of LDS
 void launch_init_slen(const ChainDesc* chains, uint32_t n_chains, uint32_t* slen, hipStream_t st);
 void launch_strand_order(const uint32_t* slen, uint32_t n_items, uint32_t* hist, uint32_t* cursor, uint32_t* perm,
@@ -118,12 +121,40 @@ static void parse_unitigs(const std::string& name, std::vector<uint32_t>& id, st
 }
 
 
+// code of a base in the last (len % 8) bases of a line: non-ACGT keeps the
+// previous code (compact_dna.hpp:108-136)
+static inline uint64_t tail_code(char ch, uint64_t c) {
+  switch (ch) {
+  case 'a': case 'A': return 0;
+  case 'c': case 'C': return 1;
+  case 'g': case 'G': return 2;
+  case 't': case 'T': return 3;
+  default: return c;
+  }
+}
+
+// host threads: the caller's count, else OMP_NUM_THREADS (the job's CPU share
+// on a shared box), else every core
+static int host_threads(int req) {
+  if (req > 0) return req;
+  if (const char* e = getenv("OMP_NUM_THREADS")) {
+    const int v = atoi(e);
+    if (v > 0) return v;
+  }
+  return (int)std::max(1u, std::thread::hardware_concurrency());
+}
+
 // host-side text accumulation with compact_dna line encoding
 struct text_builder {
   std::vector<uint64_t> words;  // MSB-first
   uint64_t n = 0;
   std::vector<uint64_t> starts{0};
   std::vector<std::string> names;
+  int threads = 1;              // host threads for the names and the slice packer
+  // Set (instead of filling `words`) by the pointer path: packs bases [b0, b0 + L)
+  // of the text into `out` (L / 32 + 2 zeroed words), so that a shard packs its own
+  // slice only.
+  std::function<void(uint64_t b0, uint64_t L, std::vector<uint64_t>& out)> pack_slice;
   void reserve(uint64_t bases) { words.reserve(bases / 32 + 2); }
   inline void put(uint64_t code) {
     const uint64_t w = n >> 5;
@@ -139,16 +170,7 @@ struct text_builder {
       put(((b >> 1) ^ (b >> 2)) & 3);
     }
     uint64_t c = 0;
-    for (size_t i = fast; i < len; ++i) {
-      switch (s[i]) {
-      case 'a': case 'A': c = 0; break;
-      case 'c': case 'C': c = 1; break;
-      case 'g': case 'G': c = 2; break;
-      case 't': case 'T': c = 3; break;
-      default: break;
-      }
-      put(c);
-    }
+    for (size_t i = fast; i < len; ++i) put(c = tail_code(s[i], c));
   }
   void end_record(const std::string& header, uint64_t start) {
     if (n > start) { names.push_back(header); starts.push_back(n); }
@@ -170,6 +192,23 @@ static void load_fasta(const char* path, text_builder& tb) {
     }
     tb.end_record(header.substr(1), start);
   }
+}
+
+// Buckets (of 4 slots) of the k-mer table for U keys, a power of two.  Load
+// <= 0.5 (slots >= 2U), so a probe sequence is short and a missed k-mer stops at
+// its first bucket; but a table that would take more than 1/8 of the device
+// (the 50M-super-read C5 shards: 2G k-mers, 137 GB at load <= 0.5) is sized to
+// load <= 0.85 instead -- linear probing over 64-B buckets stays at ~1.1
+// probes a hit there, and the presence filter keeps misses off the table.
+static uint64_t table_buckets(uint64_t U) {
+  uint64_t b = 1;
+  while (b * 2 < U) b <<= 1;
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && b * 64 > total_b / 8) {
+    b = 1;
+    while ((double)b * 4 * 0.85 < (double)U) b <<= 1;
+  }
+  return b;
 }
 
 // One sorted run of (key, value) pairs -> occurrence lists.  keys/vals hold
@@ -223,7 +262,7 @@ static RunsOut lists_from_sorted(uint64_t* keys, uint64_t* vals, uint64_t* spare
   uint64_t* fp = nullptr;
   uint32_t flog = 0;
   if (table) {
-    while (buckets * 2 < U) buckets <<= 1;  // slots = 4*buckets >= 2U: load <= 0.5
+    buckets = table_buckets(U);
     *n_buckets = buckets;
     table->alloc(4 * buckets);
     HIPCHK(hipMemsetAsync(table->p, 0xFF, table->bytes(), st));
@@ -282,10 +321,11 @@ static void build_kmer_table(pbgpu_index* ix, uint32_t km, uint32_t K, uint32_t 
     size_t free_b = 0, total_b = 0;
     HIPCHK(hipMemGetInfo(&free_b, &total_b));
     // one pass: 4 sort arrays + scan + lists ~56 B a position; partitioned: ~48 B a
-    // partition position + the finished blocks (~9 B a position) + 1 B of partition ids
+    // partition position + the finished blocks (~9 B a position) + their k-mer
+    // lists (16 B a k-mer, ~8 B a position at C4/C5 coverage) + 1 B of partition ids
     if (56.0 * N > 0.8 * (double)free_b || N >= (1ull << 31)) {
       P = 2;
-      while (P < 255 && (48.0 * N / P + 10.0 * N > 0.8 * (double)free_b || N / P >= (1ull << 31))) P *= 2;
+      while (P < 255 && (48.0 * N / P + 18.0 * N > 0.8 * (double)free_b || N / P >= (1ull << 31))) P *= 2;
       if (P > 255) P = 255;
     }
   }
@@ -365,6 +405,22 @@ static void build_kmer_table(pbgpu_index* ix, uint32_t km, uint32_t K, uint32_t 
   tmp.release();
   uint64_t U = 0, kept = 0;
   for (uint32_t p = 0; p < P; ++p) { U += ro[p].U; kept += ro[p].kept; }
+  // The blocks are laid end to end into one array.  When the array does not fit
+  // beside them, they wait in host memory instead (one copy out and back).
+  std::vector<std::vector<uint64_t>> staged;
+  {
+    size_t free_b = 0, total_b = 0;
+    HIPCHK(hipMemGetInfo(&free_b, &total_b));
+    if ((2 * U + kept + 2) * 8.0 > 0.9 * (double)free_b) {
+      staged.resize(P);
+      for (uint32_t p = 0; p < P; ++p) {
+        const uint64_t len = 2 * ro[p].U + ro[p].kept;
+        staged[p].resize(len);
+        if (len) HIPCHK(hipMemcpy(staged[p].data(), blocks[p].p, len * 8, hipMemcpyDeviceToHost));
+        blocks[p].release();
+      }
+    }
+  }
   occ.alloc(2 * U + kept + 2);
   HIPCHK(hipMemsetAsync(occ.p + 2 * U + kept, 0, 16, st));  // the null header
   std::vector<uint64_t> base(P);
@@ -372,13 +428,16 @@ static void build_kmer_table(pbgpu_index* ix, uint32_t km, uint32_t K, uint32_t 
   for (uint32_t p = 0; p < P; ++p) {
     base[p] = b;
     const uint64_t len = 2 * ro[p].U + ro[p].kept;
-    if (len) HIPCHK(hipMemcpyAsync(occ.p + b, blocks[p].p, len * 8, hipMemcpyDeviceToDevice, st));
+    if (len && staged.empty()) HIPCHK(hipMemcpyAsync(occ.p + b, blocks[p].p, len * 8, hipMemcpyDeviceToDevice, st));
+    if (len && !staged.empty()) {
+      HIPCHK(hipMemcpy(occ.p + b, staged[p].data(), len * 8, hipMemcpyHostToDevice));
+      std::vector<uint64_t>().swap(staged[p]);
+    }
     HIPCHK(hipStreamSynchronize(st));
     blocks[p].release();
     b += len;
   }
-  uint64_t buckets = 1;
-  while (buckets * 2 < U) buckets <<= 1;
+  const uint64_t buckets = table_buckets(U);
   n_buckets = buckets;
   table.alloc(4 * buckets);
   HIPCHK(hipMemsetAsync(table.p, 0xFF, table.bytes(), st));
@@ -418,25 +477,41 @@ static void build_device_index(pbgpu_index* ix, text_builder& tb) {
   // names, bwd names (frag_info.hpp:22-35), unitig ids -- of every super-read (host)
   ix->name_fwd = std::move(tb.names);
   ix->name_bwd.resize(ix->n_sr);
-  std::vector<uint32_t> uoff(ix->n_sr + 1, 0), uids, id;
-  std::vector<uint8_t> ori;
-  for (uint64_t i = 0; i < ix->n_sr; ++i) {
-    parse_unitigs(ix->name_fwd[i], id, ori);
-    uoff[i] = (uint32_t)uids.size();
-    uids.insert(uids.end(), id.begin(), id.end());
-    if (!id.empty()) {
-      std::string b;
-      for (size_t t = 0; t < id.size(); ++t) {
-        const size_t s = id.size() - 1 - t;
-        b += (t ? "_" : "") + std::to_string(id[s]) + (ori[s] ? 'F' : 'R');
+  // unitig ids and reversed names, in parallel over ranges of super-reads (50M names at C5)
+  std::vector<uint32_t> uoff(ix->n_sr + 1, 0), uids;
+  {
+    const uint64_t nsr = ix->n_sr, nparts = std::max<uint64_t>(1, std::min<uint64_t>(nsr, (uint64_t)tb.threads * 8));
+    std::vector<std::vector<uint32_t>> pids(nparts);
+    std::atomic<uint64_t> next(0);
+    run_parallel(tb.threads, [&]() {
+      std::vector<uint32_t> id;
+      std::vector<uint8_t> ori;
+      for (uint64_t q; (q = next.fetch_add(1)) < nparts;) {
+        for (uint64_t i = nsr * q / nparts; i < nsr * (q + 1) / nparts; ++i) {
+          parse_unitigs(ix->name_fwd[i], id, ori);
+          uoff[i] = (uint32_t)id.size();  // count; offsets below
+          pids[q].insert(pids[q].end(), id.begin(), id.end());
+          if (!id.empty()) {
+            std::string b;
+            for (size_t t = 0; t < id.size(); ++t) {
+              const size_t s = id.size() - 1 - t;
+              b += (t ? "_" : "") + std::to_string(id[s]) + (ori[s] ? 'F' : 'R');
+            }
+            ix->name_bwd[i] = std::move(b);
+          } else {
+            ix->name_bwd[i] = ix->name_fwd[i];
+          }
+        }
       }
-      ix->name_bwd[i] = b;
-    } else {
-      ix->name_bwd[i] = ix->name_fwd[i];
-    }
+    });
+    uint64_t tot = 0;
+    for (uint64_t i = 0; i < nsr; ++i) { const uint32_t c = uoff[i]; uoff[i] = (uint32_t)tot; tot += c; }
+    if (tot >= (1ull << 32)) throw bad_input("more than 2^32 unitig ids in the super-read names");
+    uoff[nsr] = (uint32_t)tot;
+    uids.reserve(tot);
+    for (auto& v : pids) { uids.insert(uids.end(), v.begin(), v.end()); std::vector<uint32_t>().swap(v); }
   }
-  uoff[ix->n_sr] = (uint32_t)uids.size();
-  tb.words.resize(tb.n / 32 + 2, 0);
+  if (!tb.pack_slice) tb.words.resize(tb.n / 32 + 2, 0);
   // This device's super-reads: all of them, or shard `shard` of n_shards -- the
   // super-reads starting in [total * s / S, total * (s + 1) / S) of the text --
   // plus the next k - 1 bases (the seam), so that an occurrence crossing into the
@@ -453,7 +528,10 @@ static void build_device_index(pbgpu_index* ix, text_builder& tb) {
   const uint64_t L = b1 - b0 + seam;
   ix->n = L;
   std::vector<uint64_t> words;
-  if (b0 == 0 && b1 + seam == total) {
+  if (tb.pack_slice) {
+    words.assign(L / 32 + 2, 0);
+    tb.pack_slice(b0, L, words);
+  } else if (b0 == 0 && b1 + seam == total) {
     words.swap(tb.words);
   } else {  // re-align the slice [b0, b0 + L) of the packed text to base 0
     const uint64_t W = tb.words.size(), j0 = b0 >> 5;
@@ -634,6 +712,7 @@ pbgpu_status pbgpu_index_build_fasta(const char* const* paths, size_t n_paths, c
   if (s != PBGPU_OK) return s;
   API_TRY
   text_builder tb;
+  tb.threads = host_threads(params->threads);
   for (size_t i = 0; i < n_paths; ++i) load_fasta(paths[i], tb);
   std::unique_ptr<pbgpu_index> ix(new pbgpu_index);
   ix->device = params->device; ix->k = params->k; ix->psa_min = params->psa_min; ix->fk = params->fine_k;
@@ -651,15 +730,54 @@ pbgpu_status pbgpu_index_build(const char* const* names, const char* const* seqs
   if (s != PBGPU_OK) return s;
   API_TRY
   text_builder tb;
-  uint64_t total = 0;
-  for (size_t i = 0; i < n; ++i) total += lens[i];
-  tb.reserve(total);
-  tb.words.assign(total / 32 + 2, 0);
-  for (size_t i = 0; i < n; ++i) {
-    const uint64_t start = tb.n;
-    tb.add_line(seqs[i], lens[i]);
-    tb.end_record(names[i], start);
+  tb.threads = host_threads(params->threads);
+  // every non-empty record is a super-read (end_record); the text is packed per
+  // slice by build_device_index, in parallel, each super-read one compact_dna line
+  std::vector<uint64_t> rec;  // record of each super-read
+  for (size_t i = 0; i < n; ++i)
+    if (lens[i]) { rec.push_back(i); tb.starts.push_back(tb.starts.back() + lens[i]); }
+  tb.n = tb.starts.back();
+  tb.names.resize(rec.size());
+  {
+    std::atomic<uint64_t> next(0);
+    const uint64_t nr = rec.size(), chunk = 1 << 16;
+    run_parallel(tb.threads, [&]() {
+      for (uint64_t c; (c = next.fetch_add(chunk)) < nr;)
+        for (uint64_t i = c; i < std::min(nr, c + chunk); ++i) tb.names[i] = names[rec[i]];
+    });
   }
+  const std::vector<uint64_t>& gs = tb.starts;
+  const int T = tb.threads;
+  tb.pack_slice = [&, T](uint64_t b0, uint64_t L, std::vector<uint64_t>& out) {
+    const uint64_t nw = (L + 31) / 32, chunk = 1 << 16;  // words per task (2 Mbases)
+    std::atomic<uint64_t> next(0);
+    run_parallel(T, [&]() {
+      for (uint64_t w0; (w0 = next.fetch_add(chunk)) < nw;) {
+        const uint64_t lo = w0 * 32, hi = std::min(L, (w0 + chunk) * 32);  // slice-local bases
+        uint64_t i = (uint64_t)(std::upper_bound(gs.begin(), gs.end(), b0 + lo) - gs.begin()) - 1;
+        for (uint64_t pos = lo; pos < hi; ++i) {
+          const char* sq = seqs[rec[i]];
+          const uint64_t len = lens[rec[i]], j0 = b0 + pos - gs[i];
+          const uint64_t j1 = std::min(len, j0 + (hi - pos));
+          const uint64_t fast = len & ~(uint64_t)7;
+          // compact_dna::copy_from_str (compact_dna.hpp:89-136), the line being the record:
+          // 8-aligned part by the bit trick, the tail keeping the last code over non-ACGT
+          uint64_t c = 0;
+          for (uint64_t j = fast; j < std::min(j0, len); ++j) c = tail_code(sq[j], c);
+          for (uint64_t j = j0; j < j1; ++j, ++pos) {
+            uint64_t code;
+            if (j < fast) {
+              const unsigned b = (unsigned char)sq[j];
+              code = ((b >> 1) ^ (b >> 2)) & 3;
+            } else {
+              code = c = tail_code(sq[j], c);
+            }
+            out[pos >> 5] |= code << (62 - 2 * (pos & 31));
+          }
+        }
+      }
+    });
+  };
   std::unique_ptr<pbgpu_index> ix(new pbgpu_index);
   ix->device = params->device; ix->k = params->k; ix->psa_min = params->psa_min; ix->fk = params->fine_k;
   if (params->n_shards > 1) { ix->shard = params->shard; ix->n_shards = params->n_shards; }
@@ -716,7 +834,10 @@ pbgpu_status pbgpu_index_replicate(const pbgpu_index* src, int device, pbgpu_ind
 }  // extern "C"
 namespace {
 constexpr char kCacheMagic[8] = {'P', 'B', 'G', 'P', 'U', 'I', 'X', '\0'};
-constexpr uint32_t kCacheVersion = 1;
+// The file holds raw device layouts (bucket hash, filter hash, header packing,
+// element sizes): kIndexLayout is bumped with any change to them (pbgpu_internal.h),
+// and the version also carries the ABI version.
+constexpr uint64_t kCacheVersion = ((uint64_t)PBGPU_ABI_VERSION << 32) | kIndexLayout;
 struct cache_file {
   FILE* f = nullptr;
   const char* path;
@@ -847,7 +968,17 @@ pbgpu_status pbgpu_index_load(const char* path, int device, const char* tag, pbg
   cache_get_dbuf(cf, pc, ix->filt); cache_get_dbuf(cf, pc, ix->f_occv); cache_get_dbuf(cf, pc, ix->f_table);
   cf.get(magic, 8);
   if (memcmp(magic, kCacheMagic, 8) != 0) return fail(PBGPU_ERR_IO, "'%s': index cache trailer missing", path);
-  if (ix->name_fwd.size() != ix->n_sr || ix->sr_start.size() != ix->n_sr + 1)
+  // the scalars the kernels index with must agree with the array sizes (a corrupt but
+  // untruncated file must not lead to out-of-bounds device reads)
+  const bool fine = ix->fk != 0;
+  if (ix->name_fwd.size() != ix->n_sr || ix->gstart.size() != ix->n_sr + 1 || ix->sr_begin > ix->sr_end ||
+      ix->sr_end > ix->n_sr || ix->sr_start.size() != ix->sr_end - ix->sr_begin + 1 ||
+      ix->d_sr_start.n != ix->sr_start.size() || ix->table.n != 4 * ix->buckets || ix->buckets == 0 ||
+      (ix->buckets & (ix->buckets - 1)) != 0 || ix->filt.n != (ix->filt_log2 ? 1ull << ix->filt_log2 : 0) ||
+      ix->filt_log2 >= 48 || ix->occ.n < ix->null_ptr + 2 || ix->text.n * 32 < ix->n ||
+      (fine && (ix->f_table.n != 4 * ix->f_buckets || ix->f_buckets == 0 ||
+                (ix->f_buckets & (ix->f_buckets - 1)) != 0)) ||
+      (!fine && ix->f_table.n != 0))
     return fail(PBGPU_ERR_IO, "'%s': inconsistent index cache", path);
   HIPCHK(hipDeviceSynchronize());
   ix->build_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -1108,6 +1239,7 @@ pbgpu_status pbgpu_rccl_comm_create(int device, int n_ranks, int rank, const uin
   memcpy(&u, id, 128);
   std::unique_ptr<pbgpu_comm> c(new pbgpu_comm);
   c->device = device;
+  c->n_ranks = n_ranks;
   const ncclResult_t r = ncclCommInitRank(&c->comm, n_ranks, u, rank);
   if (r != ncclSuccess) return fail(PBGPU_ERR_DEVICE, "ncclCommInitRank: %s", ncclGetErrorString(r));
   *out = c.release();
@@ -1123,13 +1255,32 @@ pbgpu_status pbgpu_rccl_comm_free(pbgpu_comm* c) {
   return PBGPU_OK;
 }
 
+uint64_t pbgpu_rccl_comm_last_bytes(const pbgpu_comm* c) { return c ? c->last_bytes : 0; }
+
 pbgpu_status pbgpu_shard_counts_allreduce(pbgpu_aligner* al, pbgpu_comm* c) {
   if (!al || !c) return fail(PBGPU_ERR_INVALID, "null argument");
   if (c->device != al->ix->device) return fail(PBGPU_ERR_INVALID, "communicator and aligner are on different devices");
   API_TRY
   HIPCHK(hipSetDevice(al->ix->device));
   if (al->gcount_n) {
-    const ncclResult_t r = ncclAllReduce(al->gcount.p, al->gcount.p, al->gcount_n, ncclUint32, ncclSum, c->comm, al->st);
+    // two saturated counts per ncclUint32 when no half can carry (count_pack.h), else u32
+    const uint64_t n = al->gcount_n;
+    ncclResult_t r;
+    if (counts_pack16_ok((uint32_t)c->n_ranks, (uint32_t)al->P.max_count)) {
+      const uint64_t nw = counts_packed_words(n);
+      al->gcount16.ensure(nw);
+      launch_counts_pack16(false, al->gcount.p, n, al->gcount16.p, al->st);
+      HIPCHK(hipGetLastError());
+      r = ncclAllReduce(al->gcount16.p, al->gcount16.p, nw, ncclUint32, ncclSum, c->comm, al->st);
+      if (r == ncclSuccess) {
+        launch_counts_pack16(true, al->gcount16.p, n, al->gcount.p, al->st);
+        HIPCHK(hipGetLastError());
+      }
+      c->last_bytes = nw * 4;
+    } else {
+      r = ncclAllReduce(al->gcount.p, al->gcount.p, n, ncclUint32, ncclSum, c->comm, al->st);
+      c->last_bytes = n * 4;
+    }
     if (r != ncclSuccess) return fail(PBGPU_ERR_DEVICE, "ncclAllReduce: %s", ncclGetErrorString(r));
   }
   HIPCHK(hipStreamSynchronize(al->st));

@@ -49,6 +49,8 @@ struct bad_input : std::runtime_error { using std::runtime_error::runtime_error;
 struct pbgpu_comm {  // an RCCL communicator of the sharded-index count exchange
   ncclComm_t comm = nullptr;
   int device = 0;
+  int n_ranks = 1;
+  uint64_t last_bytes = 0;  // payload of the last count all-reduce (count_pack.h)
 };
 struct unsupported : std::runtime_error { using std::runtime_error::runtime_error; };
 
@@ -220,6 +222,7 @@ struct pbgpu_aligner {
   dbuf<uint2> prog;
   // sharded index: per-base k-mer counts of the current batch (SEED_COUNTS, then summed)
   dbuf<uint32_t> gcount;
+  dbuf<uint32_t> gcount16;  // the counts packed two per u32 for the all-reduce (count_pack.h)
   uint64_t gcount_n = ~0ull;
   // -F: fine aligner pass (params of k_coords with align_k = fine_k, forward, unfiltered)
   bool fine = false;

@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <type_traits>
 #include "pbgpu_internal.h"
+#include "count_pack.h"
 
 namespace pbgpu {
 
@@ -2512,6 +2513,23 @@ void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const ui
                        n_kept, thr, hit_off, node_base, r0, read_list, n_list, hcap_log2, gtable, O, stats);
   }
 }
+// sharded-index count exchange: two saturated counts per u32 (count_pack.h)
+__global__ void k_counts_pack16(const uint32_t* __restrict__ c, uint64_t n, uint32_t* __restrict__ out) {
+  const uint64_t nw = counts_packed_words(n);
+  for (uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; w < nw; w += (uint64_t)gridDim.x * blockDim.x)
+    out[w] = counts_pack16(c, n, w);
+}
+__global__ void k_counts_unpack16(const uint32_t* __restrict__ in, uint64_t n, uint32_t* __restrict__ c) {
+  const uint64_t nw = counts_packed_words(n);
+  for (uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; w < nw; w += (uint64_t)gridDim.x * blockDim.x)
+    counts_unpack16(in[w], c, n, w);
+}
+void launch_counts_pack16(bool unpack, const uint32_t* src, uint64_t n, uint32_t* dst, hipStream_t st) {
+  if (!n) return;
+  if (unpack) hipLaunchKernelGGL(k_counts_unpack16, dim3(2048), dim3(256), 0, st, src, n, dst);
+  else hipLaunchKernelGGL(k_counts_pack16, dim3(2048), dim3(256), 0, st, src, n, dst);
+}
+
 void launch_sr_ul(const uint32_t* ids, uint64_t n, const int32_t* ul, uint64_t n_ul, int32_t* out, hipStream_t st) {
   if (n) hipLaunchKernelGGL(k_sr_ul, dim3(1024), dim3(256), 0, st, ids, n, ul, n_ul, out);
 }

@@ -521,7 +521,9 @@ static void runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_s
         b->id = id;
         // ramp: the first batches are small so the writer (the slowest stage) starts
         // after a short pipeline fill; then full batches (GPU efficiency)
-        const uint64_t want = std::min<uint64_t>(batch_bases, std::max<uint64_t>(1, (batch_bases >> ramp) << id));
+        // (no shift once the ramp is done: a left shift by the batch id wraps past 2^64)
+        const uint64_t sh = id >= ramp ? 0 : ramp - id;
+        const uint64_t want = sh == 0 ? batch_bases : std::max<uint64_t>(1, sh >= 64 ? 0 : batch_bases >> sh);
         const bool any = rp.fill(*b, want);
         {
           std::lock_guard<std::mutex> lk(smu);

@@ -37,7 +37,7 @@ EXPORTS = [
     "pbgpu_aligner_set_details", "pbgpu_download_details", "pbgpu_details_free", "pbgpu_format_details",
     "pbgpu_shard_counts", "pbgpu_shard_counts_download", "pbgpu_shard_counts_upload", "pbgpu_rccl_unique_id",
     "pbgpu_rccl_comm_create", "pbgpu_rccl_comm_free", "pbgpu_shard_counts_allreduce", "pbgpu_align_resident_shard",
-    "pbgpu_coords_merge",
+    "pbgpu_coords_merge", "pbgpu_rccl_comm_last_bytes",
     "pbgpu_format_device", "pbgpu_text_download", "pbgpu_host_alloc", "pbgpu_host_free", "pbgpu_format_double",
     "pbgpu_index_replicate", "pbgpu_run", "pbgpu_runner_create", "pbgpu_runner_run", "pbgpu_runner_free",
     "pbgpu_index_save", "pbgpu_index_load",
@@ -187,6 +187,8 @@ def lib():
         L.pbgpu_rccl_unique_id.argtypes = [C.c_void_p]
         L.pbgpu_rccl_comm_create.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.POINTER(vp)]
         L.pbgpu_rccl_comm_free.argtypes = [vp]
+        L.pbgpu_rccl_comm_last_bytes.argtypes = [vp]
+        L.pbgpu_rccl_comm_last_bytes.restype = C.c_uint64
         L.pbgpu_shard_counts_allreduce.argtypes = [vp, vp]
         L.pbgpu_align_resident_shard.argtypes = [vp, vp]
         L.pbgpu_coords_merge.argtypes = [C.POINTER(C.POINTER(CoordsBatch)), C.c_uint64,
@@ -657,6 +659,10 @@ class RcclComm:
         h = C.c_void_p()
         _check(lib().pbgpu_rccl_comm_create(device, n_ranks, rank, buf, C.byref(h)))
         self.h = h
+
+    def last_bytes(self):
+        """payload of the last count all-reduce on this rank (2 B a read base when packed)"""
+        return lib().pbgpu_rccl_comm_last_bytes(self.h)
 
     def close(self):
         if self.h:

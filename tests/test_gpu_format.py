@@ -91,6 +91,31 @@ def test_run_many_batches_two_indexes(small, small_dir):
     gix.close()
 
 
+def test_run_more_than_64_batches(tmp_path):
+    """Batch sizes past the ramp: the first batches hold batch_bases >> 3, >> 2,
+    >> 1 bases, then every batch takes reads up to batch_bases (a shift by the
+    batch id used to wrap to single-read batches from batch 41 on).  ~140
+    batches of ~20 reads give the one-batch bytes."""
+    from pacbio_amd import pbgpu
+    from tools.synth import Dataset
+    ds = Dataset("small", seed=5, n_pb=3000)
+    d = str(tmp_path)
+    ds.write(d)
+    ds.close()
+    gix = pbgpu.Index.from_fasta([os.path.join(d, "sr.fa")], 17)
+    pb = [os.path.join(d, "pb.fa")]
+    bb = 128_000
+    a, b = os.path.join(d, "many.coords"), os.path.join(d, "one.coords")
+    st = pbgpu.run([gix], pb, a, aligners_per_device=2, batch_bases=bb)
+    st1 = pbgpu.run([gix], pb, b, aligners_per_device=1)
+    gix.close()
+    assert st1["n_batches"] == 1 and st["n_bases"] == st1["n_bases"]
+    assert st["n_batches"] > 64
+    # each full batch holds >= bb bases: 3 ramp batches + the full ones + one partial at most
+    assert st["n_batches"] <= 3 + st["n_bases"] // bb + 1, (st["n_batches"], st["n_bases"])
+    assert open(a).read() == open(b).read()
+
+
 def test_run_gzip_input(small, small_dir):
     from pacbio_amd import pbgpu
     pb = os.path.join(small_dir, "pb.fa")

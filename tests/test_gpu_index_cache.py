@@ -101,3 +101,41 @@ def test_cli_index_cache(work):
     assert third.returncode == 0, third.stderr
     assert "not used" in third.stderr and "saved to cache" in third.stderr
     assert third.stdout == plain.stdout
+
+
+def test_save_load_shards(small, work):
+    """Shards of a sharded index survive the cache: per-shard
+    counts, the host sum and the per-shard alignment of loaded shards give the
+    built shards' merged text (shard-local starts, global names)."""
+    import numpy as np
+    from pacbio_amd import pbgpu
+    names, seqs, ps = small.sr_names(), small.sr_seqs(), small.pb_seqs()
+    nb = sum(len(s) for s in ps)
+
+    def merged_text(shards):
+        als = [pbgpu.Aligner(ix, k=17) for ix in shards]
+        rds = [al.upload(ps) for al in als]
+        total = np.zeros(nb, np.uint64)
+        for al, rd in zip(als, rds):
+            al.shard_counts(rd)
+            total += al.counts_download(nb)
+        parts = []
+        for al, rd in zip(als, rds):
+            al.counts_upload(total.astype(np.uint32))
+            al.align_resident_shard(rd)
+            parts.append(al.download())
+            rd.close()
+            al.close()
+        return pbgpu.merge_coords(parts).format(shards[0], small.pb_names(), [len(s) for s in ps])
+
+    built = [pbgpu.Index.from_records(names, seqs, 17, shard=s, n_shards=3) for s in range(3)]
+    want = merged_text(built)
+    assert want.count("\n") > 10
+    for s, ix in enumerate(built):
+        ix.save(os.path.join(work, f"shard{s}.pbix"), tag=f"s{s}")
+        ix.close()
+    loaded = [pbgpu.Index.load(os.path.join(work, f"shard{s}.pbix"), tag=f"s{s}") for s in range(3)]
+    assert [ix.info()["sr_begin"] for ix in loaded][0] == 0 and loaded[-1].info()["sr_end"] == len(names)
+    assert merged_text(loaded) == want
+    for ix in loaded:
+        ix.close()

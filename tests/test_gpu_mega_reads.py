@@ -99,7 +99,8 @@ CASES = [
     (["-T", "maximal", "-L", "0"], {}, dict(tiling="maximal", min_len=0.0)),
     (["-T", "weighted", "--trim", "match"], {}, dict(tiling="weighted", trim="match")),
     (["-T", "none", "-b", "-d", "0.05"], {}, dict(tiling="none", bases=True, density=0.05)),
-    (["-O", "1.5", "-e", "2", "--trim", "branch", "-L", "50"], {}, dict(play=1.5, errors=2.0, trim="branch",
+    # --trim branch trims nothing: create_mega_reads.cc:47-49 switches trimming on for "match" only
+    (["-O", "1.5", "-e", "2", "--trim", "branch", "-L", "50"], {}, dict(play=1.5, errors=2.0, trim="none",
                                                                          min_len=50.0)),
     (["--max-match", "-B", "10", "--stretch-cap", "500"], dict(max_match=True, bases_matching=10.0, stretch_cap=500.0),
      {}),
@@ -117,6 +118,8 @@ def test_synthetic_options(synth, tmp_path, cli, aopt, gopt):
     want = _expect(reads_for(**aopt), ul, 31, **gopt)
     assert want.count(">") >= 10
     assert open(out).read() == want
+    if "branch" in cli:  # the case must tell "branch" (no trim) from "match"
+        assert _expect(reads_for(**aopt), ul, 31, **dict(gopt, trim="match")) != want
 
 
 def test_synthetic_unitig_sequences(synth, tmp_path):

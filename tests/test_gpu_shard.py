@@ -103,6 +103,8 @@ def test_rccl_single_rank_allreduce(small):
     before = al.counts_download(sum(len(s) for s in small.pb_seqs()))
     al.counts_allreduce(comm)
     assert np.array_equal(before, al.counts_download(len(before)))
+    # one rank x (max_count + 1): two 16-bit counts per ncclUint32
+    assert comm.last_bytes() == 4 * ((len(before) + 1) // 2)
     al.align_resident_shard(rr)
     got = al.download().format(ix, small.pb_names(), [len(s) for s in small.pb_seqs()])
     comm.close()

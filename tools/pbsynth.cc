@@ -187,26 +187,51 @@ int pbsynth_make(const pbsynth_config* cfg, int threads, pbsynth_seqs* sr, pbsyn
   for (uint64_t i = 0; i < nu; ++i) (*ul)[i] = (int32_t)g.ulen[i];
 
   if (sr) {
-    std::vector<std::string> seqs(c.n_sr), names(c.n_sr);
-    parallel_for(c.n_sr, threads, [&](uint64_t i) {
+    // Two passes, written straight into the output buffers (C5: 50M SRs, ~60 Gbp):
+    // pass 1 draws each SR's walk (its own RNG stream) and sizes it, pass 2 copies.
+    const uint64_t n = c.n_sr;
+    std::vector<uint64_t> su(n);             // first unitig
+    std::vector<uint32_t> scnt(n);           // unitig count << 1 | reverse
+    std::vector<uint64_t> off(n + 1, 0), noff(n + 1, 0);
+    parallel_for(n, threads, [&](uint64_t i) {
       std::mt19937_64 r(stream_seed(c.seed, 4, i));
       uint64_t cnt = 1 + r() % c.sr_max_unitigs;
       uint64_t u = r() % nu;
       if (u + cnt > nu) cnt = nu - u;
-      bool rev = r() & 1;
-      uint64_t s = g.ustart[u], e = g.ustart[u + cnt - 1] + g.ulen[u + cnt - 1];
-      std::string seq = g.genome.substr(s, e - s), name;
+      const bool rev = r() & 1;
+      su[i] = u;
+      scnt[i] = (uint32_t)(cnt << 1 | (rev ? 1 : 0));
+      off[i + 1] = g.ustart[u + cnt - 1] + g.ulen[u + cnt - 1] - g.ustart[u];
+      uint64_t nl = 0;  // "12F_13F_14F" + NUL
+      for (uint64_t t = 0; t < cnt; ++t) nl += (t ? 1 : 0) + std::to_string(u + t).size() + 1;
+      noff[i + 1] = nl + 1;
+    });
+    for (uint64_t i = 0; i < n; ++i) { off[i + 1] += off[i]; noff[i + 1] += noff[i]; }
+    sr->n = n;
+    sr->seq = (char*)malloc(off[n] + 1);
+    sr->off = (uint64_t*)malloc((n + 1) * sizeof(uint64_t));
+    sr->names = (char*)malloc(noff[n] + 1);
+    sr->name_off = (uint64_t*)malloc((n + 1) * sizeof(uint64_t));
+    if (!sr->seq || !sr->off || !sr->names || !sr->name_off) return 2;
+    memcpy(sr->off, off.data(), (n + 1) * sizeof(uint64_t));
+    memcpy(sr->name_off, noff.data(), (n + 1) * sizeof(uint64_t));
+    sr->seq[off[n]] = 0;
+    sr->names[noff[n]] = 0;
+    parallel_for(n, threads, [&](uint64_t i) {
+      const uint64_t u = su[i], cnt = scnt[i] >> 1;
+      const bool rev = scnt[i] & 1;
+      const uint64_t s = g.ustart[u], len = off[i + 1] - off[i];
+      char* d = sr->seq + off[i];
+      std::string name;
       if (!rev) {
+        memcpy(d, g.genome.data() + s, len);
         for (uint64_t t = 0; t < cnt; ++t) name += (t ? "_" : "") + std::to_string(u + t) + "F";
       } else {
-        std::reverse(seq.begin(), seq.end());
-        for (auto& ch : seq) ch = comp(ch);
+        for (uint64_t t = 0; t < len; ++t) d[t] = comp(g.genome[s + len - 1 - t]);
         for (uint64_t t = 0; t < cnt; ++t) name += (t ? "_" : "") + std::to_string(u + cnt - 1 - t) + "R";
       }
-      seqs[i].swap(seq);
-      names[i].swap(name);
+      memcpy(sr->names + noff[i], name.c_str(), name.size() + 1);
     });
-    pack(seqs, names, sr);
   }
   if (pb) {
     std::vector<std::string> seqs(c.n_pb), names(c.n_pb);

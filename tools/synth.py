@@ -34,6 +34,10 @@ PRESETS = {
     # 250 Mbp genome with 2% 5-50-copy repeats, PB reads of 15 kb N50 (lognormal mean 12.5 kb, sigma 0.6)
     "C4": dict(genome_len=250_000_000, n_sr=10_000_000, n_pb=2_000_000, pb_len_mean=12500, pb_len_sigma=0.6,
                repeat_frac=0.02),
+    # configs[4] (one MI355X, index sharded; property tests only): whole-human scale, 50M SRs (~62 Gbp
+    # of text) over a 3.1 Gbp genome with the C4 repeat model, PB reads of 15 kb N50
+    "C5": dict(genome_len=3_100_000_000, n_sr=50_000_000, n_pb=20_000_000, pb_len_mean=12500, pb_len_sigma=0.6,
+               repeat_frac=0.02),
     "tiny": dict(genome_len=20_000, n_sr=60, n_pb=8, pb_len_mean=2000, pb_len_sigma=0.0),
     "small": dict(genome_len=200_000, n_sr=1500, n_pb=40, pb_len_mean=6000, pb_len_sigma=0.4),
 }
