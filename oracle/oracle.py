@@ -16,7 +16,7 @@ class OracleParams(C.Structure):
                 ("forward", C.c_int), ("max_match", C.c_int), ("max_count", C.c_int32),
                 ("mers_matching", C.c_double), ("bases_matching", C.c_double), ("unitigs_k", C.c_uint32),
                 ("unitig_lengths", C.POINTER(C.c_int32)), ("n_unitigs", C.c_size_t), ("legacy_no_filter", C.c_int),
-                ("fine_k", C.c_uint32)]
+                ("legacy_int_abs", C.c_int), ("fine_k", C.c_uint32)]
 
 
 class OracleRecord(C.Structure):
@@ -97,7 +97,7 @@ def _cstrs(items):
 
 def params(k=17, stretch_factor=1.3, stretch_constant=10, stretch_cap=10000.0, window_size=1, forward=False,
            max_match=False, max_count=5000, mers_matching=0.0, bases_matching=17.0, unitigs_k=0,
-           unitig_lengths=None, legacy_no_filter=False, psa_min=13, fine_k=0):
+           unitig_lengths=None, legacy_no_filter=False, psa_min=13, fine_k=0, legacy_int_abs=False):
     p = OracleParams()
     lib().oracle_params_default(C.byref(p))
     p.k = k; p.psa_min = psa_min; p.stretch_constant = stretch_constant; p.stretch_factor = stretch_factor
@@ -105,6 +105,7 @@ def params(k=17, stretch_factor=1.3, stretch_constant=10, stretch_cap=10000.0, w
     p.max_match = int(bool(max_match)); p.max_count = max_count; p.mers_matching = mers_matching
     p.bases_matching = bases_matching; p.unitigs_k = unitigs_k; p.legacy_no_filter = int(bool(legacy_no_filter))
     p.fine_k = fine_k
+    p.legacy_int_abs = int(bool(legacy_int_abs))
     keep = None
     if unitig_lengths is not None:
         keep = np.ascontiguousarray(unitig_lengths, dtype=np.int32)

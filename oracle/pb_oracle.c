@@ -670,6 +670,7 @@ static void offlist_push(offlist* l, int32_t pb, int32_t sr) {
 
 typedef struct {
   uint32_t k, unitigs_k; const int32_t* ul; size_t n_ul; int forward;
+  int int_abs;  /* oracle_params.legacy_int_abs */
 } cinfo_ctx;
 
 static void rec_canonicalize(oracle_record* r, int forward, uint32_t k) {
@@ -750,7 +751,8 @@ static void compute_coords_info(const sr_rec* sr, uint32_t sr_index, const offli
     const double bb = r->offset = ls.NB / ls.VX;
     for (uint32_t t = 0; t < L->nlis; ++t) {
       const int32_t* c = &L->off[2 * L->lis[t]];
-      e += fabs(a * (double)c[1] + bb - (double)c[0]);
+      const double d = a * (double)c[1] + bb - (double)c[0];
+      e += cx->int_abs ? (double)abs((int)d) : fabs(d);
     }
     r->avg_err = e / (double)ls.n;
   }
@@ -775,7 +777,7 @@ int oracle_coords_info(const char* sr_name, uint32_t sr_len,
   index_add_sr(&tmp, sr_name, 0, sr_len);
   offlist f = { (int32_t*)fwd, n_fwd, n_fwd, (uint32_t*)fwd_lis, n_fwd_lis, n_fwd_lis };
   offlist b = { (int32_t*)bwd, n_bwd, n_bwd, (uint32_t*)bwd_lis, n_bwd_lis, n_bwd_lis };
-  cinfo_ctx cx = { align_k, unitigs_k, ul, n_ul, forward };
+  cinfo_ctx cx = { align_k, unitigs_k, ul, n_ul, forward, 0 };
   compute_coords_info(&tmp.sr[0], 0, &f, &b, pb_size, &cx, out);
   free(tmp.sr[0].name_fwd); free(tmp.sr[0].name_bwd); free(tmp.sr[0].fwd.id); free(tmp.sr[0].fwd.ori); free(tmp.sr);
   return 0;
@@ -981,7 +983,7 @@ static oracle_record* fine_align_read(const oracle_index* ix, const oracle_param
     }
   }
   accept_t all = { 1, 0, 0, 0, 1, 0 };
-  cinfo_ctx cx = { fk, p->unitigs_k, p->unitig_lengths, p->n_unitigs, 1 };
+  cinfo_ctx cx = { fk, p->unitigs_k, p->unitig_lengths, p->n_unitigs, 1, p->legacy_int_abs };
   oracle_record* recs = xmalloc((nc ? nc : 1) * sizeof(oracle_record));
   for (size_t i = 0; i < nc; ++i) {
     fine_win* fw = &w->fw[i];
@@ -1064,7 +1066,7 @@ static int align_read_w(const oracle_index* ix, const oracle_params* p, worker_t
   }
   /* --- chaining + coords (align_sequence_max) --- */
   accept_t ac = { 0, p->stretch_factor, p->stretch_constant, p->stretch_cap, 0, p->stretch_factor };
-  cinfo_ctx cx = { k, p->unitigs_k, p->unitig_lengths, p->n_unitigs, p->forward };
+  cinfo_ctx cx = { k, p->unitigs_k, p->unitig_lengths, p->n_unitigs, p->forward, p->legacy_int_abs };
   const double Mf = p->mers_matching / 100.0, Bf = p->bases_matching / 100.0;
   size_t nrec = 0, caprec = 0; oracle_record* recs = NULL;
   for (uint32_t slot = 0; slot < w->n_touched; ++slot) {

@@ -58,6 +58,11 @@ typedef struct {
   /* test-only knob: 1 => skip SSR / toggle / count threshold (the
    * semantics tests/test_pb_aligner.cc:68 was written against) */
   int      legacy_no_filter;
+  /* test-only knob: 1 => the average error sums int abs() of each point's
+   * residual (truncated to int, as `abs` on a double resolved to the C int
+   * abs in the older aligner that wrote tests/mega_reads_output/expect_coords;
+   * least_square_2d.hpp:82-90 keeps that loop, commented out) */
+  int      legacy_int_abs;
   /* -F: fine_aligner k (0 = off).  The index must carry the fine sub-index
    * (oracle_index_build_fine) for this k. */
   uint32_t fine_k;
