@@ -92,50 +92,94 @@ static int32_t info_at(const Coord& c, bool bases, int i) {  // kmers_info / bas
   return bases ? c.bases_info[i] : c.kmers_info[i];
 }
 
-// overlap_graph::traverse (overlap_graph.cc:7-59)
+// overlap_graph::traverse (overlap_graph.cc:7-59).  Same visit order, tests and
+// early break as the reference; the per-pair sums over the overlapping unitigs
+// (u_overlap_len, common_overlap) come from per-node prefix sums computed once
+// per read, and the sorted nodes' implied positions sit in one array.  (C2
+// reads carry ~560 records and ~12k overlapping pairs each.)
 void ReadGraph::traverse(std::ostream* dot) {
   const auto& coords = *coords_;
   const double play = p_.overlap_play;
   const unsigned k = p_.k_len;
-  for (size_t i = 0; i != sort_nodes_.size(); ++i) {
-    const int it_i = sort_nodes_[i];
+  const size_t n = sort_nodes_.size();
+  // prefix sums per node j over its name's unitigs u < m:
+  //   pul[m] = sum ulen(unitig u), pco[m] = sum info[2u] - sum_{u >= 1} info[2u - 1]
+  // (int arithmetic as in the reference's loop, wrapping instead of overflowing)
+  pre_off_.resize(coords.size() + 1);
+  pre_off_[0] = 0;
+  for (size_t j = 0; j < coords.size(); ++j) pre_off_[j + 1] = pre_off_[j] + coords[j].name->size() + 1;
+  pul_.resize(pre_off_.back());
+  pco_.resize(pre_off_.back());
+  for (size_t j = 0; j < coords.size(); ++j) {
+    const Coord& cj = coords[j];
+    const unitig_list& nm = *cj.name;
+    uint32_t* ul = &pul_[pre_off_[j]];
+    uint32_t* co = &pco_[pre_off_[j]];
+    ul[0] = co[0] = 0;
+    for (size_t u = 0; u < nm.size(); ++u) {
+      ul[u + 1] = ul[u] + (uint32_t)ulen(unitig_id(nm[u]));
+      co[u + 1] = co[u] + (uint32_t)info_at(cj, p_.maximize_bases, 2 * (int)u) -
+                  (u > 0 ? (uint32_t)info_at(cj, p_.maximize_bases, 2 * (int)u - 1) : 0u);
+    }
+  }
+  sorted_.resize(n);
+  for (size_t i = 0; i < n; ++i) {
+    const int it = sort_nodes_[i];
+    const unitig_list& nm = *coords[it].name;
+    sorted_[i] = SortedNode{nodes_[it].imp_s, nodes_[it].imp_e, coords[it].avg_err, it, (int)nm.size(),
+                            nm.empty() ? 0u : nm[0],
+                            p_.maximize_bases ? coords[it].sr_cover : (unsigned)coords[it].nb_mers, nm.data()};
+  }
+  for (size_t i = 0; i != n; ++i) {
+    const int it_i = sorted_[i].idx;
     Node& ni = nodes_[it_i];
     const Coord& ci = coords[it_i];
-    if (ni.imp_e >= (double)ci.rl) continue;  // hanging off the 3' end
-    for (size_t j = i + 1; j != sort_nodes_.size(); ++j) {
-      const int it_j = sort_nodes_[j];
-      Node& nj = nodes_[it_j];
-      const Coord& cj = coords[it_j];
-      if (nj.imp_s <= 1) continue;               // hanging off the 5' end
-      if (ni.imp_e > nj.imp_e + 31) continue;    // not advancing
-      const double position_len = ni.imp_e - nj.imp_s;
-      const double error1 = ci.avg_err + cj.avg_err;
+    const double imp_e_i = sorted_[i].imp_e;
+    if (imp_e_i >= (double)ci.rl) continue;  // hanging off the 3' end
+    const unitig_list& name_i = *ci.name;
+    const int sa = (int)name_i.size();
+    const unitig_t* a = name_i.data();
+    const double err_i = sorted_[i].avg_err;
+    for (size_t j = i + 1; j != n; ++j) {
+      const SortedNode& sj = sorted_[j];
+      if (sj.imp_s <= 1) continue;               // hanging off the 5' end
+      if (imp_e_i > sj.imp_e + 31) continue;     // not advancing
+      const double position_len = imp_e_i - sj.imp_s;
+      const double error1 = err_i + sj.avg_err;
       const double error = p_.nb_errors * error1;
       if (position_len * play + error < k) break;  // implied overlap shorter than a k-mer
-      const int nb_u_overlap = name_overlap(*ci.name, *cj.name);
-      if (!nb_u_overlap) continue;
-      if (*ci.name == *cj.name) continue;  // the same super-read
-      int u_overlap_len = 0, common_overlap = 0;
-      for (int u = 0; u < nb_u_overlap; ++u) {
-        u_overlap_len += ulen(u < (int)cj.name->size() ? unitig_id((*cj.name)[u]) : INVALID_ID);
-        common_overlap += info_at(cj, p_.maximize_bases, 2 * u);
-        if (u > 0) common_overlap -= info_at(cj, p_.maximize_bases, 2 * u - 1);
+      // name_overlap(name_i, name_j) on the cached first unitig and size of name j
+      const int sb = sj.nsz;
+      if (sa < 2 || sb < 2) continue;
+      int nb_u_overlap = 0;
+      for (int t = std::max(sa - sb + 1, 1); t < sa; ++t) {
+        if (a[t] != sj.u0) continue;
+        int q = t + 1;
+        while (q < sa && a[q] == sj.name[q - t]) ++q;
+        if (q == sa) { nb_u_overlap = sa - t; break; }
       }
+      if (!nb_u_overlap) continue;
+      // the same super-read (name_i == name_j; equal names have equal sizes)
+      if (sb == sa && (sj.name == a || std::equal(a, a + sa, sj.name))) continue;
+      const int it_j = sj.idx;
+      // nb_u_overlap <= |name_j|, so every unitig of the sums is in name j
+      int u_overlap_len = (int)pul_[pre_off_[it_j] + nb_u_overlap];
+      const int common_overlap = (int)pco_[pre_off_[it_j] + nb_u_overlap];
       u_overlap_len = (int)((unsigned)u_overlap_len - (unsigned)(nb_u_overlap - 1) * (k - 1));
       if (u_overlap_len > play * position_len + error || position_len > play * (u_overlap_len + error)) continue;
       // an overlap between nodes i and j
+      Node& nj = nodes_[it_j];
       ni.end_node = false;
       nj.start_node = false;
       uf_.unite(it_i, it_j);
-      const int nlpath = (int)((unsigned)ni.lpath + (p_.maximize_bases ? cj.sr_cover : (unsigned)cj.nb_mers) -
-                               (unsigned)common_overlap);
+      const int nlpath = (int)((unsigned)ni.lpath + sj.lp_add - (unsigned)common_overlap);
       const Node& si = ni.lstart == -1 ? ni : nodes_[ni.lstart];
-      const Node& sj = nj.lstart == -1 ? nj : nodes_[nj.lstart];
-      if (nlpath > nj.lpath || (nlpath == nj.lpath && (nj.lstart == -1 || si.imp_s > sj.imp_s))) {
+      const Node& sjn = nj.lstart == -1 ? nj : nodes_[nj.lstart];
+      if (nlpath > nj.lpath || (nlpath == nj.lpath && (nj.lstart == -1 || si.imp_s > sjn.imp_s))) {
         nj.lpath = nlpath;
         nj.lstart = ni.lstart == -1 ? it_i : ni.lstart;
         nj.lprev = it_i;
-        nj.lunitigs = ni.lunitigs + (int)cj.name->size() - nb_u_overlap;
+        nj.lunitigs = ni.lunitigs + sb - nb_u_overlap;
       }
       if (dot) *dot << "n" << it_i << " -> n" << it_j << " [tooltip=\"...\", label=\"" << common_overlap << "\"];\n";
     }

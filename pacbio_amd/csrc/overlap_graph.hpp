@@ -119,6 +119,17 @@ class ReadGraph {
   std::vector<double> weights_;
   std::vector<std::pair<int, MegaRead>> comp_;  // per component root (ascending), its mega-read
   std::vector<const MegaRead*> mega_reads_;
+  // traverse()'s per-read scratch: prefix sums over each node's name, the sorted nodes
+  struct SortedNode {
+    double imp_s, imp_e, avg_err;
+    int idx, nsz;        // node index, unitigs in its name
+    unitig_t u0;         // first unitig of its name
+    unsigned lp_add;     // its path length contribution (sr_cover with -b, else nb_mers)
+    const unitig_t* name;
+  };
+  std::vector<size_t> pre_off_;
+  std::vector<uint32_t> pul_, pco_;
+  std::vector<SortedNode> sorted_;
 };
 
 }  // namespace megareads
