@@ -107,10 +107,10 @@ def _kernel_bytes(st):
         # (16 B) read, every occurrence (8 B) read once, every hit (8 B) written, chain
         # descriptors (24 B) written -- counted by the kernel for the reads it completed
         "k_group": per(st["g0_kept"] * 32 + st["g0_hits"] * 16 + st["g0_chains"] * 24, "k_group"),
-        # tier-0 k_lis_w (strands <= 255 hits), counted by the kernel: every hit read (8 B)
-        # and its lis point written (<= 8 B); per strand its item, chain descriptor (24 B),
-        # length and lis length (12 B)
-        "k_lis": per(st["l0_hits"] * 16 + st["l0_strands"] * 36, "k_lis"),
+        # tier-0 k_lis_w (strands <= 255 hits), counted by the kernel: every hit read (8 B),
+        # every lis point written (8 B); per strand its item, chain descriptor (24 B), length and
+        # lis length (12 B)
+        "k_lis": per(st["l0_hits"] * 8 + st["l0_points"] * 8 + st["l0_strands"] * 36, "k_lis"),
         # per chain its list entry (4 B), descriptor (24 B), both lis lengths (8 B), super-read
         # length + unitig range (16 B) and read range (16 B); every lis point (8 B) read once;
         # every record (96 B) written (kmers_info pairs not counted)
@@ -306,6 +306,16 @@ def main():
                        "frac": round(kb[kk] / (kms[kk] / max(1, kn[kk]) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                        "stage_ms_per_step": round(st["ms_" + STAGE_OF[kk]] / args.device_steps, 3)}
                   for kk in kb if kn.get(kk)}
+    # k_seed at its access granularity: every presence-filter check and bucket probe is a
+    # random access that moves a 64-B sector (the 8-B filter word alone is the algorithmic
+    # minimum above); against B_rand this is the kernel's random-access roofline
+    if kn.get("k_seed"):
+        sec = (st["n_bases"] + (st["n_filter"] + st["n_probes"]) * 64 + st["n_kept"] * 16) / kn["k_seed"]
+        sgbs = sec / (kms["k_seed"] / kn["k_seed"] * 1e-3) / 1e9
+        per_kernel["k_seed"]["sector_view"] = {
+            "bytes_per_launch": sec, "achieved_gbs": round(sgbs, 1), "frac": round(sgbs / HBM_PEAK_GBS, 4),
+            "frac_of_b_rand": round(sgbs / b_rand, 4) if b_rand else None,
+            "random_accesses_per_launch": (st["n_filter"] + st["n_probes"]) / kn["k_seed"]}
     # HBM traffic per launch of the dominant kernel from the committed rocprofv3 PMC
     # summary (tools/prof_r02.sh): FETCH_SIZE calibrated on the 512-B-run gather
     # microbenchmark (bytes moved / FETCH_SIZE), + WRITE_SIZE

@@ -232,6 +232,8 @@ typedef struct {
   uint64_t fit_chains, fit_points;
   /* presence-filter words read by k_seed (8 B each) before the bucket probes */
   uint64_t n_filter;
+  /* lis points written by the timed k_lis slot (tier-0 strands) */
+  uint64_t l0_points;
 } pbgpu_stats;
 pbgpu_status pbgpu_aligner_get_stats(const pbgpu_aligner* al, pbgpu_stats* s);
 pbgpu_status pbgpu_aligner_reset_stats(pbgpu_aligner* al);

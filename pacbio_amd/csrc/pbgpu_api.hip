@@ -1832,6 +1832,7 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
   al->acc.l0_hits += sv[ST_L0_HITS]; al->acc.l0_strands += sv[ST_L0_STRANDS];
   al->acc.fit_chains += sv[ST_FIT_CHAINS]; al->acc.fit_points += sv[ST_FIT_POINTS];
   al->acc.n_filter += sv[ST_FILTER];
+  al->acc.l0_points += sv[ST_L0_POINTS];
   if (al->fine) {
     al->acc.n_fine_hits += sv[ST_FINE_HITS];
     al->acc.n_fine_windows += nrec;

@@ -111,6 +111,7 @@ enum StatSlot {
   ST_FINE_HITS,                          // fine aligner: windowed hits
   ST_FIT_CHAINS, ST_FIT_POINTS,          // coarse k_coords work: chains, lis points (counted by the chain order pass)
   ST_FILTER,                             // presence-filter words read by k_seed (8 B each)
+  ST_L0_POINTS,                          // lis points written by the tier-0 k_lis_w launches
   ST_N
 };
 

@@ -1444,7 +1444,7 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
   uint16_t *snxt = s_nxt[wv], *sln = s_len[wv], *sP = s_P[wv], *sroot = s_root[wv], *srs = s_rs[wv];
   const uint32_t nwaves = gridDim.x * WPB;
   const bool fast = lp.W == 1 && !lp.mer_all;
-  uint64_t tests = 0, my_hits = 0, my_strands = 0;
+  uint64_t tests = 0, my_hits = 0, my_strands = 0, my_points = 0;
   auto desc = [&](uint32_t item, uint64_t& base, uint32_t& n) {
     const ChainDesc d = chains[item >> 1];
     base = d.hit_base + ((item & 1) ? d.nf : 0);
@@ -1719,6 +1719,7 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
       }
     }
     if (lane == 0) lisl[item] = longest;
+    my_points += longest;
     lds_fence();  // LDS reads of this strand done before the next strand's commit
   }
   tests = lane == 0 ? tests : 0;
@@ -1727,6 +1728,7 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
   if (SMAX == LISW_TINY_N && lane == 0 && my_strands) {  // per-launch work of the timed tier (bench roofline)
     atomicAdd(&stats[ST_L0_HITS], (unsigned long long)my_hits);
     atomicAdd(&stats[ST_L0_STRANDS], (unsigned long long)my_strands);
+    atomicAdd(&stats[ST_L0_POINTS], (unsigned long long)my_points);
   }
 }
 

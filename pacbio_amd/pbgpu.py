@@ -122,7 +122,7 @@ class Stats(C.Structure):
                [("kernel_ms", C.c_double * 8), ("kernel_launches", C.c_uint64 * 8)] + \
                [(n, C.c_uint64) for n in ("g0_kept", "g0_hits", "g0_chains", "l0_hits", "l0_strands",
                                           "n_fine_hits", "n_fine_windows")] + [("ms_fine", C.c_double)] + \
-               [(n, C.c_uint64) for n in ("fit_chains", "fit_points", "n_filter")]
+               [(n, C.c_uint64) for n in ("fit_chains", "fit_points", "n_filter", "l0_points")]
 
     def as_dict(self):
         d = {n: getattr(self, n) for n, _ in self._fields_ if not n.startswith("kernel_")}
