@@ -107,7 +107,7 @@ def test_run_more_than_64_batches(tmp_path):
     bb = 128_000
     a, b = os.path.join(d, "many.coords"), os.path.join(d, "one.coords")
     st = pbgpu.run([gix], pb, a, aligners_per_device=2, batch_bases=bb)
-    st1 = pbgpu.run([gix], pb, b, aligners_per_device=1)
+    st1 = pbgpu.run([gix], pb, b, aligners_per_device=1, batch_bases=1 << 30)  # ramp start 2^27 > the input
     gix.close()
     assert st1["n_batches"] == 1 and st["n_bases"] == st1["n_bases"]
     assert st["n_batches"] > 64
