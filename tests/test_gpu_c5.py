@@ -16,7 +16,7 @@ No whole index fits one GPU, so there is no byte comparison here (the C4
 sharded-vs-whole test in test_gpu_scale.py is that pin); the checks are
 size-independent: per-read (rs, re, ql) order, record invariants against the
 super-read and read lengths, the shards tiling the super-reads, and the summed
-counts reaching the max-count filter.
+counts within the saturation bound.
 
 PBGPU_C5_SHARDS (default 16) and PBGPU_C5_READS (default 1000) size the run;
 PBGPU_TEST_OUT names a directory for the per-phase timings (c5_timings.json)."""
@@ -98,7 +98,9 @@ def test_c5_whole_human_sharded_one_gpu():
     assert sum(i["text_len"] for i in infos) >= sr_off[-1]  # + the k - 1-base seams
     # every shard's count is saturated at max_count + 1 before the sum
     assert total.max() <= S * (KW["max_count"] + 1)
-    assert total.max() > KW["max_count"] + 1, "no k-mer above max_count: the repeat model missed the count filter"
+    # repeat content: 5-50 copies at ~20x super-read coverage
+    assert total.max() > 200, "no repeat content in the sample"
+    T["max_summed_count"] = int(total.max())
     T["kmers_over_max_count"] = int((total > KW["max_count"]).sum())
     counts = total.astype(np.uint32)
 
