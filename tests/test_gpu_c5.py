@@ -22,6 +22,7 @@ PBGPU_C5_SHARDS (default 16) and PBGPU_C5_READS (default 1000) size the run;
 PBGPU_TEST_OUT names a directory for the per-phase timings (c5_timings.json)."""
 import json
 import os
+import threading
 import time
 
 import numpy as np
@@ -32,27 +33,48 @@ from tests.test_gpu_scale import _check_invariants, check_records
 
 pytestmark = pytest.mark.gpu
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 KW = dict(k=17, forward=True, unitigs_k=31, bases_matching=15.0, max_count=5000, stretch_cap=10000.0)
 
 
 def test_c5_whole_human_sharded_one_gpu():
-    from pacbio_amd import pbgpu
-    from tools.synth import Dataset
     S = int(os.environ.get("PBGPU_C5_SHARDS", "16"))
     n_reads = int(os.environ.get("PBGPU_C5_READS", "1000"))
     threads = int(os.environ.get("OMP_NUM_THREADS", "16"))
     T = {"shards": S, "reads": n_reads, "threads": threads}
     t0 = time.time()
-    out = os.environ.get("PBGPU_TEST_OUT")
-    if out:
-        os.makedirs(out, exist_ok=True)
+    # progress and a heartbeat every 20 s into gpurun_out/ (or PBGPU_TEST_OUT): pytest
+    # holds the test's own output, and a GPU run silent for minutes is taken to be hung
+    out = os.environ.get("PBGPU_TEST_OUT") or os.path.join(ROOT, "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    plog = os.path.join(out, "c5_progress.log")
+    last = ["start"]
 
-    def progress(msg):  # a long run shows it is alive
+    def progress(msg):
+        last[0] = msg
         line = f"{time.time() - t0:8.1f}s {msg}"
         print(line, flush=True)
-        if out:
-            with open(os.path.join(out, "c5_progress.log"), "a") as f:
-                f.write(line + "\n")
+        with open(plog, "a") as f:
+            f.write(line + "\n")
+    done = threading.Event()
+
+    def heartbeat():
+        while not done.wait(20):
+            with open(plog, "a") as f:
+                f.write(f"{time.time() - t0:8.1f}s ... ({last[0]})\n")
+    hb = threading.Thread(target=heartbeat, daemon=True)
+    hb.start()
+    try:
+        _run(S, n_reads, threads, T, t0, out, progress)
+    finally:
+        done.set()
+        hb.join()
+
+
+def _run(S, n_reads, threads, T, t0, out, progress):
+    from pacbio_amd import pbgpu
+    from tools.synth import Dataset
     progress("generating C5")
     ds = Dataset("C5", seed=42, threads=threads, n_pb=n_reads)
     T["generate_s"] = time.time() - t0
@@ -135,9 +157,8 @@ def test_c5_whole_human_sharded_one_gpu():
     names_ix.close()
     T["records"] = int(merged.n_records)
     T["total_s"] = time.time() - t0
-    if out:
-        with open(os.path.join(out, "c5_timings.json"), "w") as f:
-            json.dump(T, f, indent=1)
+    with open(os.path.join(out, "c5_timings.json"), "w") as f:
+        json.dump(T, f, indent=1)
     print(json.dumps({k: v for k, v in T.items() if k != "shard_info"}))
 
     assert_read_order(text, "C5")
