@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PBGPU_ABI_VERSION 3
+#define PBGPU_ABI_VERSION 4
 
 typedef enum pbgpu_status {
   PBGPU_OK = 0,
@@ -268,6 +268,8 @@ pbgpu_status pbgpu_aligner_set_hit_budget(pbgpu_aligner* al, uint64_t hits);
 typedef struct pbgpu_comm pbgpu_comm;
 pbgpu_status pbgpu_shard_counts(pbgpu_aligner* al, const pbgpu_reads* reads);
 pbgpu_status pbgpu_shard_counts_download(pbgpu_aligner* al, uint32_t* host, uint64_t n);
+/* upload: n = the batch's bases; also on an aligner that has not run
+ * pbgpu_shard_counts (a shard rebuilt for the alignment pass, SURVEY 8(e) on fewer GPUs than shards) */
 pbgpu_status pbgpu_shard_counts_upload(pbgpu_aligner* al, const uint32_t* host, uint64_t n);
 /* RCCL: rank 0 makes the 128-byte id, the caller hands it to every rank (any
  * host channel), each rank creates its communicator on its aligner's device. */

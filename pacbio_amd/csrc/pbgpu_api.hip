@@ -101,18 +101,18 @@ using namespace pbgpu;
 thread_local std::string g_err;
 // ------------------------------------------------------------------ names
 // super_read_name::parse (super_read_name.cc:74-90) -> unitig ids + oris
-static void parse_unitigs(const std::string& name, std::vector<uint32_t>& id, std::vector<uint8_t>& ori) {
+static void parse_unitigs(std::string_view name, std::vector<uint32_t>& id, std::vector<uint8_t>& ori) {
   id.clear(); ori.clear();
   if (name.empty()) return;
   size_t pn = 0;
   for (;;) {
     size_t us = name.find('_', pn);
-    const char* s = name.c_str() + pn;
+    const char* s = name.data() + pn;  // NUL-terminated (NameTable)
     char* end;
     errno = 0;
     unsigned long v = strtoul(s, &end, 10);
     if (end == s || errno == ERANGE) { id.clear(); ori.clear(); return; }
-    const char oc = us != std::string::npos ? name[us - 1] : name[name.size() - 1];
+    const char oc = us != std::string_view::npos ? name[us - 1] : name[name.size() - 1];
     id.push_back((uint32_t)v & 0x7fffffffu);
     ori.push_back(oc == 'R');
     if (us == std::string::npos) break;
@@ -149,7 +149,7 @@ struct text_builder {
   std::vector<uint64_t> words;  // MSB-first
   uint64_t n = 0;
   std::vector<uint64_t> starts{0};
-  std::vector<std::string> names;
+  NameTable names;
   int threads = 1;              // host threads for the names and the slice packer
   // Set (instead of filling `words`) by the pointer path: packs bases [b0, b0 + L)
   // of the text into `out` (L / 32 + 2 zeroed words), so that a shard packs its own
@@ -172,7 +172,7 @@ struct text_builder {
     uint64_t c = 0;
     for (size_t i = fast; i < len; ++i) put(c = tail_code(s[i], c));
   }
-  void end_record(const std::string& header, uint64_t start) {
+  void end_record(std::string_view header, uint64_t start) {
     if (n > start) { names.push_back(header); starts.push_back(n); }
   }
 };
@@ -190,7 +190,7 @@ static void load_fasta(const char* path, text_builder& tb) {
       std::getline(is, line);
       tb.add_line(line.data(), line.size());
     }
-    tb.end_record(header.substr(1), start);
+    tb.end_record(std::string_view(header).substr(1), start);
   }
 }
 
@@ -476,31 +476,42 @@ static void build_device_index(pbgpu_index* ix, text_builder& tb) {
   ix->gstart = tb.starts;
   // names, bwd names (frag_info.hpp:22-35), unitig ids -- of every super-read (host)
   ix->name_fwd = std::move(tb.names);
-  ix->name_bwd.resize(ix->n_sr);
-  // unitig ids and reversed names, in parallel over ranges of super-reads (50M names at C5)
+  // unitig ids and reversed names (frag_info.hpp:22-35), in parallel over ranges of
+  // super-reads (50M names at C5): each range builds its own id list and name blob,
+  // then the ranges are laid end to end
   std::vector<uint32_t> uoff(ix->n_sr + 1, 0), uids;
   {
     const uint64_t nsr = ix->n_sr, nparts = std::max<uint64_t>(1, std::min<uint64_t>(nsr, (uint64_t)tb.threads * 8));
     std::vector<std::vector<uint32_t>> pids(nparts);
+    std::vector<std::vector<char>> pblob(nparts);
+    std::vector<uint64_t>& boff = ix->name_bwd.off;
+    boff.assign(nsr + 1, 0);
     std::atomic<uint64_t> next(0);
     run_parallel(tb.threads, [&]() {
       std::vector<uint32_t> id;
       std::vector<uint8_t> ori;
+      char num[16];
       for (uint64_t q; (q = next.fetch_add(1)) < nparts;) {
+        std::vector<char>& b = pblob[q];
         for (uint64_t i = nsr * q / nparts; i < nsr * (q + 1) / nparts; ++i) {
-          parse_unitigs(ix->name_fwd[i], id, ori);
+          const std::string_view fw = ix->name_fwd[i];
+          parse_unitigs(fw, id, ori);
           uoff[i] = (uint32_t)id.size();  // count; offsets below
           pids[q].insert(pids[q].end(), id.begin(), id.end());
+          const size_t b0 = b.size();
           if (!id.empty()) {
-            std::string b;
             for (size_t t = 0; t < id.size(); ++t) {
               const size_t s = id.size() - 1 - t;
-              b += (t ? "_" : "") + std::to_string(id[s]) + (ori[s] ? 'F' : 'R');
+              if (t) b.push_back('_');
+              const int w = snprintf(num, sizeof num, "%u", id[s]);
+              b.insert(b.end(), num, num + w);
+              b.push_back(ori[s] ? 'F' : 'R');
             }
-            ix->name_bwd[i] = std::move(b);
           } else {
-            ix->name_bwd[i] = ix->name_fwd[i];
+            b.insert(b.end(), fw.begin(), fw.end());
           }
+          b.push_back(0);
+          boff[i + 1] = b.size() - b0;  // length + NUL; offsets below
         }
       }
     });
@@ -510,6 +521,17 @@ static void build_device_index(pbgpu_index* ix, text_builder& tb) {
     uoff[nsr] = (uint32_t)tot;
     uids.reserve(tot);
     for (auto& v : pids) { uids.insert(uids.end(), v.begin(), v.end()); std::vector<uint32_t>().swap(v); }
+    for (uint64_t i = 0; i < nsr; ++i) boff[i + 1] += boff[i];
+    ix->name_bwd.blob.resize(boff[nsr]);
+    std::vector<uint64_t> pstart(nparts + 1, 0);
+    for (uint64_t q = 0; q < nparts; ++q) pstart[q + 1] = pstart[q] + pblob[q].size();
+    next = 0;
+    run_parallel(tb.threads, [&]() {
+      for (uint64_t q; (q = next.fetch_add(1)) < nparts;) {
+        if (!pblob[q].empty()) memcpy(ix->name_bwd.blob.data() + pstart[q], pblob[q].data(), pblob[q].size());
+        std::vector<char>().swap(pblob[q]);
+      }
+    });
   }
   if (!tb.pack_slice) tb.words.resize(tb.n / 32 + 2, 0);
   // This device's super-reads: all of them, or shard `shard` of n_shards -- the
@@ -737,13 +759,22 @@ pbgpu_status pbgpu_index_build(const char* const* names, const char* const* seqs
   for (size_t i = 0; i < n; ++i)
     if (lens[i]) { rec.push_back(i); tb.starts.push_back(tb.starts.back() + lens[i]); }
   tb.n = tb.starts.back();
-  tb.names.resize(rec.size());
-  {
-    std::atomic<uint64_t> next(0);
+  {  // the names into one blob: lengths, offsets, then parallel copies
     const uint64_t nr = rec.size(), chunk = 1 << 16;
+    std::vector<uint64_t>& no = tb.names.off;
+    no.assign(nr + 1, 0);
+    std::atomic<uint64_t> next(0);
     run_parallel(tb.threads, [&]() {
       for (uint64_t c; (c = next.fetch_add(chunk)) < nr;)
-        for (uint64_t i = c; i < std::min(nr, c + chunk); ++i) tb.names[i] = names[rec[i]];
+        for (uint64_t i = c; i < std::min(nr, c + chunk); ++i) no[i + 1] = strlen(names[rec[i]]) + 1;
+    });
+    for (uint64_t i = 0; i < nr; ++i) no[i + 1] += no[i];
+    tb.names.blob.resize(no[nr]);
+    next = 0;
+    run_parallel(tb.threads, [&]() {
+      for (uint64_t c; (c = next.fetch_add(chunk)) < nr;)
+        for (uint64_t i = c; i < std::min(nr, c + chunk); ++i)
+          memcpy(tb.names.blob.data() + no[i], names[rec[i]], no[i + 1] - no[i]);
     });
   }
   const std::vector<uint64_t>& gs = tb.starts;
@@ -909,8 +940,10 @@ pbgpu_status pbgpu_index_save(const pbgpu_index* ix, const char* path, const cha
                            ix->f_buckets, ix->f_kmers, ix->f_occ};
     cf.put_u64(sizeof(sc) / 8);
     cf.put(sc, sizeof(sc));
-    cf.put_u64(ix->name_fwd.size());
-    for (size_t i = 0; i < ix->name_fwd.size(); ++i) { cf.put_str(ix->name_fwd[i]); cf.put_str(ix->name_bwd[i]); }
+    for (const NameTable* t : {&ix->name_fwd, &ix->name_bwd}) {
+      cf.put_u64(t->off.size()); cf.put(t->off.data(), t->off.size() * 8);
+      cf.put_u64(t->blob.size()); cf.put(t->blob.data(), t->blob.size());
+    }
     cf.put_u64(ix->sr_start.size()); cf.put(ix->sr_start.data(), ix->sr_start.size() * 8);
     cf.put_u64(ix->gstart.size()); cf.put(ix->gstart.data(), ix->gstart.size() * 8);
     pinned_chunk pc;
@@ -952,10 +985,18 @@ pbgpu_status pbgpu_index_load(const char* path, int device, const char* tag, pbg
   ix->n_occ = sc[5]; ix->buckets = sc[6]; ix->filt_log2 = (uint32_t)sc[7]; ix->shard = (uint32_t)sc[8];
   ix->n_shards = (uint32_t)sc[9]; ix->sr_begin = sc[10]; ix->sr_end = sc[11]; ix->n_total = sc[12];
   ix->null_ptr = sc[13]; ix->fk = (uint32_t)sc[14]; ix->f_buckets = sc[15]; ix->f_kmers = sc[16]; ix->f_occ = sc[17];
-  const uint64_t nn = cf.get_u64();
-  if (nn > (1ull << 32)) return fail(PBGPU_ERR_IO, "'%s': corrupt index cache (names)", path);
-  ix->name_fwd.resize(nn); ix->name_bwd.resize(nn);
-  for (uint64_t i = 0; i < nn; ++i) { ix->name_fwd[i] = cf.get_str(1 << 24); ix->name_bwd[i] = cf.get_str(1 << 24); }
+  for (NameTable* t : {&ix->name_fwd, &ix->name_bwd}) {
+    const uint64_t no = cf.get_u64();
+    if (no == 0 || no > (1ull << 32)) return fail(PBGPU_ERR_IO, "'%s': corrupt index cache (names)", path);
+    t->off.resize(no); cf.get(t->off.data(), no * 8);
+    const uint64_t nb = cf.get_u64();
+    if (nb > (1ull << 40) || t->off[0] != 0 || t->off[no - 1] != nb)
+      return fail(PBGPU_ERR_IO, "'%s': corrupt index cache (names)", path);
+    t->blob.resize(nb); cf.get(t->blob.data(), nb);
+    for (uint64_t i = 0; i + 1 < no; ++i)  // increasing, each name NUL-terminated
+      if (t->off[i + 1] <= t->off[i] || t->blob[t->off[i + 1] - 1] != 0)
+        return fail(PBGPU_ERR_IO, "'%s': corrupt index cache (names)", path);
+  }
   uint64_t m = cf.get_u64();
   if (m > (1ull << 34)) return fail(PBGPU_ERR_IO, "'%s': corrupt index cache (starts)", path);
   ix->sr_start.resize(m); cf.get(ix->sr_start.data(), m * 8);
@@ -971,7 +1012,7 @@ pbgpu_status pbgpu_index_load(const char* path, int device, const char* tag, pbg
   // the scalars the kernels index with must agree with the array sizes (a corrupt but
   // untruncated file must not lead to out-of-bounds device reads)
   const bool fine = ix->fk != 0;
-  if (ix->name_fwd.size() != ix->n_sr || ix->gstart.size() != ix->n_sr + 1 || ix->sr_begin > ix->sr_end ||
+  if (ix->name_fwd.size() != ix->n_sr || ix->name_bwd.size() != ix->n_sr || ix->gstart.size() != ix->n_sr + 1 || ix->sr_begin > ix->sr_end ||
       ix->sr_end > ix->n_sr || ix->sr_start.size() != ix->sr_end - ix->sr_begin + 1 ||
       ix->d_sr_start.n != ix->sr_start.size() || ix->table.n != 4 * ix->buckets || ix->buckets == 0 ||
       (ix->buckets & (ix->buckets - 1)) != 0 || ix->filt.n != (ix->filt_log2 ? 1ull << ix->filt_log2 : 0) ||
@@ -996,7 +1037,7 @@ pbgpu_status pbgpu_index_get_info(const pbgpu_index* ix, pbgpu_index_info* info)
 }
 const char* pbgpu_index_sr_name(const pbgpu_index* ix, uint32_t sr, int bwd) {
   if (!ix || sr >= ix->n_sr) return nullptr;
-  return bwd ? ix->name_bwd[sr].c_str() : ix->name_fwd[sr].c_str();
+  return bwd ? ix->name_bwd.c_str(sr) : ix->name_fwd.c_str(sr);
 }
 uint32_t pbgpu_index_sr_len(const pbgpu_index* ix, uint32_t sr) {
   if (!ix || sr >= ix->n_sr) return 0;
@@ -1213,9 +1254,12 @@ pbgpu_status pbgpu_shard_counts_download(pbgpu_aligner* al, uint32_t* host, uint
 
 pbgpu_status pbgpu_shard_counts_upload(pbgpu_aligner* al, const uint32_t* host, uint64_t n) {
   if (!al || (!host && n)) return fail(PBGPU_ERR_INVALID, "null argument");
-  if (n != al->gcount_n) return fail(PBGPU_ERR_INVALID, "count buffer holds %llu entries", (unsigned long long)al->gcount_n);
   API_TRY
   HIPCHK(hipSetDevice(al->ix->device));
+  // a fresh aligner (the shard rebuilt for the alignment pass) takes the summed counts
+  // without computing its own first; pbgpu_align_resident_shard checks n against the batch
+  al->gcount.ensure(n + 1);
+  al->gcount_n = n;
   if (n) HIPCHK(hipMemcpy(al->gcount.p, host, n * 4, hipMemcpyHostToDevice));
   return PBGPU_OK;
   API_CATCH

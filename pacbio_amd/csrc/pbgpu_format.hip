@@ -102,7 +102,7 @@ static void ensure_device_names(const pbgpu_index* cix) {
   pbgpu_index* ix = const_cast<pbgpu_index*>(cix);  // lazily built cache; guarded by names_mu
   std::lock_guard<std::mutex> lk(ix->names_mu);
   if (ix->names_ready) return;
-  auto up = [&](const std::vector<std::string>& v, dbuf<char>& blob, dbuf<uint64_t>& off) {
+  auto up = [&](const NameTable& v, dbuf<char>& blob, dbuf<uint64_t>& off) {
     // names of this device's super-reads (local ids [sr_begin, sr_end))
     std::vector<uint64_t> o(ix->sr_end - ix->sr_begin + 1, 0);
     for (uint64_t i = ix->sr_begin; i < ix->sr_end; ++i) o[i - ix->sr_begin + 1] = o[i - ix->sr_begin] + v[i].size();

@@ -13,6 +13,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <string_view>
 #include <thread>
 #include <vector>
 
@@ -46,6 +47,22 @@ struct hip_error : std::runtime_error {
     }                                                                                                  \
   } while (0)
 struct bad_input : std::runtime_error { using std::runtime_error::runtime_error; };
+
+// n strings in one allocation: string i is blob[off[i], off[i + 1] - 1), NUL-terminated
+// (50M super-read names at C5: one blob frees at once, 100M std::strings did not)
+struct NameTable {
+  std::vector<char> blob;
+  std::vector<uint64_t> off{0};
+  size_t size() const { return off.size() - 1; }
+  std::string_view operator[](size_t i) const { return std::string_view(blob.data() + off[i], off[i + 1] - off[i] - 1); }
+  const char* c_str(size_t i) const { return blob.data() + off[i]; }
+  void push_back(const char* s, size_t n) {
+    blob.insert(blob.end(), s, s + n);
+    blob.push_back(0);
+    off.push_back(blob.size());
+  }
+  void push_back(std::string_view s) { push_back(s.data(), s.size()); }
+};
 struct pbgpu_comm {  // an RCCL communicator of the sharded-index count exchange
   ncclComm_t comm = nullptr;
   int device = 0;
@@ -125,7 +142,7 @@ struct pbgpu_index {
   uint32_t k = 0, psa_min = 0;
   uint64_t n = 0, n_sr = 0, n_kmers = 0, n_occ = 0, buckets = 0;
   double build_seconds = 0;
-  std::vector<std::string> name_fwd, name_bwd;
+  NameTable name_fwd, name_bwd;
   std::vector<uint64_t> sr_start;            // host copy
   dbuf<uint64_t> text, d_sr_start, occ;
   dbuf<ulonglong2> table;

@@ -21,7 +21,7 @@ namespace pbgpu {
 // Version of the device index layout above (bucket hash, presence-filter hash,
 // header packing, element sizes).  Bump it with any change to them: the on-disk
 // index cache (pbgpu_index_save / load) refuses files of another layout.
-constexpr uint32_t kIndexLayout = 2;
+constexpr uint32_t kIndexLayout = 3;
 
 constexpr uint64_t EMPTY_KEY = ~0ull;
 constexpr uint32_t SAT_COUNT = 0xFFFFFFu;

@@ -108,11 +108,13 @@ def _run(S, n_reads, threads, T, t0, out, progress):
         rd.close()
         al.close()
         t_count.append(time.time() - t)
-        progress(f"pass 1 shard {s}: build {tb:.1f}s, counts {t_count[-1]:.1f}s, {infos[-1]['device_bytes'] / 1e9:.1f} GB")
+        t = time.time()
         if s == S - 1:
             keep = ix  # still resident: pass 2 starts with it
         else:
             ix.close()
+        progress(f"pass 1 shard {s}: build {tb:.1f}s, counts {t_count[-1]:.1f}s, free {time.time() - t:.1f}s, "
+                 f"{infos[-1]['device_bytes'] / 1e9:.1f} GB")
     T["pass1_build_s"], T["pass1_count_s"] = t_build1, t_count
     T["shard_info"] = [{k: v for k, v in i.items()} for i in infos]
     assert infos[0]["sr_begin"] == 0 and infos[-1]["sr_end"] == 50_000_000
