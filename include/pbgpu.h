@@ -383,6 +383,17 @@ typedef struct {
                       const char* const* read_names, const uint64_t* read_lens, uint64_t* text_len,
                       char** side_text, uint64_t* side_len, int* status);
   void* records_user;
+  /* Part files (0 or 1 = one file).  With P > 1 the output goes to P files
+   * <coords_path>.0 .. .<P-1> (and <details_path>.p), each with its own reader,
+   * aligners and writer thread: part p holds the reads whose FASTA header
+   * starts in [p T / P, (p + 1) T / P) of the concatenated input files (T
+   * bytes), so the parts concatenated are the one-file output -- the
+   * reference's split-and-cat (mega_reads_assemble_cluster2.sh:325-354,447) in
+   * one process, without the single writer's page-cache ceiling.  The aligners
+   * are split between the parts in order (part p: aligners [p W / P, (p + 1)
+   * W / P) of the W, so with one index per part each part runs on its own
+   * device).  Plain FASTA input only; fixed at pbgpu_runner_create. */
+  uint32_t n_parts;
 } pbgpu_run_params;
 
 typedef struct {

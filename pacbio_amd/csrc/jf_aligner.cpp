@@ -10,7 +10,9 @@
 // -F runs the fine aligner on the device after the coarse one.
 // GPU-only options: --devices 0,1,.. (default 0; a device may repeat),
 // --streams (aligners per device), --batch-bases, --timing (stage times on
-// stderr as one JSON line).
+// stderr as one JSON line), --parts P (coords in P part files <coords>.0 ..
+// .P-1 written in parallel, whose concatenation is the one-file output; the
+// reference's split-and-cat, mega_reads_assemble_cluster2.sh:325-354,447).
 #include <getopt.h>
 
 #include <algorithm>
@@ -101,11 +103,11 @@ int main(int argc, char** argv) {
   std::vector<const char*> srs, pbs;
   std::vector<int> devices;
   uint64_t batch_bases = 64ull << 20;
-  uint32_t streams = 2;
+  uint32_t streams = 2, parts = 0;
   bool timing = false;
   const char* index_cache = nullptr;  // --index-cache PATH (index_cache.h)
   enum { O_PSA = 256, O_SC, O_SF, O_CAP, O_WIN, O_DETAILS, O_COORDS, O_MAXM, O_MAXC, O_COMPACT, O_NOCOMPACT, O_DEV, O_BATCH,
-         O_STREAMS, O_DEVS, O_TIMING, O_CACHE };
+         O_STREAMS, O_DEVS, O_TIMING, O_CACHE, O_PARTS };
   static struct option lo[] = {
       {"size", 1, 0, 's'}, {"mer", 1, 0, 'm'}, {"fine-mer", 1, 0, 'F'}, {"psa-min", 1, 0, O_PSA},
       {"threads", 1, 0, 't'}, {"stretch-constant", 1, 0, O_SC}, {"stretch-factor", 1, 0, O_SF},
@@ -116,7 +118,8 @@ int main(int argc, char** argv) {
       {"unitigs-sequences", 1, 0, 'u'}, {"compact", 0, 0, O_COMPACT}, {"no-compact", 0, 0, O_NOCOMPACT},
       {"k-mer", 1, 0, 'k'}, {"superreads", 1, 0, 'r'}, {"pacbio", 1, 0, 'p'},
       {"device", 1, 0, O_DEV}, {"devices", 1, 0, O_DEVS}, {"batch-bases", 1, 0, O_BATCH},
-      {"streams", 1, 0, O_STREAMS}, {"timing", 0, 0, O_TIMING}, {"index-cache", 1, 0, O_CACHE}, {0, 0, 0, 0}};
+      {"streams", 1, 0, O_STREAMS}, {"timing", 0, 0, O_TIMING}, {"index-cache", 1, 0, O_CACHE},
+      {"parts", 1, 0, O_PARTS}, {0, 0, 0, 0}};
   int c;
   while ((c = getopt_long(argc, argv, "s:m:F:t:fB:M:H0l:u:k:r:p:", lo, nullptr)) != -1) {
     switch (c) {
@@ -159,6 +162,7 @@ int main(int argc, char** argv) {
     }
     case O_TIMING: timing = true; break;
     case O_CACHE: index_cache = optarg; break;
+    case O_PARTS: parts = parse_u32(optarg, "--parts"); break;
     case O_BATCH: batch_bases = parse_suffix(optarg); break;
     case O_STREAMS: streams = std::max(1u, parse_u32(optarg, "--streams")); break;
     default: die("bad option (see jf_aligner_cmdline.yaggo)");
@@ -208,6 +212,8 @@ int main(int argc, char** argv) {
   rp.aligners_per_device = streams;
   rp.batch_bases = batch_bases;
   rp.host_threads = (int)threads;
+  rp.n_parts = parts;
+  if (parts > 1 && !coords_path) die("--parts needs --coords");
   pbgpu_run_stats st{};
   const pbgpu_status rs = pbgpu_run(per_entry.data(), per_entry.size(), &ap, &rp, &st);
   const std::string err = rs == PBGPU_OK ? "" : pbgpu_last_error();

@@ -19,9 +19,11 @@
 #include <fcntl.h>
 #include <pthread.h>
 #include <sched.h>
+#include <sys/stat.h>
 #include <unistd.h>
 #include <zlib.h>
 
+#include <atomic>
 #include <cctype>
 #include <chrono>
 #include <condition_variable>
@@ -45,15 +47,18 @@ struct RunState {
   pbgpu_status status = PBGPU_OK;
   std::string msg;
   std::condition_variable* cvs[4] = {};
+  std::atomic<bool>* any_stop = nullptr;  // shared by the parts of a run: one failure stops them all
   void fail(pbgpu_status s, const std::string& m) {
     {
       std::lock_guard<std::mutex> lk(mu);
       if (status == PBGPU_OK) { status = s; msg = m; }
       stop = true;
     }
+    if (any_stop) any_stop->store(true);
     for (auto* cv : cvs) if (cv) cv->notify_all();
   }
   bool stopped() {
+    if (any_stop && any_stop->load()) return true;
     std::lock_guard<std::mutex> lk(mu);
     return stop;
   }
@@ -111,10 +116,27 @@ struct PinnedVec {  // growable pinned byte buffer (H2D at full PCIe rate, no st
 
 // ------------------------------------------------------------ input
 // Lines of a sequence of files: plain files by read(), gzip (magic 1f 8b) by zlib.
+// With a byte range [begin, ...) over the concatenation of plain files, the
+// source starts at the first line that begins at or after `begin`; line_off()
+// is the global offset of the last line returned (part files, pbgpu_run_params.n_parts).
 class LineSource {
  public:
-  explicit LineSource(const std::vector<std::string>& paths) : paths_(paths) { buf_.resize(1 << 24); }
+  explicit LineSource(const std::vector<std::string>& paths, uint64_t begin = 0, bool ranged = false)
+      : paths_(paths), begin_(begin) {
+    buf_.resize(1 << 24);
+    if (ranged) {
+      uint64_t b = 0;
+      for (const auto& p : paths_) { base_of_.push_back(b); b += file_size(p); }
+      // whole files before `begin` are skipped
+      while (fi_ < paths_.size() && (fi_ + 1 >= paths_.size() ? b : base_of_[fi_ + 1]) <= begin_) ++fi_;
+    }
+  }
   ~LineSource() { close_cur(); }
+  static uint64_t file_size(const std::string& path) {
+    struct stat st {};
+    if (stat(path.c_str(), &st) != 0) throw bad_input("Can't open PacBio file '" + path + "'");
+    return (uint64_t)st.st_size;
+  }
   // next line without its '\n' (pointer valid until the next call); false at
   // the end of the current file -- next_file() then opens the next one
   bool line(const char*& p, size_t& len) {
@@ -122,6 +144,7 @@ class LineSource {
       if (pos_ < end_) {
         const char* s = buf_.data() + pos_;
         const char* nl = (const char*)memchr(s, '\n', end_ - pos_);
+        line_off_ = file_base_ + buf_off_ + pos_;
         if (nl) {
           p = s; len = (size_t)(nl - s);
           pos_ += len + 1;
@@ -138,22 +161,36 @@ class LineSource {
       fill();
     }
   }
+  uint64_t line_off() const { return line_off_; }
   bool next_file() {
     close_cur();
     if (fi_ >= paths_.size()) return false;
-    const std::string& path = paths_[fi_++];
+    const std::string& path = paths_[fi_];
+    file_base_ = base_of_.empty() ? 0 : base_of_[fi_];
+    ++fi_;
     fd_ = open(path.c_str(), O_RDONLY);
     if (fd_ < 0) throw bad_input("Can't open PacBio file '" + path + "'");
     unsigned char mg[2] = {0, 0};
     const ssize_t m = pread(fd_, mg, 2, 0);
+    pos_ = end_ = 0;
+    buf_off_ = 0;
+    eof_ = false;
     if (m == 2 && mg[0] == 0x1f && mg[1] == 0x8b) {
+      if (begin_ || !base_of_.empty()) throw unsupported("part files need plain (not gzip) PacBio input");
       gz_ = gzdopen(fd_, "rb");
       if (!gz_) throw bad_input("Can't open gzip PacBio file '" + path + "'");
       fd_ = -1;  // owned by gz_
       gzbuffer(gz_, 1 << 20);
     }
-    pos_ = end_ = 0;
-    eof_ = false;
+    if (begin_ > file_base_) {  // the range starts inside this file: from the line after offset begin - 1
+      const uint64_t at = begin_ - file_base_ - 1;
+      if (lseek(fd_, (off_t)at, SEEK_SET) < 0) throw bad_input("seek failed in PacBio file '" + path + "'");
+      buf_off_ = at;
+      const char* p;
+      size_t len;
+      line(p, len);  // the rest of the line holding byte begin - 1 (empty if it is a '\n')
+    }
+    begin_ = 0;  // later files are read whole
     return true;
   }
 
@@ -165,6 +202,7 @@ class LineSource {
   void fill() {
     if (pos_ > 0) {  // keep the partial line at the front
       memmove(buf_.data(), buf_.data() + pos_, end_ - pos_);
+      buf_off_ += pos_;
       end_ -= pos_;
       pos_ = 0;
     }
@@ -185,6 +223,9 @@ class LineSource {
     end_ += (size_t)got;
   }
   std::vector<std::string> paths_;
+  uint64_t begin_ = 0;
+  std::vector<uint64_t> base_of_;  // global offset of each file (range mode)
+  uint64_t file_base_ = 0, buf_off_ = 0, line_off_ = 0;  // current file's offset, file offset of buf_[0]
   size_t fi_ = 0;
   int fd_ = -1;
   gzFile gz_ = nullptr;
@@ -212,10 +253,23 @@ struct Batch {
 // whole_sequence_parser semantics (jellyfish 2.x, as used at jf_aligner.cc:206-207):
 // FASTA header = line after '>', sequence = the following lines concatenated;
 // FASTQ '@' header, one sequence line, '+' line, quality line.
+// With a range [begin, end) (part files): the reads whose FASTA header line
+// starts in it.
 class ReadParser {
  public:
-  ReadParser(const std::vector<std::string>& paths, bool keep_headers) : src_(paths), keep_(keep_headers) {
+  ReadParser(const std::vector<std::string>& paths, bool keep_headers, uint64_t begin = 0, uint64_t end = ~0ull)
+      : src_(paths, begin, begin != 0 || end != ~0ull), keep_(keep_headers), end_(end), ranged_(begin != 0 || end != ~0ull) {
     open_ = src_.next_file();
+    if (ranged_) {  // skip to the first header of the range (FASTA only)
+      const char* p;
+      size_t len;
+      for (;;) {
+        while (open_ && !src_.line(p, len)) open_ = src_.next_file();
+        if (!open_) break;
+        if (len && p[0] == '@') throw unsupported("part files need FASTA PacBio input (a FASTQ record start is ambiguous)");
+        if (len && p[0] == '>') { pending_.assign(p, len); pending_off_ = src_.line_off(); have_pending_ = true; break; }
+      }
+    }
   }
   // appends up to ~batch_bases bases worth of reads; false when nothing was added
   bool fill(Batch& b, uint64_t batch_bases) {
@@ -229,24 +283,29 @@ class ReadParser {
   bool one(Batch& b) {
     const char* p;
     size_t len;
+    uint64_t hoff;
     if (have_pending_) {
       have_pending_ = false;
       hdr_.swap(pending_);
+      hoff = pending_off_;
     } else {
       do {
         if (!src_.line(p, len)) return false;
       } while (len == 0);
       hdr_.assign(p, len);
+      hoff = src_.line_off();
     }
+    if (ranged_ && hoff >= end_) { open_ = false; return false; }  // the next part's read
     const char c0 = hdr_[0];
     if (c0 != '>' && c0 != '@') throw bad_input("PacBio input is neither FASTA nor FASTQ");
+    if (ranged_ && c0 == '@') throw unsupported("part files need FASTA PacBio input (a FASTQ record start is ambiguous)");
     if (c0 == '@') {
       if (src_.line(p, len)) b.seq.append(p, len);
       src_.line(p, len);  // '+'
       src_.line(p, len);  // quality
     } else {
       while (src_.line(p, len)) {
-        if (len && p[0] == '>') { pending_.assign(p, len); have_pending_ = true; break; }
+        if (len && p[0] == '>') { pending_.assign(p, len); pending_off_ = src_.line_off(); have_pending_ = true; break; }
         b.seq.append(p, len);
       }
     }
@@ -260,8 +319,11 @@ class ReadParser {
   }
   LineSource src_;
   bool keep_;
+  uint64_t end_;
+  bool ranged_;
   bool open_ = false;
   bool have_pending_ = false;
+  uint64_t pending_off_ = 0;
   std::string hdr_, pending_;
 };
 
@@ -452,6 +514,14 @@ struct RecordsView {
   }
 };
 
+// One output file's pipeline: its aligners (indices into the runner's), its
+// batch buffers and pinned text pool (aligners + 2 each, recycled).
+struct RunPart {
+  std::vector<size_t> al;
+  std::vector<std::unique_ptr<Batch>> batches;
+  std::unique_ptr<TextPool> texts;
+};
+
 struct pbgpu_runner {
   std::vector<pbgpu_aligner*> al;
   std::vector<std::unique_ptr<RecordsView>> views;  // per aligner (records consumer runs)
@@ -459,45 +529,28 @@ struct pbgpu_runner {
   bool details = false;
   bool side = false;  // a second output file (details, or the records consumer's side text)
   uint64_t batch_bases = 0;
-  std::vector<std::unique_ptr<Batch>> batches;  // W + 2, recycled
-  std::unique_ptr<TextPool> texts;              // W + 2
-  std::mutex run_mu;                            // one run at a time
+  std::vector<RunPart> parts;  // one, or n_parts (part files)
+  std::mutex run_mu;           // one run at a time
   ~pbgpu_runner() {
     rd.clear();
     for (auto* a : al) pbgpu_aligner_free(a);
   }
 };
 
-static void runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_stats* stats) {
-  std::lock_guard<std::mutex> run_lock(R->run_mu);
-  const double t_start = now_s();
-  pbgpu_run_stats S{};
+// One part's pipeline (all of the run unless part files): reader over the
+// part's input range, its aligners' workers, the writer of its file(s).
+static void run_part(pbgpu_runner* R, RunPart& part, const pbgpu_run_params* run, const std::vector<std::string>& paths,
+                     uint64_t range_begin, uint64_t range_end, int cfd, int dfd, bool write_header, RunState& rs,
+                     pbgpu_run_stats& S) {
   const bool details = R->details;
   const uint64_t batch_bases = R->batch_bases;
   const int hthreads = run->host_threads > 0 ? run->host_threads
                                              : (int)std::max(1u, std::thread::hardware_concurrency());
-  // outputs first (early error reporting, jf_aligner.cc:170-178)
-  int cfd = 1, dfd = -1;
-  if (run->coords_path) {
-    cfd = open(run->coords_path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
-    if (cfd < 0) throw bad_input(std::string("Failed to open coords file '") + run->coords_path + "': " + strerror(errno));
-  }
-  struct fd_guard { int& fd; ~fd_guard() { if (fd > 2) close(fd); } } cg{cfd};
-  if (R->side) {
-    dfd = open(run->details_path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
-    if (dfd < 0) throw bad_input(std::string("Failed to open details file '") + run->details_path + "': " + strerror(errno));
-  }
-  struct fd_guard2 { int& fd; ~fd_guard2() { if (fd > 2) close(fd); } } dg{dfd};
-  S.open_seconds = now_s() - t_start;
-  std::vector<std::string> paths;
-  for (size_t i = 0; i < run->n_pb_paths; ++i) paths.emplace_back(run->pb_paths[i]);
-  const size_t W = R->al.size();
-
-  RunState rs;
+  const size_t W = part.al.size();
   Queue<Batch*> inq(W + 1, rs, 0);
-  Queue<Batch*> freeq(R->batches.size() + 1, rs, 3);
-  for (auto& b : R->batches) freeq.push(b.get());
-  R->texts->start(&rs);
+  Queue<Batch*> freeq(part.batches.size() + 1, rs, 3);
+  for (auto& b : part.batches) freeq.push(b.get());
+  part.texts->start(&rs);
   std::mutex dmu;
   std::condition_variable dcv;
   rs.cvs[2] = &dcv;
@@ -512,7 +565,7 @@ static void runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_s
                                                       : (64ull << 20);
   auto reader = [&]() {
     try {
-      ReadParser rp(paths, details);
+      ReadParser rp(paths, details, range_begin, range_end);
       for (uint64_t id = 0;; ++id) {
         Batch* b = nullptr;
         if (!freeq.pop(b)) break;
@@ -543,7 +596,8 @@ static void runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_s
     inq.close();
   };
 
-  auto worker = [&](size_t wi) {
+  auto worker = [&](size_t pwi) {
+    const size_t wi = part.al[pwi];
     pbgpu_aligner* al = R->al[wi];
     pbgpu_reads* rd = R->rd[wi].get();
     try {
@@ -583,7 +637,7 @@ static void runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_s
           const uint64_t len = format_device_text(al, rd, run->compact, run->zero_match);
           HIPCHK(hipStreamSynchronize(al->st));
           t3 = now_s();
-          if (!R->texts->get(b->id, len + 1, d.text)) break;
+          if (!part.texts->get(b->id, len + 1, d.text)) break;
           t4 = now_s();
           if (len) HIPCHK(hipMemcpyAsync(d.text.p, al->text.p, len, hipMemcpyDeviceToHost, al->st));
           HIPCHK(hipStreamSynchronize(al->st));
@@ -631,11 +685,11 @@ static void runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_s
   // C2 coords out, interleaved A/B runs on two boxes: 1.32 Gbases/s mean over five
   // runs pinned, 1.25 unpinned (run-to-run spread ±10%).
   const char* wn = getenv("PBGPU_WRITER_NUMA");
-  const std::vector<int> writer_cpus = (!wn || atoi(wn)) ? gpu_node_cpus(R->al[0]->device) : std::vector<int>();
+  const std::vector<int> writer_cpus = (!wn || atoi(wn)) ? gpu_node_cpus(R->al[part.al[0]]->device) : std::vector<int>();
   auto writer = [&]() {
     pin_to(writer_cpus);
     try {
-      if (run->header && !run->records_fn) {
+      if (write_header && !run->records_fn) {
         std::string h = std::string("Rstart Rend Qstart Qend Nmers Rcons Qcons Rcover Qcover Rlen Qlen Stretch Offset Err") +
                         (run->compact ? "" : " Rname") + " Qname\n";
         write_all(cfd, h.data(), h.size(), "coords");
@@ -667,9 +721,9 @@ static void runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_s
         }
         if (d.mtext) {
           free(d.mtext);
-          R->texts->advance();
+          part.texts->advance();
         } else {
-          R->texts->put(d.text, true);
+          part.texts->put(d.text, true);
         }
       }
     } catch (...) {
@@ -694,25 +748,94 @@ static void runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_s
     std::lock_guard<std::mutex> lk(dmu);
     for (auto& kv : done) {
       if (kv.second.mtext) free(kv.second.mtext);
-      else R->texts->put(kv.second.text, false);
+      else part.texts->put(kv.second.text, false);
     }
     done.clear();
   }
-  if (rs.status != PBGPU_OK) {
-    switch (rs.status) {
-      case PBGPU_ERR_IO: throw bad_input(rs.msg);
-      case PBGPU_ERR_UNSUPPORTED: throw unsupported(rs.msg);
-      case PBGPU_ERR_NOMEM: throw std::bad_alloc();
-      default: throw std::runtime_error(rs.msg);
+}
+
+static void runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_stats* stats) {
+  std::lock_guard<std::mutex> run_lock(R->run_mu);
+  const double t_start = now_s();
+  const size_t P = R->parts.size();
+  // outputs first (early error reporting, jf_aligner.cc:170-178); part p writes
+  // <path>.p when there are several parts
+  std::vector<int> cfd(P, 1), dfd(P, -1);
+  struct fds_guard {
+    std::vector<int>& a; std::vector<int>& b;
+    ~fds_guard() { for (int f : a) if (f > 2) close(f); for (int f : b) if (f > 2) close(f); }
+  } fg{cfd, dfd};
+  auto part_path = [&](const char* p, size_t i) { return P > 1 ? std::string(p) + "." + std::to_string(i) : std::string(p); };
+  if (P > 1 && !run->coords_path) throw bad_input("part files need a coords path");
+  for (size_t i = 0; i < P; ++i) {
+    if (run->coords_path) {
+      const std::string cp = part_path(run->coords_path, i);
+      cfd[i] = open(cp.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+      if (cfd[i] < 0) throw bad_input("Failed to open coords file '" + cp + "': " + strerror(errno));
+    }
+    if (R->side) {
+      const std::string dp = part_path(run->details_path, i);
+      dfd[i] = open(dp.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+      if (dfd[i] < 0) throw bad_input("Failed to open details file '" + dp + "': " + strerror(errno));
     }
   }
-  if (cfd > 2) {
-    const double tc = now_s();
-    const int fd = cfd;
-    cfd = -1;
-    if (close(fd)) throw bad_input(std::string("closing the coords file failed: ") + strerror(errno));
-    S.close_seconds = now_s() - tc;
+  const double t_open = now_s() - t_start;
+  std::vector<std::string> paths;
+  for (size_t i = 0; i < run->n_pb_paths; ++i) paths.emplace_back(run->pb_paths[i]);
+  // part p: the reads whose header starts in [T p / P, T (p + 1) / P) of the inputs
+  uint64_t T = 0;
+  if (P > 1)
+    for (const auto& p : paths) T += LineSource::file_size(p);
+  std::atomic<bool> any_stop(false);
+  std::vector<std::unique_ptr<RunState>> rss;
+  std::vector<pbgpu_run_stats> SP(P);
+  for (size_t i = 0; i < P; ++i) {
+    rss.emplace_back(new RunState);
+    rss.back()->any_stop = &any_stop;
+    SP[i] = pbgpu_run_stats{};
   }
+  auto part_fn = [&](size_t i) {
+    const uint64_t b = P > 1 ? T * i / P : 0, e = P > 1 ? T * (i + 1) / P : ~0ull;
+    try {
+      run_part(R, R->parts[i], run, paths, b, e, cfd[i], dfd[i], run->header && i == 0, *rss[i], SP[i]);
+    } catch (...) {
+      record_exception(*rss[i]);
+    }
+  };
+  if (P == 1) {
+    part_fn(0);
+  } else {
+    std::vector<std::thread> pt;
+    for (size_t i = 0; i < P; ++i) pt.emplace_back(part_fn, i);
+    for (auto& t : pt) t.join();
+  }
+  for (auto& r : rss) {
+    if (r->status == PBGPU_OK) continue;
+    switch (r->status) {
+      case PBGPU_ERR_IO: throw bad_input(r->msg);
+      case PBGPU_ERR_UNSUPPORTED: throw unsupported(r->msg);
+      case PBGPU_ERR_NOMEM: throw std::bad_alloc();
+      default: throw std::runtime_error(r->msg);
+    }
+  }
+  pbgpu_run_stats S{};
+  for (const auto& x : SP) {  // counts and busy seconds summed over the parts
+    S.n_batches += x.n_batches; S.n_reads += x.n_reads; S.n_bases += x.n_bases; S.n_records += x.n_records;
+    S.coords_bytes += x.coords_bytes; S.details_bytes += x.details_bytes;
+    S.read_seconds += x.read_seconds; S.upload_seconds += x.upload_seconds; S.align_seconds += x.align_seconds;
+    S.format_seconds += x.format_seconds; S.d2h_seconds += x.d2h_seconds; S.write_seconds += x.write_seconds;
+    S.writer_idle_seconds += x.writer_idle_seconds;
+  }
+  S.open_seconds = t_open;
+  const double tc = now_s();
+  for (size_t i = 0; i < P; ++i) {
+    if (cfd[i] > 2) {
+      const int fd = cfd[i];
+      cfd[i] = -1;
+      if (close(fd)) throw bad_input(std::string("closing the coords file failed: ") + strerror(errno));
+    }
+  }
+  S.close_seconds = now_s() - tc;
   S.wall_seconds = now_s() - t_start;
   if (stats) *stats = S;
 }
@@ -757,11 +880,19 @@ pbgpu_status pbgpu_runner_create(pbgpu_index* const* indexes, size_t n_indexes, 
       if (R->details) pbgpu_aligner_set_details(a, 1);
     }
   const size_t W = R->al.size();
-  for (size_t i = 0; i < W + 2; ++i) {
-    R->batches.emplace_back(new Batch);
-    R->batches.back()->seq.reserve(R->batch_bases + (R->batch_bases >> 2));
+  const size_t P = run->n_parts > 1 ? run->n_parts : 1;
+  if (P > W) return fail(PBGPU_ERR_INVALID, "%zu part files need at least as many aligners (%zu)", P, W);
+  if (P > 1 && run->records_fn) return fail(PBGPU_ERR_UNSUPPORTED, "part files with a records consumer");
+  R->parts.resize(P);
+  for (size_t p = 0; p < P; ++p) {
+    RunPart& part = R->parts[p];
+    for (size_t i = W * p / P; i < W * (p + 1) / P; ++i) part.al.push_back(i);
+    for (size_t i = 0; i < part.al.size() + 2; ++i) {
+      part.batches.emplace_back(new Batch);
+      part.batches.back()->seq.reserve(R->batch_bases + (R->batch_bases >> 2));
+    }
+    part.texts.reset(new TextPool(part.al.size() + 2));
   }
-  R->texts.reset(new TextPool(W + 2));
   *out = R.release();
   return PBGPU_OK;
   API_CATCH

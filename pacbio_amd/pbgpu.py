@@ -78,7 +78,8 @@ class RunParams(C.Structure):
     _fields_ = [("pb_paths", C.POINTER(C.c_char_p)), ("n_pb_paths", C.c_size_t), ("coords_path", C.c_char_p),
                 ("details_path", C.c_char_p), ("compact", C.c_int32), ("header", C.c_int32),
                 ("zero_match", C.c_int32), ("aligners_per_device", C.c_uint32), ("batch_bases", C.c_uint64),
-                ("host_threads", C.c_int32), ("records_fn", C.c_void_p), ("records_user", C.c_void_p)]
+                ("host_threads", C.c_int32), ("records_fn", C.c_void_p), ("records_user", C.c_void_p),
+                ("n_parts", C.c_uint32)]
 
 
 class RunStats(C.Structure):
@@ -583,11 +584,11 @@ class StreamAligner:
 
 
 def _run_params(pb_paths, coords_path, details_path=None, compact=True, header=True, zero_match=False,
-                aligners_per_device=2, batch_bases=0, host_threads=0):
+                aligners_per_device=2, batch_bases=0, host_threads=0, n_parts=0):
     paths = _cstrs([p if isinstance(p, bytes) else str(p).encode() for p in pb_paths])
     rp = RunParams(paths, len(pb_paths), coords_path.encode() if coords_path else None,
                    details_path.encode() if details_path else None, int(compact), int(header), int(zero_match),
-                   aligners_per_device, int(batch_bases), host_threads, None, None)
+                   aligners_per_device, int(batch_bases), host_threads, None, None, int(n_parts))
     return rp, paths
 
 
@@ -597,7 +598,8 @@ def _index_handles(indexes):
     return (C.c_void_p * len(indexes))(*[ix.h.value if isinstance(ix.h, C.c_void_p) else ix.h for ix in indexes])
 
 
-_RUN_KEYS = ("details_path", "compact", "header", "zero_match", "aligners_per_device", "batch_bases", "host_threads")
+_RUN_KEYS = ("details_path", "compact", "header", "zero_match", "aligners_per_device", "batch_bases", "host_threads",
+             "n_parts")
 
 
 def run(indexes, pb_paths, coords_path, **kw):
@@ -616,11 +618,11 @@ def run(indexes, pb_paths, coords_path, **kw):
 class Runner:
     """pbgpu_runner: the driver's aligners and pinned buffers kept across runs."""
 
-    def __init__(self, indexes, aligners_per_device=2, batch_bases=0, details=False, **align_kw):
+    def __init__(self, indexes, aligners_per_device=2, batch_bases=0, details=False, n_parts=0, **align_kw):
         self._p, self._keep = align_params(**align_kw)
         self.details = details
         rp, _ = _run_params([], None, details_path="-" if details else None, aligners_per_device=aligners_per_device,
-                            batch_bases=batch_bases)
+                            batch_bases=batch_bases, n_parts=n_parts)
         hs = _index_handles(indexes)
         h = C.c_void_p()
         _check(lib().pbgpu_runner_create(hs, len(hs), C.byref(self._p), C.byref(rp), C.byref(h)))

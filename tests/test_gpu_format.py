@@ -116,6 +116,75 @@ def test_run_more_than_64_batches(tmp_path):
     assert open(a).read() == open(b).read()
 
 
+@pytest.fixture(scope="module")
+def many_dir(tmp_path_factory):
+    """3000 reads of the small preset, as one FASTA file and as the same reads split over two files"""
+    from tools.synth import Dataset
+    d = str(tmp_path_factory.mktemp("many"))
+    ds = Dataset("small", seed=5, n_pb=3000)
+    ds.write(d)
+    ds.close()
+    recs = open(os.path.join(d, "pb.fa")).read().split(">")[1:]
+    with open(os.path.join(d, "pb_a.fa"), "w") as f:
+        f.write("".join(">" + r for r in recs[:1234]))
+    with open(os.path.join(d, "pb_b.fa"), "w") as f:
+        f.write("".join(">" + r for r in recs[1234:]))
+    return d
+
+
+@pytest.mark.parametrize("n_parts,files", [(2, 1), (3, 2), (4, 1)])
+def test_run_part_files_concatenate(many_dir, n_parts, files):
+    """n_parts: part p holds the reads whose header starts in [p T / P, (p + 1) T / P)
+    of the inputs, written by its own writer; the parts concatenated are the
+    one-file bytes (header line in part 0 only), with one or two input files."""
+    from pacbio_amd import pbgpu
+    d = many_dir
+    gix = pbgpu.Index.from_fasta([os.path.join(d, "sr.fa")], 17)
+    rep = gix.replicate(0)
+    pb = [os.path.join(d, "pb.fa")] if files == 1 else [os.path.join(d, "pb_a.fa"), os.path.join(d, "pb_b.fa")]
+    one, part = os.path.join(d, f"one{n_parts}.coords"), os.path.join(d, f"part{n_parts}.coords")
+    st1 = pbgpu.run([gix], pb, one, aligners_per_device=2, batch_bases=200_000)
+    st = pbgpu.run([gix, rep], pb, part, aligners_per_device=2, batch_bases=200_000, n_parts=n_parts)
+    rep.close()
+    gix.close()
+    texts = [open(f"{part}.{i}").read() for i in range(n_parts)]
+    assert all(t.count("\n") > 100 for t in texts)
+    assert "".join(texts) == open(one).read()
+    assert st["n_reads"] == st1["n_reads"] == 3000 and st["coords_bytes"] == sum(len(t) for t in texts)
+
+
+def test_run_part_files_refuse_gzip_and_fastq(many_dir, tmp_path):
+    from pacbio_amd import pbgpu
+    d = many_dir
+    gix = pbgpu.Index.from_fasta([os.path.join(d, "sr.fa")], 17)
+    gz = str(tmp_path / "pb.fa.gz")
+    with open(os.path.join(d, "pb_a.fa"), "rb") as f, gzip.open(gz, "wb") as g:
+        g.write(f.read())
+    fq = str(tmp_path / "pb.fq")
+    with open(fq, "w") as f:
+        for i in range(50):
+            f.write(f"@r{i}\n{'ACGT' * 300}\n+\n{'I' * 1200}\n")
+    for path in (gz, fq):
+        with pytest.raises(pbgpu.PbgpuError) as e:
+            pbgpu.run([gix], [path], str(tmp_path / "x.coords"), aligners_per_device=2, n_parts=2)
+        assert e.value.status == 5, e.value  # PBGPU_ERR_UNSUPPORTED
+    gix.close()
+
+
+def test_cli_parts(many_dir, tmp_path):
+    """jf_aligner --devices 0,0 --parts 2: the parts concatenated are the one-file output"""
+    d = many_dir
+    base = [CLI, "-s", "1", "-m", "17", "-r", os.path.join(d, "sr.fa"), "-l", os.path.join(d, "ul.txt"), "-k", "31",
+            "-f", "-B", "15", "-p", os.path.join(d, "pb.fa")]
+    one, part = str(tmp_path / "one.coords"), str(tmp_path / "part.coords")
+    r1 = subprocess.run(base + ["--coords", one], capture_output=True, text=True, timeout=300)
+    r2 = subprocess.run(base + ["--coords", part, "--devices", "0,0", "--parts", "2"], capture_output=True, text=True,
+                        timeout=300)
+    assert r1.returncode == 0, r1.stderr
+    assert r2.returncode == 0, r2.stderr
+    assert open(part + ".0").read() + open(part + ".1").read() == open(one).read()
+
+
 def test_run_gzip_input(small, small_dir):
     from pacbio_amd import pbgpu
     pb = os.path.join(small_dir, "pb.fa")
