@@ -183,6 +183,9 @@ def main():
     ap.add_argument("--device-streams", type=int, default=1,
                     help="aligners of the device-only leg: 1 = every launch runs alone, so the per-launch event times "
                          "(the roofline) measure the kernel, not two overlapping launches")
+    ap.add_argument("--skip-default-leg", action="store_true",
+                    help="no default-flags device leg (profiling runs: every large-grid launch is then the "
+                         "production leg's)")
     ap.add_argument("--workdir", default=os.environ.get("PBGPU_BENCH_DIR", "/tmp"),
                     help="where the input FASTA and the coords output are written")
     args = ap.parse_args()
@@ -238,20 +241,22 @@ def main():
     al.close()
 
     # SURVEY 8(d)'s second flag set: the defaults, without -l / -f (device leg only)
-    al2 = pbgpu.StreamAligner(index, streams=args.device_streams, k=k)
-    reads = al2.upload(blob=blob, offsets=off)
-    al2.align_resident(reads)
-    pbgpu.device_synchronize(local)
-    comm.barrier()
-    td = time.perf_counter()
-    for _ in range(args.device_steps):
+    el_dev2, st2 = None, None
+    if not args.skip_default_leg:
+        al2 = pbgpu.StreamAligner(index, streams=args.device_streams, k=k)
+        reads = al2.upload(blob=blob, offsets=off)
         al2.align_resident(reads)
-    pbgpu.device_synchronize(local)
-    comm.barrier()
-    el_dev2 = comm.max(time.perf_counter() - td)
-    st2 = al2.stats()
-    al2.free(reads)
-    al2.close()
+        pbgpu.device_synchronize(local)
+        comm.barrier()
+        td = time.perf_counter()
+        for _ in range(args.device_steps):
+            al2.align_resident(reads)
+        pbgpu.device_synchronize(local)
+        comm.barrier()
+        el_dev2 = comm.max(time.perf_counter() - td)
+        st2 = al2.stats()
+        al2.free(reads)
+        al2.close()
 
     # ---- end to end (value): PacBio FASTA -> coords file, pbgpu_run
     # (a pbgpu_runner keeps its aligners and pinned buffers across steps: a service
@@ -292,7 +297,7 @@ def main():
     value = total_bases / elapsed
     value_device = comm.sum(bases_rank) * args.device_steps / el_dev
     # every collective runs on every rank, here, never inside the rank-0 report below
-    value_device2 = comm.sum(bases_rank) * args.device_steps / el_dev2
+    value_device2 = comm.sum(bases_rank) * args.device_steps / el_dev2 if el_dev2 else None
     kb = _kernel_bytes(st)
     kms, kn = st["kernel_ms"], st["kernel_launches"]
     # the dominant kernel: the one whose stage takes the most device time per step
@@ -316,21 +321,33 @@ def main():
             "bytes_per_launch": sec, "achieved_gbs": round(sgbs, 1), "frac": round(sgbs / HBM_PEAK_GBS, 4),
             "frac_of_b_rand": round(sgbs / b_rand, 4) if b_rand else None,
             "random_accesses_per_launch": (st["n_filter"] + st["n_probes"]) / kn["k_seed"]}
-    # HBM traffic per launch of the dominant kernel from the committed rocprofv3 PMC
-    # summary (tools/prof_r02.sh): FETCH_SIZE calibrated on the 512-B-run gather
-    # microbenchmark (bytes moved / FETCH_SIZE), + WRITE_SIZE
-    traffic, traffic_note = None, None
-    summ = os.path.join(ROOT, "profiles", "r02e_rocprof_summary.json")
-    if os.path.exists(summ):
-        try:
-            with open(summ) as f:
-                t = json.load(f).get(f"{dom}_traffic_bytes", {})
-            # k_group reads occurrence runs (FETCH_SIZE calibrated on that shape); the
-            # other kernels stream rows (the guide's 2x FETCH_SIZE correction)
-            traffic = t.get("calibrated_runs" if dom == "k_group" else "guide_2x_fetch_plus_write")
-            traffic_note = {k: t.get(k) for k in ("raw_fetch_plus_write", "guide_2x_fetch_plus_write")}
-        except Exception:
-            traffic = None
+    # HBM traffic per launch of each kernel from the committed rocprofv3 summary of the
+    # same bench (tools/prof_r03.sh, separate FETCH_SIZE / WRITE_SIZE passes over the
+    # production device leg): FETCH_SIZE corrected for the kernel's read shape (random
+    # 64-B sectors exact; occurrence runs by the 512-B-run calibration; row streams 2x)
+    traffic, traffic_note, summ_name, summ_all = None, None, None, {}
+    for name in ("r03_rocprof_summary.json", "r02e_rocprof_summary.json"):
+        summ = os.path.join(ROOT, "profiles", name)
+        if os.path.exists(summ):
+            try:
+                with open(summ) as f:
+                    summ_all = json.load(f)
+                summ_name = name
+                break
+            except Exception:
+                pass
+    for kk in per_kernel:
+        t = summ_all.get(f"{kk}_traffic_bytes")
+        if t:
+            shape = t.get("shape") or ("calibrated_runs" if kk == "k_group" else "guide_2x_fetch_plus_write")
+            per_kernel[kk]["traffic_bytes_per_launch"] = t.get(shape)
+            per_kernel[kk]["traffic_over_alg"] = round(t.get(shape) / kb[kk], 3) if t.get(shape) else None
+            per_kernel[kk]["rocprof_mean_ms"] = (summ_all.get(f"{kk}_device_leg") or {}).get("mean_ms")
+            per_kernel[kk]["profile"] = f"profiles/{summ_name}"
+    t = summ_all.get(f"{dom}_traffic_bytes", {})
+    if t:
+        traffic = per_kernel[dom].get("traffic_bytes_per_launch")
+        traffic_note = {k: t.get(k) for k in ("raw_fetch_plus_write", "guide_2x_fetch_plus_write", "calibrated_runs")}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle.oracle import OracleIndex, params
@@ -439,16 +456,16 @@ def main():
                     "flags": f"-m {k} --psa-min 13 (defaults: no -l/-k/-f, -B 17, --max-count 5000)",
                     "value_device": value_device2,
                     "ms_per_step": el_dev2 / args.device_steps * 1e3,
-                    "records_per_step": st2["n_records"] // max(1, args.device_steps)},
+                    "records_per_step": st2["n_records"] // max(1, args.device_steps)} if el_dev2 else None,
                 "end_to_end_including_build_s": round(t_index + elapsed / args.steps, 3),
                 "fit_dtype": "f64",
             },
             "roofline": {"bound": "hbm", "kernel": dom, "rocprof_kernel": ROCPROF_FILE[dom], "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "alg_bytes_per_launch": kb[dom], "avg_launch_ms": avg_ms,
-                         "traffic_source": ("profiles/r02e_rocprof_summary.json (" +
+                         "traffic_source": (f"profiles/{summ_name} (" +
                                             ("FETCH_SIZE x run-shape calibration" if dom == "k_group" else
-                                             "2 x FETCH_SIZE") + " + WRITE_SIZE, per device-leg launch)")
+                                             "FETCH_SIZE by read shape") + " + WRITE_SIZE, per device-leg launch)")
                          if traffic else None,
                          "traffic_alternatives": traffic_note,
                          "b_rand_gbs": b_rand, "frac_of_b_rand": (achieved / b_rand) if b_rand else None,

@@ -49,11 +49,18 @@ def counters(d):
     return acc, meta
 
 
-# device-leg kernels summarised: (rocprof name, key prefix in the summary)
-KERNELS = [("k_group<false, 256u>", "k_group"), ("k_coords<8>", "k_coords")]
+# device-leg kernels summarised: (rocprof name, key prefix in the summary) -- the five
+# individually timed kernels of bench.py's roofline.by_kernel
+KERNELS = [("k_seed<256, 8, 0>", "k_seed"), ("k_group<false, 256u>", "k_group"), ("k_lis_w<255, 8>", "k_lis"),
+           ("k_coords<8>", "k_coords"), ("k_rec_sort<256, 2048>", "k_rec_sort")]
+# which FETCH_SIZE correction fits each kernel's read shape: random 64-B
+# sectors (k_seed's filter words and bucket probes) are counted exactly; k_group's
+# occurrence runs by the 512-B-run calibration; row streams by the guide's 2x
+SHAPE = {"k_seed": "raw_fetch_plus_write", "k_group": "calibrated_runs", "k_lis": "guide_2x_fetch_plus_write",
+         "k_coords": "guide_2x_fetch_plus_write", "k_rec_sort": "guide_2x_fetch_plus_write"}
 
 
-def main(d, out):
+def main(d, out, run_tag="r02"):
     res = {}
     rows = trace(glob.glob(os.path.join(d, "kt", "**", "*kernel_trace.csv"), recursive=True)[0])
     stats = collections.defaultdict(list)
@@ -102,14 +109,15 @@ def main(d, out):
             w = out_c["WRITE_SIZE"] * 1024.0
             r = cal.get("k_gather_runs", {}).get("ratio_moved_over_fetch")
             res[f"{tag}_traffic_bytes"] = {"raw_fetch_plus_write": f + w, "guide_2x_fetch_plus_write": 2 * f + w,
-                                           "calibrated_runs": (f * r + w) if r else None}
-    with open(os.path.join(out, "r02_rocprof_summary.json"), "w") as fo:
+                                           "calibrated_runs": (f * r + w) if r else None,
+                                           "shape": SHAPE[tag]}
+    with open(os.path.join(out, f"{run_tag}_rocprof_summary.json"), "w") as fo:
         json.dump(res, fo, indent=1)
-    with open(os.path.join(out, "r02_kernel_stats.txt"), "w") as fo:
+    with open(os.path.join(out, f"{run_tag}_kernel_stats.txt"), "w") as fo:
         fo.write("\n".join(lines) + "\n")
     print("\n".join(lines[:25]))
     print(json.dumps(res, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else ".")
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else ".", sys.argv[3] if len(sys.argv) > 3 else "r02")
