@@ -50,6 +50,7 @@ void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const ui
 uint64_t group_table_words(uint32_t hcap_log2);
 void launch_sr_ul(const uint32_t* ids, uint64_t n, const int32_t* ul, uint64_t n_ul, int32_t* out, hipStream_t st);
 void launch_counts_pack16(bool unpack, const uint32_t* src, uint64_t n, uint32_t* dst, hipStream_t st);
+void launch_occ_sr(const uint64_t* occ, uint64_t n, uint32_t* out, hipStream_t st);
 constexpr uint32_t kGroupLdsMaxLog2 = 13;  // 8192-slot table, 96 KiB of LDS
 void launch_init_slen(const ChainDesc* chains, uint32_t n_chains, uint32_t* slen, hipStream_t st);
 void launch_strand_order(const uint32_t* slen, uint32_t n_items, uint32_t* hist, uint32_t* cursor, uint32_t* perm,
@@ -464,6 +465,16 @@ static void build_kmer_table(pbgpu_index* ix, uint32_t km, uint32_t K, uint32_t 
   n_occ = kept;
 }
 
+// IndexView::occ_sr, when PBGPU_OCC_SR=1 (4 B per occ word): derived, never cached
+static void make_occ_sr(pbgpu_index* ix, hipStream_t st) {
+  const char* e = getenv("PBGPU_OCC_SR");
+  if (!e || atoi(e) == 0 || !ix->occ.n) return;
+  ix->occ_sr.alloc(ix->occ.n);
+  launch_occ_sr(ix->occ.p, ix->occ.n, ix->occ_sr.p, st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(st));
+}
+
 static void build_device_index(pbgpu_index* ix, text_builder& tb) {
   auto t0 = std::chrono::steady_clock::now();
   HIPCHK(hipSetDevice(ix->device));
@@ -586,6 +597,7 @@ static void build_device_index(pbgpu_index* ix, text_builder& tb) {
   build_kmer_table(ix, k, k, 0, st, ix->table, ix->occ, ix->buckets, ix->n_kmers, ix->n_occ, &ix->filt,
                    &ix->filt_log2);
   ix->null_ptr = 2 * ix->n_kmers + ix->n_occ;
+  make_occ_sr(ix, st);
   if (ix->fk)
     build_kmer_table(ix, ix->fk, k, 2 * (k - ix->fk) + 1, st, ix->f_table, ix->f_occv, ix->f_buckets, ix->f_kmers,
                      ix->f_occ);
@@ -851,7 +863,7 @@ pbgpu_status pbgpu_index_replicate(const pbgpu_index* src, int device, pbgpu_ind
   };
   cp(ix->text, src->text); cp(ix->d_sr_start, src->d_sr_start); cp(ix->occ, src->occ); cp(ix->table, src->table);
   cp(ix->sr_uoff, src->sr_uoff); cp(ix->sr_uids, src->sr_uids); cp(ix->filt, src->filt);
-  cp(ix->f_occv, src->f_occv); cp(ix->f_table, src->f_table);
+  cp(ix->f_occv, src->f_occv); cp(ix->f_table, src->f_table); cp(ix->occ_sr, src->occ_sr);
   HIPCHK(hipDeviceSynchronize());
   *out = ix.release();
   return PBGPU_OK;

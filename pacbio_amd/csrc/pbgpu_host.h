@@ -145,6 +145,7 @@ struct pbgpu_index {
   NameTable name_fwd, name_bwd;
   std::vector<uint64_t> sr_start;            // host copy
   dbuf<uint64_t> text, d_sr_start, occ;
+  dbuf<uint32_t> occ_sr;  // IndexView::occ_sr (PBGPU_OCC_SR=1), derived from occ
   dbuf<ulonglong2> table;
   dbuf<uint32_t> sr_uoff, sr_uids;
   // presence filter of the coarse table's k-mers (k_seed), 2^filt_log2 words; none if empty
@@ -170,18 +171,19 @@ struct pbgpu_index {
     IndexView v;
     v.text = text.p; v.n = n; v.sr_start = d_sr_start.p; v.n_sr = (uint32_t)(sr_end - sr_begin); v.k = k;
     v.table = table.p; v.bucket_mask = buckets - 1; v.occ = occ.p; v.sr_uoff = sr_uoff.p; v.sr_uids = sr_uids.p;
+    v.occ_sr = occ_sr.n ? occ_sr.p : nullptr;
     v.filt = filt.n ? filt.p : nullptr; v.filt_shift = 64 - filt_log2;
     return v;
   }
   IndexView fine_view() const {
     IndexView v = view();
-    v.k = fk; v.table = f_table.p; v.bucket_mask = f_buckets - 1; v.occ = f_occv.p;
+    v.k = fk; v.table = f_table.p; v.bucket_mask = f_buckets - 1; v.occ = f_occv.p; v.occ_sr = nullptr;
     v.filt = nullptr;
     return v;
   }
   uint64_t device_bytes() const {
     return text.bytes() + d_sr_start.bytes() + occ.bytes() + table.bytes() + sr_uoff.bytes() + sr_uids.bytes() +
-           f_occv.bytes() + f_table.bytes() + filt.bytes();
+           f_occv.bytes() + f_table.bytes() + filt.bytes() + occ_sr.bytes();
   }
 };
 

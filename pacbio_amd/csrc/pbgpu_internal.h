@@ -36,6 +36,9 @@ struct IndexView {
   const ulonglong2* table;    // 4 slots per bucket
   uint64_t bucket_mask;
   const uint64_t* occ;
+  // optional: the super-read id (high word) of every occ word, packed (k_group's
+  // counting pass reads 4 B a hit from it instead of an 8-B entry's line); null: none
+  const uint32_t* occ_sr;
   const uint32_t* sr_uoff;    // n_sr + 1 offsets into sr_uids
   const uint32_t* sr_uids;    // unitig ids of the fwd name (super_read_name::unitig_id)
   const uint64_t* filt;       // presence filter of the table's canonical k-mers (null: none)

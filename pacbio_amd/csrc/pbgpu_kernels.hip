@@ -654,6 +654,10 @@ __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_
       // chain was slower (pass 0 7.7 vs 6.9 ms, 25k C2 reads).
       const uint32_t lane = tid & 63;
       const uint32_t n_win = (total + 63) >> 6;
+      // pass 0's super-read ids: the packed copy when the index has one, else the high
+      // words of the entries (a pointer and stride, not a branch around the load)
+      const uint32_t* sr_base = ix.occ_sr ? ix.occ_sr : reinterpret_cast<const uint32_t*>(ix.occ) + 1;
+      const uint64_t sr_stride = ix.occ_sr ? 1 : 2;
       // locate + load of the wave's GU windows of step ws, one step ahead of
       // their use, so the occurrence loads overlap the table work of the step before
       auto fetch = [&](uint32_t ws, uint64_t (&e_o)[GU], int32_t (&pb_o)[GU], bool (&fwd_o)[GU],
@@ -678,7 +682,7 @@ __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_
           // pass 0 needs the super-read id alone: a 4-byte load of the high word (an
           // 8-byte one leaves a dead half whose register the compiler reuses, which
           // again drains the loads in flight)
-          if constexpr (pass == 0) e_o[u] = (uint64_t)reinterpret_cast<const uint32_t*>(ix.occ)[2 * at + 1] << 32;
+          if constexpr (pass == 0) e_o[u] = (uint64_t)sr_base[sr_stride * at] << 32;
           else e_o[u] = ix.occ[at];
         }
       };
@@ -2515,6 +2519,15 @@ void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const ui
                        n_kept, thr, hit_off, node_base, r0, read_list, n_list, hcap_log2, gtable, O, stats);
   }
 }
+// IndexView::occ_sr: the high word of every occ word (headers included, unused)
+__global__ void k_occ_sr(const uint64_t* __restrict__ occ, uint64_t n, uint32_t* __restrict__ out) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    out[i] = (uint32_t)(occ[i] >> 32);
+}
+void launch_occ_sr(const uint64_t* occ, uint64_t n, uint32_t* out, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_occ_sr, dim3(4096), dim3(256), 0, st, occ, n, out);
+}
+
 // sharded-index count exchange: two saturated counts per u32 (count_pack.h)
 __global__ void k_counts_pack16(const uint32_t* __restrict__ c, uint64_t n, uint32_t* __restrict__ out) {
   const uint64_t nw = counts_packed_words(n);

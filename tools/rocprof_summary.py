@@ -33,8 +33,18 @@ def trace(path):
     rows = []
     with open(path) as f:
         for r in csv.DictReader(f):
-            rows.append((short(r["Kernel_Name"]), grid(r), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6))
+            rows.append((short(r["Kernel_Name"]), grid(r), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6,
+                         int(r["Start_Timestamp"])))
+    rows.sort(key=lambda x: x[3])
     return rows
+
+
+def device_leg(launches, first):
+    """bench.py --skip-default-leg runs the production device leg first: one warm-up
+    align_resident, then the timed ones, each launching every timed kernel once.
+    The first `first` launches of a kernel (in time / dispatch order) are that leg's;
+    the warm-up is dropped."""
+    return launches[1:first] if len(launches) >= first else launches[1:] or launches
 
 
 def counters(d):
@@ -56,6 +66,7 @@ KERNELS = [("k_seed<256, 8, 0>", "k_seed"), ("k_group<false, 256u>", "k_group"),
 # which FETCH_SIZE correction fits each kernel's read shape: random 64-B
 # sectors (k_seed's filter words and bucket probes) are counted exactly; k_group's
 # occurrence runs by the 512-B-run calibration; row streams by the guide's 2x
+KT_FIRST, PMC_FIRST = 4, 2  # tools/prof_r03.sh: --device-steps 3 (trace run), 1 (PMC runs)
 SHAPE = {"k_seed": "raw_fetch_plus_write", "k_group": "calibrated_runs", "k_lis": "guide_2x_fetch_plus_write",
          "k_coords": "guide_2x_fetch_plus_write", "k_rec_sort": "guide_2x_fetch_plus_write"}
 
@@ -64,7 +75,7 @@ def main(d, out, run_tag="r02"):
     res = {}
     rows = trace(glob.glob(os.path.join(d, "kt", "**", "*kernel_trace.csv"), recursive=True)[0])
     stats = collections.defaultdict(list)
-    for k, g, ms in rows:
+    for k, g, ms, _ in rows:
         stats[k].append((g, ms))
     lines = []
     for k, v in sorted(stats.items(), key=lambda kv: -sum(x[1] for x in kv[1])):
@@ -72,16 +83,16 @@ def main(d, out, run_tag="r02"):
     for kname, tag in KERNELS:
         kg = stats.get(kname, [])
         if kg:
-            gmax = max(g for g, _ in kg)
-            dev = [ms for g, ms in kg if g >= 0.5 * gmax]
-            res[f"{tag}_device_leg"] = {"launches": len(dev), "mean_ms": sum(dev) / len(dev), "grid": gmax,
+            dev = [ms for _, ms in device_leg(kg, KT_FIRST)]
+            res[f"{tag}_device_leg"] = {"launches": len(dev), "mean_ms": sum(dev) / len(dev),
+                                        "grid": device_leg(kg, KT_FIRST)[0][0],
                                         "all_launches_mean_ms": sum(x[1] for x in kg) / len(kg)}
-            lines.append(f"{kname} device-leg launches (grid >= {gmax // 2}): n={len(dev)} "
+            lines.append(f"{kname} device-leg launches (2nd to {KT_FIRST}th in time order): n={len(dev)} "
                          f"mean={sum(dev) / len(dev):.3f} ms")
     # PMC
     acc, meta = counters(d)
     per = collections.defaultdict(lambda: collections.defaultdict(list))
-    for (k, disp, src), c in acc.items():
+    for (k, disp, src), c in sorted(acc.items(), key=lambda kv: int(kv[0][1])):
         for n, v in c.items():
             per[k][n].append((meta[(k, disp, src)], v))
     cal = {}
@@ -100,8 +111,7 @@ def main(d, out, run_tag="r02"):
         out_c = {}
         for n in ("FETCH_SIZE", "WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"):
             if c.get(n):
-                gmax = max(g for g, _ in c[n])
-                vals = [v for g, v in c[n] if g >= 0.5 * gmax]
+                vals = [v for _, v in device_leg(c[n], PMC_FIRST)]
                 out_c[n] = sum(vals) / len(vals)
         res[f"{tag}_pmc_device_leg"] = out_c
         if "FETCH_SIZE" in out_c and "WRITE_SIZE" in out_c:
