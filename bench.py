@@ -183,6 +183,8 @@ def main():
     ap.add_argument("--device-streams", type=int, default=1,
                     help="aligners of the device-only leg: 1 = every launch runs alone, so the per-launch event times "
                          "(the roofline) measure the kernel, not two overlapping launches")
+    ap.add_argument("--parts", type=int, default=2,
+                    help="part files of the extra coords-out leg (value_parts; 0 = no such leg)")
     ap.add_argument("--skip-default-leg", action="store_true",
                     help="no default-flags device leg (profiling runs: every large-grid launch is then the "
                          "production leg's)")
@@ -293,11 +295,50 @@ def main():
     coords_bytes = rstats[-1]["coords_bytes"]
     runner.close()
 
+    # ---- the same coords out into P part files (pbgpu_run_params.n_parts, the reference's
+    # split-and-cat in one process): P readers / writers, 2 aligners each; the parts
+    # concatenated are the one file above.  Reported beside `value`, never as it.
+    el_parts, pstats = None, None
+    if args.parts > 1:
+        prunner = pbgpu.Runner([index], aligners_per_device=2 * args.parts, batch_bases=int(args.batch_bases),
+                               n_parts=args.parts, **akw)
+        pouts = [os.path.join(wd, f"parts{i}.coords") for i in range(args.steps + 1)]
+        pclean = []
+
+        def _rm_parts(path):
+            for j in range(args.parts):
+                try:
+                    os.unlink(f"{path}.{j}")
+                except OSError:
+                    pass
+
+        def _pstep(i):
+            if i > 0:
+                th = threading.Thread(target=_rm_parts, args=(pouts[i - 1],))
+                th.start()
+                pclean.append(th)
+            return prunner.run([pb_fa], pouts[i])
+        _pstep(0)
+        for th in pclean:
+            th.join()
+        pbgpu.device_synchronize(local)
+        comm.barrier()
+        t0 = time.perf_counter()
+        pstats = [_pstep(i) for i in range(1, args.steps + 1)]
+        pbgpu.device_synchronize(local)
+        comm.barrier()
+        el_parts = comm.max(time.perf_counter() - t0)
+        for th in pclean:
+            th.join()
+        _rm_parts(pouts[-1])
+        prunner.close()
+
     total_bases = comm.sum(bases_rank) * args.steps
     value = total_bases / elapsed
     value_device = comm.sum(bases_rank) * args.device_steps / el_dev
     # every collective runs on every rank, here, never inside the rank-0 report below
     value_device2 = comm.sum(bases_rank) * args.device_steps / el_dev2 if el_dev2 else None
+    value_parts = comm.sum(bases_rank) * args.steps / el_parts if el_parts else None
     kb = _kernel_bytes(st)
     kms, kn = st["kernel_ms"], st["kernel_launches"]
     # the dominant kernel: the one whose stage takes the most device time per step
@@ -425,6 +466,13 @@ def main():
             "value_device": value_device,
             "value_device_note": "reads resident in HBM, device path to sorted records in HBM, no formatting / "
                                  "output (round-1 definition)",
+            "value_parts": value_parts,
+            "value_parts_note": (f"the same coords out into {args.parts} part files per GPU (jf_aligner --parts, the "
+                                 "reference's split-and-cat in one process: one reader / writer per part, 2 aligners "
+                                 "each; the parts concatenated are the one-file output)") if value_parts else None,
+            "parts_stage_ms_per_step": {n: round(sum(r[n] for r in pstats) / args.steps * 1e3, 3) for n in
+                                        ("write_seconds", "align_seconds", "d2h_seconds", "writer_idle_seconds",
+                                         "wall_seconds")} if pstats else None,
             "config": {
                 "workload": {"C1": "C1: 100 PB x 10 kb vs 1k SRs, k=17",
                              "C2": "C2 E. coli-scale: 50k PB (lognormal mean 12 kb, CLR 13%) per GPU vs 200k SRs, k=17",
