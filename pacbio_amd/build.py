@@ -75,13 +75,20 @@ def build_pbgpu(force=False):
     return lib
 
 
-def build_pbgpu_variant(name, defines):
+def build_pbgpu_variant(name, defines, kernels_only=False):
     """Experiment / profiling variant libpbgpu_<name>.so built with extra -D
-    flags (tools/prof_*.py, tools/exp_*.py); never the product library."""
+    flags (tools/prof_*.py, tools/exp_*.py); never the product library.
+    kernels_only: the defines touch pbgpu_kernels.hip alone, the other objects
+    are the product's (build_pbgpu first)."""
     objdir = os.path.join(ROOT, "build", name)
     os.makedirs(objdir, exist_ok=True)
     jobs, objs = [], []
+    if kernels_only:
+        build_pbgpu()
     for s in ["pbgpu_kernels.hip", "pbgpu_api.hip", "pbgpu_format.hip", "pbgpu_run.hip"]:
+        if kernels_only and s != "pbgpu_kernels.hip":
+            objs.append(os.path.join(ROOT, "build", s + ".o"))
+            continue
         obj = os.path.join(objdir, s + ".o")
         jobs.append([HIPCC] + HIPFLAGS + list(defines) + ["-c", os.path.join(CSRC, s), "-o", obj])
         objs.append(obj)
