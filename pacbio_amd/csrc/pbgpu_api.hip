@@ -1464,17 +1464,8 @@ static void records_stage(pbgpu_aligner* al, uint32_t n, uint32_t nrec, bool tim
   HIPCHK(hipMemsetAsync(al->rec_per_read.p, 0, n * 4, st));
   HIPCHK(hipMemsetAsync(al->rec_cursor.p, 0, n * 4, st));
   launch_rec_hist(al->rec_read.p, nrec, al->rec_per_read.p, st);
-  {
-    struct RecOp {
-      const uint32_t* c; uint64_t n;
-      __host__ __device__ uint64_t operator()(const uint64_t& i) const { return i < n ? (uint64_t)c[i] : 0ull; }
-    };
-    hipcub::CountingInputIterator<uint64_t> cnt0(0);
-    hipcub::TransformInputIterator<uint64_t, RecOp, hipcub::CountingInputIterator<uint64_t>> in(cnt0, RecOp{al->rec_per_read.p, n});
-    size_t tb = 0;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, al->rec_off.p, (uint64_t)n + 1, st));
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(temp_storage(al->tmp, tb), tb, in, al->rec_off.p, (uint64_t)n + 1, st));
-  }
+  launch_excl_scan(al->rec_per_read.p, nullptr, n, al->rec_off.p,
+                   (uint64_t*)temp_storage(al->tmp, excl_scan_scratch_words(n) * 8), st);
   al->order.ensure(nrec + 1);
   al->sort_scratch.ensure(6ull * nrec + 6);
   al->recs_sorted.ensure(nrec + 1);
@@ -1636,17 +1627,8 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
               al->stats.p, gcount, ix->null_ptr, st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(al->ev[1], st));
-  {
-    struct HitOp {
-      const uint64_t* h; uint64_t n;
-      __host__ __device__ uint64_t operator()(const uint64_t& i) const { return i < n ? h[i] : 0ull; }
-    };
-    hipcub::CountingInputIterator<uint64_t> cnt(0);
-    hipcub::TransformInputIterator<uint64_t, HitOp, hipcub::CountingInputIterator<uint64_t>> in(cnt, HitOp{al->nhits.p, n});
-    size_t tb = 0;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, al->hit_off.p, (uint64_t)n + 1, st));
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(temp_storage(al->tmp, tb), tb, in, al->hit_off.p, (uint64_t)n + 1, st));
-  }
+  launch_excl_scan(nullptr, al->nhits.p, n, al->hit_off.p,
+                   (uint64_t*)temp_storage(al->tmp, excl_scan_scratch_words(n) * 8), st);
   std::vector<uint64_t> hoff(n + 1);
   HIPCHK(hipMemcpyAsync(hoff.data(), al->hit_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));

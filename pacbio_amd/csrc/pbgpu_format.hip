@@ -13,7 +13,6 @@
 // the host test entry point pbgpu_format_double, which the CPU tests check
 // against glibc's printf("%.6g").
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include "pbgpu_fmt.h"
 #include "pbgpu_host.h"
@@ -154,16 +153,8 @@ uint64_t format_device_text(pbgpu_aligner* al, const pbgpu_reads* rd, int compac
     hipLaunchKernelGGL(k_fmt_len, dim3(blocks), dim3(256), 0, st, A, rec_len, hdr_len);
     HIPCHK(hipGetLastError());
   }
-  struct LenOp {
-    const uint32_t* c; uint64_t n;
-    __host__ __device__ uint64_t operator()(const uint64_t& i) const { return i < n ? (uint64_t)c[i] : 0ull; }
-  };
   auto scan = [&](const uint32_t* len, uint64_t m, uint64_t* pos) {
-    hipcub::CountingInputIterator<uint64_t> cnt(0);
-    hipcub::TransformInputIterator<uint64_t, LenOp, hipcub::CountingInputIterator<uint64_t>> in(cnt, LenOp{len, m});
-    size_t tb = 0;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, pos, m + 1, st));
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(temp_storage(al->tmp, tb), tb, in, pos, m + 1, st));
+    launch_excl_scan(len, nullptr, m, pos, (uint64_t*)temp_storage(al->tmp, excl_scan_scratch_words(m) * 8), st);
   };
   scan(rec_len, nrec, rec_pos);
   scan(hdr_len, n, hdr_pos);

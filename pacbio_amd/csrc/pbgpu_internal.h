@@ -180,4 +180,11 @@ struct ChainOut {
   const uint32_t* emit_of;  // fine pass: per chain, the emission index of its coarse record (else null)
 };
 
+// Exclusive scan of n counts (u32 or u64, exactly one of in32 / in64 non-null) into
+// n + 1 offsets, out[n] = the total (pbgpu_kernels.hip; replaces a library scan on the
+// per-batch path).  scratch: excl_scan_scratch_words(n) words.
+uint64_t excl_scan_scratch_words(uint64_t n);
+void launch_excl_scan(const uint32_t* in32, const uint64_t* in64, uint64_t n, uint64_t* out, uint64_t* scratch,
+                      hipStream_t st);
+
 }  // namespace pbgpu

@@ -2769,4 +2769,85 @@ void launch_fine_empty(IndexView ix, uint32_t k, const ChainDesc* chains, uint32
   hipLaunchKernelGGL(k_fine_empty, dim3(g), dim3(256), 0, st, ix, k, chains, n, lisl, emit_of, O);
 }
 
+// ================================================================= scans
+// Exclusive scan of per-item counts into offsets (the per-batch hit, record and
+// text offsets): reduce per 2048-item tile, scan the tile sums in one block,
+// rescan each tile from its base.  Item n is a zero, so out[n] is the total.
+constexpr uint32_t SCAN_BLOCK = 256, SCAN_ITEMS = 8, SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
+DEV uint64_t scan_item(const uint32_t* in32, const uint64_t* in64, uint64_t n, uint64_t i) {
+  if (i >= n) return 0;
+  return in32 ? (uint64_t)in32[i] : in64[i];
+}
+// inclusive scan of one u64 per thread over the block, block total in tot
+template <uint32_t BLOCK>
+DEV uint64_t block_incl_scan_u64(uint64_t v, uint64_t* s_w, uint64_t& tot) {
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(v, o, 64);
+    if (lane >= o) v += y;
+  }
+  if (lane == 63) s_w[w] = v;
+  __syncthreads();
+  uint64_t base = 0, t = 0;
+  for (uint32_t j = 0; j < BLOCK / 64; ++j) {
+    const uint64_t x = s_w[j];
+    base += j < w ? x : 0;
+    t += x;
+  }
+  __syncthreads();
+  tot = t;
+  return base + v;
+}
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_reduce(const uint32_t* __restrict__ in32,
+                                                            const uint64_t* __restrict__ in64, uint64_t n,
+                                                            uint64_t* __restrict__ tile_sum) {
+  __shared__ uint64_t s_w[SCAN_BLOCK / 64];
+  const uint64_t i0 = (uint64_t)blockIdx.x * SCAN_TILE + threadIdx.x;
+  uint64_t v = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < SCAN_ITEMS; ++j) v += scan_item(in32, in64, n, i0 + (uint64_t)j * SCAN_BLOCK);
+  uint64_t tot;
+  block_incl_scan_u64<SCAN_BLOCK>(v, s_w, tot);
+  if (threadIdx.x == 0) tile_sum[blockIdx.x] = tot;
+}
+// one block: the tile sums, scanned exclusive in place
+__global__ __launch_bounds__(1024) void k_scan_tiles(uint64_t* __restrict__ tile_sum, uint64_t nt) {
+  __shared__ uint64_t s_w[1024 / 64];
+  uint64_t carry = 0;
+  for (uint64_t c = 0; c < nt; c += 1024) {
+    const uint64_t i = c + threadIdx.x;
+    const uint64_t v = i < nt ? tile_sum[i] : 0;
+    uint64_t tot;
+    const uint64_t inc = block_incl_scan_u64<1024>(v, s_w, tot);
+    if (i < nt) tile_sum[i] = carry + inc - v;
+    carry += tot;
+  }
+}
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_apply(const uint32_t* __restrict__ in32,
+                                                           const uint64_t* __restrict__ in64, uint64_t n,
+                                                           const uint64_t* __restrict__ tile_base,
+                                                           uint64_t* __restrict__ out) {
+  __shared__ uint64_t s_w[SCAN_BLOCK / 64];
+  // thread t takes items [t * SCAN_ITEMS, (t + 1) * SCAN_ITEMS) of the tile
+  const uint64_t i0 = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
+  uint64_t v[SCAN_ITEMS], sum = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < SCAN_ITEMS; ++j) { v[j] = scan_item(in32, in64, n, i0 + j); sum += v[j]; }
+  uint64_t tot;
+  uint64_t run = tile_base[blockIdx.x] + block_incl_scan_u64<SCAN_BLOCK>(sum, s_w, tot) - sum;
+#pragma unroll
+  for (uint32_t j = 0; j < SCAN_ITEMS; ++j) {
+    if (i0 + j <= n) out[i0 + j] = run;
+    run += v[j];
+  }
+}
+uint64_t excl_scan_scratch_words(uint64_t n) { return (n + 1 + SCAN_TILE - 1) / SCAN_TILE; }
+void launch_excl_scan(const uint32_t* in32, const uint64_t* in64, uint64_t n, uint64_t* out, uint64_t* scratch,
+                      hipStream_t st) {
+  const uint64_t nt = excl_scan_scratch_words(n);
+  hipLaunchKernelGGL(k_scan_reduce, dim3((uint32_t)nt), dim3(SCAN_BLOCK), 0, st, in32, in64, n, scratch);
+  hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(1024), 0, st, scratch, nt);
+  hipLaunchKernelGGL(k_scan_apply, dim3((uint32_t)nt), dim3(SCAN_BLOCK), 0, st, in32, in64, n, scratch, out);
+}
+
 }  // namespace pbgpu
