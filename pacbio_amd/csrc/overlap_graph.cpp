@@ -123,23 +123,26 @@ void ReadGraph::traverse(std::ostream* dot) {
     }
   }
   sorted_.resize(n);
+  state_.resize(n);
   for (size_t i = 0; i < n; ++i) {
     const int it = sort_nodes_[i];
     const unitig_list& nm = *coords[it].name;
-    sorted_[i] = SortedNode{nodes_[it].imp_s, nodes_[it].imp_e, coords[it].avg_err, it, (int)nm.size(),
+    sorted_[i] = SortedNode{nodes_[it].imp_s, nodes_[it].imp_e, coords[it].avg_err, nm.data(),
+                            &pul_[pre_off_[it]], &pco_[pre_off_[it]], it, (int)nm.size(),
                             nm.empty() ? 0u : nm[0],
-                            p_.maximize_bases ? coords[it].sr_cover : (unsigned)coords[it].nb_mers, nm.data()};
+                            p_.maximize_bases ? coords[it].sr_cover : (unsigned)coords[it].nb_mers};
+    const Node& d = nodes_[it];
+    state_[i] = PathState{d.imp_s, d.lpath, d.lstart, d.lprev, d.lunitigs, d.start_node, d.end_node};
   }
   for (size_t i = 0; i != n; ++i) {
-    const int it_i = sorted_[i].idx;
-    Node& ni = nodes_[it_i];
-    const Coord& ci = coords[it_i];
-    const double imp_e_i = sorted_[i].imp_e;
-    if (imp_e_i >= (double)ci.rl) continue;  // hanging off the 3' end
-    const unitig_list& name_i = *ci.name;
-    const int sa = (int)name_i.size();
-    const unitig_t* a = name_i.data();
-    const double err_i = sorted_[i].avg_err;
+    const SortedNode& si_ = sorted_[i];
+    const int it_i = si_.idx;
+    PathState& ni = state_[i];
+    const double imp_e_i = si_.imp_e;
+    if (imp_e_i >= (double)coords[it_i].rl) continue;  // hanging off the 3' end
+    const int sa = si_.nsz;
+    const unitig_t* a = si_.name;
+    const double err_i = si_.avg_err;
     for (size_t j = i + 1; j != n; ++j) {
       const SortedNode& sj = sorted_[j];
       if (sj.imp_s <= 1) continue;               // hanging off the 5' end
@@ -163,26 +166,33 @@ void ReadGraph::traverse(std::ostream* dot) {
       if (sb == sa && (sj.name == a || std::equal(a, a + sa, sj.name))) continue;
       const int it_j = sj.idx;
       // nb_u_overlap <= |name_j|, so every unitig of the sums is in name j
-      int u_overlap_len = (int)pul_[pre_off_[it_j] + nb_u_overlap];
-      const int common_overlap = (int)pco_[pre_off_[it_j] + nb_u_overlap];
+      int u_overlap_len = (int)sj.pul[nb_u_overlap];
+      const int common_overlap = (int)sj.pco[nb_u_overlap];
       u_overlap_len = (int)((unsigned)u_overlap_len - (unsigned)(nb_u_overlap - 1) * (k - 1));
       if (u_overlap_len > play * position_len + error || position_len > play * (u_overlap_len + error)) continue;
       // an overlap between nodes i and j
-      Node& nj = nodes_[it_j];
+      PathState& nj = state_[j];
       ni.end_node = false;
       nj.start_node = false;
-      uf_.unite(it_i, it_j);
+      // (nodes already under one parent are already one set: unite would change no root)
+      if (uf_.parent[it_i] != uf_.parent[it_j]) uf_.unite(it_i, it_j);
       const int nlpath = (int)((unsigned)ni.lpath + sj.lp_add - (unsigned)common_overlap);
-      const Node& si = ni.lstart == -1 ? ni : nodes_[ni.lstart];
-      const Node& sjn = nj.lstart == -1 ? nj : nodes_[nj.lstart];
-      if (nlpath > nj.lpath || (nlpath == nj.lpath && (nj.lstart == -1 || si.imp_s > sjn.imp_s))) {
+      // ls_imp_s: the implied start of the node's path start (nodes_[lstart].imp_s, or its own)
+      if (nlpath > nj.lpath || (nlpath == nj.lpath && (nj.lstart == -1 || ni.ls_imp_s > nj.ls_imp_s))) {
         nj.lpath = nlpath;
         nj.lstart = ni.lstart == -1 ? it_i : ni.lstart;
+        nj.ls_imp_s = ni.ls_imp_s;
         nj.lprev = it_i;
         nj.lunitigs = ni.lunitigs + sb - nb_u_overlap;
       }
       if (dot) *dot << "n" << it_i << " -> n" << it_j << " [tooltip=\"...\", label=\"" << common_overlap << "\"];\n";
     }
+  }
+  for (size_t i = 0; i < n; ++i) {
+    Node& d = nodes_[sorted_[i].idx];
+    const PathState& ps = state_[i];
+    d.lpath = ps.lpath; d.lstart = ps.lstart; d.lprev = ps.lprev; d.lunitigs = ps.lunitigs;
+    d.start_node = ps.start_node; d.end_node = ps.end_node;
   }
 }
 

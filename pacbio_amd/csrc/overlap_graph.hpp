@@ -119,14 +119,22 @@ class ReadGraph {
   std::vector<double> weights_;
   std::vector<std::pair<int, MegaRead>> comp_;  // per component root (ascending), its mega-read
   std::vector<const MegaRead*> mega_reads_;
-  // traverse()'s per-read scratch: prefix sums over each node's name, the sorted nodes
+  // traverse()'s per-read scratch: prefix sums over each node's name, the sorted
+  // nodes (read-only part, and the path state the traversal updates, in sorted order)
   struct SortedNode {
     double imp_s, imp_e, avg_err;
+    const unitig_t* name;
+    const uint32_t *pul, *pco;  // its prefix sums
     int idx, nsz;        // node index, unitigs in its name
     unitig_t u0;         // first unitig of its name
     unsigned lp_add;     // its path length contribution (sr_cover with -b, else nb_mers)
-    const unitig_t* name;
   };
+  struct PathState {
+    double ls_imp_s;     // imp_s of the node's path start (lstart, or itself)
+    int lpath, lstart, lprev, lunitigs;
+    bool start_node, end_node;
+  };
+  std::vector<PathState> state_;
   std::vector<size_t> pre_off_;
   std::vector<uint32_t> pul_, pco_;
   std::vector<SortedNode> sorted_;
