@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PBGPU_ABI_VERSION 4
+#define PBGPU_ABI_VERSION 5
 
 typedef enum pbgpu_status {
   PBGPU_OK = 0,
@@ -178,6 +178,9 @@ typedef struct {
   uint64_t n_info;
   const int32_t* kmers_info;
   const int32_t* bases_info;
+  /* create_mega_reads' overlap graph of every record, in record order, when the
+   * aligner has pbgpu_aligner_set_graph on (else NULL); see pbgpu_graph_node */
+  const struct pbgpu_graph_node* graph;
 } pbgpu_coords_batch;
 
 /* Host batch in, host records out (synchronous). */
@@ -234,6 +237,9 @@ typedef struct {
   uint64_t n_filter;
   /* lis points written by the timed k_lis slot (tier-0 strands) */
   uint64_t l0_points;
+  /* overlap graph (pbgpu_aligner_set_graph): device time, records traversed on the device */
+  double   ms_graph;
+  uint64_t graph_records;
 } pbgpu_stats;
 pbgpu_status pbgpu_aligner_get_stats(const pbgpu_aligner* al, pbgpu_stats* s);
 pbgpu_status pbgpu_aligner_reset_stats(pbgpu_aligner* al);
@@ -284,6 +290,45 @@ uint64_t pbgpu_rccl_comm_last_bytes(const pbgpu_comm* comm);
 pbgpu_status pbgpu_align_resident_shard(pbgpu_aligner* al, const pbgpu_reads* reads);
 /* Host-side merge (no device work); the result is freed with pbgpu_coords_free. */
 pbgpu_status pbgpu_coords_merge(const pbgpu_coords_batch* const* parts, uint64_t n_parts, pbgpu_coords_batch** out);
+
+/* ---------------------------------------------------------- overlap graph
+ * create_mega_reads' per-read overlap graph traversal on the device
+ * (overlap_graph::traverse, overlap_graph.cc:7-59, with node_info::reset,
+ * overlap_graph.hpp:24-34, and union_find.cc): with it on, every alignment
+ * also leaves, per record, the node state the reference's traverse() ends with
+ * -- longest path, its start and previous node, its unitig count, the
+ * start / end node flags and the union-find root -- so the host only collects
+ * the components, tiles and prints (create_mega_reads.cc:79-89).  Node indices
+ * are read-local record indices (the records of a read in pbgpu_coords_batch
+ * order).  A read with more records than the device traversal holds is marked
+ * PBGPU_GRAPH_HOST and left to the host. */
+typedef struct {
+  double overlap_play;            /* -O, --overlap-play */
+  double nb_errors;               /* -e, --errors */
+  uint32_t k_len;                 /* -k, --k-mer (k-unitigs) */
+  int32_t maximize_bases;         /* -b, --bases: path length in bases (sr_cover), else k-mers */
+  /* every super-read name as its unitig list (super_read_name::parse,
+   * super_read_name.cc:74-90): unitig u = id << 1 | (orientation 'R');
+   * n_sr + 1 offsets into units; a name that does not parse is empty */
+  uint64_t n_sr;
+  const uint64_t* name_offsets;
+  const uint32_t* name_units;
+  /* unitig lengths (-l / -u), indexed by unitig id; ids past the end count 0 */
+  const int32_t* unitig_lengths;
+  uint64_t n_unitigs;
+} pbgpu_graph_params;
+/* p = NULL turns it off.  Whole (unsharded) index only. */
+pbgpu_status pbgpu_aligner_set_graph(pbgpu_aligner* al, const pbgpu_graph_params* p);
+typedef struct pbgpu_graph_node {
+  int32_t  lpath;                 /* node_info::lpath */
+  int32_t  lstart, lprev;         /* -1 = none */
+  int32_t  lunitigs;
+  uint32_t root;                  /* union-find root of the node's component */
+  uint32_t flags;                 /* PBGPU_GRAPH_* */
+} pbgpu_graph_node;
+#define PBGPU_GRAPH_START 1u          /* node_info::start_node */
+#define PBGPU_GRAPH_END   2u          /* node_info::end_node */
+#define PBGPU_GRAPH_HOST  0x80000000u /* not traversed on the device: the host traverses the read */
 
 /* ---------------------------------------------------------------- details
  * --details (print_details, jf_aligner.cc:72-108): with details enabled, each
@@ -394,6 +439,10 @@ typedef struct {
    * W / P) of the W, so with one index per part each part runs on its own
    * device).  Plain FASTA input only; fixed at pbgpu_runner_create. */
   uint32_t n_parts;
+  /* With records_fn: create_mega_reads' overlap graph on the device for every
+   * batch (pbgpu_aligner_set_graph on each aligner; the records consumer gets
+   * pbgpu_coords_batch.graph).  NULL = off.  Fixed at pbgpu_runner_create. */
+  const pbgpu_graph_params* graph;
 } pbgpu_run_params;
 
 typedef struct {

@@ -140,7 +140,8 @@ static char* mega_reads_batch(void* user, const pbgpu_index* ix, const pbgpu_coo
             c.n_info = R.n_info;
             coords.push_back(c);
           }
-          g.process(coords, names[r], os, C.dot ? &ds : nullptr);
+          g.process(coords, names[r], os, C.dot ? &ds : nullptr,
+                    cb->graph ? cb->graph + cb->read_offsets[r] : nullptr);
         }
         out[pi] = os.str();
         if (C.dot) dout[pi] = ds.str();
@@ -190,7 +191,9 @@ int main(int argc, char** argv) {
   std::vector<const char*> srs, pbs;
   std::vector<int> devices;
   uint64_t batch_bases = 64ull << 20;
-  enum { O_PSA = 256, O_DOT, O_SC, O_SF, O_CAP, O_WIN, O_MAXM, O_MAXC, O_TRIM, O_DEVS, O_BATCH, O_STREAMS, O_TIMING, O_CACHE };
+  bool host_graph = false;  // --host-graph: traverse the overlap graph on the host (else on the GPU)
+  enum { O_PSA = 256, O_DOT, O_SC, O_SF, O_CAP, O_WIN, O_MAXM, O_MAXC, O_TRIM, O_DEVS, O_BATCH, O_STREAMS, O_TIMING, O_CACHE,
+         O_HOSTG };
   static struct option lo[] = {
       {"size", 1, 0, 's'}, {"mer", 1, 0, 'm'}, {"fine-mer", 1, 0, 'F'}, {"psa-min", 1, 0, O_PSA},
       {"unitigs-lengths", 1, 0, 'l'}, {"unitigs-sequences", 1, 0, 'u'}, {"k-mer", 1, 0, 'k'},
@@ -200,7 +203,8 @@ int main(int argc, char** argv) {
       {"mers-matching", 1, 0, 'M'}, {"max-match", 0, 0, O_MAXM}, {"max-count", 1, 0, O_MAXC}, {"bases", 0, 0, 'b'},
       {"density", 1, 0, 'd'}, {"min-length", 1, 0, 'L'}, {"tiling", 1, 0, 'T'}, {"trim", 1, 0, O_TRIM},
       {"superreads", 1, 0, 'r'}, {"pacbio", 1, 0, 'p'}, {"devices", 1, 0, O_DEVS}, {"batch-bases", 1, 0, O_BATCH},
-      {"streams", 1, 0, O_STREAMS}, {"timing", 0, 0, O_TIMING}, {"index-cache", 1, 0, O_CACHE}, {0, 0, 0, 0}};
+      {"streams", 1, 0, O_STREAMS}, {"timing", 0, 0, O_TIMING}, {"index-cache", 1, 0, O_CACHE},
+      {"host-graph", 0, 0, O_HOSTG}, {0, 0, 0, 0}};
   int c;
   while ((c = getopt_long(argc, argv, "s:m:F:l:u:k:t:o:O:e:B:M:bd:L:T:r:p:", lo, nullptr)) != -1) {
     switch (c) {
@@ -263,6 +267,7 @@ int main(int argc, char** argv) {
     case O_STREAMS: streams = std::max(1u, parse_u32(optarg, "--streams")); break;
     case O_TIMING: timing = true; break;
     case O_CACHE: index_cache = optarg; break;
+    case O_HOSTG: host_graph = true; break;
     default: die("bad option (see create_mega_reads_cmdline.yaggo)");
     }
   }
@@ -329,6 +334,27 @@ int main(int argc, char** argv) {
   rp.host_threads = (int)threads;
   rp.records_fn = mega_reads_batch;
   rp.records_user = &C;
+  // the overlap graph's traversal on the GPU (the host keeps --dot runs, whose edge
+  // lines come out in traversal order, and --host-graph)
+  std::vector<uint64_t> name_off(C.fwd.size() + 1, 0);
+  std::vector<uint32_t> name_units;
+  pbgpu_graph_params gp{};
+  if (!host_graph && !C.dot) {
+    for (size_t i = 0; i < C.fwd.size(); ++i) {
+      name_units.insert(name_units.end(), C.fwd[i].begin(), C.fwd[i].end());
+      name_off[i + 1] = name_units.size();
+    }
+    gp.overlap_play = C.gp.overlap_play;
+    gp.nb_errors = C.gp.nb_errors;
+    gp.k_len = C.gp.k_len;
+    gp.maximize_bases = C.gp.maximize_bases;
+    gp.n_sr = C.fwd.size();
+    gp.name_offsets = name_off.data();
+    gp.name_units = name_units.data();
+    gp.unitig_lengths = ul32.data();
+    gp.n_unitigs = ul32.size();
+    rp.graph = &gp;
+  }
   pbgpu_run_stats st{};
   const pbgpu_status rs = pbgpu_run(per_entry.data(), per_entry.size(), &ap, &rp, &st);
   const std::string err = rs == PBGPU_OK ? "" : pbgpu_last_error();

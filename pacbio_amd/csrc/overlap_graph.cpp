@@ -274,7 +274,7 @@ void ReadGraph::components(std::ostream* dot) {
            << std::setprecision(2) << mr.density << "\"" << color << "];\n";
     }
     if (!node.end_node || mr.density < p_.min_density || (mr.tiling_end - mr.tiling_start) < p_.min_len) continue;
-    const int root = uf_.root(i);
+    const int root = dev_ ? (int)dev_[i].root : uf_.root(i);
     auto it = std::lower_bound(comp_.begin(), comp_.end(), root,
                                [](const std::pair<int, MegaRead>& a, int r) { return a.first < r; });
     if (it == comp_.end() || it->first != root) {
@@ -453,9 +453,23 @@ void ReadGraph::print(std::ostream& out, const std::vector<int>& order, std::ost
 // leave ties in an unspecified order; here every sort is stable (ties keep the
 // input order: records in (rs, re, ql, sr_index, emit) order).
 void ReadGraph::process(const std::vector<Coord>& coords, const std::string& pb_name, std::ostream& out,
-                        std::ostream* dot) {
+                        std::ostream* dot, const pbgpu_graph_node* dev) {
   coords_ = &coords;
   const int n = (int)coords.size();
+  dev_ = dev && n && !dot && !(dev[0].flags & PBGPU_GRAPH_HOST) ? dev : nullptr;
+  if (dev_) {  // traversed on the device: its node state, the host's implied positions
+    nodes_.resize(n);
+    for (int i = 0; i < n; ++i) {
+      const Coord& c = coords[i];
+      const pbgpu_graph_node& g = dev_[i];
+      Node& d = nodes_[i];
+      d.start_node = (g.flags & PBGPU_GRAPH_START) != 0;
+      d.end_node = (g.flags & PBGPU_GRAPH_END) != 0;
+      d.imp_s = c.stretch + c.offset;
+      d.imp_e = c.stretch * (double)c.ql + c.offset;
+      d.lstart = g.lstart; d.lprev = g.lprev; d.lpath = g.lpath; d.lunitigs = g.lunitigs;
+    }
+  } else {
   // overlap_graph::thread::reset (overlap_graph.hpp:177-196) + node_info::reset (:24-34)
   nodes_.resize(n);
   sort_nodes_.resize(n);
@@ -483,6 +497,7 @@ void ReadGraph::process(const std::vector<Coord>& coords, const std::string& pb_
     }
   }
   traverse(dot);
+  }
   components(dot);  // term_node_per_comp
   switch (p_.tiling) {
     case Tiling::GREEDY:

@@ -17,6 +17,8 @@
 #include <string>
 #include <vector>
 
+#include "../../include/pbgpu.h"  // pbgpu_graph_node: the traversal done on the device
+
 namespace megareads {
 
 // super_read_name::u_id_ori (super_read_name.hpp:16-37): bit 0 = orientation (R),
@@ -97,7 +99,10 @@ struct Params {
 class ReadGraph {
  public:
   explicit ReadGraph(const Params& p) : p_(p) {}
-  void process(const std::vector<Coord>& coords, const std::string& pb_name, std::ostream& out, std::ostream* dot);
+  // dev: the read's nodes as the device traversal left them (pbgpu_aligner_set_graph),
+  // one per record; NULL, or a read marked PBGPU_GRAPH_HOST, is traversed here
+  void process(const std::vector<Coord>& coords, const std::string& pb_name, std::ostream& out, std::ostream* dot,
+               const pbgpu_graph_node* dev = nullptr);
 
  private:
   friend struct ReadGraphTest;  // tests/cpp/og_driver.cpp (tiling properties)
@@ -135,6 +140,7 @@ class ReadGraph {
     bool start_node, end_node;
   };
   std::vector<PathState> state_;
+  const pbgpu_graph_node* dev_ = nullptr;  // the current read's device traversal (roots), or NULL
   std::vector<size_t> pre_off_;
   std::vector<uint32_t> pul_, pco_;
   std::vector<SortedNode> sorted_;

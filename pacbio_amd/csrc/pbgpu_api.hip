@@ -1600,6 +1600,34 @@ static void fine_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   records_stage(al, n, (uint32_t)rec_done, false);
 }
 
+// create_mega_reads' overlap graph of the final records (pbgpu_aligner_set_graph):
+// implied positions and name prefix sums per record, the per-read sort, the traversal.
+static void graph_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
+  hipStream_t st = al->st;
+  const uint32_t n = (uint32_t)rd->n_reads;
+  const uint64_t nrec = al->last_records;
+  GraphDev G{};
+  G.recs = al->recs_sorted.p; G.rec_off = al->rec_off.p; G.roff = rd->off.p;
+  G.noff = al->g_noff.p; G.units = al->g_units.p; G.ul = al->g_ul.p; G.n_ul = al->g_n_ul;
+  G.info_m = al->info_m.p; G.info_b = al->info_b.p;
+  G.play = al->g_play; G.nb_errors = al->g_errors; G.k = al->g_k; G.bases = al->g_bases;
+  // PBGPU_GRAPH_NMAX (tests): a lower cap on the records of a read traversed on the device
+  G.nmax = GRAPH_NMAX;
+  if (const char* e = getenv("PBGPU_GRAPH_NMAX")) G.nmax = (uint32_t)std::min<long>(GRAPH_NMAX, std::max(0l, atol(e)));
+  al->g_poff.ensure(nrec + 1); al->g_sizes.ensure(nrec + 1);
+  G.poff = al->g_poff.p;
+  launch_graph_sizes(G, nrec, al->g_sizes.p, (uint64_t*)temp_storage(al->tmp, excl_scan_scratch_words(nrec) * 8), st);
+  HIPCHK(hipGetLastError());
+  uint64_t tot = 0;
+  HIPCHK(hipMemcpyAsync(&tot, al->g_poff.p + nrec, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  al->g_pre.ensure(3 * tot + 3); al->g_imp.ensure(nrec + 1); al->g_desc.ensure(nrec + 1); al->g_out.ensure(nrec + 1);
+  G.pul = al->g_pre.p; G.pco = al->g_pre.p + tot + 1; G.ounits = al->g_pre.p + 2 * (tot + 1);
+  G.imp = al->g_imp.p; G.desc = al->g_desc.p; G.out = al->g_out.p;
+  launch_graph(G, n, nrec, st);
+  HIPCHK(hipGetLastError());
+}
+
 void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, uint32_t* gcount) {
   const pbgpu_index* ix = al->ix;
   const IndexView v = ix->view();
@@ -1860,6 +1888,11 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
     fine_stage(al, rd);
     HIPCHK(hipEventRecord(al->ev[17], st));
   }
+  if (al->graph) {
+    HIPCHK(hipEventRecord(al->ev[18], st));
+    graph_stage(al, rd);
+    HIPCHK(hipEventRecord(al->ev[19], st));
+  }
   unsigned long long sv[ST_N];
   HIPCHK(hipMemcpyAsync(sv, al->stats.p, sizeof sv, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
@@ -1875,6 +1908,10 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
     al->acc.n_fine_hits += sv[ST_FINE_HITS];
     al->acc.n_fine_windows += nrec;
     al->acc.ms_fine += ev_ms(al->ev[16], al->ev[17]);
+  }
+  if (al->graph) {
+    al->acc.ms_graph += ev_ms(al->ev[18], al->ev[19]);
+    al->acc.graph_records += al->last_records;
   }
   al->acc.ms_seed += ev_ms(al->ev[0], al->ev[1]);
   al->acc.ms_group += ms_group;
@@ -1893,6 +1930,7 @@ struct coords_holder {
   std::vector<uint64_t> off;
   std::vector<pbgpu_record> recs;
   std::vector<int32_t> km, kb;
+  std::vector<pbgpu_graph_node> graph;
 };
 
 extern "C" {
@@ -1918,6 +1956,12 @@ pbgpu_status pbgpu_download(pbgpu_aligner* al, pbgpu_coords_batch** out) {
   }
   h->c.n_reads = n; h->c.n_records = nr; h->c.read_offsets = h->off.data(); h->c.records = h->recs.data();
   h->c.n_info = al->last_info; h->c.kmers_info = h->km.data(); h->c.bases_info = h->kb.data();
+  if (al->graph) {
+    static_assert(sizeof(pbgpu_graph_node) == sizeof(GraphNode), "graph node layout");
+    h->graph.resize(nr);
+    if (nr) HIPCHK(hipMemcpy(h->graph.data(), al->g_out.p, nr * sizeof(GraphNode), hipMemcpyDeviceToHost));
+    h->c.graph = h->graph.data();
+  }
   *out = &h.release()->c;
   return PBGPU_OK;
   API_CATCH
@@ -1975,6 +2019,31 @@ pbgpu_status pbgpu_coords_merge(const pbgpu_coords_batch* const* parts, uint64_t
   h->c.n_reads = n; h->c.n_records = h->recs.size(); h->c.read_offsets = h->off.data(); h->c.records = h->recs.data();
   h->c.n_info = h->km.size(); h->c.kmers_info = h->km.data(); h->c.bases_info = h->kb.data();
   *out = &h.release()->c;
+  return PBGPU_OK;
+  API_CATCH
+}
+
+pbgpu_status pbgpu_aligner_set_graph(pbgpu_aligner* al, const pbgpu_graph_params* p) {
+  if (!al) return fail(PBGPU_ERR_INVALID, "null argument");
+  if (!p) { al->graph = false; return PBGPU_OK; }
+  if (al->ix->n_shards > 1) return fail(PBGPU_ERR_UNSUPPORTED, "the device overlap graph runs on a whole index only");
+  if (p->n_sr != al->ix->n_sr) return fail(PBGPU_ERR_INVALID, "graph names: one unitig list per super-read of the index");
+  if (!p->name_offsets || (p->name_offsets[p->n_sr] && !p->name_units) || (p->n_unitigs && !p->unitig_lengths))
+    return fail(PBGPU_ERR_INVALID, "null graph array");
+  if (p->k_len == 0) return fail(PBGPU_ERR_INVALID, "graph k-mer length 0");
+  for (uint64_t i = 0; i < p->n_sr; ++i)
+    if (p->name_offsets[i + 1] < p->name_offsets[i] || p->name_offsets[i + 1] - p->name_offsets[i] > 0xFFFFu)
+      return fail(PBGPU_ERR_INVALID, "graph names: offsets not ascending, or a name of more than 65535 unitigs");
+  API_TRY
+  HIPCHK(hipSetDevice(al->ix->device));
+  const uint64_t nu = p->name_offsets[p->n_sr];
+  al->g_noff.ensure(p->n_sr + 1); al->g_units.ensure(nu + 1); al->g_ul.ensure(p->n_unitigs + 1);
+  HIPCHK(hipMemcpy(al->g_noff.p, p->name_offsets, (p->n_sr + 1) * 8, hipMemcpyHostToDevice));
+  if (nu) HIPCHK(hipMemcpy(al->g_units.p, p->name_units, nu * 4, hipMemcpyHostToDevice));
+  if (p->n_unitigs) HIPCHK(hipMemcpy(al->g_ul.p, p->unitig_lengths, p->n_unitigs * 4, hipMemcpyHostToDevice));
+  al->g_n_ul = p->n_unitigs;
+  al->g_play = p->overlap_play; al->g_errors = p->nb_errors; al->g_k = p->k_len; al->g_bases = p->maximize_bases != 0;
+  al->graph = true;
   return PBGPU_OK;
   API_CATCH
 }

@@ -233,7 +233,7 @@ struct pbgpu_aligner {
   bool have_result = false;
   // stats
   pbgpu_stats acc{};
-  hipEvent_t ev[18]{};
+  hipEvent_t ev[20]{};
   uint64_t hit_budget = 4000000000ull, rec_hint = 0, info_per_chain = 32;
   double chains_per_hit = 1.0 / 80;  // k_group tier estimate (C2: 1.1 x 1/90), refined after every batch
   dbuf<uint32_t> ovf_list, read_list;
@@ -260,6 +260,19 @@ struct pbgpu_aligner {
     std::vector<uint8_t> lis;
     void clear() { read.clear(); sr.clear(); nf.clear(); hoff.assign(1, 0); hits.clear(); lis.clear(); }
   } det;
+  // create_mega_reads' overlap graph (pbgpu_aligner_set_graph): names and unitig lengths
+  // on the device, per-batch scratch, the last alignment's nodes
+  bool graph = false;
+  double g_play = 0, g_errors = 0;
+  uint32_t g_k = 0;
+  int g_bases = 0;
+  uint64_t g_n_ul = 0;
+  dbuf<uint64_t> g_noff, g_poff;
+  dbuf<uint32_t> g_units, g_pre, g_sizes;
+  dbuf<GDesc> g_desc;
+  dbuf<int32_t> g_ul;
+  dbuf<double2> g_imp;
+  dbuf<GraphNode> g_out;
   // device coords text of the last alignment (pbgpu_format.hip)
   dbuf<uint32_t> fmt_len;
   dbuf<uint64_t> fmt_pos;

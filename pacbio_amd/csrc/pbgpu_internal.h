@@ -187,4 +187,47 @@ uint64_t excl_scan_scratch_words(uint64_t n);
 void launch_excl_scan(const uint32_t* in32, const uint64_t* in64, uint64_t n, uint64_t* out, uint64_t* scratch,
                       hipStream_t st);
 
+// create_mega_reads' overlap graph on the device (pbgpu_kernels.hip, k_graph_*):
+// node_info after overlap_graph::traverse for every record, in the record order
+// of recs_sorted (the layout of pbgpu_graph_node, include/pbgpu.h).
+struct GraphNode {
+  int32_t lpath, lstart, lprev, lunitigs;
+  uint32_t root, flags;
+};
+static_assert(sizeof(GraphNode) == 24, "GraphNode layout must match pbgpu_graph_node");
+constexpr uint32_t GRAPH_START = 1u, GRAPH_END = 2u, GRAPH_HOST = 1u << 31;  // flags
+constexpr uint32_t GRAPH_NMAX = 4096;  // records of a read traversed on the device (more: GRAPH_HOST)
+// a record in the per-read sorted order (k_graph's ring of sorted positions)
+struct GDesc {
+  double imp_s, imp_e, err;
+  uint64_t poff;               // its name's units and prefix sums
+  uint32_t idx, nsz, lp_add, pad;
+};
+struct GraphDev {
+  const Rec* recs;            // recs_sorted
+  const uint64_t* rec_off;    // per read, into recs
+  const uint64_t* roff;       // read offsets (read lengths)
+  const uint64_t* noff;       // super-read names: n_sr + 1 offsets into units
+  const uint32_t* units;      // unitig id << 1 | R (super_read_name::parse)
+  const int32_t* ul;          // unitig lengths
+  uint64_t n_ul;
+  const int32_t* info_m;      // kmers_info / bases_info
+  const int32_t* info_b;
+  double play, nb_errors;     // -O, -e
+  uint32_t k;                 // -k
+  int bases;                  // -b
+  uint32_t nmax;              // reads with more records go to the host (<= GRAPH_NMAX; tests lower it)
+  double2* imp;               // per record: implied start, end
+  uint64_t* poff;             // per record: its prefix sums' offset (nsz + 1 each)
+  uint32_t* pul;              // prefix sums of the unitig lengths along the name
+  uint32_t* pco;              // prefix sums of info[2u] - info[2u - 1]
+  uint32_t* ounits;           // the name's unitigs in the record's orientation (at poff)
+  GDesc* desc;                // per read, in sorted order
+  GraphNode* out;
+};
+// G.poff from the records' name sizes (then the caller sizes pul / pco by poff[n_recs])
+void launch_graph_sizes(const GraphDev& G, uint64_t n_recs, uint32_t* sizes, uint64_t* scan_scratch, hipStream_t st);
+// implied positions and prefix sums, per-read sort, traversal -> G.out
+void launch_graph(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hipStream_t st);
+
 }  // namespace pbgpu

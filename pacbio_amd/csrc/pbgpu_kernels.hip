@@ -669,25 +669,8 @@ __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_
           // no branch around the load (windows past the group's end load occ[0]): the
           // compiler counts the loads in flight only when every path issues them
           uint32_t lo = 0;  // s_off[0] = 0: fixed depth, branch-free
-#ifndef PBGPU_EXP_GROUP_LINLOC
 #pragma unroll
           for (uint32_t stp = B / 2; stp >= 1; stp >>= 1) lo = s_off[lo + stp] <= h ? lo + stp : lo;
-#else  // experiment: the window start's record by a wave-uniform search, then <= 3 linear steps
-          {
-            const uint32_t h0 = h - lane;
-#pragma unroll
-            for (uint32_t stp = B / 2; stp >= 1; stp >>= 1) lo = s_off[lo + stp] <= h0 ? lo + stp : lo;
-#pragma unroll
-            for (int t = 0; t < 3; ++t) {
-              const uint32_t nx = lo + 1 < B ? lo + 1 : lo;
-              lo = (nx != lo && s_off[nx] <= h) ? nx : lo;
-            }
-            if (lo + 1 < B && s_off[lo + 1] <= h) {
-              lo = 0;
-              for (uint32_t stp = B / 2; stp >= 1; stp >>= 1) lo = s_off[lo + stp] <= h ? lo + stp : lo;
-            }
-          }
-#endif
           const uint32_t local = h - s_off[lo];
           const uint2 np = s_np[lo];
           const ulonglong2 pp = s_ptr[lo];
@@ -2848,6 +2831,259 @@ void launch_excl_scan(const uint32_t* in32, const uint64_t* in64, uint64_t n, ui
   hipLaunchKernelGGL(k_scan_reduce, dim3((uint32_t)nt), dim3(SCAN_BLOCK), 0, st, in32, in64, n, scratch);
   hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(1024), 0, st, scratch, nt);
   hipLaunchKernelGGL(k_scan_apply, dim3((uint32_t)nt), dim3(SCAN_BLOCK), 0, st, in32, in64, n, scratch, out);
+}
+
+// ========================================================== overlap graph
+// create_mega_reads' per-read overlap graph (overlap_graph.cc:7-59,
+// overlap_graph::traverse, with node_info::reset, overlap_graph.hpp:24-34, and
+// union_find.cc) on the records of recs_sorted: the host then only collects the
+// components, tiles and prints (create_mega_reads.cc:79-89).  The double
+// arithmetic restates the reference's operation order with _rn intrinsics (no
+// contraction); the record order and the stable sort by implied position are
+// the host's.
+DEV uint32_t graph_unit(const GraphDev& G, uint32_t sr, uint32_t nsz, bool rev, uint32_t u) {
+  // super_read_name of the record's orientation: the bwd name is the fwd one reversed,
+  // each unitig flipped (super_read_name.cc:38-47)
+  const uint64_t o = G.noff[sr];
+  return rev ? G.units[o + nsz - 1 - u] ^ 1u : G.units[o + u];
+}
+DEV uint32_t graph_nsz(const GraphDev& G, uint32_t sr) { return (uint32_t)(G.noff[sr + 1] - G.noff[sr]); }
+__global__ void k_graph_sizes(GraphDev G, uint64_t n, uint32_t* sizes) {
+  for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < n; q += (uint64_t)gridDim.x * blockDim.x)
+    sizes[q] = graph_nsz(G, G.recs[q].sr) + 1;
+}
+// per record: implied start / end (overlap_graph.hpp:24-34), its name's unitigs in
+// its orientation, and the prefix sums over them of the unitig lengths (ulen: 0 past
+// the lengths, as the host's) and of info[2u] - info[2u - 1] (kmers_info, or
+// bases_info with -b; 0 past n_info)
+__global__ void k_graph_prep(GraphDev G, uint64_t n) {
+  for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < n; q += (uint64_t)gridDim.x * blockDim.x) {
+    const Rec R = G.recs[q];
+    G.imp[q] = make_double2(__dadd_rn(R.stretch, R.offset), __dadd_rn(__dmul_rn(R.stretch, (double)R.ql), R.offset));
+    const uint32_t nsz = graph_nsz(G, R.sr);
+    const bool rev = (R.flags & 2u) != 0;
+    const int32_t* info = G.bases ? G.info_b : G.info_m;
+    auto info_at = [&](uint32_t i) -> uint32_t { return i < R.n_info ? (uint32_t)info[R.info_off + i] : 0u; };
+    const uint64_t po = G.poff[q];
+    uint32_t a = 0, c = 0;
+    G.pul[po] = 0; G.pco[po] = 0;
+    for (uint32_t u = 0; u < nsz; ++u) {
+      const uint32_t un = graph_unit(G, R.sr, nsz, rev, u);
+      G.ounits[po + u] = un;
+      const uint32_t id = un >> 1;
+      a += id < G.n_ul ? (uint32_t)G.ul[id] : 0u;
+      c += info_at(2 * u) - (u > 0 ? info_at(2 * u - 1) : 0u);
+      G.pul[po + u + 1] = a; G.pco[po + u + 1] = c;
+    }
+  }
+}
+// order-preserving key of a double (finite; -0 sorts as +0, as operator< sees them)
+DEV uint64_t graph_dkey(double x) {
+  const uint64_t b = (uint64_t)__double_as_longlong(__dadd_rn(x, 0.0));
+  return (b >> 63) ? ~b : b | (1ull << 63);
+}
+// per read: records by (imp_s, imp_e), ties in record order (the host's stable_sort of
+// sort_nodes), written out as descriptors in that order
+constexpr uint32_t GRAPH_SORT_BLOCK = 256;
+__global__ __launch_bounds__(GRAPH_SORT_BLOCK) void k_graph_sort(GraphDev G, uint32_t n_reads) {
+  __shared__ uint64_t s_hi[GRAPH_NMAX], s_lo[GRAPH_NMAX];
+  __shared__ uint16_t s_ex[GRAPH_NMAX];
+  const uint32_t r = blockIdx.x;
+  if (r >= n_reads) return;
+  const uint64_t b = G.rec_off[r];
+  const uint32_t n = (uint32_t)(G.rec_off[r + 1] - b);
+  if (n == 0 || n > G.nmax) return;
+  uint32_t np2 = 1;
+  while (np2 < n) np2 <<= 1;
+  for (uint32_t i = threadIdx.x; i < np2; i += GRAPH_SORT_BLOCK) {
+    if (i < n) {
+      const double2 m = G.imp[b + i];
+      s_hi[i] = graph_dkey(m.x); s_lo[i] = graph_dkey(m.y); s_ex[i] = (uint16_t)i;
+    } else {
+      s_hi[i] = ~0ull; s_lo[i] = ~0ull; s_ex[i] = 0xFFFFu;
+    }
+  }
+  __syncthreads();
+  bitonic_keys<GRAPH_SORT_BLOCK>(s_hi, s_lo, s_ex, np2);
+  for (uint32_t p = threadIdx.x; p < n; p += GRAPH_SORT_BLOCK) {
+    const uint32_t i = s_ex[p];
+    const Rec& R = G.recs[b + i];
+    const double2 m = G.imp[b + i];
+    G.desc[b + p] = GDesc{m.x, m.y, R.avg_err, G.poff[b + i], i, graph_nsz(G, R.sr),
+                          G.bases ? R.sr_cover : (uint32_t)R.nb_mers, 0u};
+  }
+}
+// One wave per read: the reference's traversal with the sorted nodes' j loop 64 at a
+// time.  Per node i (sorted order, so every edge into i is already applied): lanes
+// take j = i + 1 + lane, ...; the first j that is neither skipped nor long enough
+// (the reference's break) ends the scan; lanes before it test the names' dovetail
+// overlap, the same-name case and the play / error bounds and update their own
+// node's longest path (distinct j per lane, as the reference's updates are); the
+// edges are united in j order by one lane (union by rank with path compression:
+// the reference's component roots).
+// LDS holds a ring of GRING sorted positions -- descriptor, up to GRING_U unitigs,
+// path state -- refilled 64 at a time as i advances (a node's scan reaches at least
+// GRING - 63 positions ahead; a longer one hands the whole read to the host), and the
+// union-find of the read's nodes.
+constexpr uint32_t GRING = 256, GRING_U = 8;
+__global__ __launch_bounds__(64) void k_graph(GraphDev G, uint32_t n_reads) {
+  __shared__ GDesc s_d[GRING];
+  __shared__ uint32_t s_u[GRING * GRING_U];
+  __shared__ int32_t s_lp[GRING], s_lun[GRING], s_lst[GRING], s_lpv[GRING];
+  __shared__ double s_lsi[GRING];  // implied start of the node's path start (lstart's, or its own)
+  __shared__ uint8_t s_fl[GRING];
+  __shared__ uint16_t s_par[GRAPH_NMAX];
+  __shared__ uint8_t s_rank[GRAPH_NMAX];
+  const uint32_t r = blockIdx.x;
+  if (r >= n_reads) return;
+  const uint32_t lane = threadIdx.x;
+  const uint64_t b = G.rec_off[r];
+  const uint32_t n = (uint32_t)(G.rec_off[r + 1] - b);
+  if (n == 0) return;
+  if (n > G.nmax) {  // the host traverses this read
+    for (uint32_t i = lane; i < n; i += 64) G.out[b + i] = GraphNode{0, -1, -1, 0, i, GRAPH_HOST};
+    return;
+  }
+  const double rl = (double)(G.roff[r + 1] - G.roff[r]);
+  const double play = G.play, kd = (double)G.k;
+  const uint32_t km1 = G.k - 1;
+  for (uint32_t i = lane; i < n; i += 64) { s_par[i] = (uint16_t)i; s_rank[i] = 0; }
+  auto load_pos = [&](uint32_t p) {  // node_info::reset (overlap_graph.hpp:24-34) of sorted position p
+    const uint32_t sl = p % GRING;
+    const GDesc d = G.desc[b + p];
+    s_d[sl] = d;
+    const uint32_t m = d.nsz < GRING_U ? d.nsz : GRING_U;
+    for (uint32_t u = 0; u < m; ++u) s_u[sl * GRING_U + u] = G.ounits[d.poff + u];
+    s_lp[sl] = (int32_t)d.lp_add; s_lun[sl] = (int32_t)d.nsz; s_lst[sl] = -1; s_lpv[sl] = -1;
+    s_lsi[sl] = d.imp_s; s_fl[sl] = (uint8_t)(GRAPH_START | GRAPH_END);
+  };
+  auto flush_pos = [&](uint32_t p) {
+    const uint32_t sl = p % GRING;
+    G.out[b + s_d[sl].idx] = GraphNode{s_lp[sl], s_lst[sl], s_lpv[sl], s_lun[sl], 0u, s_fl[sl]};
+  };
+  uint32_t loaded = n < GRING ? n : GRING, flushed = 0;
+  for (uint32_t p = lane; p < loaded; p += 64) load_pos(p);
+  __syncthreads();
+  bool overflow = false;
+  for (uint32_t i = 0; i < n; ++i) {
+    if ((i & 63) == 0 && i >= 64 && loaded < n) {  // positions [i - 64, i) are done: their slots take the next 64
+      flush_pos(i - 64 + lane);
+      flushed = i;
+      if (loaded + lane < n) load_pos(loaded + lane);
+      loaded = loaded + 64 < n ? loaded + 64 : n;
+      __syncthreads();
+    }
+    const uint32_t si = i % GRING;
+    const GDesc di = s_d[si];
+    if (di.imp_e >= rl) continue;  // hanging off the 3' end
+    const uint32_t it_i = di.idx, sa = di.nsz;
+    const int32_t lp_i = s_lp[si], lun_i = s_lun[si], lst_i = s_lst[si];
+    const double lsi_i = s_lsi[si];
+    auto unit_i = [&](uint32_t t) -> uint32_t { return sa <= GRING_U ? s_u[si * GRING_U + t] : G.ounits[di.poff + t]; };
+    bool any_edge = false;
+    for (uint32_t j0 = i + 1; j0 < n; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      const bool act = j < n;
+      if (__ballot(act && j >= loaded)) { overflow = true; break; }  // past the ring
+      const uint32_t sj = (act ? j : i) % GRING;
+      const GDesc dj = s_d[sj];
+      const bool skip = (dj.imp_s <= 1.0) | (di.imp_e > __dadd_rn(dj.imp_e, 31.0));  // off the 5' end | not advancing
+      const double position_len = __dadd_rn(di.imp_e, -dj.imp_s);
+      const double error = __dmul_rn(G.nb_errors, __dadd_rn(di.err, dj.err));
+      const bool brk = act & !skip & (__dadd_rn(__dmul_rn(position_len, play), error) < kd);
+      const uint64_t bm = __ballot(brk);
+      const uint32_t fb = bm ? (uint32_t)__ffsll((long long)bm) - 1 : 64u;
+      bool edge = false;
+      int32_t nb = 0, common = 0;
+      const uint32_t sb = dj.nsz;
+      if (act & !skip & (lane < fb) & (sa >= 2) & (sb >= 2)) {
+        auto unit_j = [&](uint32_t q) -> uint32_t { return sb <= GRING_U ? s_u[sj * GRING_U + q] : G.ounits[dj.poff + q]; };
+        // super_read_name::overlap (super_read_name.cc:49-72)
+        const uint32_t u0 = unit_j(0);
+        const int t0 = (int)sa - (int)sb + 1;
+        for (uint32_t t = t0 > 1 ? (uint32_t)t0 : 1u; t < sa; ++t) {
+          if (unit_i(t) != u0) continue;
+          uint32_t q = t + 1;
+          while (q < sa && unit_i(q) == unit_j(q - t)) ++q;
+          if (q == sa) { nb = (int32_t)(sa - t); break; }
+        }
+        bool same = false;
+        if (nb && sb == sa) {  // the same super-read name
+          same = true;
+          for (uint32_t u = 0; u < sa && same; ++u) same = unit_i(u) == unit_j(u);
+        }
+        if (nb && !same) {
+          const uint64_t po = dj.poff + (uint32_t)nb;
+          const int32_t uol = (int32_t)(G.pul[po] - (uint32_t)(nb - 1) * km1);
+          common = (int32_t)G.pco[po];
+          const double duol = (double)uol;
+          edge = !((duol > __dadd_rn(__dmul_rn(play, position_len), error)) |
+                   (position_len > __dmul_rn(play, __dadd_rn(duol, error))));
+        }
+      }
+      if (edge) {  // node_info update (overlap_graph.cc:41-56); this lane owns node j
+        s_fl[sj] &= (uint8_t)~GRAPH_START;
+        const int32_t nlpath = (int32_t)((uint32_t)lp_i + dj.lp_add - (uint32_t)common);
+        const int32_t lp_j = s_lp[sj];
+        const bool upd = nlpath > lp_j || (nlpath == lp_j && (s_lst[sj] == -1 || lsi_i > s_lsi[sj]));
+        if (upd) {
+          s_lp[sj] = nlpath;
+          s_lst[sj] = lst_i == -1 ? (int32_t)it_i : lst_i;
+          s_lsi[sj] = lsi_i;
+          s_lpv[sj] = (int32_t)it_i;
+          s_lun[sj] = lun_i + (int32_t)sb - nb;
+        }
+      }
+      // union_sets(it_i, it_j) for the edges in j order (union_find.cc:13-23), by lane 0
+      uint64_t em = __ballot(edge);
+      any_edge |= em != 0;
+      while (em) {
+        const uint32_t l = (uint32_t)__ffsll((long long)em) - 1;
+        em &= em - 1;
+        const uint32_t jj = (uint32_t)__shfl((int)dj.idx, (int)l, 64);
+        if (lane == 0) {
+          auto root = [&](uint32_t s) -> uint32_t {
+            uint32_t q = s;
+            while (s_par[q] != q) q = s_par[q];
+            while (s_par[s] != q) { const uint32_t nx = s_par[s]; s_par[s] = (uint16_t)q; s = nx; }
+            return q;
+          };
+          const uint32_t r1 = root(it_i), r2 = root(jj);
+          if (s_rank[r1] > s_rank[r2]) s_par[r2] = (uint16_t)r1;
+          else if (s_rank[r1] < s_rank[r2]) s_par[r1] = (uint16_t)r2;
+          else if (r1 != r2) { s_par[r2] = (uint16_t)r1; ++s_rank[r1]; }
+        }
+      }
+      if (bm) break;  // the reference's break
+    }
+    if (overflow) break;
+    if (any_edge && lane == 0) s_fl[si] &= (uint8_t)~GRAPH_END;
+    __syncthreads();  // (one wave: orders this node's LDS updates before the next node reads them)
+  }
+  __syncthreads();
+  if (overflow) {  // a scan longer than the ring: the host traverses the read
+    for (uint32_t i = lane; i < n; i += 64) G.out[b + i] = GraphNode{0, -1, -1, 0, i, GRAPH_HOST};
+    return;
+  }
+  for (uint32_t p = flushed + lane; p < n; p += 64) flush_pos(p);
+  __threadfence();  // the node stores above before the root stores below (same addresses)
+  for (uint32_t i = lane; i < n; i += 64) {
+    uint32_t q = i;
+    while (s_par[q] != q) q = s_par[q];
+    G.out[b + i].root = q;
+  }
+}
+void launch_graph_sizes(const GraphDev& G, uint64_t n_recs, uint32_t* sizes, uint64_t* scan_scratch, hipStream_t st) {
+  if (n_recs) hipLaunchKernelGGL(k_graph_sizes, dim3((uint32_t)std::min<uint64_t>((n_recs + 255) / 256, 65535)), dim3(256),
+                                 0, st, G, n_recs, sizes);
+  launch_excl_scan(sizes, nullptr, n_recs, G.poff, scan_scratch, st);
+}
+void launch_graph(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hipStream_t st) {
+  if (!n_recs || !n_reads) return;
+  hipLaunchKernelGGL(k_graph_prep, dim3((uint32_t)std::min<uint64_t>((n_recs + 255) / 256, 65535)), dim3(256), 0, st,
+                     G, n_recs);
+  hipLaunchKernelGGL(k_graph_sort, dim3(n_reads), dim3(GRAPH_SORT_BLOCK), 0, st, G, n_reads);
+  hipLaunchKernelGGL(k_graph, dim3(n_reads), dim3(64), 0, st, G, n_reads);
 }
 
 }  // namespace pbgpu

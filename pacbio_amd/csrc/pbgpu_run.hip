@@ -492,7 +492,7 @@ void pin_to(const std::vector<int>& cpus) {
 // pbgpu_coords_batch view (the records consumer's input): no zero-filled
 // vectors, no pageable staging copies; valid until the next download.
 struct RecordsView {
-  PinnedVec off, recs, km, kb;
+  PinnedVec off, recs, km, kb, graph;
   pbgpu_coords_batch c{};
   void download(pbgpu_aligner* al) {
     const uint64_t n = al->last_reads, nr = al->last_records, ni = al->last_info;
@@ -505,12 +505,17 @@ struct RecordsView {
       HIPCHK(hipMemcpyAsync(km.p, al->info_m.p, ni * 4, hipMemcpyDeviceToHost, al->st));
       HIPCHK(hipMemcpyAsync(kb.p, al->info_b.p, ni * 4, hipMemcpyDeviceToHost, al->st));
     }
+    if (al->graph) {
+      graph.reserve(std::max<uint64_t>(nr, 1) * sizeof(GraphNode));
+      if (nr) HIPCHK(hipMemcpyAsync(graph.p, al->g_out.p, nr * sizeof(GraphNode), hipMemcpyDeviceToHost, al->st));
+    }
     HIPCHK(hipStreamSynchronize(al->st));
     pbgpu_record* r = (pbgpu_record*)recs.p;
     if (al->ix->sr_begin)  // a shard's device super-read ids are local
       for (uint64_t i = 0; i < nr; ++i) r[i].sr_index += (uint32_t)al->ix->sr_begin;
     c.n_reads = n; c.n_records = nr; c.read_offsets = (const uint64_t*)off.p; c.records = r;
     c.n_info = ni; c.kmers_info = (const int32_t*)km.p; c.bases_info = (const int32_t*)kb.p;
+    c.graph = al->graph ? (const pbgpu_graph_node*)graph.p : nullptr;
   }
 };
 
@@ -878,6 +883,10 @@ pbgpu_status pbgpu_runner_create(pbgpu_index* const* indexes, size_t n_indexes, 
       R->rd.emplace_back(new pbgpu_reads);
       R->views.emplace_back(new RecordsView);
       if (R->details) pbgpu_aligner_set_details(a, 1);
+      if (run->records_fn && run->graph) {
+        const pbgpu_status g = pbgpu_aligner_set_graph(a, run->graph);
+        if (g != PBGPU_OK) return g;
+      }
     }
   const size_t W = R->al.size();
   const size_t P = run->n_parts > 1 ? run->n_parts : 1;

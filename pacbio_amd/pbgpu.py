@@ -40,7 +40,7 @@ EXPORTS = [
     "pbgpu_coords_merge", "pbgpu_rccl_comm_last_bytes",
     "pbgpu_format_device", "pbgpu_text_download", "pbgpu_host_alloc", "pbgpu_host_free", "pbgpu_format_double",
     "pbgpu_index_replicate", "pbgpu_run", "pbgpu_runner_create", "pbgpu_runner_run", "pbgpu_runner_free",
-    "pbgpu_index_save", "pbgpu_index_load",
+    "pbgpu_index_save", "pbgpu_index_load", "pbgpu_aligner_set_graph",
 ]
 
 
@@ -79,7 +79,7 @@ class RunParams(C.Structure):
                 ("details_path", C.c_char_p), ("compact", C.c_int32), ("header", C.c_int32),
                 ("zero_match", C.c_int32), ("aligners_per_device", C.c_uint32), ("batch_bases", C.c_uint64),
                 ("host_threads", C.c_int32), ("records_fn", C.c_void_p), ("records_user", C.c_void_p),
-                ("n_parts", C.c_uint32)]
+                ("n_parts", C.c_uint32), ("graph", C.c_void_p)]
 
 
 class RunStats(C.Structure):
@@ -106,7 +106,21 @@ assert RECORD_DTYPE.itemsize == 96
 class CoordsBatch(C.Structure):
     _fields_ = [("n_reads", C.c_uint64), ("n_records", C.c_uint64), ("read_offsets", C.POINTER(C.c_uint64)),
                 ("records", C.c_void_p), ("n_info", C.c_uint64), ("kmers_info", C.POINTER(C.c_int32)),
-                ("bases_info", C.POINTER(C.c_int32))]
+                ("bases_info", C.POINTER(C.c_int32)), ("graph", C.c_void_p)]
+
+
+# pbgpu_graph_node (create_mega_reads' overlap graph, pbgpu_aligner_set_graph)
+GRAPH_NODE_DTYPE = np.dtype([("lpath", "<i4"), ("lstart", "<i4"), ("lprev", "<i4"), ("lunitigs", "<i4"),
+                             ("root", "<u4"), ("flags", "<u4")])
+assert GRAPH_NODE_DTYPE.itemsize == 24
+GRAPH_START, GRAPH_END, GRAPH_HOST = 1, 2, 0x80000000
+
+
+class GraphParams(C.Structure):
+    _fields_ = [("overlap_play", C.c_double), ("nb_errors", C.c_double), ("k_len", C.c_uint32),
+                ("maximize_bases", C.c_int32), ("n_sr", C.c_uint64), ("name_offsets", C.POINTER(C.c_uint64)),
+                ("name_units", C.POINTER(C.c_uint32)), ("unitig_lengths", C.POINTER(C.c_int32)),
+                ("n_unitigs", C.c_uint64)]
 
 
 class DetailsBatch(C.Structure):
@@ -123,7 +137,8 @@ class Stats(C.Structure):
                [("kernel_ms", C.c_double * 8), ("kernel_launches", C.c_uint64 * 8)] + \
                [(n, C.c_uint64) for n in ("g0_kept", "g0_hits", "g0_chains", "l0_hits", "l0_strands",
                                           "n_fine_hits", "n_fine_windows")] + [("ms_fine", C.c_double)] + \
-               [(n, C.c_uint64) for n in ("fit_chains", "fit_points", "n_filter", "l0_points")]
+               [(n, C.c_uint64) for n in ("fit_chains", "fit_points", "n_filter", "l0_points")] + \
+               [("ms_graph", C.c_double), ("graph_records", C.c_uint64)]
 
     def as_dict(self):
         d = {n: getattr(self, n) for n, _ in self._fields_ if not n.startswith("kernel_")}

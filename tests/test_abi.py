@@ -33,11 +33,14 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert pbgpu.lib().pbgpu_abi_version() == 4
+    assert pbgpu.lib().pbgpu_abi_version() == 5
 
 
 def test_record_layout_matches_header():
     assert pbgpu.RECORD_DTYPE.itemsize == 96
+    assert pbgpu.GRAPH_NODE_DTYPE.itemsize == 24
+    # pbgpu_coords_batch: 7 words + the graph pointer (ABI 5)
+    assert C.sizeof(pbgpu.CoordsBatch) == 64
 
 
 def test_params_default_matches_yaggo_defaults():

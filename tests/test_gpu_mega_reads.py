@@ -180,3 +180,38 @@ def test_graph_error_exits_cleanly(synth, tmp_path):
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 1, (r.returncode, r.stderr[-500:])
     assert "unitig id beyond the unitig sequences" in r.stderr
+
+
+@pytest.mark.parametrize("cli", [c[0] for c in CASES], ids=[" ".join(c[0]) or "defaults" for c in CASES])
+def test_device_graph_equals_host_graph(synth, tmp_path, cli):
+    """the traversal on the GPU (default) against the host's (--host-graph), and with
+    PBGPU_GRAPH_NMAX=40 (reads of more than 40 records left to the host): same bytes"""
+    d, _, _ = synth
+    base = ["-s", "1M", "-m", "17", "-k", "31", "-l", os.path.join(d, "ul.txt"), "-t", "4", *cli,
+            "-r", os.path.join(d, "sr.fa"), "-p", os.path.join(d, "pb.fa")]
+    outs = []
+    for extra, env in (([], None), (["--host-graph"], None), ([], {"PBGPU_GRAPH_NMAX": "40"})):
+        o = str(tmp_path / f"mr{len(outs)}")
+        r = subprocess.run([CMR, *base, *extra, "-o", o], capture_output=True, text=True, timeout=120,
+                           env=dict(os.environ, **(env or {})))
+        assert r.returncode == 0, r.stderr
+        outs.append(open(o).read())
+    assert outs[0].count(">") >= 10
+    assert outs[0] == outs[1] == outs[2]
+
+
+def test_device_graph_c2_reads(tmp_path):
+    """C2 (200k super-reads, production aligner flags) on 1500 reads: the device
+    traversal gives the host traversal's bytes (~560 records and ~12k edges a read)"""
+    from tools.synth import Dataset
+    ds = Dataset("C2", seed=42, threads=16, n_pb=1500)
+    ds.write(str(tmp_path))
+    ds.close()
+    base = ["-s", "1M", "-m", "17", "--psa-min", "13", "-k", "31", "-l", str(tmp_path / "ul.txt"), "-B", "15",
+            "--max-count", "5000", "--stretch-cap", "10000", "-t", "16",
+            "-r", str(tmp_path / "sr.fa"), "-p", str(tmp_path / "pb.fa")]
+    a, b = str(tmp_path / "dev"), str(tmp_path / "host")
+    _run([*base, "-o", a], timeout=300)
+    _run([*base, "--host-graph", "-o", b], timeout=300)
+    ta = open(a).read()
+    assert ta.count(">") > 1000 and ta == open(b).read()

@@ -53,6 +53,12 @@ def main():
         out["create_mega_reads"]["reads_with_mega_reads"] = mr.count(">")
         out["create_mega_reads"]["mega_reads"] = mr.count("\n") - mr.count(">")
         out["create_mega_reads"]["bases_per_s"] = t["bases"] / t["wall_s"]
+        out["create_mega_reads"]["graph"] = "device traversal (default)"
+        # the same run with the overlap graph traversed on the host: same bytes
+        wall, t = _run([os.path.join(ROOT, "pacbio_amd", "bin", "create_mega_reads"), *flags, "--host-graph", "-o",
+                        os.path.join(d, "mega_reads_host")])
+        out["create_mega_reads_host_graph"] = dict(process_wall_s=wall, **t, bases_per_s=t["bases"] / t["wall_s"])
+        out["create_mega_reads_host_graph"]["identical_output"] = open(os.path.join(d, "mega_reads_host")).read() == mr
         out["workload"] = f"C2: {a.reads} PB reads vs 200k SRs, production flags, -t {a.threads}"
         print(json.dumps(out))
     finally:

@@ -9,9 +9,6 @@ V = {
     "gonly": G,
     "p0": G + ["-DPBGPU_EXP_SKIP_PASS1"],
     "p0notab": G + ["-DPBGPU_EXP_SKIP_PASS1", "-DPBGPU_EXP_P0_NOTABLE"],
-    "gonly_lin": G + ["-DPBGPU_EXP_GROUP_LINLOC"],
-    "p0_lin": G + ["-DPBGPU_EXP_SKIP_PASS1", "-DPBGPU_EXP_GROUP_LINLOC"],
-    "lin": ["-DPBGPU_EXP_GROUP_LINLOC"],
 }
 for n in (sys.argv[1:] or V):
     print(build_pbgpu_variant(n, V[n]))
