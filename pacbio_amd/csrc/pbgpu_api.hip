@@ -1622,7 +1622,7 @@ static void graph_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   HIPCHK(hipMemcpyAsync(&tot, al->g_poff.p + nrec, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   al->g_pre.ensure(3 * tot + 3); al->g_imp.ensure(nrec + 1); al->g_desc.ensure(nrec + 1); al->g_out.ensure(nrec + 1);
-  G.pul = al->g_pre.p; G.pco = al->g_pre.p + tot + 1; G.ounits = al->g_pre.p + 2 * (tot + 1);
+  G.pp = (uint2*)al->g_pre.p; G.ounits = al->g_pre.p + 2 * (tot + 1);
   G.imp = al->g_imp.p; G.desc = al->g_desc.p; G.out = al->g_out.p;
   launch_graph(G, n, nrec, st);
   HIPCHK(hipGetLastError());

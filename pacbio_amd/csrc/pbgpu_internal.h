@@ -219,8 +219,7 @@ struct GraphDev {
   uint32_t nmax;              // reads with more records go to the host (<= GRAPH_NMAX; tests lower it)
   double2* imp;               // per record: implied start, end
   uint64_t* poff;             // per record: its prefix sums' offset (nsz + 1 each)
-  uint32_t* pul;              // prefix sums of the unitig lengths along the name
-  uint32_t* pco;              // prefix sums of info[2u] - info[2u - 1]
+  uint2* pp;                  // prefix sums along the name: {unitig lengths, info[2u] - info[2u - 1]}
   uint32_t* ounits;           // the name's unitigs in the record's orientation (at poff)
   GDesc* desc;                // per read, in sorted order
   GraphNode* out;

@@ -2866,14 +2866,14 @@ __global__ void k_graph_prep(GraphDev G, uint64_t n) {
     auto info_at = [&](uint32_t i) -> uint32_t { return i < R.n_info ? (uint32_t)info[R.info_off + i] : 0u; };
     const uint64_t po = G.poff[q];
     uint32_t a = 0, c = 0;
-    G.pul[po] = 0; G.pco[po] = 0;
+    G.pp[po] = make_uint2(0u, 0u);
     for (uint32_t u = 0; u < nsz; ++u) {
       const uint32_t un = graph_unit(G, R.sr, nsz, rev, u);
       G.ounits[po + u] = un;
       const uint32_t id = un >> 1;
       a += id < G.n_ul ? (uint32_t)G.ul[id] : 0u;
       c += info_at(2 * u) - (u > 0 ? info_at(2 * u - 1) : 0u);
-      G.pul[po + u + 1] = a; G.pco[po + u + 1] = c;
+      G.pp[po + u + 1] = make_uint2(a, c);
     }
   }
 }
@@ -2925,22 +2925,31 @@ __global__ __launch_bounds__(GRAPH_SORT_BLOCK) void k_graph_sort(GraphDev G, uin
 // path state -- refilled 64 at a time as i advances (a node's scan reaches at least
 // GRING - 63 positions ahead; a longer one hands the whole read to the host), and the
 // union-find of the read's nodes.
-constexpr uint32_t GRING = 256, GRING_U = 8;
+#ifndef PBGPU_GRING
+#define PBGPU_GRING 256
+#endif
+constexpr uint32_t GRING = PBGPU_GRING, GRING_U = 8;
+constexpr uint32_t GRAPH_NMAX_K = 2048;  // reads of more records go to the host (LDS union-find)
 __global__ __launch_bounds__(64) void k_graph(GraphDev G, uint32_t n_reads) {
-  __shared__ GDesc s_d[GRING];
+  // the ring: implied start / end and error, {idx | nsz << 16, lp_add}, name offset, the
+  // first GRING_U unitigs and prefix sums 1..GRING_U - 1 of names of <= GRING_U unitigs,
+  // and the path state
+  __shared__ double s_is[GRING], s_ie[GRING], s_er[GRING], s_lsi[GRING];
+  __shared__ uint2 s_meta[GRING];
+  __shared__ uint64_t s_po[GRING];
   __shared__ uint32_t s_u[GRING * GRING_U];
+  __shared__ uint2 s_pp[GRING * (GRING_U - 1)];
   __shared__ int32_t s_lp[GRING], s_lun[GRING], s_lst[GRING], s_lpv[GRING];
-  __shared__ double s_lsi[GRING];  // implied start of the node's path start (lstart's, or its own)
   __shared__ uint8_t s_fl[GRING];
-  __shared__ uint16_t s_par[GRAPH_NMAX];
-  __shared__ uint8_t s_rank[GRAPH_NMAX];
+  __shared__ uint16_t s_par[GRAPH_NMAX_K];
+  __shared__ uint8_t s_rank[GRAPH_NMAX_K];
   const uint32_t r = blockIdx.x;
   if (r >= n_reads) return;
   const uint32_t lane = threadIdx.x;
   const uint64_t b = G.rec_off[r];
   const uint32_t n = (uint32_t)(G.rec_off[r + 1] - b);
   if (n == 0) return;
-  if (n > G.nmax) {  // the host traverses this read
+  if (n > G.nmax || n > GRAPH_NMAX_K) {  // the host traverses this read
     for (uint32_t i = lane; i < n; i += 64) G.out[b + i] = GraphNode{0, -1, -1, 0, i, GRAPH_HOST};
     return;
   }
@@ -2951,20 +2960,37 @@ __global__ __launch_bounds__(64) void k_graph(GraphDev G, uint32_t n_reads) {
   auto load_pos = [&](uint32_t p) {  // node_info::reset (overlap_graph.hpp:24-34) of sorted position p
     const uint32_t sl = p % GRING;
     const GDesc d = G.desc[b + p];
-    s_d[sl] = d;
+    s_is[sl] = d.imp_s; s_ie[sl] = d.imp_e; s_er[sl] = d.err; s_po[sl] = d.poff;
+    s_meta[sl] = make_uint2(d.idx | (d.nsz << 16), d.lp_add);
     const uint32_t m = d.nsz < GRING_U ? d.nsz : GRING_U;
     for (uint32_t u = 0; u < m; ++u) s_u[sl * GRING_U + u] = G.ounits[d.poff + u];
+    if (d.nsz <= GRING_U)
+      for (uint32_t u = 1; u < m; ++u) s_pp[sl * (GRING_U - 1) + u - 1] = G.pp[d.poff + u];
     s_lp[sl] = (int32_t)d.lp_add; s_lun[sl] = (int32_t)d.nsz; s_lst[sl] = -1; s_lpv[sl] = -1;
     s_lsi[sl] = d.imp_s; s_fl[sl] = (uint8_t)(GRAPH_START | GRAPH_END);
   };
   auto flush_pos = [&](uint32_t p) {
     const uint32_t sl = p % GRING;
-    G.out[b + s_d[sl].idx] = GraphNode{s_lp[sl], s_lst[sl], s_lpv[sl], s_lun[sl], 0u, s_fl[sl]};
+    G.out[b + (s_meta[sl].x & 0xFFFFu)] = GraphNode{s_lp[sl], s_lst[sl], s_lpv[sl], s_lun[sl], 0u, s_fl[sl]};
+  };
+  // union-find root with path halving (every write links a node to an ancestor, so
+  // concurrent lanes keep a valid forest with the same roots)
+  auto find = [&](uint32_t q) -> uint32_t {
+    while (s_par[q] != q) {
+      const uint32_t g = s_par[s_par[q]];
+      s_par[q] = (uint16_t)g;
+      q = g;
+    }
+    return q;
   };
   uint32_t loaded = n < GRING ? n : GRING, flushed = 0;
   for (uint32_t p = lane; p < loaded; p += 64) load_pos(p);
   __syncthreads();
   bool overflow = false;
+#ifdef PBGPU_PROF
+  uint64_t pf[6] = {0, 0, 0, 0, 0, 0};
+  const uint64_t pf0 = __builtin_amdgcn_s_memtime();
+#endif
   for (uint32_t i = 0; i < n; ++i) {
     if ((i & 63) == 0 && i >= 64 && loaded < n) {  // positions [i - 64, i) are done: their slots take the next 64
       flush_pos(i - 64 + lane);
@@ -2974,56 +3000,89 @@ __global__ __launch_bounds__(64) void k_graph(GraphDev G, uint32_t n_reads) {
       __syncthreads();
     }
     const uint32_t si = i % GRING;
-    const GDesc di = s_d[si];
-    if (di.imp_e >= rl) continue;  // hanging off the 3' end
-    const uint32_t it_i = di.idx, sa = di.nsz;
+    const double ie_i = s_ie[si];
+    if (ie_i >= rl) continue;  // hanging off the 3' end
+    const uint2 mi = s_meta[si];
+    const uint32_t it_i = mi.x & 0xFFFFu, sa = mi.x >> 16;
+    const double err_i = s_er[si];
+    const uint64_t po_i = s_po[si];
     const int32_t lp_i = s_lp[si], lun_i = s_lun[si], lst_i = s_lst[si];
     const double lsi_i = s_lsi[si];
-    auto unit_i = [&](uint32_t t) -> uint32_t { return sa <= GRING_U ? s_u[si * GRING_U + t] : G.ounits[di.poff + t]; };
+    // name i's first GRING_U unitigs in registers (the same for every lane)
+    uint32_t a[GRING_U];
+#pragma unroll
+    for (uint32_t u = 0; u < GRING_U; ++u) a[u] = s_u[si * GRING_U + u];
+    auto unit_i = [&](uint32_t t) -> uint32_t { return sa <= GRING_U ? s_u[si * GRING_U + t] : G.ounits[po_i + t]; };
     bool any_edge = false;
     for (uint32_t j0 = i + 1; j0 < n; j0 += 64) {
+      PROF_T(pa);
       const uint32_t j = j0 + lane;
       const bool act = j < n;
       if (__ballot(act && j >= loaded)) { overflow = true; break; }  // past the ring
       const uint32_t sj = (act ? j : i) % GRING;
-      const GDesc dj = s_d[sj];
-      const bool skip = (dj.imp_s <= 1.0) | (di.imp_e > __dadd_rn(dj.imp_e, 31.0));  // off the 5' end | not advancing
-      const double position_len = __dadd_rn(di.imp_e, -dj.imp_s);
-      const double error = __dmul_rn(G.nb_errors, __dadd_rn(di.err, dj.err));
+      const double is_j = s_is[sj], ie_j = s_ie[sj];
+      const bool skip = (is_j <= 1.0) | (ie_i > __dadd_rn(ie_j, 31.0));  // off the 5' end | not advancing
+      const double position_len = __dadd_rn(ie_i, -is_j);
+      const double error = __dmul_rn(G.nb_errors, __dadd_rn(err_i, s_er[sj]));
       const bool brk = act & !skip & (__dadd_rn(__dmul_rn(position_len, play), error) < kd);
       const uint64_t bm = __ballot(brk);
       const uint32_t fb = bm ? (uint32_t)__ffsll((long long)bm) - 1 : 64u;
       bool edge = false;
       int32_t nb = 0, common = 0;
-      const uint32_t sb = dj.nsz;
+      const uint2 mj = s_meta[sj];
+      const uint32_t sb = mj.x >> 16;
+      PROF_T(pb);
       if (act & !skip & (lane < fb) & (sa >= 2) & (sb >= 2)) {
-        auto unit_j = [&](uint32_t q) -> uint32_t { return sb <= GRING_U ? s_u[sj * GRING_U + q] : G.ounits[dj.poff + q]; };
-        // super_read_name::overlap (super_read_name.cc:49-72)
-        const uint32_t u0 = unit_j(0);
-        const int t0 = (int)sa - (int)sb + 1;
-        for (uint32_t t = t0 > 1 ? (uint32_t)t0 : 1u; t < sa; ++t) {
-          if (unit_i(t) != u0) continue;
-          uint32_t q = t + 1;
-          while (q < sa && unit_i(q) == unit_j(q - t)) ++q;
-          if (q == sa) { nb = (int32_t)(sa - t); break; }
-        }
-        bool same = false;
-        if (nb && sb == sa) {  // the same super-read name
-          same = true;
-          for (uint32_t u = 0; u < sa && same; ++u) same = unit_i(u) == unit_j(u);
+        bool same;
+        uint2 v;
+        if ((sa <= GRING_U) & (sb <= GRING_U)) {
+          // super_read_name::overlap (super_read_name.cc:49-72) in registers: the smallest
+          // t >= max(sa - sb + 1, 1) with name_i[t..sa) == name_j[0..sa - t)
+          uint32_t bu[GRING_U];
+#pragma unroll
+          for (uint32_t u = 0; u < GRING_U; ++u) bu[u] = s_u[sj * GRING_U + u];
+          const int t0 = (int)sa - (int)sb + 1;
+#pragma unroll
+          for (int t = (int)GRING_U - 1; t >= 1; --t) {
+            bool m = (t < (int)sa) & (t >= t0) & (a[t] == bu[0]);
+#pragma unroll
+            for (int q = t + 1; q < (int)GRING_U; ++q) m &= (q >= (int)sa) | (a[q] == bu[q - t]);
+            nb = m ? (int32_t)sa - t : nb;
+          }
+          same = sb == sa;
+#pragma unroll
+          for (uint32_t u = 0; u < GRING_U; ++u) same &= (u >= sa) | (a[u] == bu[u]);
+          v = nb ? s_pp[sj * (GRING_U - 1) + (uint32_t)nb - 1] : make_uint2(0u, 0u);
+        } else {
+          const uint64_t po_j = s_po[sj];
+          auto unit_j = [&](uint32_t q) -> uint32_t { return sb <= GRING_U ? s_u[sj * GRING_U + q] : G.ounits[po_j + q]; };
+          const uint32_t u0 = unit_j(0);
+          const int t0 = (int)sa - (int)sb + 1;
+          for (uint32_t t = t0 > 1 ? (uint32_t)t0 : 1u; t < sa; ++t) {
+            if (unit_i(t) != u0) continue;
+            uint32_t q = t + 1;
+            while (q < sa && unit_i(q) == unit_j(q - t)) ++q;
+            if (q == sa) { nb = (int32_t)(sa - t); break; }
+          }
+          same = false;
+          if (nb && sb == sa) {  // the same super-read name
+            same = true;
+            for (uint32_t u = 0; u < sa && same; ++u) same = unit_i(u) == unit_j(u);
+          }
+          v = nb ? G.pp[po_j + (uint32_t)nb] : make_uint2(0u, 0u);
         }
         if (nb && !same) {
-          const uint64_t po = dj.poff + (uint32_t)nb;
-          const int32_t uol = (int32_t)(G.pul[po] - (uint32_t)(nb - 1) * km1);
-          common = (int32_t)G.pco[po];
+          const int32_t uol = (int32_t)(v.x - (uint32_t)(nb - 1) * km1);
+          common = (int32_t)v.y;
           const double duol = (double)uol;
           edge = !((duol > __dadd_rn(__dmul_rn(play, position_len), error)) |
                    (position_len > __dmul_rn(play, __dadd_rn(duol, error))));
         }
       }
+      PROF_T(pc);
       if (edge) {  // node_info update (overlap_graph.cc:41-56); this lane owns node j
         s_fl[sj] &= (uint8_t)~GRAPH_START;
-        const int32_t nlpath = (int32_t)((uint32_t)lp_i + dj.lp_add - (uint32_t)common);
+        const int32_t nlpath = (int32_t)((uint32_t)lp_i + mj.y - (uint32_t)common);
         const int32_t lp_j = s_lp[sj];
         const bool upd = nlpath > lp_j || (nlpath == lp_j && (s_lst[sj] == -1 || lsi_i > s_lsi[sj]));
         if (upd) {
@@ -3034,26 +3093,46 @@ __global__ __launch_bounds__(64) void k_graph(GraphDev G, uint32_t n_reads) {
           s_lun[sj] = lun_i + (int32_t)sb - nb;
         }
       }
-      // union_sets(it_i, it_j) for the edges in j order (union_find.cc:13-23), by lane 0
+      PROF_T(pd);
+      // union_sets(it_i, it_j) for the edges in j order (union_find.cc:13-23).  The roots
+      // before this scan are found in parallel (path compression never changes a root,
+      // and the roots are all the output needs); a root already met in this scan, or i's
+      // own, is in i's set (a no-op union); the rest are merged into i's set one after
+      // another in j order, with the reference's rank rule, in registers.
       uint64_t em = __ballot(edge);
-      any_edge |= em != 0;
-      while (em) {
-        const uint32_t l = (uint32_t)__ffsll((long long)em) - 1;
-        em &= em - 1;
-        const uint32_t jj = (uint32_t)__shfl((int)dj.idx, (int)l, 64);
-        if (lane == 0) {
-          auto root = [&](uint32_t s) -> uint32_t {
-            uint32_t q = s;
-            while (s_par[q] != q) q = s_par[q];
-            while (s_par[s] != q) { const uint32_t nx = s_par[s]; s_par[s] = (uint16_t)q; s = nx; }
-            return q;
-          };
-          const uint32_t r1 = root(it_i), r2 = root(jj);
-          if (s_rank[r1] > s_rank[r2]) s_par[r2] = (uint16_t)r1;
-          else if (s_rank[r1] < s_rank[r2]) s_par[r1] = (uint16_t)r2;
-          else if (r1 != r2) { s_par[r2] = (uint16_t)r1; ++s_rank[r1]; }
+      if (em) {
+        any_edge = true;
+        const uint32_t r1 = find(it_i);
+        const uint32_t R = edge ? find(mj.x & 0xFFFFu) : r1;
+        const uint32_t rk = s_rank[R];
+        bool first = edge & (R != r1);
+        for (uint64_t m = em; m; m &= m - 1) {
+          const uint32_t l = (uint32_t)__ffsll((long long)m) - 1;
+          const uint32_t vv = (uint32_t)__builtin_amdgcn_readlane((int)R, (int)l);
+          first &= !((lane > l) & (R == vv));
+        }
+        uint32_t cur = r1, crank = s_rank[r1];
+        for (uint64_t fm = __ballot(first); fm; fm &= fm - 1) {
+          const uint32_t l = (uint32_t)__ffsll((long long)fm) - 1;
+          const uint32_t vv = (uint32_t)__builtin_amdgcn_readlane((int)R, (int)l);
+          const uint32_t vr = (uint32_t)__builtin_amdgcn_readlane((int)rk, (int)l);
+          if (crank > vr) {
+            if (lane == 0) s_par[vv] = (uint16_t)cur;
+          } else if (crank < vr) {
+            if (lane == 0) s_par[cur] = (uint16_t)vv;
+            cur = vv; crank = vr;
+          } else {
+            ++crank;
+            if (lane == 0) { s_par[vv] = (uint16_t)cur; s_rank[cur] = (uint8_t)crank; }
+          }
         }
       }
+#ifdef PBGPU_PROF
+      {
+        const uint64_t pe = __builtin_amdgcn_s_memtime();
+        pf[0] += pb - pa; pf[1] += pc - pb; pf[2] += pd - pc; pf[3] += pe - pd; pf[4] += 1;
+      }
+#endif
       if (bm) break;  // the reference's break
     }
     if (overflow) break;
@@ -3061,6 +3140,11 @@ __global__ __launch_bounds__(64) void k_graph(GraphDev G, uint32_t n_reads) {
     __syncthreads();  // (one wave: orders this node's LDS updates before the next node reads them)
   }
   __syncthreads();
+#ifdef PBGPU_PROF
+  // slots 80..: chunk scan, names + sums, node updates, unions, chunks, nodes, wave total, waves
+  PROF_ADD(80, pf[0]); PROF_ADD(81, pf[1]); PROF_ADD(82, pf[2]); PROF_ADD(83, pf[3]); PROF_ADD(84, pf[4]);
+  PROF_ADD(85, n); PROF_ADD(86, __builtin_amdgcn_s_memtime() - pf0); PROF_ADD(87, 1);
+#endif
   if (overflow) {  // a scan longer than the ring: the host traverses the read
     for (uint32_t i = lane; i < n; i += 64) G.out[b + i] = GraphNode{0, -1, -1, 0, i, GRAPH_HOST};
     return;

@@ -368,6 +368,10 @@ class Coords:
             self.records = np.frombuffer(buf, dtype=RECORD_DTYPE).copy()
         else:
             self.records = np.zeros(0, dtype=RECORD_DTYPE)
+        self.graph = None  # pbgpu_graph_node per record (GRAPH_NODE_DTYPE) when the aligner's graph is on
+        if c.graph and nr:
+            gbuf = (C.c_char * (nr * GRAPH_NODE_DTYPE.itemsize)).from_address(c.graph)
+            self.graph = np.frombuffer(gbuf, dtype=GRAPH_NODE_DTYPE).copy()
         if c.n_info:
             self.kmers_info = np.ctypeslib.as_array(c.kmers_info, shape=(c.n_info,)).copy()
             self.bases_info = np.ctypeslib.as_array(c.bases_info, shape=(c.n_info,)).copy()
@@ -451,6 +455,34 @@ class Aligner:
 
     def reset_stats(self):
         _check(lib().pbgpu_aligner_reset_stats(self.h))
+
+    def set_graph(self, names, unitig_lengths, k_len, overlap_play=1.3, nb_errors=3.0, maximize_bases=False):
+        """pbgpu_aligner_set_graph: create_mega_reads' overlap graph after every alignment.
+        names: per super-read of the index its unitig list (id << 1 | R); None turns it off."""
+        if names is None:
+            _check(lib().pbgpu_aligner_set_graph(self.h, None))
+            return
+        off = np.zeros(len(names) + 1, np.uint64)
+        off[1:] = np.cumsum([len(u) for u in names])
+        units = np.ascontiguousarray(np.concatenate([np.asarray(u, np.uint32) for u in names]) if int(off[-1])
+                                     else np.zeros(1, np.uint32), dtype=np.uint32)
+        ul = np.ascontiguousarray(unitig_lengths, dtype=np.int32)
+        self._graph_keep = (off, units, ul)
+        g = GraphParams(float(overlap_play), float(nb_errors), int(k_len), int(bool(maximize_bases)), len(names),
+                        off.ctypes.data_as(C.POINTER(C.c_uint64)), units.ctypes.data_as(C.POINTER(C.c_uint32)),
+                        ul.ctypes.data_as(C.POINTER(C.c_int32)), len(ul))
+        _check(lib().pbgpu_aligner_set_graph(self.h, C.byref(g)))
+
+
+def parse_unitigs(name):
+    """super_read_name::parse (super_read_name.cc:74-90) for the synthetic names: 12F_13R -> [24, 27]"""
+    out = []
+    for tok in name.split("_"):
+        digits = tok.rstrip("FR")
+        if not digits.isdigit():
+            return []
+        out.append(int(digits) << 1 | (tok.endswith("R")))
+    return out
 
     def shard_counts(self, reads):
         """Sharded index, step 1: this shard's saturated k-mer counts of the batch
