@@ -181,6 +181,16 @@ typedef struct {
   /* create_mega_reads' overlap graph of every record, in record order, when the
    * aligner has pbgpu_aligner_set_graph on (else NULL); see pbgpu_graph_node */
   const struct pbgpu_graph_node* graph;
+  /* pbgpu_graph_params.mega_reads: per read, its printed mega-reads in print order
+   * (n_reads + 1 offsets into mega; a read with none prints nothing), or, where
+   * mega_host[r] is set, nothing from the device: the read is finished on the
+   * host from its records, graph nodes and info, which are then the only ones in
+   * records / graph / kmers_info (read_offsets index them; the other reads'
+   * ranges are empty). */
+  const uint64_t* mega_offsets;
+  const struct pbgpu_mega_read* mega;
+  const uint32_t* mega_units;
+  const uint8_t* mega_host;
 } pbgpu_coords_batch;
 
 /* Host batch in, host records out (synchronous). */
@@ -316,7 +326,35 @@ typedef struct {
   /* unitig lengths (-l / -u), indexed by unitig id; ids past the end count 0 */
   const int32_t* unitig_lengths;
   uint64_t n_unitigs;
+  /* mega_reads != 0: the rest of the per-read work on the device too -- the
+   * components' terminal nodes (mega_reads_per_comp, overlap_graph.cc:116-161,
+   * with trim_match), the tiling (tile_greedy / tile_maximal,
+   * overlap_graph.cc:163-252) and the unitig paths and numbers each printed
+   * mega-read needs (print_mega_reads, overlap_graph.cc:254-299): the batch
+   * then carries pbgpu_coords_batch.mega* instead of records for every read
+   * traversed on the device. */
+  int32_t mega_reads;
+  int32_t tiling;                 /* PBGPU_TILING_*  (-T) */
+  int32_t trim;                   /* 0 none, 1 match (--trim; "branch" is none, create_mega_reads.cc:47-49) */
+  double min_density;             /* -d */
+  double min_len;                 /* -L */
 } pbgpu_graph_params;
+#define PBGPU_TILING_NONE     0
+#define PBGPU_TILING_GREEDY   1
+#define PBGPU_TILING_MAXIMAL  2
+#define PBGPU_TILING_WEIGHTED 3
+/* One printed mega-read of print_mega_reads (overlap_graph.cc:254-299):
+ * "imp_s imp_e rs re qs qend lpath density name sr_len" with the unitig path
+ * (n_units unitigs at unit_offset of pbgpu_coords_batch.mega_units) as name;
+ * start_unitig / nb_unitigs select the path's unitigs whose sequence -u prints. */
+typedef struct pbgpu_mega_read {
+  double   imp_s, imp_e, density;
+  int32_t  rs, re, qs, lpath;     /* start node's rs, end node's re, start node's qs - start offset */
+  int32_t  sr_len, start_unitig, nb_unitigs;
+  uint32_t n_units;
+  uint64_t qend;
+  uint64_t unit_offset;
+} pbgpu_mega_read;
 /* p = NULL turns it off.  Whole (unsharded) index only. */
 pbgpu_status pbgpu_aligner_set_graph(pbgpu_aligner* al, const pbgpu_graph_params* p);
 typedef struct pbgpu_graph_node {

@@ -126,6 +126,11 @@ static char* mega_reads_batch(void* user, const pbgpu_index* ix, const pbgpu_coo
         if (pi >= parts) break;
         std::ostringstream os, ds;
         for (uint64_t r = n * pi / parts; r < n * (pi + 1) / parts; ++r) {
+          if (cb->mega && !cb->mega_host[r]) {  // finished on the device: print only
+            g.print_device(os, names[r], cb->mega + cb->mega_offsets[r], cb->mega_offsets[r + 1] - cb->mega_offsets[r],
+                           cb->mega_units);
+            continue;
+          }
           coords.clear();
           for (uint64_t i = cb->read_offsets[r]; i < cb->read_offsets[r + 1]; ++i) {
             const pbgpu_record& R = cb->records[i];
@@ -353,6 +358,14 @@ int main(int argc, char** argv) {
     gp.name_units = name_units.data();
     gp.unitig_lengths = ul32.data();
     gp.n_unitigs = ul32.size();
+    // components, tiling and the printed paths on the device too (the host prints)
+    gp.mega_reads = 1;
+    gp.tiling = C.gp.tiling == Tiling::NONE ? PBGPU_TILING_NONE
+              : C.gp.tiling == Tiling::GREEDY ? PBGPU_TILING_GREEDY
+              : C.gp.tiling == Tiling::MAXIMAL ? PBGPU_TILING_MAXIMAL : PBGPU_TILING_WEIGHTED;
+    gp.trim = C.gp.trim != Trim::NONE;
+    gp.min_density = C.gp.min_density;
+    gp.min_len = C.gp.min_len;
     rp.graph = &gp;
   }
   pbgpu_run_stats st{};

@@ -449,6 +449,25 @@ void ReadGraph::print(std::ostream& out, const std::vector<int>& order, std::ost
   }
 }
 
+void ReadGraph::print_device(std::ostream& out, const std::string& pb_name, const pbgpu_mega_read* m, uint64_t n,
+                             const uint32_t* units) const {
+  if (!n) return;
+  out << '>' << pb_name << '\n';
+  for (uint64_t t = 0; t < n; ++t) {
+    const pbgpu_mega_read& mr = m[t];
+    const unitig_list sr(units + mr.unit_offset, units + mr.unit_offset + mr.n_units);
+    out << std::fixed << std::setprecision(2) << mr.imp_s << ' ' << mr.imp_e << ' ' << mr.rs << ' ' << mr.re << ' '
+        << mr.qs << ' ' << mr.qend << ' ' << mr.lpath << ' ' << std::setprecision(4) << mr.density << ' ';
+    print_name(out, sr);
+    out << ' ' << mr.sr_len;
+    if (p_.unitig_sequences) {
+      out << ' ';
+      print_sequence(out, sr, mr.start_unitig, mr.nb_unitigs);
+    }
+    out << '\n';
+  }
+}
+
 // create_mega_reads.cc:79-89 for one read.  The reference's std::sort calls
 // leave ties in an unspecified order; here every sort is stable (ties keep the
 // input order: records in (rs, re, ql, sr_index, emit) order).

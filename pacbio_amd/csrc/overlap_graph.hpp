@@ -103,6 +103,10 @@ class ReadGraph {
   // one per record; NULL, or a read marked PBGPU_GRAPH_HOST, is traversed here
   void process(const std::vector<Coord>& coords, const std::string& pb_name, std::ostream& out, std::ostream* dot,
                const pbgpu_graph_node* dev = nullptr);
+  // the read's mega-reads computed on the device (pbgpu_graph_params.mega_reads), printed
+  // as print_mega_reads prints them (overlap_graph.hpp:253-262, overlap_graph.cc:254-299)
+  void print_device(std::ostream& out, const std::string& pb_name, const pbgpu_mega_read* m, uint64_t n,
+                    const uint32_t* units) const;
 
  private:
   friend struct ReadGraphTest;  // tests/cpp/og_driver.cpp (tiling properties)

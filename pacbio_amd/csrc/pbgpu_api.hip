@@ -1626,6 +1626,53 @@ static void graph_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   G.imp = al->g_imp.p; G.desc = al->g_desc.p; G.out = al->g_out.p;
   launch_graph(G, n, nrec, st);
   HIPCHK(hipGetLastError());
+  al->g_mtotal = al->g_munits_used = 0;
+  al->g_hosts = 0;
+  if (!al->g_mega) return;
+  // components, tiling and the printed mega-reads' paths on the device
+  G.mega = 1; G.tiling = al->g_tiling; G.trim = al->g_trim;
+  G.min_density = al->g_min_density; G.min_len = al->g_min_len;
+  al->g_cand.ensure(nrec + 1); al->g_ord.ensure(3 * nrec + 3); al->g_ivs.ensure(2 * nrec + 2);
+  al->g_mo.ensure(nrec + 1); al->g_mcount.ensure(n + 1); al->g_mhost.ensure(n + 1); al->g_moff.ensure(n + 1);
+  al->g_munits.ensure(tot + 1); al->g_uused.ensure(1); al->g_nhost.ensure(1);
+  G.cand = al->g_cand.p; G.ord = al->g_ord.p; G.ivs = al->g_ivs.p; G.mo = al->g_mo.p;
+  G.mcount = al->g_mcount.p; G.mhost = al->g_mhost.p; G.munits = al->g_munits.p; G.units_used = al->g_uused.p;
+  G.units_cap = tot; G.n_recs = nrec; G.n_host = al->g_nhost.p;
+  HIPCHK(hipMemsetAsync(al->g_uused.p, 0, 8, st));
+  HIPCHK(hipMemsetAsync(al->g_nhost.p, 0, 4, st));
+  launch_mega(G, n, st);
+  HIPCHK(hipGetLastError());
+  launch_excl_scan(al->g_mcount.p, nullptr, n, al->g_moff.p,
+                   (uint64_t*)temp_storage(al->tmp, excl_scan_scratch_words(n) * 8), st);
+  uint64_t cnt[3] = {0, 0, 0};
+  HIPCHK(hipMemcpyAsync(&cnt[0], al->g_moff.p + n, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&cnt[1], al->g_uused.p, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&cnt[2], al->g_nhost.p, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  al->g_mtotal = cnt[0];
+  al->g_munits_used = std::min<uint64_t>(cnt[1], tot);
+  al->g_hosts = cnt[2];
+  al->g_mc.ensure(cnt[0] + 1);
+  launch_mega_pack(G, n, al->g_moff.p, al->g_mc.p, st);
+  HIPCHK(hipGetLastError());
+  al->g_hrecs = al->g_hinfos = 0;
+  if (!al->g_hosts) return;
+  // the reads left to the host: their records, nodes and info packed (a small download)
+  al->g_rsize.ensure(n + 1); al->g_isize.ensure(nrec + 1); al->g_hroff.ensure(n + 1); al->g_hioff.ensure(nrec + 1);
+  launch_host_sizes(G, n, al->g_rsize.p, al->g_isize.p, st);
+  launch_excl_scan(al->g_rsize.p, nullptr, n, al->g_hroff.p,
+                   (uint64_t*)temp_storage(al->tmp, excl_scan_scratch_words(nrec) * 8), st);
+  launch_excl_scan(al->g_isize.p, nullptr, nrec, al->g_hioff.p,
+                   (uint64_t*)temp_storage(al->tmp, excl_scan_scratch_words(nrec) * 8), st);
+  uint64_t hc[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(&hc[0], al->g_hroff.p + n, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&hc[1], al->g_hioff.p + nrec, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  al->g_hrecs = hc[0]; al->g_hinfos = hc[1];
+  al->g_hrec.ensure(hc[0] + 1); al->g_hgraph.ensure(hc[0] + 1); al->g_hinfo.ensure(2 * hc[1] + 2);
+  launch_host_pack(G, n, al->g_hroff.p, al->g_hioff.p, al->g_hrec.p, al->g_hgraph.p, al->g_hinfo.p,
+                   al->g_hinfo.p + hc[1] + 1, st);
+  HIPCHK(hipGetLastError());
 }
 
 void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, uint32_t* gcount) {
@@ -1931,7 +1978,27 @@ struct coords_holder {
   std::vector<pbgpu_record> recs;
   std::vector<int32_t> km, kb;
   std::vector<pbgpu_graph_node> graph;
+  std::vector<uint64_t> moff;
+  std::vector<pbgpu_mega_read> mega;
+  std::vector<uint32_t> munits;
+  std::vector<uint8_t> mhost;
 };
+// the device mega-reads of the aligner's last alignment into host vectors
+static void download_mega(pbgpu_aligner* al, std::vector<uint64_t>& moff, std::vector<pbgpu_mega_read>& mega,
+                          std::vector<uint32_t>& munits, std::vector<uint8_t>& mhost) {
+  static_assert(sizeof(pbgpu_mega_read) == sizeof(MegaOut), "mega-read layout");
+  const uint64_t n = al->last_reads;
+  moff.resize(n + 1); mhost.resize(n + 1); mega.resize(al->g_mtotal); munits.resize(al->g_munits_used);
+  if (n && al->last_records) {
+    HIPCHK(hipMemcpy(moff.data(), al->g_moff.p, (n + 1) * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(mhost.data(), al->g_mhost.p, n, hipMemcpyDeviceToHost));
+  } else {
+    std::fill(moff.begin(), moff.end(), 0ull);
+    std::fill(mhost.begin(), mhost.end(), (uint8_t)0);
+  }
+  if (!mega.empty()) HIPCHK(hipMemcpy(mega.data(), al->g_mc.p, mega.size() * sizeof(MegaOut), hipMemcpyDeviceToHost));
+  if (!munits.empty()) HIPCHK(hipMemcpy(munits.data(), al->g_munits.p, munits.size() * 4, hipMemcpyDeviceToHost));
+}
 
 extern "C" {
 
@@ -1941,26 +2008,38 @@ pbgpu_status pbgpu_download(pbgpu_aligner* al, pbgpu_coords_batch** out) {
   API_TRY
   HIPCHK(hipSetDevice(al->ix->device));
   std::unique_ptr<coords_holder> h(new coords_holder);
-  const uint64_t n = al->last_reads, nr = al->last_records;
-  h->off.resize(n + 1);
-  HIPCHK(hipMemcpy(h->off.data(), al->rec_off.p, (n + 1) * 8, hipMemcpyDeviceToHost));
+  const uint64_t n = al->last_reads;
+  // device mega-reads: the records of the reads left to the host only, packed
+  const bool dev_mega = al->graph && al->g_mega;
+  const uint64_t nr = dev_mega ? al->g_hrecs : al->last_records, ni = dev_mega ? al->g_hinfos : al->last_info;
+  h->off.assign(n + 1, 0);
+  if (!dev_mega || al->g_hosts)
+    HIPCHK(hipMemcpy(h->off.data(), dev_mega ? al->g_hroff.p : al->rec_off.p, (n + 1) * 8, hipMemcpyDeviceToHost));
   h->recs.resize(nr);
   static_assert(sizeof(pbgpu_record) == sizeof(Rec), "record layout");
-  if (nr) HIPCHK(hipMemcpy(h->recs.data(), al->recs_sorted.p, nr * sizeof(Rec), hipMemcpyDeviceToHost));
+  if (nr)
+    HIPCHK(hipMemcpy(h->recs.data(), dev_mega ? al->g_hrec.p : al->recs_sorted.p, nr * sizeof(Rec), hipMemcpyDeviceToHost));
   if (al->ix->sr_begin)  // a shard's device super-read ids are local
     for (auto& r : h->recs) r.sr_index += (uint32_t)al->ix->sr_begin;
-  if (al->last_info) {
-    h->km.resize(al->last_info); h->kb.resize(al->last_info);
-    HIPCHK(hipMemcpy(h->km.data(), al->info_m.p, al->last_info * 4, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(h->kb.data(), al->info_b.p, al->last_info * 4, hipMemcpyDeviceToHost));
+  if (ni) {
+    h->km.resize(ni); h->kb.resize(ni);
+    HIPCHK(hipMemcpy(h->km.data(), dev_mega ? al->g_hinfo.p : al->info_m.p, ni * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(h->kb.data(), dev_mega ? al->g_hinfo.p + ni + 1 : al->info_b.p, ni * 4, hipMemcpyDeviceToHost));
   }
   h->c.n_reads = n; h->c.n_records = nr; h->c.read_offsets = h->off.data(); h->c.records = h->recs.data();
-  h->c.n_info = al->last_info; h->c.kmers_info = h->km.data(); h->c.bases_info = h->kb.data();
+  h->c.n_info = ni; h->c.kmers_info = h->km.data(); h->c.bases_info = h->kb.data();
   if (al->graph) {
     static_assert(sizeof(pbgpu_graph_node) == sizeof(GraphNode), "graph node layout");
     h->graph.resize(nr);
-    if (nr) HIPCHK(hipMemcpy(h->graph.data(), al->g_out.p, nr * sizeof(GraphNode), hipMemcpyDeviceToHost));
+    if (nr)
+      HIPCHK(hipMemcpy(h->graph.data(), dev_mega ? al->g_hgraph.p : al->g_out.p, nr * sizeof(GraphNode),
+                       hipMemcpyDeviceToHost));
     h->c.graph = h->graph.data();
+  }
+  if (dev_mega) {
+    download_mega(al, h->moff, h->mega, h->munits, h->mhost);
+    h->c.mega_offsets = h->moff.data(); h->c.mega = h->mega.data(); h->c.mega_units = h->munits.data();
+    h->c.mega_host = h->mhost.data();
   }
   *out = &h.release()->c;
   return PBGPU_OK;
@@ -2031,6 +2110,8 @@ pbgpu_status pbgpu_aligner_set_graph(pbgpu_aligner* al, const pbgpu_graph_params
   if (!p->name_offsets || (p->name_offsets[p->n_sr] && !p->name_units) || (p->n_unitigs && !p->unitig_lengths))
     return fail(PBGPU_ERR_INVALID, "null graph array");
   if (p->k_len == 0) return fail(PBGPU_ERR_INVALID, "graph k-mer length 0");
+  if (p->mega_reads && (p->tiling < PBGPU_TILING_NONE || p->tiling > PBGPU_TILING_WEIGHTED))
+    return fail(PBGPU_ERR_INVALID, "graph tiling %d", p->tiling);
   for (uint64_t i = 0; i < p->n_sr; ++i)
     if (p->name_offsets[i + 1] < p->name_offsets[i] || p->name_offsets[i + 1] - p->name_offsets[i] > 0xFFFFu)
       return fail(PBGPU_ERR_INVALID, "graph names: offsets not ascending, or a name of more than 65535 unitigs");
@@ -2043,6 +2124,9 @@ pbgpu_status pbgpu_aligner_set_graph(pbgpu_aligner* al, const pbgpu_graph_params
   if (p->n_unitigs) HIPCHK(hipMemcpy(al->g_ul.p, p->unitig_lengths, p->n_unitigs * 4, hipMemcpyHostToDevice));
   al->g_n_ul = p->n_unitigs;
   al->g_play = p->overlap_play; al->g_errors = p->nb_errors; al->g_k = p->k_len; al->g_bases = p->maximize_bases != 0;
+  al->g_mega = p->mega_reads != 0;
+  al->g_tiling = p->tiling; al->g_trim = p->trim != 0;
+  al->g_min_density = p->min_density; al->g_min_len = p->min_len;
   al->graph = true;
   return PBGPU_OK;
   API_CATCH

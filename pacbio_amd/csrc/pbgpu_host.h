@@ -273,6 +273,26 @@ struct pbgpu_aligner {
   dbuf<int32_t> g_ul;
   dbuf<double2> g_imp;
   dbuf<GraphNode> g_out;
+  // mega-reads on the device (pbgpu_graph_params.mega_reads)
+  bool g_mega = false;
+  int g_tiling = 0, g_trim = 0;
+  double g_min_density = 0, g_min_len = 0;
+  dbuf<MegaTmp> g_cand;
+  dbuf<int32_t> g_ord;
+  dbuf<double2> g_ivs;
+  dbuf<MegaOut> g_mo, g_mc;
+  dbuf<uint32_t> g_mcount, g_munits, g_nhost;
+  dbuf<uint8_t> g_mhost;
+  dbuf<uint64_t> g_moff;
+  dbuf<unsigned long long> g_uused;
+  uint64_t g_mtotal = 0, g_munits_used = 0, g_hosts = 0;  // the last alignment's
+  // the reads left to the host, packed: read offsets, records, nodes, info
+  dbuf<uint32_t> g_rsize, g_isize;
+  dbuf<uint64_t> g_hroff, g_hioff;
+  dbuf<Rec> g_hrec;
+  dbuf<GraphNode> g_hgraph;
+  dbuf<int32_t> g_hinfo;
+  uint64_t g_hrecs = 0, g_hinfos = 0;
   // device coords text of the last alignment (pbgpu_format.hip)
   dbuf<uint32_t> fmt_len;
   dbuf<uint64_t> fmt_pos;

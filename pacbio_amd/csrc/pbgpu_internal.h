@@ -223,7 +223,46 @@ struct GraphDev {
   uint32_t* ounits;           // the name's unitigs in the record's orientation (at poff)
   GDesc* desc;                // per read, in sorted order
   GraphNode* out;
+  // mega-reads on the device (pbgpu_graph_params.mega_reads)
+  int mega, tiling, trim;
+  double min_density, min_len;
+  struct MegaTmp* cand;       // per read region [rec_off[r], rec_off[r + 1]): scratch
+  int32_t* ord;               // 3 int scratch regions of n_recs each
+  double2* ivs;               // 2 double2 scratch regions of n_recs each
+  struct MegaOut* mo;         // per read region: its printed mega-reads in print order
+  uint32_t* mcount;           // per read: printed mega-reads
+  uint8_t* mhost;             // per read: 1 = left to the host
+  uint32_t* munits;           // the printed paths' unitigs (units_cap), allocated by units_used
+  unsigned long long* units_used;
+  uint64_t units_cap;
+  uint64_t n_recs;
+  uint32_t* n_host;           // reads left to the host
 };
+// mega_read_info (overlap_graph.hpp:48-58) of a candidate, with its node's lpath and root
+struct MegaTmp {
+  double imp_s, imp_e, tiling_start, tiling_end, density;
+  int32_t start_node, end_node, start_unitig, end_unitig, start_offset, end_offset, nb_unitigs, lpath;
+  uint32_t root, pad;
+};
+// the layout of pbgpu_mega_read (include/pbgpu.h)
+struct MegaOut {
+  double imp_s, imp_e, density;
+  int32_t rs, re, qs, lpath;
+  int32_t sr_len, start_unitig, nb_unitigs;
+  uint32_t n_units;
+  uint64_t qend;
+  uint64_t unit_offset;
+};
+static_assert(sizeof(MegaOut) == 72, "MegaOut layout must match pbgpu_mega_read");
+// after launch_graph: components, tiling and print paths per read (mega != 0)
+void launch_mega(const GraphDev& G, uint32_t n_reads, hipStream_t st);
+// the printed mega-reads of every read packed in read order: mc[moff[r] ..]
+void launch_mega_pack(const GraphDev& G, uint32_t n_reads, const uint64_t* moff, MegaOut* mc, hipStream_t st);
+// the reads left to the host (mhost): per record its info size if its read is one (else 0)
+void launch_host_sizes(const GraphDev& G, uint32_t n_reads, uint32_t* rsize, uint32_t* isize, hipStream_t st);
+// their records (info offsets rebased), graph nodes and kmers / bases info, packed in read order
+void launch_host_pack(const GraphDev& G, uint32_t n_reads, const uint64_t* hroff, const uint64_t* hioff, Rec* hrec,
+                      GraphNode* hgraph, int32_t* hinfo_m, int32_t* hinfo_b, hipStream_t st);
 // G.poff from the records' name sizes (then the caller sizes pul / pco by poff[n_recs])
 void launch_graph_sizes(const GraphDev& G, uint64_t n_recs, uint32_t* sizes, uint64_t* scan_scratch, hipStream_t st);
 // implied positions and prefix sums, per-read sort, traversal -> G.out

@@ -18,6 +18,7 @@
 #include <stdint.h>
 #include <algorithm>
 #include <type_traits>
+#include "pbgpu.h"
 #include "pbgpu_internal.h"
 #include "count_pack.h"
 
@@ -2929,7 +2930,7 @@ __global__ __launch_bounds__(GRAPH_SORT_BLOCK) void k_graph_sort(GraphDev G, uin
 #define PBGPU_GRING 256
 #endif
 constexpr uint32_t GRING = PBGPU_GRING, GRING_U = 8;
-constexpr uint32_t GRAPH_NMAX_K = 2048;  // reads of more records go to the host (LDS union-find)
+constexpr uint32_t GRAPH_NMAX_K = GRAPH_NMAX;  // reads of more records go to the host (LDS union-find)
 __global__ __launch_bounds__(64) void k_graph(GraphDev G, uint32_t n_reads) {
   // the ring: implied start / end and error, {idx | nsz << 16, lp_add}, name offset, the
   // first GRING_U unitigs and prefix sums 1..GRING_U - 1 of names of <= GRING_U unitigs,
@@ -3156,6 +3157,320 @@ __global__ __launch_bounds__(64) void k_graph(GraphDev G, uint32_t n_reads) {
     while (s_par[q] != q) q = s_par[q];
     G.out[b + i].root = q;
   }
+}
+// ====================================================== mega-reads (device)
+// The rest of create_mega_reads' per-read work after the traversal, on the
+// device: overlap_graph::mega_reads_per_comp (overlap_graph.cc:116-161) with
+// make / trim_match (:61-114), tile_greedy / tile_maximal (:163-252) and the
+// path and numbers of every printed mega-read (print_mega_reads, :254-299); the
+// host only formats them.  One wave per read: the candidates (end nodes passing
+// the density and length filters) lane-parallel, the rest -- a handful of
+// candidates a read -- by lane 0, in the reference's order, with per-read
+// scratch regions in HBM.  std::min / std::max are restated as their
+// definitions (b < a ? b : a, a < b ? b : a).
+DEV double std_min(double a, double b) { return b < a ? b : a; }
+DEV double std_max(double a, double b) { return a < b ? b : a; }
+DEV int32_t graph_ulen(const GraphDev& G, uint32_t id) { return id < G.n_ul ? G.ul[id] : 0; }  // ReadGraph::ulen
+constexpr uint32_t UNIT_INVALID = 0x7fffffffu;  // super_read_name::invalid_id
+__global__ __launch_bounds__(64) void k_mega(GraphDev G, uint32_t n_reads) {
+  const uint32_t r = blockIdx.x;
+  if (r >= n_reads) return;
+  const uint32_t lane = threadIdx.x;
+  const uint64_t b = G.rec_off[r];
+  const uint32_t n = (uint32_t)(G.rec_off[r + 1] - b);
+  if (n == 0) {
+    if (lane == 0) { G.mcount[r] = 0; G.mhost[r] = 0; }
+    return;
+  }
+  if (G.out[b].flags & GRAPH_HOST) {
+    if (lane == 0) { G.mcount[r] = 0; G.mhost[r] = 1; atomicAdd(G.n_host, 1u); }
+    return;
+  }
+  const uint32_t k = G.k;
+  const double rl = (double)(G.roff[r + 1] - G.roff[r]);
+  MegaTmp* cand = G.cand + b;
+  // ---- candidates, in node order (mega_reads_per_comp's loop body up to the filter)
+  uint32_t nc = 0;
+  for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+    const uint32_t i = i0 + lane;
+    bool keep = false;
+    MegaTmp m{};
+    if (i < n) {
+      const GraphNode g = G.out[b + i];
+      const uint32_t sn = g.lstart == -1 ? i : (uint32_t)g.lstart;
+      const Rec& Rs = G.recs[b + sn];
+      const Rec& Re = G.recs[b + i];
+      m.start_node = (int32_t)sn; m.end_node = (int32_t)i; m.start_unitig = 0;
+      m.nb_unitigs = g.lunitigs; m.end_unitig = (int32_t)(Re.n_info / 2);
+      m.imp_s = __dadd_rn(Rs.stretch, Rs.offset);
+      m.imp_e = __dadd_rn(__dmul_rn(Re.stretch, (double)Re.ql), Re.offset);
+      m.tiling_start = (double)Rs.rs; m.tiling_end = (double)Re.re;
+      m.start_offset = 0; m.end_offset = 0; m.lpath = g.lpath; m.root = g.root;
+      if (G.trim) {  // overlap_graph::trim_match (overlap_graph.cc:78-114)
+        if (G.imp[b + sn].x < 1) {
+          const uint32_t nsz = graph_nsz(G, Rs.sr);
+          const uint32_t* un = G.ounits + G.poff[b + sn];
+          int32_t offset = 0, su;
+          for (su = 0; su < (int32_t)Rs.n_info; su += 2) {
+            if (G.info_m[Rs.info_off + (uint32_t)su]) break;
+            const int32_t u = su / 2;
+            offset += graph_ulen(G, u < (int32_t)nsz ? un[u] >> 1 : UNIT_INVALID);
+          }
+          su /= 2;
+          m.start_unitig = su;
+          m.nb_unitigs -= su;
+          offset = (int32_t)((uint32_t)offset - (k - 1) * (uint32_t)su);
+          m.start_offset = offset;
+          m.imp_s = __dadd_rn(__dmul_rn(Rs.stretch, (double)(offset + 1)), Rs.offset);
+        }
+        if (G.imp[b + i].y > (double)Re.ql) {
+          const uint32_t nsz = graph_nsz(G, Re.sr);
+          const uint32_t* un = G.ounits + G.poff[b + i];
+          int32_t offset = 0, eu;
+          for (eu = (int32_t)Re.n_info - 1; eu >= 0; eu -= 2) {
+            if (G.info_m[Re.info_off + (uint32_t)eu]) break;
+            const int32_t u = eu / 2;
+            offset += graph_ulen(G, u < (int32_t)nsz ? un[u] >> 1 : UNIT_INVALID);
+          }
+          eu /= 2;
+          m.end_unitig = eu;
+          const int32_t removed = (int32_t)(Re.n_info / 2) - eu;
+          m.nb_unitigs -= removed;
+          offset = (int32_t)((uint32_t)offset - (k - 1) * (uint32_t)removed);
+          m.end_offset = offset;
+          m.imp_e = __dadd_rn(__dmul_rn(Re.stretch, (double)((uint64_t)Re.ql - (uint64_t)(int64_t)offset)), Re.offset);
+        }
+      }
+      const double imp_len = __dadd_rn(std_min(__dadd_rn(rl, 0.5), m.tiling_end), -std_max(0.5, m.tiling_start));
+      m.density = __ddiv_rn((double)g.lpath, imp_len);
+      keep = (g.flags & GRAPH_END) && !(m.density < G.min_density) &&
+             !(__dadd_rn(m.tiling_end, -m.tiling_start) < G.min_len);
+    }
+    const uint64_t km = __ballot(keep);
+    if (keep) cand[nc + (uint32_t)__builtin_popcountll(km & ((1ull << lane) - 1))] = m;
+    nc += (uint32_t)__builtin_popcountll(km);
+  }
+  __threadfence_block();
+  __syncthreads();
+  if (lane != 0) return;
+  // ---- components: per union-find root, in root order, the best terminal node
+  int32_t* comp = G.ord + b;           // candidate index per component, sorted by root
+  int32_t* order = G.ord + G.n_recs + b;
+  int32_t* tiled = G.ord + 2 * G.n_recs + b;
+  uint32_t m = 0;
+  for (uint32_t c = 0; c < nc; ++c) {
+    const uint32_t root = cand[c].root;
+    uint32_t lo = 0, hi = m;  // lower_bound by root
+    while (lo < hi) { const uint32_t mid = (lo + hi) / 2; if (cand[comp[mid]].root < root) lo = mid + 1; else hi = mid; }
+    if (lo == m || cand[comp[lo]].root != root) {
+      for (uint32_t q = m; q > lo; --q) comp[q] = comp[q - 1];
+      comp[lo] = (int32_t)c; ++m;
+    } else {
+      const MegaTmp& cur = cand[comp[lo]];
+      if (cand[c].lpath > cur.lpath || (cand[c].lpath == cur.lpath && cand[c].density > cur.density)) comp[lo] = (int32_t)c;
+    }
+  }
+  auto M = [&](int32_t t) -> const MegaTmp& { return cand[comp[t]]; };  // mega_reads_[t]
+  for (uint32_t t = 0; t < m; ++t) order[t] = (int32_t)t;
+  uint32_t nt = 0;  // tiled_mr_
+  const double play = G.play;
+  const double kplay = __dmul_rn((double)k, play);
+  auto stable_sort = [&](int32_t* a, uint32_t cnt, auto less) {  // insertion sort: stable
+    for (uint32_t x = 1; x < cnt; ++x) {
+      const int32_t v = a[x];
+      uint32_t y = x;
+      while (y > 0 && less(v, a[y - 1])) { a[y] = a[y - 1]; --y; }
+      a[y] = v;
+    }
+  };
+  if (G.tiling == PBGPU_TILING_GREEDY || G.tiling == PBGPU_TILING_WEIGHTED) {
+    if (G.tiling == PBGPU_TILING_GREEDY) {
+      stable_sort(order, m, [&](int32_t x, int32_t y) { return M(y).lpath < M(x).lpath; });
+    } else {
+      double* w = (double*)(G.ivs + b);  // weights_[t]
+      for (uint32_t t = 0; t < m; ++t) {
+        const MegaTmp& q = M((int32_t)t);
+        const int32_t span = G.recs[b + q.end_node].re - G.recs[b + q.start_node].rs + 1;
+        w[t] = __dmul_rn(__dmul_rn(q.density, q.density), (double)span);
+      }
+      stable_sort(order, m, [&](int32_t x, int32_t y) { return w[y] < w[x]; });
+    }
+    // tile_greedy (overlap_graph.cc:163-197): covered = joined right-open intervals
+    double2* cov = G.ivs + b;                 // (weights are read before this)
+    double2* placed = G.ivs + G.n_recs + b;
+    uint32_t ncov = 0, npl = 0;
+    for (uint32_t t = 0; t < m; ++t) {
+      const int32_t it = order[t];
+      const MegaTmp& q = M(it);
+      const double lo = q.tiling_start, hi = q.tiling_end;
+      const double span = hi > lo ? __dadd_rn(hi, -lo) : 0.0;
+      const double max_overlap = std_max(kplay, __dmul_rn(span, __dadd_rn(play, -0.9)));
+      bool large = false;
+      for (uint32_t c = 0; c < ncov && !large; ++c) {
+        const double a = std_max(lo, cov[c].x), bb = std_min(hi, cov[c].y);
+        large = a < bb && __dadd_rn(bb, -a) >= max_overlap;
+      }
+      if (large) continue;
+      bool contains = false;
+      for (uint32_t c = 0; c < npl && !contains; ++c)
+        contains = !(lo < hi) || (placed[c].x < placed[c].y && placed[c].x <= lo && hi <= placed[c].y);
+      if (contains) continue;
+      if (lo < hi) {  // IntervalSet::add
+        uint32_t s0 = 0;
+        while (s0 < ncov && cov[s0].y < lo) ++s0;
+        uint32_t e = s0;
+        double l2 = lo, h2 = hi;
+        while (e < ncov && cov[e].x <= h2) { l2 = std_min(l2, cov[e].x); h2 = std_max(h2, cov[e].y); ++e; }
+        const uint32_t rem = e - s0;  // replaced by one interval at s0
+        if (rem == 0) {
+          for (uint32_t q2 = ncov; q2 > s0; --q2) cov[q2] = cov[q2 - 1];
+          ++ncov;
+        } else {
+          for (uint32_t q2 = s0 + 1; q2 + rem - 1 < ncov; ++q2) cov[q2] = cov[q2 + rem - 1];
+          ncov -= rem - 1;
+        }
+        cov[s0] = make_double2(l2, h2);
+      }
+      placed[npl++] = make_double2(lo, hi);
+      tiled[nt++] = it;
+    }
+  } else if (G.tiling == PBGPU_TILING_MAXIMAL) {
+    stable_sort(order, m, [&](int32_t x, int32_t y) { return M(x).tiling_end < M(y).tiling_end; });
+    // tile_maximal (overlap_graph.cc:199-252): info {score, pos, node, previous, length}
+    double* ipos = (double*)(G.ivs + b);               // pos
+    int4* ilink = (int4*)(G.ivs + G.n_recs + b);     // {previous, length, score, node}
+    uint32_t ni = 0;
+    if (m) {
+      ipos[0] = M(order[0]).tiling_end;
+      ilink[0] = make_int4(-1, 1, M(order[0]).lpath, order[0]);
+      ni = 1;
+      for (uint32_t t = 1; t < m; ++t) {
+        const MegaTmp& q = M(order[t]);
+        const double lstart = q.tiling_start;
+        const double key = std_min(__dadd_rn(lstart, kplay), q.tiling_end);
+        uint32_t lo = 0, hi = ni;  // upper_bound: the first info with key < pos
+        while (lo < hi) { const uint32_t mid = (lo + hi) / 2; if (key < ipos[mid]) hi = mid; else lo = mid + 1; }
+        int32_t x = (int32_t)lo - 1;
+        while (x >= 0 && M(ilink[x].w).tiling_start >= lstart) x = ilink[x].x;
+        const int32_t nscore = (x >= 0 ? ilink[x].z : 0) + q.lpath;
+        if (nscore > ilink[ni - 1].z) {
+          ipos[ni] = q.tiling_end;
+          ilink[ni] = make_int4(x, (x >= 0 ? ilink[x].y : 0) + 1, nscore, order[t]);
+          ++ni;
+        }
+      }
+      nt = (uint32_t)ilink[ni - 1].y;
+      int32_t ptr = (int32_t)ni - 1;
+      for (int32_t q = (int32_t)nt - 1; q >= 0; --q) { tiled[q] = ilink[ptr].w; ptr = ilink[ptr].x; }
+    }
+  }
+  if (G.tiling != PBGPU_TILING_NONE)
+    stable_sort(tiled, nt, [&](int32_t x, int32_t y) {
+      return M(x).imp_s < M(y).imp_s || (M(x).imp_s == M(y).imp_s && M(x).imp_e < M(y).imp_e);
+    });
+  // ---- print_mega_reads: what each printed mega-read needs (overlap_graph.cc:254-299)
+  const int32_t* pr = nt ? tiled : order;
+  const uint32_t npr = nt ? nt : m;  // print(tiled_mr_.empty() ? sort_tiling_ : tiled_mr_)
+  uint32_t done = 0;
+  bool host = false;
+  for (uint32_t t = 0; t < npr && !host; ++t) {
+    const MegaTmp& q = M(pr[t]);
+    const GraphNode ge = G.out[b + (uint32_t)q.end_node];
+    const Rec& Re = G.recs[b + (uint32_t)q.end_node];
+    const Rec& Rs = G.recs[b + (uint32_t)q.start_node];
+    const uint64_t nu = ge.lunitigs > 0 ? (uint64_t)ge.lunitigs : 0ull;
+    const unsigned long long uo = atomicAdd(G.units_used, (unsigned long long)nu);
+    if (uo + nu > G.units_cap) { host = true; break; }
+    uint32_t* sr = G.munits + uo;
+    for (uint64_t x = 0; x < nu; ++x) sr[x] = 0;
+    // super_read_name::prepend (super_read_name.cc:29-36)
+    auto prepend = [&](uint64_t offset, uint32_t node, uint64_t first, uint64_t last) -> uint64_t {
+      const Rec& R = G.recs[b + node];
+      const uint64_t sz = graph_nsz(G, R.sr);
+      if (first > last || first >= sz) return offset;
+      const uint64_t to_copy = (last < sz - 1 ? last : sz - 1) - first + 1;
+      if (to_copy > offset) return offset;
+      const uint64_t no = offset - to_copy;
+      const uint32_t* un = G.ounits + G.poff[b + node];
+      for (uint64_t x = 0; x < to_copy; ++x) sr[no + x] = un[first + x];
+      return no;
+    };
+    uint64_t offset = prepend(nu, (uint32_t)q.end_node, 0, graph_nsz(G, Re.sr) - 1);
+    int32_t node_j = q.end_node, node_i = ge.lprev;
+    while (node_i >= 0) {
+      const GraphNode gi = G.out[b + (uint32_t)node_i], gj = G.out[b + (uint32_t)node_j];
+      const uint64_t nszi = graph_nsz(G, G.recs[b + (uint32_t)node_i].sr), nszj = graph_nsz(G, G.recs[b + (uint32_t)node_j].sr);
+      const uint64_t overlap = (uint64_t)(int64_t)gi.lunitigs + nszj - (uint64_t)(int64_t)gj.lunitigs;
+      offset = prepend(offset, (uint32_t)node_i, 0, nszi - 1 - overlap);
+      node_j = node_i;
+      node_i = gi.lprev;
+    }
+    int32_t sr_len = 0;
+    for (int32_t x = q.start_unitig; x < q.start_unitig + q.nb_unitigs; ++x)
+      sr_len += graph_ulen(G, x >= 0 && (uint64_t)x < nu ? sr[x] >> 1 : UNIT_INVALID);
+    sr_len = (int32_t)((uint32_t)sr_len - (uint32_t)(q.nb_unitigs - 1) * (k - 1));
+    MegaOut o;
+    o.imp_s = q.imp_s; o.imp_e = q.imp_e; o.density = q.density;
+    o.rs = Rs.rs; o.re = Re.re; o.qs = Rs.qs - q.start_offset; o.lpath = ge.lpath;
+    o.sr_len = sr_len; o.start_unitig = q.start_unitig; o.nb_unitigs = q.nb_unitigs; o.n_units = (uint32_t)nu;
+    o.qend = (uint64_t)(int64_t)(sr_len + q.end_offset) - ((uint64_t)Re.ql - (uint64_t)(int64_t)Re.qe);
+    o.unit_offset = uo;
+    G.mo[b + done++] = o;
+  }
+  G.mcount[r] = host ? 0u : done;
+  G.mhost[r] = host ? 1 : 0;
+  if (host) atomicAdd(G.n_host, 1u);
+}
+__global__ void k_mega_pack(GraphDev G, uint32_t n_reads, const uint64_t* __restrict__ moff, MegaOut* __restrict__ mc) {
+  const uint32_t r = blockIdx.x;
+  if (r >= n_reads) return;
+  const uint64_t b = G.rec_off[r], o = moff[r];
+  const uint32_t c = G.mcount[r];
+  for (uint32_t t = threadIdx.x; t < c; t += blockDim.x) mc[o + t] = G.mo[b + t];
+}
+// sizes for the host's share: per read its record count if left to the host (rsize),
+// per record its info length if its read is (isize)
+__global__ void k_host_sizes(GraphDev G, uint32_t n_reads, uint32_t* __restrict__ rsize, uint32_t* __restrict__ isize) {
+  const uint32_t r = blockIdx.x;
+  if (r >= n_reads) return;
+  const uint64_t b = G.rec_off[r];
+  const uint32_t n = (uint32_t)(G.rec_off[r + 1] - b);
+  const bool h = G.mhost[r] != 0;
+  if (threadIdx.x == 0) rsize[r] = h ? n : 0u;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) isize[b + i] = h ? G.recs[b + i].n_info : 0u;
+}
+__global__ void k_host_pack(GraphDev G, uint32_t n_reads, const uint64_t* __restrict__ hroff,
+                            const uint64_t* __restrict__ hioff, Rec* __restrict__ hrec, GraphNode* __restrict__ hgraph,
+                            int32_t* __restrict__ hinfo_m, int32_t* __restrict__ hinfo_b) {
+  const uint32_t r = blockIdx.x;
+  if (r >= n_reads || !G.mhost[r]) return;
+  const uint64_t b = G.rec_off[r];
+  const uint32_t n = (uint32_t)(G.rec_off[r + 1] - b);
+  const uint64_t o = hroff[r];
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    Rec R = G.recs[b + i];
+    const uint64_t io = hioff[b + i];
+    for (uint32_t x = 0; x < R.n_info; ++x) { hinfo_m[io + x] = G.info_m[R.info_off + x]; hinfo_b[io + x] = G.info_b[R.info_off + x]; }
+    R.info_off = io;
+    hrec[o + i] = R;
+    hgraph[o + i] = G.out[b + i];
+  }
+}
+void launch_host_sizes(const GraphDev& G, uint32_t n_reads, uint32_t* rsize, uint32_t* isize, hipStream_t st) {
+  if (n_reads) hipLaunchKernelGGL(k_host_sizes, dim3(n_reads), dim3(64), 0, st, G, n_reads, rsize, isize);
+}
+void launch_host_pack(const GraphDev& G, uint32_t n_reads, const uint64_t* hroff, const uint64_t* hioff, Rec* hrec,
+                      GraphNode* hgraph, int32_t* hinfo_m, int32_t* hinfo_b, hipStream_t st) {
+  if (n_reads)
+    hipLaunchKernelGGL(k_host_pack, dim3(n_reads), dim3(64), 0, st, G, n_reads, hroff, hioff, hrec, hgraph, hinfo_m, hinfo_b);
+}
+void launch_mega(const GraphDev& G, uint32_t n_reads, hipStream_t st) {
+  if (!n_reads) return;
+  hipLaunchKernelGGL(k_mega, dim3(n_reads), dim3(64), 0, st, G, n_reads);
+}
+void launch_mega_pack(const GraphDev& G, uint32_t n_reads, const uint64_t* moff, MegaOut* mc, hipStream_t st) {
+  if (!n_reads) return;
+  hipLaunchKernelGGL(k_mega_pack, dim3(n_reads), dim3(64), 0, st, G, n_reads, moff, mc);
 }
 void launch_graph_sizes(const GraphDev& G, uint64_t n_recs, uint32_t* sizes, uint64_t* scan_scratch, hipStream_t st) {
   if (n_recs) hipLaunchKernelGGL(k_graph_sizes, dim3((uint32_t)std::min<uint64_t>((n_recs + 255) / 256, 65535)), dim3(256),

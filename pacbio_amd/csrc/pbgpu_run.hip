@@ -492,22 +492,49 @@ void pin_to(const std::vector<int>& cpus) {
 // pbgpu_coords_batch view (the records consumer's input): no zero-filled
 // vectors, no pageable staging copies; valid until the next download.
 struct RecordsView {
-  PinnedVec off, recs, km, kb, graph;
+  PinnedVec off, recs, km, kb, graph, moff, mega, munits, mhost;
   pbgpu_coords_batch c{};
+  // on growth, room for the next batches of a ramp (PinnedVec grows by 1.5x)
+  static void room(PinnedVec& v, uint64_t bytes) { if (v.cap < bytes) v.reserve(std::max<uint64_t>(bytes, 1) * 2); }
   void download(pbgpu_aligner* al) {
-    const uint64_t n = al->last_reads, nr = al->last_records, ni = al->last_info;
+    const uint64_t n = al->last_reads;
     static_assert(sizeof(pbgpu_record) == sizeof(Rec), "record layout");
-    off.reserve((n + 1) * 8); recs.reserve(std::max<uint64_t>(nr, 1) * sizeof(Rec));
-    km.reserve(std::max<uint64_t>(ni, 1) * 4); kb.reserve(std::max<uint64_t>(ni, 1) * 4);
-    HIPCHK(hipMemcpyAsync(off.p, al->rec_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, al->st));
-    if (nr) HIPCHK(hipMemcpyAsync(recs.p, al->recs_sorted.p, nr * sizeof(Rec), hipMemcpyDeviceToHost, al->st));
+    c = pbgpu_coords_batch{};
+    // device mega-reads: the records of the reads left to the host only, packed
+    const bool dev_mega = al->graph && al->g_mega;
+    const uint64_t nr = dev_mega ? al->g_hrecs : al->last_records, ni = dev_mega ? al->g_hinfos : al->last_info;
+    const uint64_t* d_off = dev_mega ? al->g_hroff.p : al->rec_off.p;
+    const Rec* d_rec = dev_mega ? al->g_hrec.p : al->recs_sorted.p;
+    const GraphNode* d_graph = dev_mega ? al->g_hgraph.p : al->g_out.p;
+    const int32_t* d_km = dev_mega ? al->g_hinfo.p : al->info_m.p;
+    const int32_t* d_kb = dev_mega ? al->g_hinfo.p + al->g_hinfos + 1 : al->info_b.p;
+    room(off, (n + 1) * 8);
+    if (!dev_mega || al->g_hosts) HIPCHK(hipMemcpyAsync(off.p, d_off, (n + 1) * 8, hipMemcpyDeviceToHost, al->st));
+    else memset(off.p, 0, (n + 1) * 8);
+    room(recs, nr * sizeof(Rec)); room(km, ni * 4); room(kb, ni * 4);
+    if (nr) HIPCHK(hipMemcpyAsync(recs.p, d_rec, nr * sizeof(Rec), hipMemcpyDeviceToHost, al->st));
     if (ni) {
-      HIPCHK(hipMemcpyAsync(km.p, al->info_m.p, ni * 4, hipMemcpyDeviceToHost, al->st));
-      HIPCHK(hipMemcpyAsync(kb.p, al->info_b.p, ni * 4, hipMemcpyDeviceToHost, al->st));
+      HIPCHK(hipMemcpyAsync(km.p, d_km, ni * 4, hipMemcpyDeviceToHost, al->st));
+      HIPCHK(hipMemcpyAsync(kb.p, d_kb, ni * 4, hipMemcpyDeviceToHost, al->st));
     }
     if (al->graph) {
-      graph.reserve(std::max<uint64_t>(nr, 1) * sizeof(GraphNode));
-      if (nr) HIPCHK(hipMemcpyAsync(graph.p, al->g_out.p, nr * sizeof(GraphNode), hipMemcpyDeviceToHost, al->st));
+      room(graph, nr * sizeof(GraphNode));
+      if (nr) HIPCHK(hipMemcpyAsync(graph.p, d_graph, nr * sizeof(GraphNode), hipMemcpyDeviceToHost, al->st));
+    }
+    if (dev_mega) {
+      const uint64_t nm = al->g_mtotal, nu = al->g_munits_used;
+      room(moff, (n + 1) * 8); room(mhost, n + 1); room(mega, nm * sizeof(MegaOut)); room(munits, nu * 4);
+      if (al->last_records) {
+        HIPCHK(hipMemcpyAsync(moff.p, al->g_moff.p, (n + 1) * 8, hipMemcpyDeviceToHost, al->st));
+        HIPCHK(hipMemcpyAsync(mhost.p, al->g_mhost.p, n, hipMemcpyDeviceToHost, al->st));
+      } else {
+        memset(moff.p, 0, (n + 1) * 8);
+        memset(mhost.p, 0, n + 1);
+      }
+      if (nm) HIPCHK(hipMemcpyAsync(mega.p, al->g_mc.p, nm * sizeof(MegaOut), hipMemcpyDeviceToHost, al->st));
+      if (nu) HIPCHK(hipMemcpyAsync(munits.p, al->g_munits.p, nu * 4, hipMemcpyDeviceToHost, al->st));
+      c.mega_offsets = (const uint64_t*)moff.p; c.mega = (const pbgpu_mega_read*)mega.p;
+      c.mega_units = (const uint32_t*)munits.p; c.mega_host = (const uint8_t*)mhost.p;
     }
     HIPCHK(hipStreamSynchronize(al->st));
     pbgpu_record* r = (pbgpu_record*)recs.p;

@@ -106,7 +106,8 @@ assert RECORD_DTYPE.itemsize == 96
 class CoordsBatch(C.Structure):
     _fields_ = [("n_reads", C.c_uint64), ("n_records", C.c_uint64), ("read_offsets", C.POINTER(C.c_uint64)),
                 ("records", C.c_void_p), ("n_info", C.c_uint64), ("kmers_info", C.POINTER(C.c_int32)),
-                ("bases_info", C.POINTER(C.c_int32)), ("graph", C.c_void_p)]
+                ("bases_info", C.POINTER(C.c_int32)), ("graph", C.c_void_p), ("mega_offsets", C.c_void_p),
+                ("mega", C.c_void_p), ("mega_units", C.c_void_p), ("mega_host", C.c_void_p)]
 
 
 # pbgpu_graph_node (create_mega_reads' overlap graph, pbgpu_aligner_set_graph)
@@ -114,13 +115,19 @@ GRAPH_NODE_DTYPE = np.dtype([("lpath", "<i4"), ("lstart", "<i4"), ("lprev", "<i4
                              ("root", "<u4"), ("flags", "<u4")])
 assert GRAPH_NODE_DTYPE.itemsize == 24
 GRAPH_START, GRAPH_END, GRAPH_HOST = 1, 2, 0x80000000
+# pbgpu_mega_read (pbgpu_graph_params.mega_reads)
+MEGA_DTYPE = np.dtype([("imp_s", "<f8"), ("imp_e", "<f8"), ("density", "<f8"), ("rs", "<i4"), ("re", "<i4"),
+                       ("qs", "<i4"), ("lpath", "<i4"), ("sr_len", "<i4"), ("start_unitig", "<i4"),
+                       ("nb_unitigs", "<i4"), ("n_units", "<u4"), ("qend", "<u8"), ("unit_offset", "<u8")])
+assert MEGA_DTYPE.itemsize == 72
 
 
 class GraphParams(C.Structure):
     _fields_ = [("overlap_play", C.c_double), ("nb_errors", C.c_double), ("k_len", C.c_uint32),
                 ("maximize_bases", C.c_int32), ("n_sr", C.c_uint64), ("name_offsets", C.POINTER(C.c_uint64)),
                 ("name_units", C.POINTER(C.c_uint32)), ("unitig_lengths", C.POINTER(C.c_int32)),
-                ("n_unitigs", C.c_uint64)]
+                ("n_unitigs", C.c_uint64), ("mega_reads", C.c_int32), ("tiling", C.c_int32), ("trim", C.c_int32),
+                ("min_density", C.c_double), ("min_len", C.c_double)]
 
 
 class DetailsBatch(C.Structure):

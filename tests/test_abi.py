@@ -39,8 +39,9 @@ def test_abi_version():
 def test_record_layout_matches_header():
     assert pbgpu.RECORD_DTYPE.itemsize == 96
     assert pbgpu.GRAPH_NODE_DTYPE.itemsize == 24
-    # pbgpu_coords_batch: 7 words + the graph pointer (ABI 5)
-    assert C.sizeof(pbgpu.CoordsBatch) == 64
+    assert pbgpu.MEGA_DTYPE.itemsize == 72
+    # pbgpu_coords_batch: 7 words + the graph and mega-read pointers (ABI 5)
+    assert C.sizeof(pbgpu.CoordsBatch) == 96
 
 
 def test_params_default_matches_yaggo_defaults():
