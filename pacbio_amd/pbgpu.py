@@ -481,16 +481,6 @@ class Aligner:
         _check(lib().pbgpu_aligner_set_graph(self.h, C.byref(g)))
 
 
-def parse_unitigs(name):
-    """super_read_name::parse (super_read_name.cc:74-90) for the synthetic names: 12F_13R -> [24, 27]"""
-    out = []
-    for tok in name.split("_"):
-        digits = tok.rstrip("FR")
-        if not digits.isdigit():
-            return []
-        out.append(int(digits) << 1 | (tok.endswith("R")))
-    return out
-
     def shard_counts(self, reads):
         """Sharded index, step 1: this shard's saturated k-mer counts of the batch
         into the aligner's count buffer."""
@@ -781,3 +771,14 @@ class ResidentReads:
             self.close()
         except Exception:
             pass
+
+
+def parse_unitigs(name):
+    """super_read_name::parse (super_read_name.cc:74-90) for the synthetic names: 12F_13R -> [24, 27]"""
+    out = []
+    for tok in name.split("_"):
+        digits = tok.rstrip("FR")
+        if not digits.isdigit():
+            return []
+        out.append(int(digits) << 1 | (tok.endswith("R")))
+    return out
