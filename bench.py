@@ -185,6 +185,8 @@ def main():
                          "(the roofline) measure the kernel, not two overlapping launches")
     ap.add_argument("--parts", type=int, default=2,
                     help="part files of the extra coords-out leg (value_parts; 0 = no such leg)")
+    ap.add_argument("--cmr-steps", type=int, default=2,
+                    help="runs of bin/create_mega_reads over the same files (value_create_mega_reads; 0 = none)")
     ap.add_argument("--skip-default-leg", action="store_true",
                     help="no default-flags device leg (profiling runs: every large-grid launch is then the "
                          "production leg's)")
@@ -333,6 +335,28 @@ def main():
         _rm_parts(pouts[-1])
         prunner.close()
 
+    # ---- create_mega_reads (row f3, the aligner's production caller): the CLI over the
+    # same files, overlap graph / tiling on the GPU; its own clock (--timing wall_s: first
+    # batch read -> mega-reads file closed; the index build is before it), one warm-up run
+    el_cmr, cmr_t = None, None
+    if args.cmr_steps > 0:
+        import json as _json
+        import subprocess
+        cmr = os.path.join(ROOT, "pacbio_amd", "bin", "create_mega_reads")
+        cflags = ["-s", "1M", "-m", str(k), "--psa-min", "13", "-k", "31", "-l", ul_txt, "-B", "15", "--max-count",
+                  "5000", "--stretch-cap", "10000", "-t", str(threads), "-r", sr_fa, "-p", pb_fa, "--timing",
+                  "--devices", str(local), "-o", os.path.join(wd, "mega_reads")]
+        walls = []
+        for i in range(args.cmr_steps + 1):
+            r = subprocess.run([cmr, *cflags], capture_output=True, text=True)
+            if r.returncode:
+                raise RuntimeError(f"create_mega_reads failed: {r.stderr[-2000:]}")
+            cmr_t = _json.loads(r.stderr.strip().splitlines()[-1])
+            if i:
+                walls.append(cmr_t["wall_s"])
+        el_cmr = comm.max(sum(walls))
+    value_cmr = comm.sum(bases_rank) * args.cmr_steps / el_cmr if el_cmr else None
+
     total_bases = comm.sum(bases_rank) * args.steps
     value = total_bases / elapsed
     value_device = comm.sum(bases_rank) * args.device_steps / el_dev
@@ -367,7 +391,7 @@ def main():
     # production device leg): FETCH_SIZE corrected for the kernel's read shape (random
     # 64-B sectors exact; occurrence runs by the 512-B-run calibration; row streams 2x)
     traffic, traffic_note, summ_name, summ_all = None, None, None, {}
-    for name in ("r03_rocprof_summary.json", "r02e_rocprof_summary.json"):
+    for name in ("r03k_rocprof_summary.json", "r03_rocprof_summary.json", "r02e_rocprof_summary.json"):
         summ = os.path.join(ROOT, "profiles", name)
         if os.path.exists(summ):
             try:
@@ -466,6 +490,12 @@ def main():
             "value_device": value_device,
             "value_device_note": "reads resident in HBM, device path to sorted records in HBM, no formatting / "
                                  "output (round-1 definition)",
+            "value_create_mega_reads": value_cmr,
+            "value_create_mega_reads_note": ("bin/create_mega_reads over the same files (overlap graph, tiling and "
+                                             "paths on the GPU, text on the host), mega-reads written per second, "
+                                             f"{args.cmr_steps} cold runs, -t {threads}") if value_cmr else None,
+            "create_mega_reads_stage_s": ({kk: cmr_t[kk] for kk in ("wall_s", "align_s", "download_s", "graph_s",
+                                                                     "output_bytes")} if cmr_t else None),
             "value_parts": value_parts,
             "value_parts_note": (f"the same coords out into {args.parts} part files per GPU (jf_aligner --parts, the "
                                  "reference's split-and-cat in one process: one reader / writer per part, 2 aligners "

@@ -10,9 +10,9 @@ TAG=${1:-r03}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 D=gpurun_out/prof_$TAG
 mkdir -p $D
-timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $D/kt -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --skip-default-leg > $D/bench.json 2> $D/kt.err || { tail -20 $D/kt.err; exit 1; }
+timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $D/kt -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --skip-default-leg --cmr-steps 0 > $D/bench.json 2> $D/kt.err || { tail -20 $D/kt.err; exit 1; }
 echo "kernel trace done"
-B="python3 bench.py --steps 1 --warmup 0 --device-steps 1 --no-cpu-baseline --no-brand --skip-default-leg"
+B="python3 bench.py --steps 1 --warmup 0 --device-steps 1 --no-cpu-baseline --no-brand --skip-default-leg --cmr-steps 0"
 RE="k_seed|k_group|k_lis_w|k_coords|k_rec_sort|k_gather"
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 300 rocprofv3 --pmc $C --kernel-include-regex "$RE" --output-format csv -d $D/p_$C -o run -- $B > $D/p_$C.log 2>&1 || { tail -20 $D/p_$C.log; exit 1; }
