@@ -77,6 +77,10 @@ uint32_t len_buckets();
 void launch_strand_order(const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen, int2* X,
                          hipStream_t st);
 uint32_t big_bucket();
+void launch_fine_win_sort(const Rec* recs, const uint64_t* rec_off, uint32_t n_reads, uint64_t* gscratch, uint32_t* idx,
+                          hipStream_t st);
+void launch_fine_sort(const uint32_t* keys, const int2* vals, const uint64_t* woff, const uint64_t* hit_off, uint32_t r0,
+                      uint32_t nr, uint64_t w_sub0, uint32_t* gcount, uint32_t* okeys, int2* ovals, hipStream_t st);
 void launch_fine_windows(const Rec* recs, uint32_t n, uint64_t* keys, uint32_t* idx, int phase, const uint64_t* roff,
                          uint32_t fk, FineWin* out, hipStream_t st);
 void launch_fine_hits(bool emit, IndexView fx, const uint8_t* seq, const uint64_t* roff, uint32_t r0, uint32_t nr,
@@ -1490,17 +1494,10 @@ static void fine_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   std::vector<uint64_t> woff(n + 1);
   HIPCHK(hipMemcpyAsync(woff.data(), al->rec_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, st));
   // windows sorted by (read, super-read) (the lookup side of prime_frags_pos's std::map)
-  al->fwin.ensure(nwin + 1);
-  al->fwk[0].ensure(nwin + 1); al->fwk[1].ensure(nwin + 1); al->fwi[0].ensure(nwin + 1); al->fwi[1].ensure(nwin + 1);
-  launch_fine_windows(al->recs_sorted.p, nwin, al->fwk[0].p, al->fwi[0].p, 0, rd->off.p, al->PF.k, nullptr, st);
-  {
-    hipcub::DoubleBuffer<uint64_t> dk(al->fwk[0].p, al->fwk[1].p);
-    hipcub::DoubleBuffer<uint32_t> dv(al->fwi[0].p, al->fwi[1].p);
-    size_t tb = 0;
-    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, dk, dv, nwin, 0, 64, st));
-    HIPCHK(hipcub::DeviceRadixSort::SortPairs(temp_storage(al->tmp, tb), tb, dk, dv, nwin, 0, 64, st));
-    launch_fine_windows(al->recs_sorted.p, nwin, nullptr, dv.Current(), 1, rd->off.p, al->PF.k, al->fwin.p, st);
-  }
+  al->fwin.ensure(nwin + 1); al->fwi[0].ensure(nwin + 1);
+  al->sort_scratch.ensure(6ull * nwin + 6);
+  launch_fine_win_sort(al->recs_sorted.p, al->rec_off.p, n, al->sort_scratch.p, al->fwi[0].p, st);
+  launch_fine_windows(al->recs_sorted.p, nwin, nullptr, al->fwi[0].p, 1, rd->off.p, al->PF.k, al->fwin.p, st);
   HIPCHK(hipGetLastError());
   // windowed hits per read
   al->fread_hits.ensure(n + 1);
@@ -1526,8 +1523,8 @@ static void fine_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
     const uint32_t nws = (uint32_t)(woff[r1] - ws0);
     if (nws == 0) { r0 = r1; continue; }
     // sub-batch-relative hit offsets of its reads
-    std::vector<uint64_t> rel(r1 - r0);
-    for (uint32_t r = r0; r < r1; ++r) rel[r - r0] = hoff[r] - hoff[r0];
+    std::vector<uint64_t> rel(r1 - r0 + 1);  // (+ the end of the last read: k_fine_sort)
+    for (uint32_t r = r0; r <= r1; ++r) rel[r - r0] = hoff[r] - hoff[r0];
     al->hit_off.ensure(n + 1);
     HIPCHK(hipMemcpyAsync(al->hit_off.p + r0, rel.data(), rel.size() * 8, hipMemcpyHostToDevice, st));
     al->fkeys[0].ensure(Hs + 1); al->fkeys[1].ensure(Hs + 1);
@@ -1535,17 +1532,12 @@ static void fine_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
     launch_fine_hits(true, fv, rd->seq.p, rd->off.p, r0, r1 - r0, al->fwin.p, al->rec_off.p, nullptr, al->hit_off.p,
                      ws0, al->fkeys[0].p, al->X.p, al->stats.p, st);
     HIPCHK(hipGetLastError());
-    int nbits = 1;
-    while ((1ull << nbits) < 2ull * nws) ++nbits;
-    {
-      hipcub::DoubleBuffer<uint32_t> dk(al->fkeys[0].p, al->fkeys[1].p);
-      hipcub::DoubleBuffer<uint64_t> dv((uint64_t*)al->X.p, (uint64_t*)al->X2.p);
-      size_t tb = 0;
-      HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, dk, dv, Hs, 0, nbits, st));
-      HIPCHK(hipcub::DeviceRadixSort::SortPairs(temp_storage(al->tmp, tb), tb, dk, dv, Hs, 0, nbits, st));
-      if (dk.Current() != al->fkeys[0].p) al->fkeys[0].swap(al->fkeys[1]);
-      if ((int2*)dv.Current() != al->X.p) al->X.swap(al->X2);
-    }
+    al->lstart.ensure(2ull * nws);  // (also the sort's key counts of reads with many windows)
+    launch_fine_sort(al->fkeys[0].p, al->X.p, al->rec_off.p, al->hit_off.p, r0, r1 - r0, ws0, al->lstart.p,
+                     al->fkeys[1].p, al->X2.p, st);
+    HIPCHK(hipGetLastError());
+    al->fkeys[0].swap(al->fkeys[1]);
+    al->X.swap(al->X2);
     al->lstart.ensure(2ull * nws); al->lend.ensure(2ull * nws);
     HIPCHK(hipMemsetAsync(al->lstart.p, 0, 2ull * nws * 4, st));
     HIPCHK(hipMemsetAsync(al->lend.p, 0, 2ull * nws * 4, st));

@@ -2716,6 +2716,116 @@ void launch_rec_sort(const Rec* recs, const uint64_t* rec_off, const uint32_t* o
 }
 
 // ------------------------------------------------------------ fine launchers
+// The coarse records of each read (recs_sorted, grouped by read) as fine windows in
+// (super-read, record) order -- the (read, super-read) order of the windows'
+// std::map lookup (fine_aligner.hpp:50-58), ties in record order as a stable sort
+// leaves them: a bitonic sort per read of (sr, record) keys, in LDS, or in the
+// records-stage scratch (6 words a record) for reads of more than LCAP records.
+template <int BLOCK, int LCAP>
+__global__ __launch_bounds__(BLOCK) void k_fine_win_sort(const Rec* __restrict__ recs, const uint64_t* __restrict__ rec_off,
+                                                         uint32_t n_reads, uint64_t* gscratch, uint32_t* __restrict__ idx) {
+  __shared__ uint64_t s_hi[LCAP], s_lo[LCAP];
+  __shared__ uint32_t s_ex[LCAP];
+  const uint32_t r = blockIdx.x;
+  if (r >= n_reads) return;
+  const uint64_t b = rec_off[r];
+  const uint32_t n = (uint32_t)(rec_off[r + 1] - b);
+  if (n == 0) return;
+  uint32_t np2 = 1;
+  while (np2 < n) np2 <<= 1;
+  if (np2 <= LCAP) {
+    for (uint32_t i = threadIdx.x; i < np2; i += BLOCK) {
+      s_hi[i] = i < n ? (uint64_t)recs[b + i].sr : ~0ull;
+      s_lo[i] = 0;
+      s_ex[i] = i < n ? i : ~0u;
+    }
+    __syncthreads();
+    bitonic_keys<BLOCK>(s_hi, s_lo, s_ex, np2);
+    for (uint32_t i = threadIdx.x; i < n; i += BLOCK) idx[b + i] = (uint32_t)b + s_ex[i];
+  } else {
+    uint64_t* hi = gscratch + 6 * b;
+    uint64_t* lo = hi + np2;
+    uint64_t* ex = lo + np2;
+    for (uint32_t i = threadIdx.x; i < np2; i += BLOCK) {
+      hi[i] = i < n ? (uint64_t)recs[b + i].sr : ~0ull;
+      lo[i] = 0;
+      ex[i] = i < n ? i : ~0ull;
+    }
+    __threadfence_block();
+    __syncthreads();
+    bitonic_keys<BLOCK>(hi, lo, ex, np2);
+    for (uint32_t i = threadIdx.x; i < n; i += BLOCK) idx[b + i] = (uint32_t)(b + ex[i]);
+  }
+}
+void launch_fine_win_sort(const Rec* recs, const uint64_t* rec_off, uint32_t n_reads, uint64_t* gscratch, uint32_t* idx,
+                          hipStream_t st) {
+  if (n_reads) hipLaunchKernelGGL((k_fine_win_sort<256, 2048>), dim3(n_reads), dim3(256), 0, st, recs, rec_off, n_reads,
+                                  gscratch, idx);
+}
+
+// The fine hits of a sub-batch (k_fine_hits: each read's hits contiguous, in
+// (k-mer, occurrence) order, keyed 2 (window - w_sub0) + strand, a read's keys
+// contiguous) stable-sorted by key, so every window's fwd and bwd lists come out in
+// the reference's order, contiguous: one wave per read, a counting sort -- the
+// read's key counts (LDS, or a global region for reads with more than KCAP keys),
+// their exclusive scan, then the hits placed 64 at a time in order, equal keys of a
+// tile ranked by lane.
+template <uint32_t KCAP>
+__global__ __launch_bounds__(64) void k_fine_sort(const uint32_t* __restrict__ keys, const int2* __restrict__ vals,
+                                                  const uint64_t* __restrict__ woff, const uint64_t* __restrict__ hit_off,
+                                                  uint32_t r0, uint32_t nr, uint64_t w_sub0, uint32_t* gcount,
+                                                  uint32_t* __restrict__ okeys, int2* __restrict__ ovals) {
+  __shared__ uint32_t s_cnt[KCAP];
+  if (blockIdx.x >= nr) return;
+  const uint32_t r = r0 + blockIdx.x, lane = threadIdx.x;
+  const uint64_t h0 = hit_off[r], nh = hit_off[r + 1] - h0;
+  if (nh == 0) return;
+  const uint32_t kb = (uint32_t)(2 * (woff[r] - w_sub0)), nk = (uint32_t)(2 * (woff[r + 1] - woff[r]));
+  uint32_t* cnt = nk <= KCAP ? s_cnt : gcount + kb;
+  for (uint32_t x = lane; x < nk; x += 64) cnt[x] = 0;
+  __threadfence_block();
+  __syncthreads();
+  for (uint64_t i = lane; i < nh; i += 64) atomicAdd(&cnt[keys[h0 + i] - kb], 1u);
+  __threadfence_block();
+  __syncthreads();
+  uint32_t carry = 0;  // counts -> read-relative list starts (the cursors)
+  for (uint32_t x0 = 0; x0 < nk; x0 += 64) {
+    const uint32_t x = x0 + lane;
+    const uint32_t v = x < nk ? cnt[x] : 0u;
+    uint32_t inc = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o, 64);
+      if ((int)lane >= o) inc += y;
+    }
+    if (x < nk) cnt[x] = carry + inc - v;
+    carry += (uint32_t)__shfl((int)inc, 63, 64);
+  }
+  __threadfence_block();
+  __syncthreads();
+  for (uint64_t t0 = 0; t0 < nh; t0 += 64) {
+    const uint64_t i = t0 + lane;
+    const bool act = i < nh;
+    const uint32_t k = act ? keys[h0 + i] - kb : 0xFFFFFFFFu;
+    const int2 v = act ? vals[h0 + i] : make_int2(0, 0);
+    uint32_t dest = 0;
+    for (uint64_t rem = __ballot(act); rem;) {
+      const uint32_t leader = (uint32_t)__ffsll((long long)rem) - 1;
+      const uint32_t kl = (uint32_t)__builtin_amdgcn_readlane((int)k, (int)leader);
+      const uint64_t m = __ballot(act && k == kl);
+      uint32_t base = lane == leader ? cnt[kl] : 0u;
+      base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader);
+      if (lane == leader) cnt[kl] = base + (uint32_t)__builtin_popcountll(m);
+      if (act && k == kl) dest = base + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1));
+      rem &= ~m;
+    }
+    if (act) { okeys[h0 + dest] = k + kb; ovals[h0 + dest] = v; }
+  }
+}
+void launch_fine_sort(const uint32_t* keys, const int2* vals, const uint64_t* woff, const uint64_t* hit_off, uint32_t r0,
+                      uint32_t nr, uint64_t w_sub0, uint32_t* gcount, uint32_t* okeys, int2* ovals, hipStream_t st) {
+  if (nr) hipLaunchKernelGGL((k_fine_sort<8192>), dim3(nr), dim3(64), 0, st, keys, vals, woff, hit_off, r0, nr, w_sub0,
+                             gcount, okeys, ovals);
+}
 void launch_fine_windows(const Rec* recs, uint32_t n, uint64_t* keys, uint32_t* idx, int phase, const uint64_t* roff,
                          uint32_t fk, FineWin* out, hipStream_t st) {
   const uint32_t g = std::max<uint32_t>(1, std::min<uint32_t>(4096, (n + 255) / 256));

@@ -9,4 +9,4 @@ if [ -n "$TESTS" ]; then
   timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu $TESTS > gpurun_out/check_tests.log 2>&1
   rc=$?; tail -5 gpurun_out/check_tests.log; [ $rc -eq 0 ] || exit $rc
 fi
-[ $# -gt 0 ] && bash tools/exp/ab_group_ms.sh "$@"
+if [ $# -gt 0 ]; then bash tools/exp/ab_group_ms.sh "$@"; fi

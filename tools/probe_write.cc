@@ -32,11 +32,15 @@ int main(int argc, char** argv) {
   for (size_t i = 0; i < N; ++i) srcp[i] = "ACGT 0123456789\n"[i & 15];
   for (int a = 3; a < argc; ++a) {
     const int T = atoi(argv[a]);
-    for (int mode = 0; mode < 4; ++mode) {
+    for (int mode = 0; mode < 6; ++mode) {
       if (mode == 0 && T != 1) continue;
       unlink(path);
-      int fd = open(path, O_CREAT | O_RDWR | O_TRUNC | (mode == 3 ? O_DIRECT : 0), 0644);
+      int fd = open(path, O_CREAT | O_RDWR | O_TRUNC | (mode >= 3 ? O_DIRECT : 0), 0644);
       if (fd < 0) { perror("open"); return 1; }
+      // modes 4 / 5: the file sized first (fallocate / sparse ftruncate), so the direct
+      // writes do not extend it (file systems may then take the inode lock shared)
+      if (mode == 4 && fallocate(fd, 0, 0, (off_t)N)) { perror("fallocate"); return 1; }
+      if (mode == 5 && ftruncate(fd, (off_t)N)) { perror("ftruncate"); return 1; }
       const double t0 = now();
       if (mode == 0) {
         size_t o = 0;
@@ -49,7 +53,7 @@ int main(int argc, char** argv) {
             while (a0 < a1) { ssize_t w = pwrite(fd, src.data() + a0, std::min<size_t>(a1 - a0, 64 << 20), (off_t)a0); if (w <= 0) { perror("pwrite"); exit(1); } a0 += (size_t)w; }
           });
         for (auto& x : th) x.join();
-      } else if (mode == 3) {  // O_DIRECT pwrite of aligned 64 MiB pieces from T threads
+      } else if (mode >= 3) {  // O_DIRECT pwrite of aligned 64 MiB pieces from T threads
         std::vector<std::thread> th;
         const size_t piece = 64 << 20;
         std::atomic<size_t> next(0);
@@ -76,7 +80,8 @@ int main(int argc, char** argv) {
       }
       close(fd);
       const double dt = now() - t0;
-      printf("%s threads=%d %.2f GB/s (%.3f s)\n", mode == 0 ? "write" : mode == 1 ? "pwrite" : mode == 2 ? "mmap" : "odirect", T, N / dt / 1e9, dt);
+      static const char* names[] = {"write", "pwrite", "mmap", "odirect", "odirect_fallocated", "odirect_sized"};
+      printf("%s threads=%d %.2f GB/s (%.3f s)\n", names[mode], T, N / dt / 1e9, dt);
       fflush(stdout);
     }
   }
