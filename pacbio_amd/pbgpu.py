@@ -375,6 +375,20 @@ class Coords:
             self.records = np.frombuffer(buf, dtype=RECORD_DTYPE).copy()
         else:
             self.records = np.zeros(0, dtype=RECORD_DTYPE)
+        self.mega = None  # (offsets per read, MEGA_DTYPE records, units, host flags) with the device mega-reads
+        if c.mega_offsets:
+            moff = np.ctypeslib.as_array(C.cast(c.mega_offsets, C.POINTER(C.c_uint64)), shape=(n + 1,)).copy()
+            nm = int(moff[-1])
+            recs = np.zeros(0, MEGA_DTYPE)
+            if nm:
+                mbuf = (C.c_char * (nm * MEGA_DTYPE.itemsize)).from_address(c.mega)
+                recs = np.frombuffer(mbuf, dtype=MEGA_DTYPE).copy()
+            nu = int((recs["unit_offset"] + recs["n_units"]).max()) if nm else 0
+            units = (np.ctypeslib.as_array(C.cast(c.mega_units, C.POINTER(C.c_uint32)), shape=(nu,)).copy()
+                     if nu else np.zeros(0, np.uint32))
+            host = np.ctypeslib.as_array(C.cast(c.mega_host, C.POINTER(C.c_uint8)), shape=(n,)).copy() if n else \
+                np.zeros(0, np.uint8)
+            self.mega = (moff, recs, units, host)
         self.graph = None  # pbgpu_graph_node per record (GRAPH_NODE_DTYPE) when the aligner's graph is on
         if c.graph and nr:
             gbuf = (C.c_char * (nr * GRAPH_NODE_DTYPE.itemsize)).from_address(c.graph)
@@ -463,8 +477,10 @@ class Aligner:
     def reset_stats(self):
         _check(lib().pbgpu_aligner_reset_stats(self.h))
 
-    def set_graph(self, names, unitig_lengths, k_len, overlap_play=1.3, nb_errors=3.0, maximize_bases=False):
-        """pbgpu_aligner_set_graph: create_mega_reads' overlap graph after every alignment.
+    def set_graph(self, names, unitig_lengths, k_len, overlap_play=1.3, nb_errors=3.0, maximize_bases=False,
+                  mega_reads=False, tiling="greedy", trim=False, min_density=0.029, min_len=100.0):
+        """pbgpu_aligner_set_graph: create_mega_reads' overlap graph after every alignment
+        (and with mega_reads the components, tiling and printed paths too).
         names: per super-read of the index its unitig list (id << 1 | R); None turns it off."""
         if names is None:
             _check(lib().pbgpu_aligner_set_graph(self.h, None))
@@ -475,9 +491,11 @@ class Aligner:
                                      else np.zeros(1, np.uint32), dtype=np.uint32)
         ul = np.ascontiguousarray(unitig_lengths, dtype=np.int32)
         self._graph_keep = (off, units, ul)
+        til = {"none": 0, "greedy": 1, "maximal": 2, "weighted": 3}[tiling]
         g = GraphParams(float(overlap_play), float(nb_errors), int(k_len), int(bool(maximize_bases)), len(names),
                         off.ctypes.data_as(C.POINTER(C.c_uint64)), units.ctypes.data_as(C.POINTER(C.c_uint32)),
-                        ul.ctypes.data_as(C.POINTER(C.c_int32)), len(ul))
+                        ul.ctypes.data_as(C.POINTER(C.c_int32)), len(ul), int(bool(mega_reads)), til, int(bool(trim)),
+                        float(min_density), float(min_len))
         _check(lib().pbgpu_aligner_set_graph(self.h, C.byref(g)))
 
 

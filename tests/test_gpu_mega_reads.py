@@ -215,3 +215,35 @@ def test_device_graph_c2_reads(tmp_path):
     _run([*base, "--host-graph", "-o", b], timeout=300)
     ta = open(a).read()
     assert ta.count(">") > 1000 and ta == open(b).read()
+
+
+def _format_device_mega(name, moff, recs, units, r):
+    """print_mega_reads' text of read r from the device mega-reads (the C ABI batch)"""
+    out = []
+    for m in recs[int(moff[r]):int(moff[r + 1])]:
+        u = units[int(m["unit_offset"]):int(m["unit_offset"]) + int(m["n_units"])]
+        nm = "_".join(f"{int(x) >> 1}{'R' if int(x) & 1 else 'F'}" for x in u)
+        out.append(f"{m['imp_s']:.2f} {m['imp_e']:.2f} {m['rs']} {m['re']} {m['qs']} {m['qend']} {m['lpath']} "
+                   f"{m['density']:.4f} {nm} {m['sr_len']}\n")
+    return (f">{name}\n" + "".join(out)) if out else ""
+
+
+@pytest.mark.parametrize("tiling", ["greedy", "maximal"])
+def test_abi_device_mega_reads_match_cli(synth, tmp_path, tiling):
+    """the mega-reads through the C ABI (pbgpu_aligner_set_graph with mega_reads,
+    pbgpu_download's mega arrays), formatted here, equal the CLI's file"""
+    from pacbio_amd import pbgpu
+    d, ul, _ = synth
+    out = str(tmp_path / "mr")
+    _run(["-s", "1M", "-m", "17", "-k", "31", "-l", os.path.join(d, "ul.txt"), "-T", tiling, "-L", "0", "-o", out,
+          "-r", os.path.join(d, "sr.fa"), "-p", os.path.join(d, "pb.fa")])
+    names, seqs = read_fasta(os.path.join(d, "sr.fa"))
+    pn, ps = read_fasta(os.path.join(d, "pb.fa"))
+    ix = pbgpu.Index.from_records(names, seqs, 17)
+    al = pbgpu.Aligner(ix, k=17, forward=True, unitigs_k=31, unitig_lengths=ul)
+    al.set_graph([pbgpu.parse_unitigs(n) for n in names], ul, 31, mega_reads=True, tiling=tiling, min_len=0.0)
+    c = al.align(ps)
+    moff, recs, units, host = c.mega
+    assert not host.any() and len(recs) >= 10
+    got = "".join(_format_device_mega(n.split()[0], moff, recs, units, r) for r, n in enumerate(pn))
+    assert got == open(out).read()
