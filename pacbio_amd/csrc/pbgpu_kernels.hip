@@ -3041,6 +3041,7 @@ __global__ __launch_bounds__(GRAPH_SORT_BLOCK) void k_graph_sort(GraphDev G, uin
 #endif
 constexpr uint32_t GRING = PBGPU_GRING, GRING_U = 8;
 constexpr uint32_t GRAPH_NMAX_K = GRAPH_NMAX;  // reads of more records go to the host (LDS union-find)
+static_assert(GRAPH_NMAX_K <= 4096, "k_graph matches roots by 12 bits");
 __global__ __launch_bounds__(64) void k_graph(GraphDev G, uint32_t n_reads) {
   // the ring: implied start / end and error, {idx | nsz << 16, lp_add}, name offset, the
   // first GRING_U unitigs and prefix sums 1..GRING_U - 1 of names of <= GRING_U unitigs,
@@ -3048,8 +3049,8 @@ __global__ __launch_bounds__(64) void k_graph(GraphDev G, uint32_t n_reads) {
   __shared__ double s_is[GRING], s_ie[GRING], s_er[GRING], s_lsi[GRING];
   __shared__ uint2 s_meta[GRING];
   __shared__ uint64_t s_po[GRING];
-  __shared__ uint32_t s_u[GRING * GRING_U];
-  __shared__ uint2 s_pp[GRING * (GRING_U - 1)];
+  __shared__ uint32_t s_u[GRING_U * GRING];        // [u * GRING + slot]: a lane per slot, no bank conflicts
+  __shared__ uint2 s_pp[(GRING_U - 1) * GRING];
   __shared__ int32_t s_lp[GRING], s_lun[GRING], s_lst[GRING], s_lpv[GRING];
   __shared__ uint8_t s_fl[GRING];
   __shared__ uint16_t s_par[GRAPH_NMAX_K];
@@ -3074,9 +3075,9 @@ __global__ __launch_bounds__(64) void k_graph(GraphDev G, uint32_t n_reads) {
     s_is[sl] = d.imp_s; s_ie[sl] = d.imp_e; s_er[sl] = d.err; s_po[sl] = d.poff;
     s_meta[sl] = make_uint2(d.idx | (d.nsz << 16), d.lp_add);
     const uint32_t m = d.nsz < GRING_U ? d.nsz : GRING_U;
-    for (uint32_t u = 0; u < m; ++u) s_u[sl * GRING_U + u] = G.ounits[d.poff + u];
+    for (uint32_t u = 0; u < m; ++u) s_u[u * GRING + sl] = G.ounits[d.poff + u];
     if (d.nsz <= GRING_U)
-      for (uint32_t u = 1; u < m; ++u) s_pp[sl * (GRING_U - 1) + u - 1] = G.pp[d.poff + u];
+      for (uint32_t u = 1; u < m; ++u) s_pp[(u - 1) * GRING + sl] = G.pp[d.poff + u];
     s_lp[sl] = (int32_t)d.lp_add; s_lun[sl] = (int32_t)d.nsz; s_lst[sl] = -1; s_lpv[sl] = -1;
     s_lsi[sl] = d.imp_s; s_fl[sl] = (uint8_t)(GRAPH_START | GRAPH_END);
   };
@@ -3122,8 +3123,8 @@ __global__ __launch_bounds__(64) void k_graph(GraphDev G, uint32_t n_reads) {
     // name i's first GRING_U unitigs in registers (the same for every lane)
     uint32_t a[GRING_U];
 #pragma unroll
-    for (uint32_t u = 0; u < GRING_U; ++u) a[u] = s_u[si * GRING_U + u];
-    auto unit_i = [&](uint32_t t) -> uint32_t { return sa <= GRING_U ? s_u[si * GRING_U + t] : G.ounits[po_i + t]; };
+    for (uint32_t u = 0; u < GRING_U; ++u) a[u] = s_u[u * GRING + si];
+    auto unit_i = [&](uint32_t t) -> uint32_t { return sa <= GRING_U ? s_u[t * GRING + si] : G.ounits[po_i + t]; };
     bool any_edge = false;
     for (uint32_t j0 = i + 1; j0 < n; j0 += 64) {
       PROF_T(pa);
@@ -3151,7 +3152,7 @@ __global__ __launch_bounds__(64) void k_graph(GraphDev G, uint32_t n_reads) {
           // t >= max(sa - sb + 1, 1) with name_i[t..sa) == name_j[0..sa - t)
           uint32_t bu[GRING_U];
 #pragma unroll
-          for (uint32_t u = 0; u < GRING_U; ++u) bu[u] = s_u[sj * GRING_U + u];
+          for (uint32_t u = 0; u < GRING_U; ++u) bu[u] = s_u[u * GRING + sj];
           const int t0 = (int)sa - (int)sb + 1;
 #pragma unroll
           for (int t = (int)GRING_U - 1; t >= 1; --t) {
@@ -3163,10 +3164,10 @@ __global__ __launch_bounds__(64) void k_graph(GraphDev G, uint32_t n_reads) {
           same = sb == sa;
 #pragma unroll
           for (uint32_t u = 0; u < GRING_U; ++u) same &= (u >= sa) | (a[u] == bu[u]);
-          v = nb ? s_pp[sj * (GRING_U - 1) + (uint32_t)nb - 1] : make_uint2(0u, 0u);
+          v = nb ? s_pp[((uint32_t)nb - 1) * GRING + sj] : make_uint2(0u, 0u);
         } else {
           const uint64_t po_j = s_po[sj];
-          auto unit_j = [&](uint32_t q) -> uint32_t { return sb <= GRING_U ? s_u[sj * GRING_U + q] : G.ounits[po_j + q]; };
+          auto unit_j = [&](uint32_t q) -> uint32_t { return sb <= GRING_U ? s_u[q * GRING + sj] : G.ounits[po_j + q]; };
           const uint32_t u0 = unit_j(0);
           const int t0 = (int)sa - (int)sb + 1;
           for (uint32_t t = t0 > 1 ? (uint32_t)t0 : 1u; t < sa; ++t) {
@@ -3216,12 +3217,14 @@ __global__ __launch_bounds__(64) void k_graph(GraphDev G, uint32_t n_reads) {
         const uint32_t r1 = find(it_i);
         const uint32_t R = edge ? find(mj.x & 0xFFFFu) : r1;
         const uint32_t rk = s_rank[R];
-        bool first = edge & (R != r1);
-        for (uint64_t m = em; m; m &= m - 1) {
-          const uint32_t l = (uint32_t)__ffsll((long long)m) - 1;
-          const uint32_t vv = (uint32_t)__builtin_amdgcn_readlane((int)R, (int)l);
-          first &= !((lane > l) & (R == vv));
+        // the edge lanes holding the same root: a ballot per bit of R (node indices < 2^12)
+        uint64_t same = em;
+#pragma unroll
+        for (uint32_t bit = 0; bit < 12; ++bit) {
+          const uint64_t bb = __ballot((R >> bit) & 1u);
+          same &= ((R >> bit) & 1u) ? bb : ~bb;
         }
+        const bool first = edge & (R != r1) & ((same & ((1ull << lane) - 1)) == 0);
         uint32_t cur = r1, crank = s_rank[r1];
         for (uint64_t fm = __ballot(first); fm; fm &= fm - 1) {
           const uint32_t l = (uint32_t)__ffsll((long long)fm) - 1;
