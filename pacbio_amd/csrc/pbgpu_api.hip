@@ -1613,6 +1613,8 @@ static void graph_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   uint64_t tot = 0;
   HIPCHK(hipMemcpyAsync(&tot, al->g_poff.p + nrec, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  // k_graph keeps name offsets as 32 bits (a batch of 2^32 unitigs would be 48 GB of names)
+  if (tot >= (1ull << 32)) throw bad_input("more than 2^32 name unitigs in one batch's records");
   al->g_pre.ensure(3 * tot + 3); al->g_imp.ensure(nrec + 1); al->g_desc.ensure(nrec + 1); al->g_out.ensure(nrec + 1);
   G.pp = (uint2*)al->g_pre.p; G.ounits = al->g_pre.p + 2 * (tot + 1);
   G.imp = al->g_imp.p; G.desc = al->g_desc.p; G.out = al->g_out.p;

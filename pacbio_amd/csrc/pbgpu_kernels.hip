@@ -2995,15 +2995,24 @@ DEV uint64_t graph_dkey(double x) {
 }
 // per read: records by (imp_s, imp_e), ties in record order (the host's stable_sort of
 // sort_nodes), written out as descriptors in that order
-constexpr uint32_t GRAPH_SORT_BLOCK = 256;
+// Two tiers by the read's record count (LDS sized to the tier, so the common
+// reads of <= GRAPH_NM_SMALL records run many blocks a CU): NM = GRAPH_NM_SMALL
+// takes those, NM = GRAPH_NMAX the rest.
+constexpr uint32_t GRAPH_SORT_BLOCK = 256, GRAPH_NM_SMALL = 1024;
+template <uint32_t NM>
+DEV bool graph_tier(const GraphDev& G, uint32_t n) {
+  if (n == 0 || n > G.nmax || n > GRAPH_NMAX) return false;
+  return n <= NM && (NM == GRAPH_NM_SMALL || n > GRAPH_NM_SMALL);
+}
+template <uint32_t NM>
 __global__ __launch_bounds__(GRAPH_SORT_BLOCK) void k_graph_sort(GraphDev G, uint32_t n_reads) {
-  __shared__ uint64_t s_hi[GRAPH_NMAX], s_lo[GRAPH_NMAX];
-  __shared__ uint16_t s_ex[GRAPH_NMAX];
+  __shared__ uint64_t s_hi[NM], s_lo[NM];
+  __shared__ uint16_t s_ex[NM];
   const uint32_t r = blockIdx.x;
   if (r >= n_reads) return;
   const uint64_t b = G.rec_off[r];
   const uint32_t n = (uint32_t)(G.rec_off[r + 1] - b);
-  if (n == 0 || n > G.nmax) return;
+  if (!graph_tier<NM>(G, n)) return;
   uint32_t np2 = 1;
   while (np2 < n) np2 <<= 1;
   for (uint32_t i = threadIdx.x; i < np2; i += GRAPH_SORT_BLOCK) {
@@ -3042,29 +3051,35 @@ __global__ __launch_bounds__(GRAPH_SORT_BLOCK) void k_graph_sort(GraphDev G, uin
 constexpr uint32_t GRING = PBGPU_GRING, GRING_U = 8;
 constexpr uint32_t GRAPH_NMAX_K = GRAPH_NMAX;  // reads of more records go to the host (LDS union-find)
 static_assert(GRAPH_NMAX_K <= 4096, "k_graph matches roots by 12 bits");
+template <uint32_t NM>
 __global__ __launch_bounds__(64) void k_graph(GraphDev G, uint32_t n_reads) {
   // the ring: implied start / end and error, {idx | nsz << 16, lp_add}, name offset, the
   // first GRING_U unitigs and prefix sums 1..GRING_U - 1 of names of <= GRING_U unitigs,
   // and the path state
   __shared__ double s_is[GRING], s_ie[GRING], s_er[GRING], s_lsi[GRING];
   __shared__ uint2 s_meta[GRING];
-  __shared__ uint64_t s_po[GRING];
+  __shared__ uint32_t s_po[GRING];  // < 2^32 (checked on the host)
   __shared__ uint32_t s_u[GRING_U * GRING];        // [u * GRING + slot]: a lane per slot, no bank conflicts
+#ifdef PBGPU_GRAPH_PP_LDS
   __shared__ uint2 s_pp[(GRING_U - 1) * GRING];
-  __shared__ int32_t s_lp[GRING], s_lun[GRING], s_lst[GRING], s_lpv[GRING];
+#endif
+  __shared__ int32_t s_lp[GRING], s_lun[GRING];
+  __shared__ int16_t s_lst[GRING], s_lpv[GRING];  // node indices < 4096, or -1
   __shared__ uint8_t s_fl[GRING];
-  __shared__ uint16_t s_par[GRAPH_NMAX_K];
-  __shared__ uint8_t s_rank[GRAPH_NMAX_K];
+  __shared__ uint16_t s_par[NM];
+  __shared__ uint8_t s_rank[NM];
   const uint32_t r = blockIdx.x;
   if (r >= n_reads) return;
   const uint32_t lane = threadIdx.x;
   const uint64_t b = G.rec_off[r];
   const uint32_t n = (uint32_t)(G.rec_off[r + 1] - b);
   if (n == 0) return;
-  if (n > G.nmax || n > GRAPH_NMAX_K) {  // the host traverses this read
-    for (uint32_t i = lane; i < n; i += 64) G.out[b + i] = GraphNode{0, -1, -1, 0, i, GRAPH_HOST};
+  if (n > G.nmax || n > GRAPH_NMAX_K) {  // the host traverses this read (marked by the top tier)
+    if (NM == GRAPH_NMAX)
+      for (uint32_t i = lane; i < n; i += 64) G.out[b + i] = GraphNode{0, -1, -1, 0, i, GRAPH_HOST};
     return;
   }
+  if (!graph_tier<NM>(G, n)) return;
   const double rl = (double)(G.roff[r + 1] - G.roff[r]);
   const double play = G.play, kd = (double)G.k;
   const uint32_t km1 = G.k - 1;
@@ -3072,12 +3087,14 @@ __global__ __launch_bounds__(64) void k_graph(GraphDev G, uint32_t n_reads) {
   auto load_pos = [&](uint32_t p) {  // node_info::reset (overlap_graph.hpp:24-34) of sorted position p
     const uint32_t sl = p % GRING;
     const GDesc d = G.desc[b + p];
-    s_is[sl] = d.imp_s; s_ie[sl] = d.imp_e; s_er[sl] = d.err; s_po[sl] = d.poff;
+    s_is[sl] = d.imp_s; s_ie[sl] = d.imp_e; s_er[sl] = d.err; s_po[sl] = (uint32_t)d.poff;
     s_meta[sl] = make_uint2(d.idx | (d.nsz << 16), d.lp_add);
     const uint32_t m = d.nsz < GRING_U ? d.nsz : GRING_U;
     for (uint32_t u = 0; u < m; ++u) s_u[u * GRING + sl] = G.ounits[d.poff + u];
+#ifdef PBGPU_GRAPH_PP_LDS
     if (d.nsz <= GRING_U)
       for (uint32_t u = 1; u < m; ++u) s_pp[(u - 1) * GRING + sl] = G.pp[d.poff + u];
+#endif
     s_lp[sl] = (int32_t)d.lp_add; s_lun[sl] = (int32_t)d.nsz; s_lst[sl] = -1; s_lpv[sl] = -1;
     s_lsi[sl] = d.imp_s; s_fl[sl] = (uint8_t)(GRAPH_START | GRAPH_END);
   };
@@ -3117,7 +3134,7 @@ __global__ __launch_bounds__(64) void k_graph(GraphDev G, uint32_t n_reads) {
     const uint2 mi = s_meta[si];
     const uint32_t it_i = mi.x & 0xFFFFu, sa = mi.x >> 16;
     const double err_i = s_er[si];
-    const uint64_t po_i = s_po[si];
+    const uint32_t po_i = s_po[si];
     const int32_t lp_i = s_lp[si], lun_i = s_lun[si], lst_i = s_lst[si];
     const double lsi_i = s_lsi[si];
     // name i's first GRING_U unitigs in registers (the same for every lane)
@@ -3164,9 +3181,13 @@ __global__ __launch_bounds__(64) void k_graph(GraphDev G, uint32_t n_reads) {
           same = sb == sa;
 #pragma unroll
           for (uint32_t u = 0; u < GRING_U; ++u) same &= (u >= sa) | (a[u] == bu[u]);
+#ifdef PBGPU_GRAPH_PP_LDS
           v = nb ? s_pp[((uint32_t)nb - 1) * GRING + sj] : make_uint2(0u, 0u);
+#else
+          v = nb ? G.pp[s_po[sj] + (uint32_t)nb] : make_uint2(0u, 0u);
+#endif
         } else {
-          const uint64_t po_j = s_po[sj];
+          const uint32_t po_j = s_po[sj];
           auto unit_j = [&](uint32_t q) -> uint32_t { return sb <= GRING_U ? s_u[q * GRING + sj] : G.ounits[po_j + q]; };
           const uint32_t u0 = unit_j(0);
           const int t0 = (int)sa - (int)sb + 1;
@@ -3199,9 +3220,9 @@ __global__ __launch_bounds__(64) void k_graph(GraphDev G, uint32_t n_reads) {
         const bool upd = nlpath > lp_j || (nlpath == lp_j && (s_lst[sj] == -1 || lsi_i > s_lsi[sj]));
         if (upd) {
           s_lp[sj] = nlpath;
-          s_lst[sj] = lst_i == -1 ? (int32_t)it_i : lst_i;
+          s_lst[sj] = (int16_t)(lst_i == -1 ? (int32_t)it_i : lst_i);
           s_lsi[sj] = lsi_i;
-          s_lpv[sj] = (int32_t)it_i;
+          s_lpv[sj] = (int16_t)it_i;
           s_lun[sj] = lun_i + (int32_t)sb - nb;
         }
       }
@@ -3594,8 +3615,10 @@ void launch_graph(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hipStrea
   if (!n_recs || !n_reads) return;
   hipLaunchKernelGGL(k_graph_prep, dim3((uint32_t)std::min<uint64_t>((n_recs + 255) / 256, 65535)), dim3(256), 0, st,
                      G, n_recs);
-  hipLaunchKernelGGL(k_graph_sort, dim3(n_reads), dim3(GRAPH_SORT_BLOCK), 0, st, G, n_reads);
-  hipLaunchKernelGGL(k_graph, dim3(n_reads), dim3(64), 0, st, G, n_reads);
+  hipLaunchKernelGGL(k_graph_sort<GRAPH_NM_SMALL>, dim3(n_reads), dim3(GRAPH_SORT_BLOCK), 0, st, G, n_reads);
+  hipLaunchKernelGGL(k_graph_sort<GRAPH_NMAX>, dim3(n_reads), dim3(GRAPH_SORT_BLOCK), 0, st, G, n_reads);
+  hipLaunchKernelGGL(k_graph<GRAPH_NM_SMALL>, dim3(n_reads), dim3(64), 0, st, G, n_reads);
+  hipLaunchKernelGGL(k_graph<GRAPH_NMAX>, dim3(n_reads), dim3(64), 0, st, G, n_reads);
 }
 
 }  // namespace pbgpu
