@@ -3303,6 +3303,16 @@ __global__ __launch_bounds__(64) void k_graph(GraphDev G, uint32_t n_reads) {
 // scratch regions in HBM.  std::min / std::max are restated as their
 // definitions (b < a ? b : a, a < b ? b : a).
 DEV double std_min(double a, double b) { return b < a ? b : a; }
+DEV uint32_t rl_u32(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
+DEV double rl_f64(double v, uint32_t l) {  // lane l's value, l wave-uniform
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  return __longlong_as_double((long long)(((uint64_t)rl_u32((uint32_t)(u >> 32), l) << 32) | rl_u32((uint32_t)u, l)));
+}
+DEV uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
 DEV double std_max(double a, double b) { return a < b ? b : a; }
 DEV int32_t graph_ulen(const GraphDev& G, uint32_t id) { return id < G.n_ul ? G.ul[id] : 0; }  // ReadGraph::ulen
 constexpr uint32_t UNIT_INVALID = 0x7fffffffu;  // super_read_name::invalid_id
@@ -3323,6 +3333,7 @@ __global__ __launch_bounds__(64) void k_mega(GraphDev G, uint32_t n_reads) {
   const uint32_t k = G.k;
   const double rl = (double)(G.roff[r + 1] - G.roff[r]);
   MegaTmp* cand = G.cand + b;
+  PROF_T(km0);
   // ---- candidates, in node order (mega_reads_per_comp's loop body up to the filter)
   uint32_t nc = 0;
   for (uint32_t i0 = 0; i0 < n; i0 += 64) {
@@ -3386,29 +3397,23 @@ __global__ __launch_bounds__(64) void k_mega(GraphDev G, uint32_t n_reads) {
   }
   __threadfence_block();
   __syncthreads();
-  if (lane != 0) return;
-  // ---- components: per union-find root, in root order, the best terminal node
+  PROF_T(km1);
+  // ---- components (per union-find root, in root order, the best terminal node), the
+  // tiling order and tile_greedy / weighted with every lane: each of the reference's
+  // O(m^2) comparison loops as 64-wide register rows broadcast by readlane, the interval
+  // sets in LDS.  A NaN density or weight makes the reference's comparison chains
+  // order-dependent; such a read runs the serial lane-0 restatement instead.
   int32_t* comp = G.ord + b;           // candidate index per component, sorted by root
   int32_t* order = G.ord + G.n_recs + b;
   int32_t* tiled = G.ord + 2 * G.n_recs + b;
-  uint32_t m = 0;
-  for (uint32_t c = 0; c < nc; ++c) {
-    const uint32_t root = cand[c].root;
-    uint32_t lo = 0, hi = m;  // lower_bound by root
-    while (lo < hi) { const uint32_t mid = (lo + hi) / 2; if (cand[comp[mid]].root < root) lo = mid + 1; else hi = mid; }
-    if (lo == m || cand[comp[lo]].root != root) {
-      for (uint32_t q = m; q > lo; --q) comp[q] = comp[q - 1];
-      comp[lo] = (int32_t)c; ++m;
-    } else {
-      const MegaTmp& cur = cand[comp[lo]];
-      if (cand[c].lpath > cur.lpath || (cand[c].lpath == cur.lpath && cand[c].density > cur.density)) comp[lo] = (int32_t)c;
-    }
-  }
   auto M = [&](int32_t t) -> const MegaTmp& { return cand[comp[t]]; };  // mega_reads_[t]
-  for (uint32_t t = 0; t < m; ++t) order[t] = (int32_t)t;
-  uint32_t nt = 0;  // tiled_mr_
+  auto weight = [&](const MegaTmp& q) -> double {  // weights_[t] (tile_weighted)
+    const int32_t span = G.recs[b + q.end_node].re - G.recs[b + q.start_node].rs + 1;
+    return __dmul_rn(__dmul_rn(q.density, q.density), (double)span);
+  };
   const double play = G.play;
   const double kplay = __dmul_rn((double)k, play);
+  uint32_t m = 0, nt = 0;  // components, tiled_mr_
   auto stable_sort = [&](int32_t* a, uint32_t cnt, auto less) {  // insertion sort: stable
     for (uint32_t x = 1; x < cnt; ++x) {
       const int32_t v = a[x];
@@ -3417,143 +3422,387 @@ __global__ __launch_bounds__(64) void k_mega(GraphDev G, uint32_t n_reads) {
       a[y] = v;
     }
   };
-  if (G.tiling == PBGPU_TILING_GREEDY || G.tiling == PBGPU_TILING_WEIGHTED) {
-    if (G.tiling == PBGPU_TILING_GREEDY) {
-      stable_sort(order, m, [&](int32_t x, int32_t y) { return M(y).lpath < M(x).lpath; });
-    } else {
-      double* w = (double*)(G.ivs + b);  // weights_[t]
+  bool odd = false;
+  for (uint32_t c = lane; c < nc; c += 64) {
+    const MegaTmp& q = cand[c];
+    odd |= isnan(q.density) | ((G.tiling == PBGPU_TILING_WEIGHTED) && isnan(weight(q)));
+  }
+  const bool serial = __ballot(odd) != 0;
+  if (!serial) {
+    __shared__ uint64_t s_roots[GRAPH_NMAX / 64];  // the winners' roots (node indices)
+    __shared__ uint32_t s_rpre[GRAPH_NMAX / 64];
+    static_assert(GRAPH_NMAX == 64 * 64, "one root word a lane");
+    s_roots[lane] = 0;
+    __syncthreads();
+    // a candidate wins its root if no candidate of the root has a larger (lpath,
+    // density) and none before it an equal one: where the reference's fold (replace on
+    // strictly better, in candidate order) ends
+    for (uint32_t c0 = 0; c0 < nc; c0 += 64) {
+      const uint32_t c = c0 + lane;
+      const bool ok = c < nc;
+      const uint32_t rt = ok ? cand[c].root : 0xFFFFFFFFu;
+      const int32_t lp = ok ? cand[c].lpath : 0;
+      const double d = ok ? cand[c].density : 0.0;
+      bool win = ok;
+      for (uint32_t e0 = 0; e0 < nc; e0 += 64) {
+        const uint32_t e = e0 + lane;
+        const uint32_t rte = e < nc ? cand[e].root : 0xFFFFFFFEu;
+        const int32_t lpe = e < nc ? cand[e].lpath : 0;
+        const double de = e < nc ? cand[e].density : 0.0;
+        const uint32_t cnt = nc - e0 < 64 ? nc - e0 : 64;
+        for (uint32_t x = 0; x < cnt; ++x) {
+          const uint32_t r2 = rl_u32(rte, x);
+          const int32_t lp2 = (int32_t)rl_u32((uint32_t)lpe, x);
+          const double d2 = rl_f64(de, x);
+          const bool better = (lp2 > lp) | ((lp2 == lp) & (d2 > d));
+          const bool tie_before = (lp2 == lp) & (d2 == d) & (e0 + x < c);
+          win &= !((r2 == rt) & (better | tie_before));
+        }
+      }
+      if (win) atomicOr((unsigned long long*)&s_roots[rt >> 6], 1ull << (rt & 63));
+      if (ok) tiled[c] = win ? 1 : 0;  // (scratch until the tiling)
+    }
+    __threadfence_block();
+    __syncthreads();
+    // a winner's component index = its root's rank among the winners' roots
+    const uint32_t pc = (uint32_t)__builtin_popcountll(s_roots[lane]);
+    uint32_t incl = pc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t v = __shfl_up(incl, o, 64);
+      if (lane >= (uint32_t)o) incl += v;
+    }
+    s_rpre[lane] = incl - pc;
+    m = (uint32_t)__shfl(incl, 63, 64);
+    __syncthreads();
+    for (uint32_t c = lane; c < nc; c += 64)
+      if (tiled[c]) {
+        const uint32_t rt = cand[c].root;
+        comp[s_rpre[rt >> 6] + (uint32_t)__builtin_popcountll(s_roots[rt >> 6] & ((1ull << (rt & 63)) - 1))] = (int32_t)c;
+      }
+    __threadfence_block();
+    __syncthreads();
+    // the tiling order, the reference's stable insertion sorts as ranks: lpath
+    // descending (greedy), weight descending (weighted), tiling_end ascending
+    // (maximal); none keeps component order.  key: ascending, exact (negation).
+    auto key = [&](uint32_t t) -> double {
+      const MegaTmp& q = M((int32_t)t);
+      return G.tiling == PBGPU_TILING_GREEDY ? -(double)q.lpath
+             : G.tiling == PBGPU_TILING_WEIGHTED ? -weight(q) : q.tiling_end;
+    };
+    for (uint32_t t0 = 0; t0 < m; t0 += 64) {
+      const uint32_t t = t0 + lane;
+      const bool ok = t < m;
+      uint32_t rank = t;
+      if (G.tiling != PBGPU_TILING_NONE) {
+        const double kt = ok ? key(t) : 0.0;
+        rank = 0;
+        for (uint32_t u0 = 0; u0 < m; u0 += 64) {
+          const double ku = u0 + lane < m ? key(u0 + lane) : 0.0;
+          const uint32_t cnt = m - u0 < 64 ? m - u0 : 64;
+          for (uint32_t x = 0; x < cnt; ++x) {
+            const double k2 = rl_f64(ku, x);
+            rank += (uint32_t)((k2 < kt) | ((k2 == kt) & (u0 + x < t)));
+          }
+        }
+      }
+      if (ok) order[rank] = (int32_t)t;
+    }
+    __threadfence_block();
+    __syncthreads();
+    if (G.tiling == PBGPU_TILING_GREEDY || G.tiling == PBGPU_TILING_WEIGHTED) {
+      // tile_greedy (overlap_graph.cc:163-197) in component order: the overlap and
+      // containment tests over every lane, the joined right-open interval set kept
+      // sorted with strict gaps, so an insert [lo, hi) merges exactly the intervals
+      // [s0, e) with s0 = #{y < lo}, e = #{x <= hi}
+      constexpr uint32_t GCAP = 256;
+      __shared__ double2 s_cov[GCAP], s_pl[GCAP], s_tile[GCAP];
+      __shared__ int32_t s_it[GCAP];
+      const bool in_lds = m <= GCAP;
+      double2* cov = in_lds ? s_cov : G.ivs + b;
+      double2* placed = in_lds ? s_pl : G.ivs + G.n_recs + b;
+      if (in_lds) {  // the components' [tiling_start, tiling_end) in tiling order
+        for (uint32_t t = lane; t < m; t += 64) {
+          const int32_t it = order[t];
+          const MegaTmp& q = M(it);
+          s_it[t] = it; s_tile[t] = make_double2(q.tiling_start, q.tiling_end);
+        }
+        __syncthreads();
+      }
+      uint32_t ncov = 0, npl = 0;
       for (uint32_t t = 0; t < m; ++t) {
-        const MegaTmp& q = M((int32_t)t);
-        const int32_t span = G.recs[b + q.end_node].re - G.recs[b + q.start_node].rs + 1;
-        w[t] = __dmul_rn(__dmul_rn(q.density, q.density), (double)span);
-      }
-      stable_sort(order, m, [&](int32_t x, int32_t y) { return w[y] < w[x]; });
-    }
-    // tile_greedy (overlap_graph.cc:163-197): covered = joined right-open intervals
-    double2* cov = G.ivs + b;                 // (weights are read before this)
-    double2* placed = G.ivs + G.n_recs + b;
-    uint32_t ncov = 0, npl = 0;
-    for (uint32_t t = 0; t < m; ++t) {
-      const int32_t it = order[t];
-      const MegaTmp& q = M(it);
-      const double lo = q.tiling_start, hi = q.tiling_end;
-      const double span = hi > lo ? __dadd_rn(hi, -lo) : 0.0;
-      const double max_overlap = std_max(kplay, __dmul_rn(span, __dadd_rn(play, -0.9)));
-      bool large = false;
-      for (uint32_t c = 0; c < ncov && !large; ++c) {
-        const double a = std_max(lo, cov[c].x), bb = std_min(hi, cov[c].y);
-        large = a < bb && __dadd_rn(bb, -a) >= max_overlap;
-      }
-      if (large) continue;
-      bool contains = false;
-      for (uint32_t c = 0; c < npl && !contains; ++c)
-        contains = !(lo < hi) || (placed[c].x < placed[c].y && placed[c].x <= lo && hi <= placed[c].y);
-      if (contains) continue;
-      if (lo < hi) {  // IntervalSet::add
-        uint32_t s0 = 0;
-        while (s0 < ncov && cov[s0].y < lo) ++s0;
-        uint32_t e = s0;
-        double l2 = lo, h2 = hi;
-        while (e < ncov && cov[e].x <= h2) { l2 = std_min(l2, cov[e].x); h2 = std_max(h2, cov[e].y); ++e; }
-        const uint32_t rem = e - s0;  // replaced by one interval at s0
-        if (rem == 0) {
-          for (uint32_t q2 = ncov; q2 > s0; --q2) cov[q2] = cov[q2 - 1];
-          ++ncov;
-        } else {
-          for (uint32_t q2 = s0 + 1; q2 + rem - 1 < ncov; ++q2) cov[q2] = cov[q2 + rem - 1];
-          ncov -= rem - 1;
+        const int32_t it = in_lds ? s_it[t] : order[t];
+        const double2 tl = in_lds ? s_tile[t] : make_double2(M(it).tiling_start, M(it).tiling_end);
+        const double lo = tl.x, hi = tl.y;
+        const double span = hi > lo ? __dadd_rn(hi, -lo) : 0.0;
+        const double max_overlap = std_max(kplay, __dmul_rn(span, __dadd_rn(play, -0.9)));
+        bool large = false;
+        for (uint32_t c = lane; c < ncov; c += 64) {
+          const double2 v = cov[c];
+          const double a = std_max(lo, v.x), bb = std_min(hi, v.y);
+          large |= a < bb && __dadd_rn(bb, -a) >= max_overlap;
         }
-        cov[s0] = make_double2(l2, h2);
-      }
-      placed[npl++] = make_double2(lo, hi);
-      tiled[nt++] = it;
-    }
-  } else if (G.tiling == PBGPU_TILING_MAXIMAL) {
-    stable_sort(order, m, [&](int32_t x, int32_t y) { return M(x).tiling_end < M(y).tiling_end; });
-    // tile_maximal (overlap_graph.cc:199-252): info {score, pos, node, previous, length}
-    double* ipos = (double*)(G.ivs + b);               // pos
-    int4* ilink = (int4*)(G.ivs + G.n_recs + b);     // {previous, length, score, node}
-    uint32_t ni = 0;
-    if (m) {
-      ipos[0] = M(order[0]).tiling_end;
-      ilink[0] = make_int4(-1, 1, M(order[0]).lpath, order[0]);
-      ni = 1;
-      for (uint32_t t = 1; t < m; ++t) {
-        const MegaTmp& q = M(order[t]);
-        const double lstart = q.tiling_start;
-        const double key = std_min(__dadd_rn(lstart, kplay), q.tiling_end);
-        uint32_t lo = 0, hi = ni;  // upper_bound: the first info with key < pos
-        while (lo < hi) { const uint32_t mid = (lo + hi) / 2; if (key < ipos[mid]) hi = mid; else lo = mid + 1; }
-        int32_t x = (int32_t)lo - 1;
-        while (x >= 0 && M(ilink[x].w).tiling_start >= lstart) x = ilink[x].x;
-        const int32_t nscore = (x >= 0 ? ilink[x].z : 0) + q.lpath;
-        if (nscore > ilink[ni - 1].z) {
-          ipos[ni] = q.tiling_end;
-          ilink[ni] = make_int4(x, (x >= 0 ? ilink[x].y : 0) + 1, nscore, order[t]);
-          ++ni;
+        if (__ballot(large)) continue;
+        bool contains = false;
+        for (uint32_t c = lane; c < npl; c += 64) {
+          const double2 v = placed[c];
+          contains |= !(lo < hi) || (v.x < v.y && v.x <= lo && hi <= v.y);
         }
+        if (__ballot(contains)) continue;
+        if (lo < hi) {  // IntervalSet::add
+          uint32_t s0 = 0, e = 0;
+          for (uint32_t c = lane; c < ncov; c += 64) {
+            const double2 v = cov[c];
+            s0 += v.y < lo; e += v.x <= hi;
+          }
+          s0 = wave_sum_u32(s0); e = wave_sum_u32(e);
+          double l2 = lo, h2 = hi;
+          if (e > s0) { l2 = std_min(lo, cov[s0].x); h2 = std_max(hi, cov[e - 1].y); }
+          // cov[e, ncov) moves to s0 + 1: from the back when it moves right
+          const uint32_t len = ncov - e, dst = s0 + 1;
+          if (dst > e) {
+            for (int32_t c0 = len ? (int32_t)((len - 1) & ~63u) : -64; c0 >= 0; c0 -= 64) {
+              const uint32_t c = (uint32_t)c0 + lane;
+              double2 v = make_double2(0.0, 0.0);
+              if (c < len) v = cov[e + c];
+              if (c < len) cov[dst + c] = v;
+              __threadfence_block();
+            }
+          } else if (dst < e) {
+            for (uint32_t c0 = 0; c0 < len; c0 += 64) {
+              const uint32_t c = c0 + lane;
+              double2 v = make_double2(0.0, 0.0);
+              if (c < len) v = cov[e + c];
+              if (c < len) cov[dst + c] = v;
+              __threadfence_block();
+            }
+          }
+          __threadfence_block();
+          if (lane == 0) cov[s0] = make_double2(l2, h2);
+          ncov = dst + len;
+        }
+        if (lane == 0) { placed[npl] = make_double2(lo, hi); tiled[nt] = it; }
+        ++npl; ++nt;
+        __threadfence_block();
+        __syncthreads();
       }
-      nt = (uint32_t)ilink[ni - 1].y;
-      int32_t ptr = (int32_t)ni - 1;
-      for (int32_t q = (int32_t)nt - 1; q >= 0; --q) { tiled[q] = ilink[ptr].w; ptr = ilink[ptr].x; }
+    }
+    if (G.tiling == PBGPU_TILING_MAXIMAL && lane == 0) {
+      // tile_maximal (overlap_graph.cc:199-252): info {score, pos, node, previous, length}
+      double* ipos = (double*)(G.ivs + b);               // pos
+      int4* ilink = (int4*)(G.ivs + G.n_recs + b);     // {previous, length, score, node}
+      uint32_t ni = 0;
+      if (m) {
+        ipos[0] = M(order[0]).tiling_end;
+        ilink[0] = make_int4(-1, 1, M(order[0]).lpath, order[0]);
+        ni = 1;
+        for (uint32_t t = 1; t < m; ++t) {
+          const MegaTmp& q = M(order[t]);
+          const double lstart = q.tiling_start;
+          const double key = std_min(__dadd_rn(lstart, kplay), q.tiling_end);
+          uint32_t lo = 0, hi = ni;  // upper_bound: the first info with key < pos
+          while (lo < hi) { const uint32_t mid = (lo + hi) / 2; if (key < ipos[mid]) hi = mid; else lo = mid + 1; }
+          int32_t x = (int32_t)lo - 1;
+          while (x >= 0 && M(ilink[x].w).tiling_start >= lstart) x = ilink[x].x;
+          const int32_t nscore = (x >= 0 ? ilink[x].z : 0) + q.lpath;
+          if (nscore > ilink[ni - 1].z) {
+            ipos[ni] = q.tiling_end;
+            ilink[ni] = make_int4(x, (x >= 0 ? ilink[x].y : 0) + 1, nscore, order[t]);
+            ++ni;
+          }
+        }
+        nt = (uint32_t)ilink[ni - 1].y;
+        int32_t ptr = (int32_t)ni - 1;
+        for (int32_t q = (int32_t)nt - 1; q >= 0; --q) { tiled[q] = ilink[ptr].w; ptr = ilink[ptr].x; }
+      }
+    }
+  } else if (lane == 0) {
+    for (uint32_t c = 0; c < nc; ++c) {
+      const uint32_t root = cand[c].root;
+      uint32_t lo = 0, hi = m;  // lower_bound by root
+      while (lo < hi) { const uint32_t mid = (lo + hi) / 2; if (cand[comp[mid]].root < root) lo = mid + 1; else hi = mid; }
+      if (lo == m || cand[comp[lo]].root != root) {
+        for (uint32_t q = m; q > lo; --q) comp[q] = comp[q - 1];
+        comp[lo] = (int32_t)c; ++m;
+      } else {
+        const MegaTmp& cur = cand[comp[lo]];
+        if (cand[c].lpath > cur.lpath || (cand[c].lpath == cur.lpath && cand[c].density > cur.density)) comp[lo] = (int32_t)c;
+      }
+    }
+    for (uint32_t t = 0; t < m; ++t) order[t] = (int32_t)t;
+    if (G.tiling == PBGPU_TILING_GREEDY || G.tiling == PBGPU_TILING_WEIGHTED) {
+      if (G.tiling == PBGPU_TILING_GREEDY) {
+        stable_sort(order, m, [&](int32_t x, int32_t y) { return M(y).lpath < M(x).lpath; });
+      } else {
+        double* w = (double*)(G.ivs + b);  // weights_[t]
+        for (uint32_t t = 0; t < m; ++t) {
+          const MegaTmp& q = M((int32_t)t);
+          const int32_t span = G.recs[b + q.end_node].re - G.recs[b + q.start_node].rs + 1;
+          w[t] = __dmul_rn(__dmul_rn(q.density, q.density), (double)span);
+        }
+        stable_sort(order, m, [&](int32_t x, int32_t y) { return w[y] < w[x]; });
+      }
+      // tile_greedy (overlap_graph.cc:163-197): covered = joined right-open intervals
+      double2* cov = G.ivs + b;                 // (weights are read before this)
+      double2* placed = G.ivs + G.n_recs + b;
+      uint32_t ncov = 0, npl = 0;
+      for (uint32_t t = 0; t < m; ++t) {
+        const int32_t it = order[t];
+        const MegaTmp& q = M(it);
+        const double lo = q.tiling_start, hi = q.tiling_end;
+        const double span = hi > lo ? __dadd_rn(hi, -lo) : 0.0;
+        const double max_overlap = std_max(kplay, __dmul_rn(span, __dadd_rn(play, -0.9)));
+        bool large = false;
+        for (uint32_t c = 0; c < ncov && !large; ++c) {
+          const double a = std_max(lo, cov[c].x), bb = std_min(hi, cov[c].y);
+          large = a < bb && __dadd_rn(bb, -a) >= max_overlap;
+        }
+        if (large) continue;
+        bool contains = false;
+        for (uint32_t c = 0; c < npl && !contains; ++c)
+          contains = !(lo < hi) || (placed[c].x < placed[c].y && placed[c].x <= lo && hi <= placed[c].y);
+        if (contains) continue;
+        if (lo < hi) {  // IntervalSet::add
+          uint32_t s0 = 0;
+          while (s0 < ncov && cov[s0].y < lo) ++s0;
+          uint32_t e = s0;
+          double l2 = lo, h2 = hi;
+          while (e < ncov && cov[e].x <= h2) { l2 = std_min(l2, cov[e].x); h2 = std_max(h2, cov[e].y); ++e; }
+          const uint32_t rem = e - s0;  // replaced by one interval at s0
+          if (rem == 0) {
+            for (uint32_t q2 = ncov; q2 > s0; --q2) cov[q2] = cov[q2 - 1];
+            ++ncov;
+          } else {
+            for (uint32_t q2 = s0 + 1; q2 + rem - 1 < ncov; ++q2) cov[q2] = cov[q2 + rem - 1];
+            ncov -= rem - 1;
+          }
+          cov[s0] = make_double2(l2, h2);
+        }
+        placed[npl++] = make_double2(lo, hi);
+        tiled[nt++] = it;
+      }
+    } else if (G.tiling == PBGPU_TILING_MAXIMAL) {
+      stable_sort(order, m, [&](int32_t x, int32_t y) { return M(x).tiling_end < M(y).tiling_end; });
+      // tile_maximal (overlap_graph.cc:199-252): info {score, pos, node, previous, length}
+      double* ipos = (double*)(G.ivs + b);               // pos
+      int4* ilink = (int4*)(G.ivs + G.n_recs + b);     // {previous, length, score, node}
+      uint32_t ni = 0;
+      if (m) {
+        ipos[0] = M(order[0]).tiling_end;
+        ilink[0] = make_int4(-1, 1, M(order[0]).lpath, order[0]);
+        ni = 1;
+        for (uint32_t t = 1; t < m; ++t) {
+          const MegaTmp& q = M(order[t]);
+          const double lstart = q.tiling_start;
+          const double key = std_min(__dadd_rn(lstart, kplay), q.tiling_end);
+          uint32_t lo = 0, hi = ni;  // upper_bound: the first info with key < pos
+          while (lo < hi) { const uint32_t mid = (lo + hi) / 2; if (key < ipos[mid]) hi = mid; else lo = mid + 1; }
+          int32_t x = (int32_t)lo - 1;
+          while (x >= 0 && M(ilink[x].w).tiling_start >= lstart) x = ilink[x].x;
+          const int32_t nscore = (x >= 0 ? ilink[x].z : 0) + q.lpath;
+          if (nscore > ilink[ni - 1].z) {
+            ipos[ni] = q.tiling_end;
+            ilink[ni] = make_int4(x, (x >= 0 ? ilink[x].y : 0) + 1, nscore, order[t]);
+            ++ni;
+          }
+        }
+        nt = (uint32_t)ilink[ni - 1].y;
+        int32_t ptr = (int32_t)ni - 1;
+        for (int32_t q = (int32_t)nt - 1; q >= 0; --q) { tiled[q] = ilink[ptr].w; ptr = ilink[ptr].x; }
+      }
     }
   }
-  if (G.tiling != PBGPU_TILING_NONE)
+  PROF_T(km2);
+  __threadfence_block();
+  __syncthreads();
+  m = (uint32_t)__shfl((int)m, 0, 64);
+  nt = (uint32_t)__shfl((int)nt, 0, 64);
+  PROF_T(km3);
+  if (G.tiling != PBGPU_TILING_NONE && lane == 0)
     stable_sort(tiled, nt, [&](int32_t x, int32_t y) {
       return M(x).imp_s < M(y).imp_s || (M(x).imp_s == M(y).imp_s && M(x).imp_e < M(y).imp_e);
     });
-  // ---- print_mega_reads: what each printed mega-read needs (overlap_graph.cc:254-299)
+  __threadfence_block();
+  __syncthreads();
+  // ---- print_mega_reads: what each printed mega-read needs (overlap_graph.cc:254-299),
+  // the wave walking each path together (lane-parallel copies and sums).  A node's
+  // name size and unitigs come from its prefix-sum offsets (poff[q + 1] - poff[q] =
+  // size + 1), so a path step waits on one load, and the next node's is issued first.
+  PROF_T(km4);
   const int32_t* pr = nt ? tiled : order;
   const uint32_t npr = nt ? nt : m;  // print(tiled_mr_.empty() ? sort_tiling_ : tiled_mr_)
   uint32_t done = 0;
   bool host = false;
-  for (uint32_t t = 0; t < npr && !host; ++t) {
+  for (uint32_t t = 0; t < npr; ++t) {
     const MegaTmp& q = M(pr[t]);
     const GraphNode ge = G.out[b + (uint32_t)q.end_node];
     const Rec& Re = G.recs[b + (uint32_t)q.end_node];
     const Rec& Rs = G.recs[b + (uint32_t)q.start_node];
     const uint64_t nu = ge.lunitigs > 0 ? (uint64_t)ge.lunitigs : 0ull;
-    const unsigned long long uo = atomicAdd(G.units_used, (unsigned long long)nu);
+    unsigned long long uo = 0;
+    if (lane == 0) uo = atomicAdd(G.units_used, (unsigned long long)nu);
+    uo = (unsigned long long)__shfl((long long)uo, 0, 64);
     if (uo + nu > G.units_cap) { host = true; break; }
     uint32_t* sr = G.munits + uo;
-    for (uint64_t x = 0; x < nu; ++x) sr[x] = 0;
-    // super_read_name::prepend (super_read_name.cc:29-36)
-    auto prepend = [&](uint64_t offset, uint32_t node, uint64_t first, uint64_t last) -> uint64_t {
-      const Rec& R = G.recs[b + node];
-      const uint64_t sz = graph_nsz(G, R.sr);
+    for (uint64_t x = lane; x < nu; x += 64) sr[x] = 0;
+    __threadfence_block();
+    // super_read_name::prepend (super_read_name.cc:29-36) of node's name, whose unitigs
+    // start at un and number sz
+    auto prepend = [&](uint64_t offset, const uint32_t* un, uint64_t sz, uint64_t first, uint64_t last) -> uint64_t {
       if (first > last || first >= sz) return offset;
       const uint64_t to_copy = (last < sz - 1 ? last : sz - 1) - first + 1;
       if (to_copy > offset) return offset;
       const uint64_t no = offset - to_copy;
-      const uint32_t* un = G.ounits + G.poff[b + node];
-      for (uint64_t x = 0; x < to_copy; ++x) sr[no + x] = un[first + x];
+      for (uint64_t x = lane; x < to_copy; x += 64) sr[no + x] = un[first + x];
       return no;
     };
-    uint64_t offset = prepend(nu, (uint32_t)q.end_node, 0, graph_nsz(G, Re.sr) - 1);
-    int32_t node_j = q.end_node, node_i = ge.lprev;
+    const uint64_t pe0 = G.poff[b + (uint32_t)q.end_node], nsze = G.poff[b + (uint32_t)q.end_node + 1] - pe0 - 1;
+    int32_t node_i = ge.lprev;
+    int32_t prev_i = 0, lun_i = 0;  // node i's lprev, lunitigs
+    if (node_i >= 0) { prev_i = G.out[b + (uint32_t)node_i].lprev; lun_i = G.out[b + (uint32_t)node_i].lunitigs; }
+    uint64_t offset = prepend(nu, G.ounits + pe0, nsze, 0, nsze - 1);
+    int32_t lun_j = ge.lunitigs;
+    uint64_t nszj = nsze;
     while (node_i >= 0) {
-      const GraphNode gi = G.out[b + (uint32_t)node_i], gj = G.out[b + (uint32_t)node_j];
-      const uint64_t nszi = graph_nsz(G, G.recs[b + (uint32_t)node_i].sr), nszj = graph_nsz(G, G.recs[b + (uint32_t)node_j].sr);
-      const uint64_t overlap = (uint64_t)(int64_t)gi.lunitigs + nszj - (uint64_t)(int64_t)gj.lunitigs;
-      offset = prepend(offset, (uint32_t)node_i, 0, nszi - 1 - overlap);
-      node_j = node_i;
-      node_i = gi.lprev;
+      const uint64_t p0 = G.poff[b + (uint32_t)node_i], nszi = G.poff[b + (uint32_t)node_i + 1] - p0 - 1;
+      const int32_t nxt = prev_i;
+      int32_t prev_n = 0, lun_n = 0;
+      if (nxt >= 0) { prev_n = G.out[b + (uint32_t)nxt].lprev; lun_n = G.out[b + (uint32_t)nxt].lunitigs; }
+      const uint64_t overlap = (uint64_t)(int64_t)lun_i + nszj - (uint64_t)(int64_t)lun_j;
+      offset = prepend(offset, G.ounits + p0, nszi, 0, nszi - 1 - overlap);
+      lun_j = lun_i; nszj = nszi;
+      node_i = nxt; prev_i = prev_n; lun_i = lun_n;
     }
-    int32_t sr_len = 0;
-    for (int32_t x = q.start_unitig; x < q.start_unitig + q.nb_unitigs; ++x)
-      sr_len += graph_ulen(G, x >= 0 && (uint64_t)x < nu ? sr[x] >> 1 : UNIT_INVALID);
-    sr_len = (int32_t)((uint32_t)sr_len - (uint32_t)(q.nb_unitigs - 1) * (k - 1));
-    MegaOut o;
-    o.imp_s = q.imp_s; o.imp_e = q.imp_e; o.density = q.density;
-    o.rs = Rs.rs; o.re = Re.re; o.qs = Rs.qs - q.start_offset; o.lpath = ge.lpath;
-    o.sr_len = sr_len; o.start_unitig = q.start_unitig; o.nb_unitigs = q.nb_unitigs; o.n_units = (uint32_t)nu;
-    o.qend = (uint64_t)(int64_t)(sr_len + q.end_offset) - ((uint64_t)Re.ql - (uint64_t)(int64_t)Re.qe);
-    o.unit_offset = uo;
-    G.mo[b + done++] = o;
+    __threadfence_block();
+    __syncthreads();
+    uint32_t sl = 0;  // sr_len: the unitig lengths summed modulo 2^32, as the int32 sum
+    for (int64_t x = (int64_t)q.start_unitig + lane; x < (int64_t)q.start_unitig + q.nb_unitigs; x += 64)
+      sl += (uint32_t)graph_ulen(G, x >= 0 && (uint64_t)x < nu ? sr[x] >> 1 : UNIT_INVALID);
+    sl = wave_sum_u32(sl);
+    const int32_t sr_len = (int32_t)(sl - (uint32_t)(q.nb_unitigs - 1) * (k - 1));
+    if (lane == 0) {
+      MegaOut o;
+      o.imp_s = q.imp_s; o.imp_e = q.imp_e; o.density = q.density;
+      o.rs = Rs.rs; o.re = Re.re; o.qs = Rs.qs - q.start_offset; o.lpath = ge.lpath;
+      o.sr_len = sr_len; o.start_unitig = q.start_unitig; o.nb_unitigs = q.nb_unitigs; o.n_units = (uint32_t)nu;
+      o.qend = (uint64_t)(int64_t)(sr_len + q.end_offset) - ((uint64_t)Re.ql - (uint64_t)(int64_t)Re.qe);
+      o.unit_offset = uo;
+      G.mo[b + done] = o;
+    }
+    ++done;
   }
+  if (lane != 0) return;
   G.mcount[r] = host ? 0u : done;
   G.mhost[r] = host ? 1 : 0;
   if (host) atomicAdd(G.n_host, 1u);
+#ifdef PBGPU_PROF
+  {  // slots 88..: candidates, components, sort + tiling, final sort, paths, waves, max wave, candidates / comps
+    PROF_T(km5);
+    atomicAdd(&g_prof[88], km1 - km0); atomicAdd(&g_prof[89], km2 - km1); atomicAdd(&g_prof[90], km3 - km2);
+    atomicAdd(&g_prof[91], km4 - km3); atomicAdd(&g_prof[92], km5 - km4); atomicAdd(&g_prof[93], 1ull);
+    atomicMax(&g_prof[94], km5 - km0); atomicAdd(&g_prof[95], ((unsigned long long)nc << 32) | m);
+  }
+#endif
 }
 __global__ void k_mega_pack(GraphDev G, uint32_t n_reads, const uint64_t* __restrict__ moff, MegaOut* __restrict__ mc) {
   const uint32_t r = blockIdx.x;

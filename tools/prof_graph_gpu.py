@@ -23,7 +23,7 @@ def main():
     ul = [int(x) for x in ds.unitig_lengths]
     al = pbgpu.Aligner(ix, k=17, forward=True, unitigs_k=31, unitig_lengths=ul, bases_matching=15.0,
                        max_count=5000, stretch_cap=10000.0)
-    al.set_graph([pbgpu.parse_unitigs(n) for n in names], ul, 31)
+    al.set_graph([pbgpu.parse_unitigs(n) for n in names], ul, 31, mega_reads=True)
     blob, off = ds.pb_blob()
     rr = al.upload(blob=blob, offsets=off)
     al.align_resident(rr)
@@ -48,6 +48,12 @@ def main():
               f"ticks a node {v[6] / max(1, v[5]):.0f}")
         for nm, x in zip(["chunk scan", "names + sums", "node updates", "unions"], v[:4]):
             print(f"  {nm:14s} {x / max(1, v[5]):8.0f} ticks a node ({100.0 * x / tot:5.1f}%)")
+        w = list(buf)[88:96]
+        nw = max(1, w[5])
+        print(f"k_mega: waves {w[5]}, candidates {w[7] >> 32}, components {w[7] & 0xffffffff}, "
+              f"longest wave {w[6]} ticks")
+        for nm, x in zip(["candidates", "components", "sort + tiling", "final sort", "paths"], w[:5]):
+            print(f"  {nm:14s} {x / nw:10.0f} ticks a wave")
     ds.close()
 
 
