@@ -1215,6 +1215,9 @@ pbgpu_status pbgpu_aligner_free(pbgpu_aligner* al) {
   if (!al) return PBGPU_OK;
   (void)hipSetDevice(al->device);  // not al->ix: the index may be freed first
   for (auto& e : al->ev) if (e) (void)hipEventDestroy(e);
+  if (al->g_fork) (void)hipEventDestroy(al->g_fork);
+  if (al->g_join) (void)hipEventDestroy(al->g_join);
+  if (al->g_side) (void)hipStreamDestroy(al->g_side);
   if (al->st) (void)hipStreamDestroy(al->st);
   delete al;
   return PBGPU_OK;
@@ -1618,7 +1621,7 @@ static void graph_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   al->g_pre.ensure(3 * tot + 3); al->g_imp.ensure(nrec + 1); al->g_desc.ensure(nrec + 1); al->g_out.ensure(nrec + 1);
   G.pp = (uint2*)al->g_pre.p; G.ounits = al->g_pre.p + 2 * (tot + 1);
   G.imp = al->g_imp.p; G.desc = al->g_desc.p; G.out = al->g_out.p;
-  launch_graph(G, n, nrec, st);
+  launch_graph(G, n, nrec, st, al->g_side, al->g_fork, al->g_join);
   HIPCHK(hipGetLastError());
   al->g_mtotal = al->g_munits_used = 0;
   al->g_hosts = 0;
@@ -2121,6 +2124,11 @@ pbgpu_status pbgpu_aligner_set_graph(pbgpu_aligner* al, const pbgpu_graph_params
   al->g_mega = p->mega_reads != 0;
   al->g_tiling = p->tiling; al->g_trim = p->trim != 0;
   al->g_min_density = p->min_density; al->g_min_len = p->min_len;
+  if (!al->g_side) {
+    HIPCHK(hipStreamCreateWithFlags(&al->g_side, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&al->g_fork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&al->g_join, hipEventDisableTiming));
+  }
   al->graph = true;
   return PBGPU_OK;
   API_CATCH

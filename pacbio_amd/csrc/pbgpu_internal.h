@@ -266,6 +266,9 @@ void launch_host_pack(const GraphDev& G, uint32_t n_reads, const uint64_t* hroff
 // G.poff from the records' name sizes (then the caller sizes pul / pco by poff[n_recs])
 void launch_graph_sizes(const GraphDev& G, uint64_t n_recs, uint32_t* sizes, uint64_t* scan_scratch, hipStream_t st);
 // implied positions and prefix sums, per-read sort, traversal -> G.out
-void launch_graph(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hipStream_t st);
+// side: a second stream for the reads of more than GRAPH_NM_SMALL records (their
+// traversal runs beside the others'); fork / join: events ordering it with st
+void launch_graph(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hipStream_t st, hipStream_t side,
+                  hipEvent_t fork, hipEvent_t join);
 
 }  // namespace pbgpu
