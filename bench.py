@@ -185,7 +185,7 @@ def main():
                          "(the roofline) measure the kernel, not two overlapping launches")
     ap.add_argument("--parts", type=int, default=2,
                     help="part files of the extra coords-out leg (value_parts; 0 = no such leg)")
-    ap.add_argument("--cmr-steps", type=int, default=2,
+    ap.add_argument("--cmr-steps", type=int, default=3,
                     help="runs of bin/create_mega_reads over the same files (value_create_mega_reads; 0 = none)")
     ap.add_argument("--skip-default-leg", action="store_true",
                     help="no default-flags device leg (profiling runs: every large-grid launch is then the "
@@ -354,8 +354,10 @@ def main():
             cmr_t = _json.loads(r.stderr.strip().splitlines()[-1])
             if i:
                 walls.append(cmr_t["wall_s"])
-        el_cmr = comm.max(sum(walls))
-    value_cmr = comm.sum(bases_rank) * args.cmr_steps / el_cmr if el_cmr else None
+        # the median run: a cold process's device allocations (hipMalloc) now and then block
+        # for seconds; every run's wall is reported beside it
+        el_cmr = comm.max(sorted(walls)[len(walls) // 2])
+    value_cmr = comm.sum(bases_rank) / el_cmr if el_cmr else None
 
     total_bases = comm.sum(bases_rank) * args.steps
     value = total_bases / elapsed
@@ -492,10 +494,12 @@ def main():
                                  "output (round-1 definition)",
             "value_create_mega_reads": value_cmr,
             "value_create_mega_reads_note": ("bin/create_mega_reads over the same files (overlap graph, tiling and "
-                                             "paths on the GPU, text on the host), mega-reads written per second, "
-                                             f"{args.cmr_steps} cold runs, -t {threads}") if value_cmr else None,
+                                             "paths on the GPU, text on the host), PacBio bases per second of the "
+                                             f"median of {args.cmr_steps} cold runs (after one warm-up run; each "
+                                             f"run's own --timing wall), -t {threads}") if value_cmr else None,
             "create_mega_reads_stage_s": ({kk: cmr_t[kk] for kk in ("wall_s", "align_s", "download_s", "graph_s",
                                                                      "output_bytes")} if cmr_t else None),
+            "create_mega_reads_walls_s": walls if args.cmr_steps > 0 else None,
             "value_parts": value_parts,
             "value_parts_note": (f"the same coords out into {args.parts} part files per GPU (jf_aligner --parts, the "
                                  "reference's split-and-cat in one process: one reader / writer per part, 2 aligners "

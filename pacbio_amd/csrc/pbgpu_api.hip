@@ -104,6 +104,17 @@ using namespace pbgpu;
 
 // error state, dbuf, temp_storage: pbgpu_host.h
 thread_local std::string g_err;
+bool stall_debug() {
+  static const bool on = getenv("PBGPU_DEBUG_STALL") != nullptr;
+  return on;
+}
+bool stall_debug_allocs() {
+  static const bool on = getenv("PBGPU_DEBUG_STALL") && atoi(getenv("PBGPU_DEBUG_STALL")) >= 2;
+  return on;
+}
+void stall_report(double seconds, const char* call, const char* file, int line) {
+  fprintf(stderr, "pbgpu stall: %.3f s in %s (%s:%d)\n", seconds, call, file, line);
+}
 // ------------------------------------------------------------------ names
 // super_read_name::parse (super_read_name.cc:74-90) -> unitig ids + oris
 static void parse_unitigs(std::string_view name, std::vector<uint32_t>& id, std::vector<uint8_t>& ori) {

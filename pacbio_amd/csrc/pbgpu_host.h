@@ -6,6 +6,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -37,9 +38,20 @@ struct hip_error : std::runtime_error {
   hipError_t e;
   hip_error(hipError_t e_, const char* what) : std::runtime_error(what), e(e_) {}
 };
+// PBGPU_DEBUG_STALL=1: report any HIP call that blocks the host for more than half a second
+// (file:line and the call), to find where a slow run waits
+bool stall_debug();
+bool stall_debug_allocs();  // PBGPU_DEBUG_STALL=2: also every device allocation
+void stall_report(double seconds, const char* call, const char* file, int line);
 #define HIPCHK(x)                                                                                      \
   do {                                                                                                 \
+    const bool _dbg = stall_debug();                                                                   \
+    const auto _t0 = _dbg ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point{}; \
     hipError_t _e = (x);                                                                               \
+    if (_dbg) {                                                                                        \
+      const double _dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - _t0).count(); \
+      if (_dt > 0.5) stall_report(_dt, #x, __FILE__, __LINE__);                                        \
+    }                                                                                                  \
     if (_e != hipSuccess) {                                                                            \
       char _b[512];                                                                                    \
       snprintf(_b, sizeof _b, "%s failed at %s:%d: %s", #x, __FILE__, __LINE__, hipGetErrorString(_e)); \
@@ -113,8 +125,18 @@ struct dbuf {
   dbuf& operator=(const dbuf&) = delete;
   ~dbuf() { release(); }
   void release() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
-  void alloc(size_t cnt) { release(); if (cnt) { HIPCHK(hipMalloc((void**)&p, cnt * sizeof(T))); n = cnt; } }
-  void ensure(size_t cnt) { if (cnt > n) alloc(std::max(cnt, n + n / 4)); }
+  void alloc(size_t cnt) {
+    release();
+    if (cnt) {
+      if (stall_debug_allocs()) stall_report(0.0, "hipMalloc (MiB in the line field)", "dbuf", (int)((cnt * sizeof(T)) >> 20));
+      HIPCHK(hipMalloc((void**)&p, cnt * sizeof(T)));
+      n = cnt;
+    }
+  }
+  // A per-batch buffer grows to at least twice its size (first: 5/4 of the request): a
+  // run's batches vary, and every reallocation is a device-wide hipFree plus a hipMalloc,
+  // which now and then blocks for seconds (PBGPU_DEBUG_STALL)
+  void ensure(size_t cnt) { if (cnt > n) alloc(std::max(cnt + cnt / 4, 2 * n)); }
   // grow keeping the first `keep` elements (stream-ordered copy)
   void grow_keep(size_t cnt, size_t keep, hipStream_t st) {
     if (cnt <= n) return;

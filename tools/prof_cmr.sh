@@ -12,4 +12,4 @@ ds = Dataset('C2', seed=42, threads=16, n_pb=$N); ds.write('$D'); ds.close()" ||
 F="-s 1M -m 17 --psa-min 13 -k 31 -l $D/ul.txt -B 15 --max-count 5000 --stretch-cap 10000 -t 16 -r $D/sr.fa -p $D/pb.fa --timing"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_cmr -o run -- pacbio_amd/bin/create_mega_reads $F -o $D/mr > gpurun_out/prof_cmr.log 2>&1 || { tail -20 gpurun_out/prof_cmr.log; exit 1; }
 f=$(find gpurun_out/prof_cmr -name "*kernel_stats.csv" | head -1)
-head -25 "$f"
+if [ -n "$f" ]; then head -25 "$f"; else ls gpurun_out/prof_cmr; fi
