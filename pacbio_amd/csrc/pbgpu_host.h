@@ -58,6 +58,17 @@ void stall_report(double seconds, const char* call, const char* file, int line);
       throw hip_error(_e, _b);                                                                         \
     }                                                                                                  \
   } while (0)
+// a call whose status is ignored (frees), timed like HIPCHK under PBGPU_DEBUG_STALL
+#define HIPFREE(x)                                                                                     \
+  do {                                                                                                 \
+    const bool _dbg = stall_debug();                                                                   \
+    const auto _t0 = _dbg ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point{}; \
+    (void)(x);                                                                                         \
+    if (_dbg) {                                                                                        \
+      const double _dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - _t0).count(); \
+      if (_dt > 0.5) stall_report(_dt, #x, __FILE__, __LINE__);                                        \
+    }                                                                                                  \
+  } while (0)
 struct bad_input : std::runtime_error { using std::runtime_error::runtime_error; };
 
 // n strings in one allocation: string i is blob[off[i], off[i + 1] - 1), NUL-terminated
@@ -124,7 +135,7 @@ struct dbuf {
   dbuf(const dbuf&) = delete;
   dbuf& operator=(const dbuf&) = delete;
   ~dbuf() { release(); }
-  void release() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
+  void release() { if (p) HIPFREE(hipFree(p)); p = nullptr; n = 0; }
   void alloc(size_t cnt) {
     release();
     if (cnt) {

@@ -103,7 +103,7 @@ struct PinnedVec {  // growable pinned byte buffer (H2D at full PCIe rate, no st
     char* q = nullptr;
     HIPCHK(hipHostMalloc((void**)&q, nc, hipHostMallocDefault));
     if (n) memcpy(q, p, n);
-    if (p) (void)hipHostFree(p);
+    if (p) HIPFREE(hipHostFree(p));
     p = q;
     cap = nc;
   }
@@ -391,11 +391,12 @@ class TextPool {
     free_.pop_back();
     lk.unlock();
     if (out.cap < need) {
-      if (out.p) (void)hipHostFree(out.p);
+      if (out.p) HIPFREE(hipHostFree(out.p));
       out.p = nullptr;
       out.cap = 0;
       const size_t cap = need + need / 4;
-      const hipError_t e = hipHostMalloc((void**)&out.p, cap, hipHostMallocDefault);
+      hipError_t e = hipSuccess;
+      HIPFREE(e = hipHostMalloc((void**)&out.p, cap, hipHostMallocDefault));
       if (e != hipSuccess) { put(Pinned{}, false); HIPCHK(e); }
       out.cap = cap;
     }
