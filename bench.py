@@ -348,6 +348,8 @@ def main():
                   "--devices", str(local), "-o", os.path.join(wd, "mega_reads")]
         walls = []
         for i in range(args.cmr_steps + 1):
+            if i:  # the previous process's device memory is released after it exits
+                time.sleep(2.0)
             r = subprocess.run([cmr, *cflags], capture_output=True, text=True)
             if r.returncode:
                 raise RuntimeError(f"create_mega_reads failed: {r.stderr[-2000:]}")

@@ -12,6 +12,7 @@ from tools.synth import Dataset
 ds = Dataset('C2', seed=42, threads=16, n_pb=$N); ds.write('$D'); ds.close()" || exit 1
 F="-s 1M -m 17 --psa-min 13 -k 31 -l $D/ul.txt -B 15 --max-count 5000 --stretch-cap 10000 -t 16 -r $D/sr.fa -p $D/pb.fa --timing"
 for i in $(seq 1 $R); do
+  [ -n "$PAUSE" ] && [ $i -gt 1 ] && sleep $PAUSE
   s=$(date +%s.%N)
   timeout -k 10 120 pacbio_amd/bin/create_mega_reads $F "$@" -o $D/mr > /dev/null 2> gpurun_out/rep_$i.err || { tail -5 gpurun_out/rep_$i.err; exit 1; }
   e=$(date +%s.%N)
