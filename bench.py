@@ -46,6 +46,50 @@ def _dist():
     return rank, world, local
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawn_ranks(n, argv):
+    """`bench.py --gpus N` without a launcher: start N fresh rank processes (one per
+    GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment) and wait for
+    them.  Called before this process touches the GPU, and it never execs: the ranks
+    are children.  Rank 0 inherits stdout and prints the one JSON line; the others'
+    stdout goes to stderr.  Returns the worst exit code (a failed rank fails the job)."""
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                                      stdout=None if r == 0 else sys.stderr.fileno()))
+    rc = 0
+    for p in procs:
+        c = p.wait()
+        if c and not rc:
+            rc = c
+            for q in procs:  # one rank failed: the others would wait at a barrier forever
+                if q.poll() is None:
+                    q.terminate()
+    return rc
+
+
+def _check_world(gpus):
+    """`--gpus N` and the launcher's WORLD_SIZE must agree.  Returns True when this
+    process is a rank (launched by torchrun, by _spawn_ranks, or N == 1) and False
+    when it should spawn the N ranks itself."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None:
+        return gpus <= 1
+    if int(ws) != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={ws}: the launcher and the flag disagree")
+    return True
+
+
 class Comm:
     """Barrier + max/sum over ranks.  gloo on the host: the path itself has no
     exchange step (read sharding), so no RCCL traffic is needed."""
@@ -192,10 +236,21 @@ def main():
                          "production leg's)")
     ap.add_argument("--workdir", default=os.environ.get("PBGPU_BENCH_DIR", "/tmp"),
                     help="where the input FASTA and the coords output are written")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU work: the ranks meet at the barrier and rank 0 prints n_gpus (launch rehearsal)")
     args = ap.parse_args()
 
+    if not _check_world(args.gpus):
+        sys.exit(_spawn_ranks(args.gpus, sys.argv[1:]))
     rank, world, local = _dist()
     comm = Comm(world)
+    if args.dry_run:
+        comm.barrier()
+        ranks = comm.sum(1.0)
+        if rank == 0:
+            print(json.dumps({"metric": "PacBio bases aligned/sec (coords out)", "value": None, "n_gpus": world,
+                              "ranks_at_barrier": int(ranks), "dry_run": True}), flush=True)
+        return
     from pacbio_amd import pbgpu
     from tools.synth import Dataset, PRESETS
 

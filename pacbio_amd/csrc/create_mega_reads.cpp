@@ -5,10 +5,13 @@
 //
 // The coarse (and, with -F, fine) alignment runs on MI355X GPUs through
 // pbgpu_run, exactly as jf_aligner's: forward = true and unitig lengths
-// required (create_mega_reads.cc:140-148).  Each batch's records come back to
-// the host and the per-read overlap graph, longest path, tiling and mega-read
-// printing (overlap_graph.cpp) run on a pool of host threads; the mega-reads of
-// each batch are written in input order (the reference's output with -t 1).
+// required (create_mega_reads.cc:140-148).  By default the per-read overlap
+// graph, longest path, components, tiling and printed unitig paths run on the
+// GPU after each batch's records are sorted (k_graph*, k_mega; ABI 5,
+// pbgpu_aligner_set_graph); the host only writes the text, on -t threads.  The
+// host restatement (overlap_graph.cpp) runs --dot, --host-graph and the reads
+// the device leaves to it (more than 4,096 records).  The mega-reads of each
+// batch are written in input order (the reference's output with -t 1).
 // GPU options as in jf_aligner: --devices, --streams, --batch-bases, --timing
 // (stage times as JSON on stderr).
 #include <getopt.h>

@@ -5,7 +5,8 @@
 // at ~1 us a record.  Here the records never leave HBM as binary:
 //   k_fmt_len    one thread per record: its line length (CountSink), and per
 //                read the length of its compact ">n name" header line;
-//   scans        exclusive sums of both (hipcub) -> every line's byte offset;
+//   scans        exclusive sums of both (launch_excl_scan, hand-written) -> every
+//                line's byte offset;
 //   k_fmt_write  one thread per record / read header: the line itself
 //                (ByteSink: dword stores inside the line, bytes at its ends).
 // The text is then one contiguous device buffer the driver copies to pinned

@@ -51,3 +51,29 @@ def test_two_rank_stdout_is_one_json_line(tmp_path):
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, r.stdout
     assert json.loads(lines[0]) == {"sum": 2.0}
+
+
+def test_gpus_flag_spawns_ranks_without_launcher(tmp_path):
+    """`bench.py --gpus 2` with no torchrun around it must run two ranks, not
+    silently measure one GPU (round-3 review): the parent spawns the ranks before
+    any GPU call, they meet at the gloo barrier, rank 0 prints n_gpus 2."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=240, cwd=str(tmp_path), env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["ranks_at_barrier"] == 2
+
+
+def test_gpus_flag_disagreeing_with_launcher_fails(tmp_path):
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, cwd=str(tmp_path), env=env)
+    assert r.returncode != 0 and "disagree" in r.stderr
