@@ -393,7 +393,7 @@ def main():
     # ---- create_mega_reads (row f3, the aligner's production caller): the CLI over the
     # same files, overlap graph / tiling on the GPU; its own clock (--timing wall_s: first
     # batch read -> mega-reads file closed; the index build is before it), one warm-up run
-    el_cmr, cmr_t = None, None
+    el_cmr, cmr_t, worst_cmr = None, None, None
     if args.cmr_steps > 0:
         import json as _json
         import subprocess
@@ -403,17 +403,15 @@ def main():
                   "--devices", str(local), "-o", os.path.join(wd, "mega_reads")]
         walls = []
         for i in range(args.cmr_steps + 1):
-            if i:  # the previous process's device memory is released after it exits
-                time.sleep(2.0)
             r = subprocess.run([cmr, *cflags], capture_output=True, text=True)
             if r.returncode:
                 raise RuntimeError(f"create_mega_reads failed: {r.stderr[-2000:]}")
             cmr_t = _json.loads(r.stderr.strip().splitlines()[-1])
             if i:
                 walls.append(cmr_t["wall_s"])
-        # the median run: a cold process's device allocations (hipMalloc) now and then block
-        # for seconds; every run's wall is reported beside it
+        # the median run, the worst beside it (every run's wall is listed too)
         el_cmr = comm.max(sorted(walls)[len(walls) // 2])
+        worst_cmr = comm.max(max(walls))
     value_cmr = comm.sum(bases_rank) / el_cmr if el_cmr else None
 
     total_bases = comm.sum(bases_rank) * args.steps
@@ -557,6 +555,10 @@ def main():
             "create_mega_reads_stage_s": ({kk: cmr_t[kk] for kk in ("wall_s", "align_s", "download_s", "graph_s",
                                                                      "output_bytes")} if cmr_t else None),
             "create_mega_reads_walls_s": walls if args.cmr_steps > 0 else None,
+            "create_mega_reads_worst_wall_s": worst_cmr,
+            "create_mega_reads_allocs": ({kk: cmr_t.get(kk) for kk in ("device_allocs", "device_allocs_late",
+                                                                       "pinned_allocs", "pinned_allocs_late")}
+                                         if cmr_t else None),
             "value_parts": value_parts,
             "value_parts_note": (f"the same coords out into {args.parts} part files per GPU (jf_aligner --parts, the "
                                  "reference's split-and-cat in one process: one reader / writer per part, 2 aligners "
@@ -582,6 +584,9 @@ def main():
                           "device_bytes": info["device_bytes"], "build_s": round(t_index, 3),
                           "generate_and_write_s": round(t_gen, 3)},
                 "stage_ms_per_step": stage,
+                # device / pinned allocations inside the timed steps (the runner is warm: 0)
+                "allocs_in_timed_steps": {n: sum(r[n] for r in rstats) for n in
+                                          ("n_device_allocs", "n_pinned_allocs")},
                 "device_leg": {"ms_per_step": el_dev / args.device_steps * 1e3, "streams": args.device_streams,
                                "stage_ms_per_step": {s: round(st["ms_" + s] / args.device_steps, 3) for s in
                                                      ("seed", "group", "lis", "fit", "records")},

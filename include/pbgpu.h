@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PBGPU_ABI_VERSION 5
+#define PBGPU_ABI_VERSION 6
 
 typedef enum pbgpu_status {
   PBGPU_OK = 0,
@@ -496,6 +496,12 @@ typedef struct {
   double   writer_idle_seconds;   /* writer: waiting for the next batch in order */
   double   open_seconds;          /* opening (creating / truncating) the output files */
   double   close_seconds;         /* closing the coords file after the last write */
+  /* allocations made by the workers during the run: device (hipMalloc) and
+   * pinned host; _late = in any worker's batches after its first (the run
+   * path sizes its per-batch buffers for a full batch when they first grow,
+   * so these are 0 unless a batch needs more than 2x the first's density) */
+  uint64_t n_device_allocs, n_device_allocs_late;
+  uint64_t n_pinned_allocs, n_pinned_allocs_late;
 } pbgpu_run_stats;
 
 pbgpu_status pbgpu_run(pbgpu_index* const* indexes, size_t n_indexes, const pbgpu_align_params* params,

@@ -1632,7 +1632,7 @@ static void graph_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   al->g_pre.ensure(3 * tot + 3); al->g_imp.ensure(nrec + 1); al->g_desc.ensure(nrec + 1); al->g_out.ensure(nrec + 1);
   G.pp = (uint2*)al->g_pre.p; G.ounits = al->g_pre.p + 2 * (tot + 1);
   G.imp = al->g_imp.p; G.desc = al->g_desc.p; G.out = al->g_out.p;
-  launch_graph(G, n, nrec, st, al->g_side, al->g_fork, al->g_join);
+  HIPCHK(launch_graph(G, n, nrec, st, al->g_side, al->g_fork, al->g_join));
   HIPCHK(hipGetLastError());
   al->g_mtotal = al->g_munits_used = 0;
   al->g_hosts = 0;
@@ -1669,7 +1669,7 @@ static void graph_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   al->g_rsize.ensure(n + 1); al->g_isize.ensure(nrec + 1); al->g_hroff.ensure(n + 1); al->g_hioff.ensure(nrec + 1);
   launch_host_sizes(G, n, al->g_rsize.p, al->g_isize.p, st);
   launch_excl_scan(al->g_rsize.p, nullptr, n, al->g_hroff.p,
-                   (uint64_t*)temp_storage(al->tmp, excl_scan_scratch_words(nrec) * 8), st);
+                   (uint64_t*)temp_storage(al->tmp, excl_scan_scratch_words(n) * 8), st);
   launch_excl_scan(al->g_isize.p, nullptr, nrec, al->g_hioff.p,
                    (uint64_t*)temp_storage(al->tmp, excl_scan_scratch_words(nrec) * 8), st);
   uint64_t hc[2] = {0, 0};
@@ -1815,7 +1815,7 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
         } else {
           const uint64_t words = group_table_words(lg);
           const uint32_t grp = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_ovf, (1ull << 28) / words));
-          al->gtable.ensure((uint64_t)grp * words);
+          al->gtable.ensure_fixed((uint64_t)grp * words);
           for (uint32_t s0 = 0; s0 < n_ovf; s0 += grp) {
             const uint32_t m = std::min(grp, n_ovf - s0);
             HIPCHK(hipMemsetAsync(al->gtable.p, 0, (size_t)m * words * 4, st));

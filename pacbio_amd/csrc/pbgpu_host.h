@@ -127,6 +127,23 @@ void run_parallel(int threads, F&& work) {
 }
 
 // --------------------------------------------------------- device buffer
+// Allocation accounting and sizing of the per-batch buffers.  Every device
+// allocation (hipMalloc of a dbuf) and pinned host allocation is counted on the
+// thread that makes it: in pbgpu_run each aligner runs on its own worker
+// thread, so the counts after a worker's first batch are what the run path
+// still allocates (pbgpu_run_stats.n_device_allocs_late; round-3 review: a
+// growing buffer's hipFree + hipMalloc now and then blocked a cold run for
+// seconds).  tl_grow_scale is set by the worker to batch_bases / the batch's
+// bases (the first batches of a run are ramped, 1/8 .. 1/2 of a full batch):
+// a per-batch buffer that must grow is then sized for a full batch with 2x
+// headroom (a ramped first batch holds few reads, so its hit and record
+// densities vary), and the full batches that follow allocate nothing.
+inline thread_local uint64_t tl_dev_allocs = 0, tl_pinned_allocs = 0;
+inline thread_local double tl_grow_scale = 1.0;
+inline size_t grow_target(size_t cnt) {
+  const double s = tl_grow_scale;
+  return s > 1.0 ? (size_t)((double)cnt * s * 2.0) + 1 : cnt + cnt / 4;
+}
 template <typename T>
 struct dbuf {
   T* p = nullptr;
@@ -141,19 +158,23 @@ struct dbuf {
     if (cnt) {
       if (stall_debug_allocs()) stall_report(0.0, "hipMalloc (MiB in the line field)", "dbuf", (int)((cnt * sizeof(T)) >> 20));
       HIPCHK(hipMalloc((void**)&p, cnt * sizeof(T)));
+      ++tl_dev_allocs;
       n = cnt;
     }
   }
-  // A per-batch buffer grows to at least twice its size (first: 5/4 of the request): a
-  // run's batches vary, and every reallocation is a device-wide hipFree plus a hipMalloc,
-  // which now and then blocks for seconds (PBGPU_DEBUG_STALL)
-  void ensure(size_t cnt) { if (cnt > n) alloc(std::max(cnt + cnt / 4, 2 * n)); }
+  // A per-batch buffer grows to at least twice its size (first: grow_target of the
+  // request): a run's batches vary, and every reallocation is a device-wide hipFree
+  // plus a hipMalloc, which now and then blocks for seconds (PBGPU_DEBUG_STALL)
+  void ensure(size_t cnt) { if (cnt > n) alloc(std::max(grow_target(cnt), 2 * n)); }
+  // a buffer whose size does not follow the batch's (never scaled by tl_grow_scale)
+  void ensure_fixed(size_t cnt) { if (cnt > n) alloc(std::max(cnt + cnt / 4, 2 * n)); }
   // grow keeping the first `keep` elements (stream-ordered copy)
   void grow_keep(size_t cnt, size_t keep, hipStream_t st) {
     if (cnt <= n) return;
     T* q = nullptr;
-    const size_t nn = std::max(cnt, n + n / 2);
+    const size_t nn = std::max(tl_grow_scale > 1.0 ? grow_target(cnt) : cnt, n + n / 2);
     HIPCHK(hipMalloc((void**)&q, nn * sizeof(T)));
+    ++tl_dev_allocs;
     if (p && keep) HIPCHK(hipMemcpyAsync(q, p, keep * sizeof(T), hipMemcpyDeviceToDevice, st));
     HIPCHK(hipStreamSynchronize(st));
     release();

@@ -268,7 +268,7 @@ void launch_graph_sizes(const GraphDev& G, uint64_t n_recs, uint32_t* sizes, uin
 // implied positions and prefix sums, per-read sort, traversal -> G.out
 // side: a second stream for the reads of more than GRAPH_NM_SMALL records (their
 // traversal runs beside the others'); fork / join: events ordering it with st
-void launch_graph(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hipStream_t st, hipStream_t side,
+hipError_t launch_graph(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hipStream_t st, hipStream_t side,
                   hipEvent_t fork, hipEvent_t join);
 
 }  // namespace pbgpu

@@ -3860,20 +3860,23 @@ void launch_graph_sizes(const GraphDev& G, uint64_t n_recs, uint32_t* sizes, uin
                                  0, st, G, n_recs, sizes);
   launch_excl_scan(sizes, nullptr, n_recs, G.poff, scan_scratch, st);
 }
-void launch_graph(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hipStream_t st, hipStream_t side,
-                  hipEvent_t fork, hipEvent_t join) {
-  if (!n_recs || !n_reads) return;
+hipError_t launch_graph(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hipStream_t st, hipStream_t side,
+                        hipEvent_t fork, hipEvent_t join) {
+  if (!n_recs || !n_reads) return hipSuccess;
   hipLaunchKernelGGL(k_graph_prep, dim3((uint32_t)std::min<uint64_t>((n_recs + 255) / 256, 65535)), dim3(256), 0, st,
                      G, n_recs);
-  // the long reads' tier first, on the side stream: its waves are the longest
-  (void)hipEventRecord(fork, st);
-  (void)hipStreamWaitEvent(side, fork, 0);
+  // the long reads' tier first, on the side stream: its waves are the longest.  A
+  // failed fork or join would let k_mega read G.out while the side tier still writes
+  // it, so each is checked (the caller raises)
+  hipError_t e = hipEventRecord(fork, st);
+  if (e == hipSuccess) e = hipStreamWaitEvent(side, fork, 0);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_graph_sort<GRAPH_NMAX>, dim3(n_reads), dim3(GRAPH_SORT_BLOCK), 0, side, G, n_reads);
   hipLaunchKernelGGL(k_graph<GRAPH_NMAX>, dim3(n_reads), dim3(64), 0, side, G, n_reads);
-  (void)hipEventRecord(join, side);
+  if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_graph_sort<GRAPH_NM_SMALL>, dim3(n_reads), dim3(GRAPH_SORT_BLOCK), 0, st, G, n_reads);
   hipLaunchKernelGGL(k_graph<GRAPH_NM_SMALL>, dim3(n_reads), dim3(64), 0, st, G, n_reads);
-  (void)hipStreamWaitEvent(st, join, 0);
+  return hipStreamWaitEvent(st, join, 0);
 }
 
 }  // namespace pbgpu

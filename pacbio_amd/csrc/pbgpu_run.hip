@@ -102,6 +102,7 @@ struct PinnedVec {  // growable pinned byte buffer (H2D at full PCIe rate, no st
     const size_t nc = std::max(c, cap + cap / 2);
     char* q = nullptr;
     HIPCHK(hipHostMalloc((void**)&q, nc, hipHostMallocDefault));
+    ++tl_pinned_allocs;
     if (n) memcpy(q, p, n);
     if (p) HIPFREE(hipHostFree(p));
     p = q;
@@ -394,10 +395,11 @@ class TextPool {
       if (out.p) HIPFREE(hipHostFree(out.p));
       out.p = nullptr;
       out.cap = 0;
-      const size_t cap = need + need / 4;
+      const size_t cap = grow_target(need);
       hipError_t e = hipSuccess;
       HIPFREE(e = hipHostMalloc((void**)&out.p, cap, hipHostMallocDefault));
       if (e != hipSuccess) { put(Pinned{}, false); HIPCHK(e); }
+      ++tl_pinned_allocs;
       out.cap = cap;
     }
     return true;
@@ -496,7 +498,9 @@ struct RecordsView {
   PinnedVec off, recs, km, kb, graph, moff, mega, munits, mhost;
   pbgpu_coords_batch c{};
   // on growth, room for the next batches of a ramp (PinnedVec grows by 1.5x)
-  static void room(PinnedVec& v, uint64_t bytes) { if (v.cap < bytes) v.reserve(std::max<uint64_t>(bytes, 1) * 2); }
+  static void room(PinnedVec& v, uint64_t bytes) {
+    if (v.cap < bytes) v.reserve(std::max<uint64_t>(grow_target(std::max<uint64_t>(bytes, 1)), 2 * bytes));
+  }
   void download(pbgpu_aligner* al) {
     const uint64_t n = al->last_reads;
     static_assert(sizeof(pbgpu_record) == sizeof(Rec), "record layout");
@@ -636,8 +640,12 @@ static void run_part(pbgpu_runner* R, RunPart& part, const pbgpu_run_params* run
     try {
       HIPCHK(hipSetDevice(al->device));
       Batch* b = nullptr;
+      bool first = true;
       while (inq.pop(b)) {
         pbgpu_read_batch rb{b->n(), b->seq.p, b->off.data(), b->names.data(), b->name_off.data()};
+        // buffers that grow in this batch are sized for a full batch (pbgpu_host.h)
+        tl_grow_scale = b->seq.n ? std::min(64.0, std::max(1.0, (double)batch_bases / (double)b->seq.n)) : 1.0;
+        const uint64_t a0 = tl_dev_allocs, p0 = tl_pinned_allocs;
         const double t0 = now_s();
         upload_reads_into(al, &rb, rd);
         const double t1 = now_s();
@@ -702,7 +710,14 @@ static void run_part(pbgpu_runner* R, RunPart& part, const pbgpu_run_params* run
           S.n_reads += nreads;
           S.n_bases += nbases;
           S.n_records += al->last_records;
+          S.n_device_allocs += tl_dev_allocs - a0;
+          S.n_pinned_allocs += tl_pinned_allocs - p0;
+          if (!first) {
+            S.n_device_allocs_late += tl_dev_allocs - a0;
+            S.n_pinned_allocs_late += tl_pinned_allocs - p0;
+          }
         }
+        first = false;
         {
           std::lock_guard<std::mutex> lk(dmu);
           done.emplace(id, std::move(d));
@@ -816,9 +831,18 @@ static void runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_s
   std::vector<std::string> paths;
   for (size_t i = 0; i < run->n_pb_paths; ++i) paths.emplace_back(run->pb_paths[i]);
   // part p: the reads whose header starts in [T p / P, T (p + 1) / P) of the inputs
+  // (byte ranges need sizes: a FIFO, a process substitution or a device reports 0
+  // and would give every part an empty range, so only regular files are split)
   uint64_t T = 0;
   if (P > 1)
-    for (const auto& p : paths) T += LineSource::file_size(p);
+    for (const auto& p : paths) {
+      struct stat st {};
+      if (stat(p.c_str(), &st) != 0) throw bad_input("Can't open PacBio file '" + p + "'");
+      if (!S_ISREG(st.st_mode))
+        throw unsupported("part files need regular PacBio files to split by byte range; '" + p +
+                          "' is a pipe or device");
+      T += (uint64_t)st.st_size;
+    }
   std::atomic<bool> any_stop(false);
   std::vector<std::unique_ptr<RunState>> rss;
   std::vector<pbgpu_run_stats> SP(P);
@@ -858,6 +882,8 @@ static void runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_s
     S.read_seconds += x.read_seconds; S.upload_seconds += x.upload_seconds; S.align_seconds += x.align_seconds;
     S.format_seconds += x.format_seconds; S.d2h_seconds += x.d2h_seconds; S.write_seconds += x.write_seconds;
     S.writer_idle_seconds += x.writer_idle_seconds;
+    S.n_device_allocs += x.n_device_allocs; S.n_device_allocs_late += x.n_device_allocs_late;
+    S.n_pinned_allocs += x.n_pinned_allocs; S.n_pinned_allocs_late += x.n_pinned_allocs_late;
   }
   S.open_seconds = t_open;
   const double tc = now_s();

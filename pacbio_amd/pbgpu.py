@@ -88,7 +88,9 @@ class RunStats(C.Structure):
                                           "details_bytes")] + \
                [(n, C.c_double) for n in ("read_seconds", "upload_seconds", "align_seconds", "format_seconds",
                                           "d2h_seconds", "write_seconds", "writer_idle_seconds", "open_seconds",
-                                          "close_seconds")]
+                                          "close_seconds")] + \
+               [(n, C.c_uint64) for n in ("n_device_allocs", "n_device_allocs_late", "n_pinned_allocs",
+                                          "n_pinned_allocs_late")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

@@ -164,7 +164,11 @@ def test_run_part_files_refuse_gzip_and_fastq(many_dir, tmp_path):
     with open(fq, "w") as f:
         for i in range(50):
             f.write(f"@r{i}\n{'ACGT' * 300}\n+\n{'I' * 1200}\n")
-    for path in (gz, fq):
+    # a FIFO (or <(zcat ...)) reports size 0: split by byte range it would give every part
+    # an empty range and write empty files without an error, so it is refused before it is opened
+    fifo = str(tmp_path / "pb.fifo")
+    os.mkfifo(fifo)
+    for path in (gz, fq, fifo):
         with pytest.raises(pbgpu.PbgpuError) as e:
             pbgpu.run([gix], [path], str(tmp_path / "x.coords"), aligners_per_device=2, n_parts=2)
         assert e.value.status == 5, e.value  # PBGPU_ERR_UNSUPPORTED

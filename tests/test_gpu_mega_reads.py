@@ -247,3 +247,27 @@ def test_abi_device_mega_reads_match_cli(synth, tmp_path, tiling):
     assert not host.any() and len(recs) >= 10
     got = "".join(_format_device_mega(n.split()[0], moff, recs, units, r) for r, n in enumerate(pn))
     assert got == open(out).read()
+
+
+def test_no_device_allocation_after_first_batch(tmp_path):
+    """The run path allocates nothing after each aligner's first batch (round-3 review:
+    a growing buffer's hipFree + hipMalloc blocked cold runs for seconds): 3000 C2
+    reads in >= 12 ramped batches over two aligners, --timing's device_allocs_late and
+    pinned_allocs_late are 0, and the mega-reads equal a one-batch run's."""
+    import json
+    from tools.synth import Dataset
+    ds = Dataset("C2", seed=42, threads=16, n_pb=3000)
+    ds.write(str(tmp_path))
+    ds.close()
+    base = ["-s", "1M", "-m", "17", "--psa-min", "13", "-k", "31", "-l", str(tmp_path / "ul.txt"), "-B", "15",
+            "--max-count", "5000", "--stretch-cap", "10000", "-t", "16", "--timing",
+            "-r", str(tmp_path / "sr.fa"), "-p", str(tmp_path / "pb.fa")]
+    a, b = str(tmp_path / "many"), str(tmp_path / "one")
+    r = _run([*base, "--batch-bases", "3200000", "-o", a], timeout=300)
+    t = json.loads(r.stderr.strip().splitlines()[-1])
+    assert t["batches"] >= 12, t
+    assert t["device_allocs"] > 0, t  # counted at all: the first batches allocate
+    assert t["device_allocs_late"] == 0 and t["pinned_allocs_late"] == 0, t
+    _run([*base, "--batch-bases", "1000000000", "-o", b], timeout=300)
+    ta = open(a).read()
+    assert ta.count(">") > 2000 and ta == open(b).read()
