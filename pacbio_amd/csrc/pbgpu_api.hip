@@ -1,6 +1,7 @@
 // pbgpu_api.hip -- host side of the C ABI (include/pbgpu.h): FASTA loading
 // with the reference's compact_dna rules, device index build, the per-batch
 // pipeline on one HIP stream, result download and coords formatting.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <rccl/rccl.h>
@@ -114,6 +115,12 @@ bool stall_debug_allocs() {
 }
 void stall_report(double seconds, const char* call, const char* file, int line) {
   fprintf(stderr, "pbgpu stall: %.3f s in %s (%s:%d)\n", seconds, call, file, line);
+}
+void alloc_note(size_t bytes, const void* caller) {
+  Dl_info di{};
+  const uintptr_t base = dladdr(caller, &di) ? (uintptr_t)di.dli_fbase : 0;
+  fprintf(stderr, "pbgpu alloc: %zu bytes, scale %.2f, allocs on this thread %llu, caller +0x%zx\n", bytes,
+          tl_grow_scale, (unsigned long long)tl_dev_allocs, (size_t)((uintptr_t)caller - base));
 }
 // ------------------------------------------------------------------ names
 // super_read_name::parse (super_read_name.cc:74-90) -> unitig ids + oris
@@ -1153,7 +1160,8 @@ void upload_reads_into(pbgpu_aligner* al, const pbgpu_read_batch* b, pbgpu_reads
       no[i] = b->n_reads ? b->name_offsets[i] - n0 : 0;
       if (i && no[i] < no[i - 1]) throw std::invalid_argument("name offsets must be non-decreasing");
     }
-    r->names.ensure(no[b->n_reads] + 1);
+    // (name lengths grow with the read ids of a file: 32 bytes a read at least)
+    r->names.ensure(std::max<uint64_t>(no[b->n_reads] + 1, 32 * (b->n_reads + 1)));
     if (no[b->n_reads]) HIPCHK(hipMemcpyAsync(r->names.p, b->names + n0, no[b->n_reads], hipMemcpyHostToDevice, st));
     r->name_off.ensure(b->n_reads + 1);
     HIPCHK(hipMemcpyAsync(r->name_off.p, no.data(), (b->n_reads + 1) * 8, hipMemcpyHostToDevice, st));
@@ -1664,9 +1672,13 @@ static void graph_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   launch_mega_pack(G, n, al->g_moff.p, al->g_mc.p, st);
   HIPCHK(hipGetLastError());
   al->g_hrecs = al->g_hinfos = 0;
+  // the reads left to the host (few, long): their packing buffers are sized with every
+  // batch, not only when a batch first has such a read (no allocation after the first)
+  al->g_rsize.ensure(n + 1); al->g_isize.ensure(nrec + 1); al->g_hroff.ensure(n + 1); al->g_hioff.ensure(nrec + 1);
+  al->g_hrec.ensure(nrec / 8 + 4096); al->g_hgraph.ensure(nrec / 8 + 4096);
+  al->g_hinfo.ensure(2 * (al->last_info / 8 + 4096));
   if (!al->g_hosts) return;
   // the reads left to the host: their records, nodes and info packed (a small download)
-  al->g_rsize.ensure(n + 1); al->g_isize.ensure(nrec + 1); al->g_hroff.ensure(n + 1); al->g_hioff.ensure(nrec + 1);
   launch_host_sizes(G, n, al->g_rsize.p, al->g_isize.p, st);
   launch_excl_scan(al->g_rsize.p, nullptr, n, al->g_hroff.p,
                    (uint64_t*)temp_storage(al->tmp, excl_scan_scratch_words(n) * 8), st);
@@ -1719,6 +1731,7 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
   const uint64_t budget = al->hit_budget;
   const uint32_t hcap_log2 = 11;
   al->ovf_reads.ensure(n);
+  al->ovf_list.ensure(n);  // (used only by batches with reads past the first group tier)
   uint64_t rec_done = 0, info_done = 0;
   double ms_group = 0, ms_lis = 0, ms_fit = 0;
   double k_ms[PBGPU_KERNEL_N] = {};

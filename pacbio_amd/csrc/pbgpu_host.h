@@ -43,6 +43,9 @@ struct hip_error : std::runtime_error {
 bool stall_debug();
 bool stall_debug_allocs();  // PBGPU_DEBUG_STALL=2: also every device allocation
 void stall_report(double seconds, const char* call, const char* file, int line);
+// PBGPU_DEBUG_STALL=2: one line per device allocation with its size and the caller's
+// offset in libpbgpu.so (nm -C maps it to the function that grew the buffer)
+void alloc_note(size_t bytes, const void* caller);
 #define HIPCHK(x)                                                                                      \
   do {                                                                                                 \
     const bool _dbg = stall_debug();                                                                   \
@@ -153,10 +156,10 @@ struct dbuf {
   dbuf& operator=(const dbuf&) = delete;
   ~dbuf() { release(); }
   void release() { if (p) HIPFREE(hipFree(p)); p = nullptr; n = 0; }
-  void alloc(size_t cnt) {
+  __attribute__((noinline)) void alloc(size_t cnt) {
     release();
     if (cnt) {
-      if (stall_debug_allocs()) stall_report(0.0, "hipMalloc (MiB in the line field)", "dbuf", (int)((cnt * sizeof(T)) >> 20));
+      if (stall_debug_allocs()) alloc_note(cnt * sizeof(T), __builtin_return_address(0));
       HIPCHK(hipMalloc((void**)&p, cnt * sizeof(T)));
       ++tl_dev_allocs;
       n = cnt;
@@ -169,10 +172,11 @@ struct dbuf {
   // a buffer whose size does not follow the batch's (never scaled by tl_grow_scale)
   void ensure_fixed(size_t cnt) { if (cnt > n) alloc(std::max(cnt + cnt / 4, 2 * n)); }
   // grow keeping the first `keep` elements (stream-ordered copy)
-  void grow_keep(size_t cnt, size_t keep, hipStream_t st) {
+  __attribute__((noinline)) void grow_keep(size_t cnt, size_t keep, hipStream_t st) {
     if (cnt <= n) return;
     T* q = nullptr;
     const size_t nn = std::max(tl_grow_scale > 1.0 ? grow_target(cnt) : cnt, n + n / 2);
+    if (stall_debug_allocs()) alloc_note(nn * sizeof(T), __builtin_return_address(0));
     HIPCHK(hipMalloc((void**)&q, nn * sizeof(T)));
     ++tl_dev_allocs;
     if (p && keep) HIPCHK(hipMemcpyAsync(q, p, keep * sizeof(T), hipMemcpyDeviceToDevice, st));
@@ -184,8 +188,10 @@ struct dbuf {
   void swap(dbuf& o) { std::swap(p, o.p); std::swap(n, o.n); }
 };
 
+// scan scratch (a few words per tile of the scanned array): 1 MB at least, so
+// that a batch's later and larger scans do not grow it one by one
 inline void* temp_storage(dbuf<uint8_t>& t, size_t bytes) {
-  t.ensure(bytes ? bytes : 1);
+  t.ensure_fixed(std::max<size_t>(bytes, 1 << 20));
   return t.p;
 }
 

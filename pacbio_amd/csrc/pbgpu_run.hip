@@ -516,14 +516,18 @@ struct RecordsView {
     room(off, (n + 1) * 8);
     if (!dev_mega || al->g_hosts) HIPCHK(hipMemcpyAsync(off.p, d_off, (n + 1) * 8, hipMemcpyDeviceToHost, al->st));
     else memset(off.p, 0, (n + 1) * 8);
-    room(recs, nr * sizeof(Rec)); room(km, ni * 4); room(kb, ni * 4);
+    // (with device mega-reads only the reads left to the host come down: a batch's first
+    // such read must not grow the buffers, so they hold an eighth of its records at least)
+    const uint64_t nr_room = dev_mega ? std::max<uint64_t>(nr, al->last_records / 8 + 4096) : nr;
+    const uint64_t ni_room = dev_mega ? std::max<uint64_t>(ni, al->last_info / 8 + 4096) : ni;
+    room(recs, nr_room * sizeof(Rec)); room(km, ni_room * 4); room(kb, ni_room * 4);
     if (nr) HIPCHK(hipMemcpyAsync(recs.p, d_rec, nr * sizeof(Rec), hipMemcpyDeviceToHost, al->st));
     if (ni) {
       HIPCHK(hipMemcpyAsync(km.p, d_km, ni * 4, hipMemcpyDeviceToHost, al->st));
       HIPCHK(hipMemcpyAsync(kb.p, d_kb, ni * 4, hipMemcpyDeviceToHost, al->st));
     }
     if (al->graph) {
-      room(graph, nr * sizeof(GraphNode));
+      room(graph, nr_room * sizeof(GraphNode));
       if (nr) HIPCHK(hipMemcpyAsync(graph.p, d_graph, nr * sizeof(GraphNode), hipMemcpyDeviceToHost, al->st));
     }
     if (dev_mega) {
