@@ -137,7 +137,9 @@ void run_parallel(int threads, F&& work) {
 // still allocates (pbgpu_run_stats.n_device_allocs_late; round-3 review: a
 // growing buffer's hipFree + hipMalloc now and then blocked a cold run for
 // seconds).  tl_grow_scale is set by the worker to batch_bases / the batch's
-// bases (the first batches of a run are ramped, 1/8 .. 1/2 of a full batch):
+// target when the batch is a ramped one filled to its target (the first
+// batches of a run are 1/8 .. 1/2 of a full batch; a batch cut short by the
+// end of the input has no full batches after it and keeps 1):
 // a per-batch buffer that must grow is then sized for a full batch with 2x
 // headroom (a ramped first batch holds few reads, so its hit and record
 // densities vary), and the full batches that follow allocate nothing.

@@ -237,6 +237,9 @@ class LineSource {
 
 struct Batch {
   uint64_t id = 0;
+  // a ramped batch filled to its target: the full batches after it are this much larger
+  // (tl_grow_scale while it is aligned); 1 for full batches and for the input's last one
+  double grow_scale = 1.0;
   PinnedVec seq;
   std::string names;
   std::vector<uint64_t> off{0}, name_off{0};
@@ -619,6 +622,7 @@ static void run_part(pbgpu_runner* R, RunPart& part, const pbgpu_run_params* run
         const uint64_t sh = id >= ramp ? 0 : ramp - id;
         const uint64_t want = sh == 0 ? batch_bases : std::max<uint64_t>(1, sh >= 64 ? 0 : batch_bases >> sh);
         const bool any = rp.fill(*b, want);
+        b->grow_scale = sh && b->seq.n >= want ? (double)batch_bases / (double)want : 1.0;
         {
           std::lock_guard<std::mutex> lk(smu);
           S.read_seconds += now_s() - t0;
@@ -648,7 +652,7 @@ static void run_part(pbgpu_runner* R, RunPart& part, const pbgpu_run_params* run
       while (inq.pop(b)) {
         pbgpu_read_batch rb{b->n(), b->seq.p, b->off.data(), b->names.data(), b->name_off.data()};
         // buffers that grow in this batch are sized for a full batch (pbgpu_host.h)
-        tl_grow_scale = b->seq.n ? std::min(64.0, std::max(1.0, (double)batch_bases / (double)b->seq.n)) : 1.0;
+        tl_grow_scale = std::min(64.0, std::max(1.0, b->grow_scale));
         const uint64_t a0 = tl_dev_allocs, p0 = tl_pinned_allocs;
         const double t0 = now_s();
         upload_reads_into(al, &rb, rd);
