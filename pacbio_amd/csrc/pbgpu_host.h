@@ -337,6 +337,9 @@ struct pbgpu_aligner {
   dbuf<int32_t> g_ul;
   dbuf<double2> g_imp;
   dbuf<GraphNode> g_out;
+  dbuf<uint32_t> g_ecnt;
+  dbuf<uint64_t> g_eoff;
+  dbuf<uint2> g_edges;
   // mega-reads on the device (pbgpu_graph_params.mega_reads)
   bool g_mega = false;
   int g_tiling = 0, g_trim = 0;

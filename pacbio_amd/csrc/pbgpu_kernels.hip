@@ -3033,78 +3033,160 @@ __global__ __launch_bounds__(GRAPH_SORT_BLOCK) void k_graph_sort(GraphDev G, uin
                           G.bases ? R.sr_cover : (uint32_t)R.nb_mers, 0u};
   }
 }
-// One wave per read: the reference's traversal with the sorted nodes' j loop 64 at a
-// time.  Per node i (sorted order, so every edge into i is already applied): lanes
-// take j = i + 1 + lane, ...; the first j that is neither skipped nor long enough
-// (the reference's break) ends the scan; lanes before it test the names' dovetail
-// overlap, the same-name case and the play / error bounds and update their own
-// node's longest path (distinct j per lane, as the reference's updates are); the
-// edges are united in j order by one lane (union by rank with path compression:
-// the reference's component roots).
-// LDS holds a ring of GRING sorted positions -- descriptor, up to GRING_U unitigs,
-// path state -- refilled 64 at a time as i advances (a node's scan reaches at least
-// GRING - 63 positions ahead; a longer one hands the whole read to the host), and the
-// union-find of the read's nodes.
-#ifndef PBGPU_GRING
-#define PBGPU_GRING 256
-#endif
-constexpr uint32_t GRING = PBGPU_GRING, GRING_U = 8;
-constexpr uint32_t GRAPH_NMAX_K = GRAPH_NMAX;  // reads of more records go to the host (LDS union-find)
-static_assert(GRAPH_NMAX_K <= 4096, "k_graph matches roots by 12 bits");
+// The traversal (overlap_graph.cc:7-59) in two phases.  Everything the reference
+// tests for a pair (i, j) -- the 5' / not-advancing skips, the break, the names'
+// dovetail overlap, the same-name case, the play / error bounds, and the edge's
+// path increment (nb_mers or sr_cover minus the common k-mers) and unitig count --
+// reads only static node data, so it runs for every node at once
+// (k_graph_edges); only the longest-path relaxation and the unions, in the
+// reference's (i, then j) order, are serial per read (k_graph_relax).
+//
+// k_graph_edges: one wave per node i (sorted position), lanes j = i + 1 + lane, ...
+// 64 at a time until the reference's break.  PASS 0 counts each node's edges
+// (ecnt); an exclusive scan gives every node's offset, so the edges of a read are
+// one contiguous stream in (i, j) order; PASS 1 writes them as
+// {j's record index | (unitigs added) << 16, path increment}.
+constexpr uint32_t GRAPH_U = 8;  // names of at most this many unitigs are matched in registers
+constexpr uint32_t GRAPH_NMAX_K = GRAPH_NMAX;  // reads of more records go to the host (LDS state)
+static_assert(GRAPH_NMAX_K <= 4096, "k_graph_relax matches roots by 12 bits and keeps 16-bit indices");
+constexpr uint32_t GRAPH_EDGE_BLOCK = 256;
+DEV bool graph_on_device(const GraphDev& G, uint32_t n) { return n > 0 && n <= G.nmax && n <= GRAPH_NMAX_K; }
+template <int PASS>
+__global__ __launch_bounds__(GRAPH_EDGE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n_recs) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t nw = (uint64_t)gridDim.x * (GRAPH_EDGE_BLOCK / 64);
+  for (uint64_t q = (uint64_t)blockIdx.x * (GRAPH_EDGE_BLOCK / 64) + (threadIdx.x >> 6); q < n_recs; q += nw) {
+    const uint32_t r = G.recs[q].read;  // records are grouped per read: q is sorted position q - b of read r
+    const uint64_t b = G.rec_off[r];
+    const uint32_t n = (uint32_t)(G.rec_off[r + 1] - b);
+    uint32_t cnt = 0;
+    const GDesc di = G.desc[q];
+    const double rl = (double)(G.roff[r + 1] - G.roff[r]);
+    if (graph_on_device(G, n) && !(di.imp_e >= rl)) {  // (imp_e >= rl: hanging off the 3' end)
+      const uint32_t pi = (uint32_t)(q - b);
+      const double ie_i = di.imp_e, err_i = di.err, play = G.play, kd = (double)G.k;
+      const uint32_t km1 = G.k - 1, sa = di.nsz;
+      const uint64_t po_i = di.poff;
+      uint32_t a[GRAPH_U];
+#pragma unroll
+      for (uint32_t u = 0; u < GRAPH_U; ++u) a[u] = u < sa ? G.ounits[po_i + u] : 0u;
+      auto unit_i = [&](uint32_t t) -> uint32_t { return G.ounits[po_i + t]; };
+      uint64_t* eo = PASS ? &G.eoff[q] : nullptr;
+      const uint64_t e0 = PASS ? *eo : 0;
+      for (uint32_t j0 = pi + 1; j0 < n; j0 += 64) {
+        const uint32_t j = j0 + lane;
+        const bool act = j < n;
+        const GDesc dj = G.desc[b + (act ? j : pi)];
+        const double is_j = dj.imp_s, ie_j = dj.imp_e;
+        const bool skip = (is_j <= 1.0) | (ie_i > __dadd_rn(ie_j, 31.0));  // off the 5' end | not advancing
+        const double position_len = __dadd_rn(ie_i, -is_j);
+        const double error = __dmul_rn(G.nb_errors, __dadd_rn(err_i, dj.err));
+        const bool brk = act & !skip & (__dadd_rn(__dmul_rn(position_len, play), error) < kd);
+        const uint64_t bm = __ballot(brk);
+        const uint32_t fb = bm ? (uint32_t)__ffsll((long long)bm) - 1 : 64u;
+        const uint32_t sb = dj.nsz;
+        bool edge = false;
+        int32_t nb = 0, common = 0;
+        if (act & !skip & (lane < fb) & (sa >= 2) & (sb >= 2)) {
+          bool same;
+          uint2 v;
+          if ((sa <= GRAPH_U) & (sb <= GRAPH_U)) {
+            // super_read_name::overlap (super_read_name.cc:49-72) in registers: the smallest
+            // t >= max(sa - sb + 1, 1) with name_i[t..sa) == name_j[0..sa - t)
+            uint32_t bu[GRAPH_U];
+#pragma unroll
+            for (uint32_t u = 0; u < GRAPH_U; ++u) bu[u] = u < sb ? G.ounits[dj.poff + u] : 0u;
+            const int t0 = (int)sa - (int)sb + 1;
+#pragma unroll
+            for (int t = (int)GRAPH_U - 1; t >= 1; --t) {
+              bool m = (t < (int)sa) & (t >= t0) & (a[t] == bu[0]);
+#pragma unroll
+              for (int qq = t + 1; qq < (int)GRAPH_U; ++qq) m &= (qq >= (int)sa) | (a[qq] == bu[qq - t]);
+              nb = m ? (int32_t)sa - t : nb;
+            }
+            same = sb == sa;
+#pragma unroll
+            for (uint32_t u = 0; u < GRAPH_U; ++u) same &= (u >= sa) | (a[u] == bu[u]);
+          } else {
+            const uint64_t po_j = dj.poff;
+            auto unit_j = [&](uint32_t qq) -> uint32_t { return G.ounits[po_j + qq]; };
+            const uint32_t u0 = unit_j(0);
+            const int t0 = (int)sa - (int)sb + 1;
+            for (uint32_t t = t0 > 1 ? (uint32_t)t0 : 1u; t < sa; ++t) {
+              if (unit_i(t) != u0) continue;
+              uint32_t qq = t + 1;
+              while (qq < sa && unit_i(qq) == unit_j(qq - t)) ++qq;
+              if (qq == sa) { nb = (int32_t)(sa - t); break; }
+            }
+            same = false;
+            if (nb && sb == sa) {  // the same super-read name
+              same = true;
+              for (uint32_t u = 0; u < sa && same; ++u) same = unit_i(u) == unit_j(u);
+            }
+          }
+          v = nb ? G.pp[dj.poff + (uint32_t)nb] : make_uint2(0u, 0u);
+          if (nb && !same) {
+            const int32_t uol = (int32_t)(v.x - (uint32_t)(nb - 1) * km1);
+            common = (int32_t)v.y;
+            const double duol = (double)uol;
+            edge = !((duol > __dadd_rn(__dmul_rn(play, position_len), error)) |
+                     (position_len > __dmul_rn(play, __dadd_rn(duol, error))));
+          }
+        }
+        const uint64_t em = __ballot(edge);
+        if (PASS && edge) {
+          const uint32_t at = cnt + (uint32_t)__builtin_popcountll(em & ((1ull << lane) - 1));
+          // the edge's path increment (nb_mers or sr_cover of j minus the common k-mers) and
+          // the unitigs it adds (overlap_graph.cc:47-53)
+          G.edges[e0 + at] = make_uint2(dj.idx | ((sb - (uint32_t)nb) << 16), dj.lp_add - (uint32_t)common);
+        }
+        cnt += (uint32_t)__builtin_popcountll(em);
+        if (bm) break;  // the reference's break
+      }
+    }
+    if (!PASS && lane == 0) G.ecnt[q] = cnt;
+  }
+}
+
+// k_graph_relax: one wave per read.  The nodes in sorted order; node i's edges
+// (the stream, 64 at a time, the next chunk in flight) update their own node j
+// each (distinct j per lane, as the reference's updates for one i are
+// independent), then are united in j order: the pre-scan roots are found in
+// parallel (path halving; a root never changes by compression, and the roots are
+// what the output needs), a root already met, or i's own, is a no-op, the rest are
+// merged in registers with the reference's rank rule (union_find.cc:13-23).  Node
+// state lives in LDS by record index, sized by the tier (NM records).
 template <uint32_t NM>
-__global__ __launch_bounds__(64) void k_graph(GraphDev G, uint32_t n_reads) {
-  // the ring: implied start / end and error, {idx | nsz << 16, lp_add}, name offset, the
-  // first GRING_U unitigs and prefix sums 1..GRING_U - 1 of names of <= GRING_U unitigs,
-  // and the path state
-  __shared__ double s_is[GRING], s_ie[GRING], s_er[GRING], s_lsi[GRING];
-  __shared__ uint2 s_meta[GRING];
-  __shared__ uint32_t s_po[GRING];  // < 2^32 (checked on the host)
-  __shared__ uint32_t s_u[GRING_U * GRING];        // [u * GRING + slot]: a lane per slot, no bank conflicts
-#ifdef PBGPU_GRAPH_PP_LDS
-  __shared__ uint2 s_pp[(GRING_U - 1) * GRING];
-#endif
-  __shared__ int32_t s_lp[GRING], s_lun[GRING];
-  __shared__ int16_t s_lst[GRING], s_lpv[GRING];  // node indices < 4096, or -1
-  __shared__ uint8_t s_fl[GRING];
-  __shared__ uint16_t s_par[NM];
-  __shared__ uint8_t s_rank[NM];
+__global__ __launch_bounds__(64) void k_graph_relax(GraphDev G, uint32_t n_reads) {
+  __shared__ double s_lsi[NM];
+  __shared__ int32_t s_lp[NM], s_lun[NM];
+  __shared__ int16_t s_lst[NM], s_lpv[NM];
+  __shared__ uint16_t s_idx[NM], s_ec[NM], s_par[NM];
+  __shared__ uint8_t s_fl[NM], s_rank[NM];
   const uint32_t r = blockIdx.x;
   if (r >= n_reads) return;
   const uint32_t lane = threadIdx.x;
   const uint64_t b = G.rec_off[r];
   const uint32_t n = (uint32_t)(G.rec_off[r + 1] - b);
   if (n == 0) return;
-  if (n > G.nmax || n > GRAPH_NMAX_K) {  // the host traverses this read (marked by the top tier)
+  if (!graph_on_device(G, n)) {  // the host traverses this read (marked by the top tier)
     if (NM == GRAPH_NMAX)
       for (uint32_t i = lane; i < n; i += 64) G.out[b + i] = GraphNode{0, -1, -1, 0, i, GRAPH_HOST};
     return;
   }
   if (!graph_tier<NM>(G, n)) return;
-  const double rl = (double)(G.roff[r + 1] - G.roff[r]);
-  const double play = G.play, kd = (double)G.k;
-  const uint32_t km1 = G.k - 1;
-  for (uint32_t i = lane; i < n; i += 64) { s_par[i] = (uint16_t)i; s_rank[i] = 0; }
-  auto load_pos = [&](uint32_t p) {  // node_info::reset (overlap_graph.hpp:24-34) of sorted position p
-    const uint32_t sl = p % GRING;
+  // node_info::reset (overlap_graph.hpp:24-34) of every node
+  for (uint32_t p = lane; p < n; p += 64) {
     const GDesc d = G.desc[b + p];
-    s_is[sl] = d.imp_s; s_ie[sl] = d.imp_e; s_er[sl] = d.err; s_po[sl] = (uint32_t)d.poff;
-    s_meta[sl] = make_uint2(d.idx | (d.nsz << 16), d.lp_add);
-    const uint32_t m = d.nsz < GRING_U ? d.nsz : GRING_U;
-    for (uint32_t u = 0; u < m; ++u) s_u[u * GRING + sl] = G.ounits[d.poff + u];
-#ifdef PBGPU_GRAPH_PP_LDS
-    if (d.nsz <= GRING_U)
-      for (uint32_t u = 1; u < m; ++u) s_pp[(u - 1) * GRING + sl] = G.pp[d.poff + u];
-#endif
-    s_lp[sl] = (int32_t)d.lp_add; s_lun[sl] = (int32_t)d.nsz; s_lst[sl] = -1; s_lpv[sl] = -1;
-    s_lsi[sl] = d.imp_s; s_fl[sl] = (uint8_t)(GRAPH_START | GRAPH_END);
-  };
-  auto flush_pos = [&](uint32_t p) {
-    const uint32_t sl = p % GRING;
-    G.out[b + (s_meta[sl].x & 0xFFFFu)] = GraphNode{s_lp[sl], s_lst[sl], s_lpv[sl], s_lun[sl], 0u, s_fl[sl]};
-  };
-  // union-find root with path halving (every write links a node to an ancestor, so
-  // concurrent lanes keep a valid forest with the same roots)
-  auto find = [&](uint32_t q) -> uint32_t {
+    const uint32_t it = d.idx;
+    s_idx[p] = (uint16_t)it;
+    s_ec[p] = (uint16_t)G.ecnt[b + p];
+    s_lp[it] = (int32_t)d.lp_add; s_lun[it] = (int32_t)d.nsz; s_lst[it] = -1; s_lpv[it] = -1;
+    s_lsi[it] = d.imp_s; s_fl[it] = (uint8_t)(GRAPH_START | GRAPH_END);
+    s_par[it] = (uint16_t)it; s_rank[it] = 0;
+  }
+  __syncthreads();
+  auto find = [&](uint32_t q) -> uint32_t {  // union-find root with path halving
     while (s_par[q] != q) {
       const uint32_t g = s_par[s_par[q]];
       s_par[q] = (uint16_t)g;
@@ -3112,184 +3194,79 @@ __global__ __launch_bounds__(64) void k_graph(GraphDev G, uint32_t n_reads) {
     }
     return q;
   };
-  uint32_t loaded = n < GRING ? n : GRING, flushed = 0;
-  for (uint32_t p = lane; p < loaded; p += 64) load_pos(p);
-  __syncthreads();
-  bool overflow = false;
-#ifdef PBGPU_PROF
-  uint64_t pf[6] = {0, 0, 0, 0, 0, 0};
-  const uint64_t pf0 = __builtin_amdgcn_s_memtime();
-#endif
-  for (uint32_t i = 0; i < n; ++i) {
-    if ((i & 63) == 0 && i >= 64 && loaded < n) {  // positions [i - 64, i) are done: their slots take the next 64
-      flush_pos(i - 64 + lane);
-      flushed = i;
-      if (loaded + lane < n) load_pos(loaded + lane);
-      loaded = loaded + 64 < n ? loaded + 64 : n;
-      __syncthreads();
-    }
-    const uint32_t si = i % GRING;
-    const double ie_i = s_ie[si];
-    if (ie_i >= rl) continue;  // hanging off the 3' end
-    const uint2 mi = s_meta[si];
-    const uint32_t it_i = mi.x & 0xFFFFu, sa = mi.x >> 16;
-    const double err_i = s_er[si];
-    const uint32_t po_i = s_po[si];
-    const int32_t lp_i = s_lp[si], lun_i = s_lun[si], lst_i = s_lst[si];
-    const double lsi_i = s_lsi[si];
-    // name i's first GRING_U unitigs in registers (the same for every lane)
-    uint32_t a[GRING_U];
-#pragma unroll
-    for (uint32_t u = 0; u < GRING_U; ++u) a[u] = s_u[u * GRING + si];
-    auto unit_i = [&](uint32_t t) -> uint32_t { return sa <= GRING_U ? s_u[t * GRING + si] : G.ounits[po_i + t]; };
-    bool any_edge = false;
-    for (uint32_t j0 = i + 1; j0 < n; j0 += 64) {
-      PROF_T(pa);
-      const uint32_t j = j0 + lane;
-      const bool act = j < n;
-      if (__ballot(act && j >= loaded)) { overflow = true; break; }  // past the ring
-      const uint32_t sj = (act ? j : i) % GRING;
-      const double is_j = s_is[sj], ie_j = s_ie[sj];
-      const bool skip = (is_j <= 1.0) | (ie_i > __dadd_rn(ie_j, 31.0));  // off the 5' end | not advancing
-      const double position_len = __dadd_rn(ie_i, -is_j);
-      const double error = __dmul_rn(G.nb_errors, __dadd_rn(err_i, s_er[sj]));
-      const bool brk = act & !skip & (__dadd_rn(__dmul_rn(position_len, play), error) < kd);
-      const uint64_t bm = __ballot(brk);
-      const uint32_t fb = bm ? (uint32_t)__ffsll((long long)bm) - 1 : 64u;
-      bool edge = false;
-      int32_t nb = 0, common = 0;
-      const uint2 mj = s_meta[sj];
-      const uint32_t sb = mj.x >> 16;
-      PROF_T(pb);
-      if (act & !skip & (lane < fb) & (sa >= 2) & (sb >= 2)) {
-        bool same;
-        uint2 v;
-        if ((sa <= GRING_U) & (sb <= GRING_U)) {
-          // super_read_name::overlap (super_read_name.cc:49-72) in registers: the smallest
-          // t >= max(sa - sb + 1, 1) with name_i[t..sa) == name_j[0..sa - t)
-          uint32_t bu[GRING_U];
-#pragma unroll
-          for (uint32_t u = 0; u < GRING_U; ++u) bu[u] = s_u[u * GRING + sj];
-          const int t0 = (int)sa - (int)sb + 1;
-#pragma unroll
-          for (int t = (int)GRING_U - 1; t >= 1; --t) {
-            bool m = (t < (int)sa) & (t >= t0) & (a[t] == bu[0]);
-#pragma unroll
-            for (int q = t + 1; q < (int)GRING_U; ++q) m &= (q >= (int)sa) | (a[q] == bu[q - t]);
-            nb = m ? (int32_t)sa - t : nb;
-          }
-          same = sb == sa;
-#pragma unroll
-          for (uint32_t u = 0; u < GRING_U; ++u) same &= (u >= sa) | (a[u] == bu[u]);
-#ifdef PBGPU_GRAPH_PP_LDS
-          v = nb ? s_pp[((uint32_t)nb - 1) * GRING + sj] : make_uint2(0u, 0u);
-#else
-          v = nb ? G.pp[s_po[sj] + (uint32_t)nb] : make_uint2(0u, 0u);
-#endif
-        } else {
-          const uint32_t po_j = s_po[sj];
-          auto unit_j = [&](uint32_t q) -> uint32_t { return sb <= GRING_U ? s_u[q * GRING + sj] : G.ounits[po_j + q]; };
-          const uint32_t u0 = unit_j(0);
-          const int t0 = (int)sa - (int)sb + 1;
-          for (uint32_t t = t0 > 1 ? (uint32_t)t0 : 1u; t < sa; ++t) {
-            if (unit_i(t) != u0) continue;
-            uint32_t q = t + 1;
-            while (q < sa && unit_i(q) == unit_j(q - t)) ++q;
-            if (q == sa) { nb = (int32_t)(sa - t); break; }
-          }
-          same = false;
-          if (nb && sb == sa) {  // the same super-read name
-            same = true;
-            for (uint32_t u = 0; u < sa && same; ++u) same = unit_i(u) == unit_j(u);
-          }
-          v = nb ? G.pp[po_j + (uint32_t)nb] : make_uint2(0u, 0u);
-        }
-        if (nb && !same) {
-          const int32_t uol = (int32_t)(v.x - (uint32_t)(nb - 1) * km1);
-          common = (int32_t)v.y;
-          const double duol = (double)uol;
-          edge = !((duol > __dadd_rn(__dmul_rn(play, position_len), error)) |
-                   (position_len > __dmul_rn(play, __dadd_rn(duol, error))));
-        }
+  // the read's edge stream, 64 at a time: cur holds [c0, c0 + 64), nxt the next chunk
+  const uint2* E = G.edges + G.eoff[b];
+  const uint32_t ne = (uint32_t)(G.eoff[b + n] - G.eoff[b]);
+  uint2 cur = lane < ne ? E[lane] : make_uint2(0u, 0u);
+  uint2 nxt = 64 + lane < ne ? E[64 + lane] : make_uint2(0u, 0u);
+  uint32_t c0 = 0, s = 0;
+  for (uint32_t p = 0; p < n; ++p) {
+    const uint32_t ec = s_ec[p];
+    if (ec == 0) continue;
+    const uint32_t it_i = s_idx[p];
+    const int32_t lp_i = s_lp[it_i], lun_i = s_lun[it_i], lst_i = s_lst[it_i];
+    const double lsi_i = s_lsi[it_i];
+    const uint32_t end = s + ec;
+    while (s < end) {
+      if (s >= c0 + 64) {  // next chunk; the one after it goes in flight
+        cur = nxt;
+        c0 += 64;
+        nxt = c0 + 64 + lane < ne ? E[c0 + 64 + lane] : make_uint2(0u, 0u);
       }
-      PROF_T(pc);
+      const uint32_t k = c0 + lane;
+      const bool edge = (k >= s) & (k < end);
+      const uint32_t it_j = cur.x & 0xFFFFu;
       if (edge) {  // node_info update (overlap_graph.cc:41-56); this lane owns node j
-        s_fl[sj] &= (uint8_t)~GRAPH_START;
-        const int32_t nlpath = (int32_t)((uint32_t)lp_i + mj.y - (uint32_t)common);
-        const int32_t lp_j = s_lp[sj];
-        const bool upd = nlpath > lp_j || (nlpath == lp_j && (s_lst[sj] == -1 || lsi_i > s_lsi[sj]));
+        s_fl[it_j] &= (uint8_t)~GRAPH_START;
+        const int32_t nlpath = (int32_t)((uint32_t)lp_i + cur.y);
+        const int32_t lp_j = s_lp[it_j];
+        const bool upd = nlpath > lp_j || (nlpath == lp_j && (s_lst[it_j] == -1 || lsi_i > s_lsi[it_j]));
         if (upd) {
-          s_lp[sj] = nlpath;
-          s_lst[sj] = (int16_t)(lst_i == -1 ? (int32_t)it_i : lst_i);
-          s_lsi[sj] = lsi_i;
-          s_lpv[sj] = (int16_t)it_i;
-          s_lun[sj] = lun_i + (int32_t)sb - nb;
+          s_lp[it_j] = nlpath;
+          s_lst[it_j] = (int16_t)(lst_i == -1 ? (int32_t)it_i : lst_i);
+          s_lsi[it_j] = lsi_i;
+          s_lpv[it_j] = (int16_t)it_i;
+          s_lun[it_j] = lun_i + (int32_t)(cur.x >> 16);
         }
       }
-      PROF_T(pd);
-      // union_sets(it_i, it_j) for the edges in j order (union_find.cc:13-23).  The roots
-      // before this scan are found in parallel (path compression never changes a root,
-      // and the roots are all the output needs); a root already met in this scan, or i's
-      // own, is in i's set (a no-op union); the rest are merged into i's set one after
-      // another in j order, with the reference's rank rule, in registers.
-      uint64_t em = __ballot(edge);
-      if (em) {
-        any_edge = true;
-        const uint32_t r1 = find(it_i);
-        const uint32_t R = edge ? find(mj.x & 0xFFFFu) : r1;
-        const uint32_t rk = s_rank[R];
-        // the edge lanes holding the same root: a ballot per bit of R (node indices < 2^12)
-        uint64_t same = em;
+      // union_sets(it_i, it_j) for this chunk's edges in j order
+      const uint64_t em = __ballot(edge);
+      const uint32_t r1 = find(it_i);
+      const uint32_t R = edge ? find(it_j) : r1;
+      const uint32_t rk = s_rank[R];
+      // the edge lanes holding the same root: a ballot per bit of R (node indices < 2^12)
+      uint64_t same = em;
 #pragma unroll
-        for (uint32_t bit = 0; bit < 12; ++bit) {
-          const uint64_t bb = __ballot((R >> bit) & 1u);
-          same &= ((R >> bit) & 1u) ? bb : ~bb;
-        }
-        const bool first = edge & (R != r1) & ((same & ((1ull << lane) - 1)) == 0);
-        uint32_t cur = r1, crank = s_rank[r1];
-        for (uint64_t fm = __ballot(first); fm; fm &= fm - 1) {
-          const uint32_t l = (uint32_t)__ffsll((long long)fm) - 1;
-          const uint32_t vv = (uint32_t)__builtin_amdgcn_readlane((int)R, (int)l);
-          const uint32_t vr = (uint32_t)__builtin_amdgcn_readlane((int)rk, (int)l);
-          if (crank > vr) {
-            if (lane == 0) s_par[vv] = (uint16_t)cur;
-          } else if (crank < vr) {
-            if (lane == 0) s_par[cur] = (uint16_t)vv;
-            cur = vv; crank = vr;
-          } else {
-            ++crank;
-            if (lane == 0) { s_par[vv] = (uint16_t)cur; s_rank[cur] = (uint8_t)crank; }
-          }
+      for (uint32_t bit = 0; bit < 12; ++bit) {
+        const uint64_t bb = __ballot((R >> bit) & 1u);
+        same &= ((R >> bit) & 1u) ? bb : ~bb;
+      }
+      const bool first = edge & (R != r1) & ((same & ((1ull << lane) - 1)) == 0);
+      uint32_t cr = r1, crank = s_rank[r1];
+      for (uint64_t fm = __ballot(first); fm; fm &= fm - 1) {
+        const uint32_t l = (uint32_t)__ffsll((long long)fm) - 1;
+        const uint32_t vv = (uint32_t)__builtin_amdgcn_readlane((int)R, (int)l);
+        const uint32_t vr = (uint32_t)__builtin_amdgcn_readlane((int)rk, (int)l);
+        if (crank > vr) {
+          if (lane == 0) s_par[vv] = (uint16_t)cr;
+        } else if (crank < vr) {
+          if (lane == 0) s_par[cr] = (uint16_t)vv;
+          cr = vv; crank = vr;
+        } else {
+          ++crank;
+          if (lane == 0) { s_par[vv] = (uint16_t)cr; s_rank[cr] = (uint8_t)crank; }
         }
       }
-#ifdef PBGPU_PROF
-      {
-        const uint64_t pe = __builtin_amdgcn_s_memtime();
-        pf[0] += pb - pa; pf[1] += pc - pb; pf[2] += pd - pc; pf[3] += pe - pd; pf[4] += 1;
-      }
-#endif
-      if (bm) break;  // the reference's break
+      s = end < c0 + 64 ? end : c0 + 64;
+      __syncthreads();  // (one wave: this chunk's LDS updates before the next reads)
     }
-    if (overflow) break;
-    if (any_edge && lane == 0) s_fl[si] &= (uint8_t)~GRAPH_END;
-    __syncthreads();  // (one wave: orders this node's LDS updates before the next node reads them)
+    if (lane == 0) s_fl[it_i] &= (uint8_t)~GRAPH_END;
+    __syncthreads();
   }
-  __syncthreads();
-#ifdef PBGPU_PROF
-  // slots 80..: chunk scan, names + sums, node updates, unions, chunks, nodes, wave total, waves
-  PROF_ADD(80, pf[0]); PROF_ADD(81, pf[1]); PROF_ADD(82, pf[2]); PROF_ADD(83, pf[3]); PROF_ADD(84, pf[4]);
-  PROF_ADD(85, n); PROF_ADD(86, __builtin_amdgcn_s_memtime() - pf0); PROF_ADD(87, 1);
-#endif
-  if (overflow) {  // a scan longer than the ring: the host traverses the read
-    for (uint32_t i = lane; i < n; i += 64) G.out[b + i] = GraphNode{0, -1, -1, 0, i, GRAPH_HOST};
-    return;
-  }
-  for (uint32_t p = flushed + lane; p < n; p += 64) flush_pos(p);
-  __threadfence();  // the node stores above before the root stores below (same addresses)
   for (uint32_t i = lane; i < n; i += 64) {
     uint32_t q = i;
     while (s_par[q] != q) q = s_par[q];
-    G.out[b + i].root = q;
+    G.out[b + i] = GraphNode{s_lp[i], s_lst[i], s_lpv[i], s_lun[i], q, s_fl[i]};
   }
 }
 // ====================================================== mega-reads (device)
@@ -3861,21 +3838,40 @@ void launch_graph_sizes(const GraphDev& G, uint64_t n_recs, uint32_t* sizes, uin
   launch_excl_scan(sizes, nullptr, n_recs, G.poff, scan_scratch, st);
 }
 hipError_t launch_graph(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hipStream_t st, hipStream_t side,
-                        hipEvent_t fork, hipEvent_t join) {
+                        hipEvent_t fork, hipEvent_t join, uint64_t* scan_scratch, uint64_t* n_edges) {
+  *n_edges = 0;
   if (!n_recs || !n_reads) return hipSuccess;
   hipLaunchKernelGGL(k_graph_prep, dim3((uint32_t)std::min<uint64_t>((n_recs + 255) / 256, 65535)), dim3(256), 0, st,
                      G, n_recs);
-  // the long reads' tier first, on the side stream: its waves are the longest.  A
-  // failed fork or join would let k_mega read G.out while the side tier still writes
-  // it, so each is checked (the caller raises)
+  // the per-read sorts: the long reads' tier on the side stream, beside the short one.  A
+  // failed fork or join would let a kernel read what the other stream still writes, so
+  // each is checked (the caller raises)
   hipError_t e = hipEventRecord(fork, st);
   if (e == hipSuccess) e = hipStreamWaitEvent(side, fork, 0);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_graph_sort<GRAPH_NMAX>, dim3(n_reads), dim3(GRAPH_SORT_BLOCK), 0, side, G, n_reads);
-  hipLaunchKernelGGL(k_graph<GRAPH_NMAX>, dim3(n_reads), dim3(64), 0, side, G, n_reads);
   if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_graph_sort<GRAPH_NM_SMALL>, dim3(n_reads), dim3(GRAPH_SORT_BLOCK), 0, st, G, n_reads);
-  hipLaunchKernelGGL(k_graph<GRAPH_NM_SMALL>, dim3(n_reads), dim3(64), 0, st, G, n_reads);
+  if ((e = hipStreamWaitEvent(st, join, 0)) != hipSuccess) return e;
+  // every node's edges: counted, offsets, written
+  const uint32_t eg = (uint32_t)std::min<uint64_t>((n_recs + GRAPH_EDGE_BLOCK / 64 - 1) / (GRAPH_EDGE_BLOCK / 64), 1u << 20);
+  hipLaunchKernelGGL(k_graph_edges<0>, dim3(eg), dim3(GRAPH_EDGE_BLOCK), 0, st, G, n_recs);
+  launch_excl_scan(G.ecnt, nullptr, n_recs, G.eoff, scan_scratch, st);
+  if ((e = hipMemcpyAsync(n_edges, G.eoff + n_recs, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+  return hipStreamSynchronize(st);
+}
+hipError_t launch_graph_relax(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hipStream_t st, hipStream_t side,
+                              hipEvent_t fork, hipEvent_t join) {
+  if (!n_recs || !n_reads) return hipSuccess;
+  const uint32_t eg = (uint32_t)std::min<uint64_t>((n_recs + GRAPH_EDGE_BLOCK / 64 - 1) / (GRAPH_EDGE_BLOCK / 64), 1u << 20);
+  hipLaunchKernelGGL(k_graph_edges<1>, dim3(eg), dim3(GRAPH_EDGE_BLOCK), 0, st, G, n_recs);
+  // the long reads' relaxation on the side stream: its waves are the longest
+  hipError_t e = hipEventRecord(fork, st);
+  if (e == hipSuccess) e = hipStreamWaitEvent(side, fork, 0);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_graph_relax<GRAPH_NMAX>, dim3(n_reads), dim3(64), 0, side, G, n_reads);
+  if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_graph_relax<GRAPH_NM_SMALL>, dim3(n_reads), dim3(64), 0, st, G, n_reads);
   return hipStreamWaitEvent(st, join, 0);
 }
 

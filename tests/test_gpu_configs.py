@@ -71,3 +71,36 @@ def test_c3_full_index():
     from tools.synth import Dataset
     ds = Dataset("C3", seed=42, threads=16, n_pb=1500)
     _compare(ds, _prod(ds, 21), "C3 production")
+
+
+def test_c4_repeat_model_oracle():
+    """C4's repeat model (2% of the genome in 5-50-copy repeats, 15-kb-N50 reads) at a size the
+    oracle holds (tools/synth.py "C4r": 16 Mbp genome, 800k super-reads at C4's ~50x coverage,
+    1000 reads), byte for byte against the oracle with the production flags and with
+    --max-count 2000: the 99% threshold and the max-count filter (coarse_aligner.cc:104-125) on
+    multi-copy repeats and long reads, beyond the property checks of the C4/C5 tests."""
+    from oracle.oracle import OracleIndex, params
+    from pacbio_amd import pbgpu
+    from tools.synth import Dataset
+    ds = Dataset("C4r", seed=42, threads=16)
+    names, seqs = ds.sr_names(), ds.sr_seqs()
+    pnames, pseqs = ds.pb_names(), ds.pb_seqs()
+    gix = pbgpu.Index.from_records(names, seqs, 17)
+    oix = OracleIndex.from_records(names, seqs, 17, threads=16)
+    outs = {}
+    for mc in (5000, 2000):
+        kw = dict(_prod(ds, 17), max_count=mc)
+        al = pbgpu.Aligner(gix, **kw)
+        rd = al.upload(pseqs, names=pnames)
+        al.align_resident(rd)
+        got = al.format_device(rd)
+        rd.close()
+        al.close()
+        exp = oix.align_format(params(**kw), pnames, pseqs, threads=16)
+        assert exp.count("\n") > 100 * len(pseqs), f"C4r max_count {mc}: too few records"
+        assert_same_coords(got, exp, f"C4r max_count {mc}")
+        outs[mc] = exp
+    oix.close()
+    gix.close()
+    # the repeats reach the limit: --max-count 2000 drops k-mers that 5000 keeps
+    assert outs[2000] != outs[5000] and outs[2000].count("\n") < outs[5000].count("\n")

@@ -38,6 +38,10 @@ PRESETS = {
     # of text) over a 3.1 Gbp genome with the C4 repeat model, PB reads of 15 kb N50
     "C5": dict(genome_len=3_100_000_000, n_sr=50_000_000, n_pb=20_000_000, pb_len_mean=12500, pb_len_sigma=0.6,
                repeat_frac=0.02),
+    # C4's repeat model (2% of the genome in 5-50-copy repeats, PB reads of 15 kb N50) at a size the
+    # CPU oracle holds: a 16 Mbp genome at C4's ~50x super-read coverage (800k SRs, ~1 Gbp of text)
+    "C4r": dict(genome_len=16_000_000, n_sr=800_000, n_pb=1000, pb_len_mean=12500, pb_len_sigma=0.6,
+                repeat_frac=0.02),
     "tiny": dict(genome_len=20_000, n_sr=60, n_pb=8, pb_len_mean=2000, pb_len_sigma=0.0),
     "small": dict(genome_len=200_000, n_sr=1500, n_pb=40, pb_len_mean=6000, pb_len_sigma=0.4),
 }
