@@ -63,6 +63,11 @@ pbgpu_status pbgpu_measure_gather(int device, uint64_t buffer_bytes, double* gbp
  * pbgpu_measure_gather) or 512 (random 512-B runs read as 64 consecutive 8-B
  * words, the shape of k_group's occurrence-list reads). */
 pbgpu_status pbgpu_measure_gather_shape(int device, uint64_t buffer_bytes, uint32_t unit_bytes, double* gbps);
+/* Self-check of the fit's reciprocal (least_square_2d.hpp:47-67 divides by the
+ * point count n): the device's shortened RN(1/n) against a correctly rounded
+ * division for every n in [1, n_max]; *mismatches = the count that differ
+ * (0 expected). */
+pbgpu_status pbgpu_check_reciprocal(int device, uint32_t n_max, uint64_t* mismatches);
 
 /* ------------------------------------------------------------------ index
  * Replaces superread_parse() + sequence_psa (superread_parser.hpp:53-224):

@@ -718,6 +718,22 @@ pbgpu_status pbgpu_measure_gather(int device, uint64_t buffer_bytes, double* gbp
   return pbgpu_measure_gather_shape(device, buffer_bytes, 64, gbps);
 }
 
+pbgpu_status pbgpu_check_reciprocal(int device, uint32_t n_max, uint64_t* mismatches) {
+  if (!mismatches || n_max == 0) return fail(PBGPU_ERR_INVALID, "bad argument");
+  API_TRY
+  HIPCHK(hipSetDevice(device));
+  dbuf<unsigned long long> bad;
+  bad.ensure_fixed(1);
+  HIPCHK(hipMemset(bad.p, 0, 8));
+  launch_check_recip(n_max, bad.p, nullptr);
+  HIPCHK(hipGetLastError());
+  unsigned long long nb = 0;
+  HIPCHK(hipMemcpy(&nb, bad.p, 8, hipMemcpyDeviceToHost));
+  *mismatches = nb;
+  return PBGPU_OK;
+  API_CATCH
+}
+
 pbgpu_status pbgpu_measure_gather_shape(int device, uint64_t buffer_bytes, uint32_t unit_bytes, double* gbps) {
   if (!gbps || buffer_bytes < (1u << 20) || (unit_bytes != 64 && unit_bytes != 512))
     return fail(PBGPU_ERR_INVALID, "bad argument");

@@ -183,6 +183,8 @@ struct ChainOut {
 // Exclusive scan of n counts (u32 or u64, exactly one of in32 / in64 non-null) into
 // n + 1 offsets, out[n] = the total (pbgpu_kernels.hip; replaces a library scan on the
 // per-batch path).  scratch: excl_scan_scratch_words(n) words.
+// every d in [1, n_max]: the fit's reciprocal (recip_int) against __ddiv_rn(1.0, d); mismatches added to *bad
+void launch_check_recip(uint32_t n_max, unsigned long long* bad, hipStream_t st);
 uint64_t excl_scan_scratch_words(uint64_t n);
 void launch_excl_scan(const uint32_t* in32, const uint64_t* in64, uint64_t n, uint64_t* out, uint64_t* scratch,
                       hipStream_t st);

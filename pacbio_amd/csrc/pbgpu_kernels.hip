@@ -1883,13 +1883,41 @@ DEV double div_rcp(double a, double b, double y) {
 
 // least_square_2d::add (least_square_2d.hpp:47-67), x = sr offset, y = pb offset;
 // the four divisions by n share one correctly rounded reciprocal
+// RN(1 / d) for an integer 1 <= d < 2^32: the compiler's __ddiv_rn(1.0, d) less the
+// operand scaling (v_div_scale) and special-case fixup (v_div_fixup), which change
+// nothing for such d -- the same reciprocal and Newton steps and the same final
+// correction fma(1 - d y, y, y) (v_div_fmas without scaling).  7 instructions
+// instead of 11; checked against __ddiv_rn for every d < 2^24 on the device
+// (pbgpu_check_reciprocal, tests/test_gpu_edge.py).
+DEV double recip_int(double d) {
+  double y = __builtin_amdgcn_rcp(d);
+  double e = __fma_rn(-d, y, 1.0);
+  y = __fma_rn(y, e, y);
+  e = __fma_rn(-d, y, 1.0);
+  y = __fma_rn(y, e, y);
+  const double r = __fma_rn(-d, y, 1.0);
+  return __fma_rn(r, y, y);
+}
+__global__ void k_check_recip(uint32_t n_max, unsigned long long* bad) {
+  unsigned long long nb = 0;
+  for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x + 1; d <= n_max; d += gridDim.x * blockDim.x) {
+    const double dd = (double)d;
+    nb += __double_as_longlong(recip_int(dd)) != __double_as_longlong(__ddiv_rn(1.0, dd));
+  }
+  if (nb) atomicAdd(bad, nb);
+}
+void launch_check_recip(uint32_t n_max, unsigned long long* bad, hipStream_t st) {
+  hipLaunchKernelGGL(k_check_recip, dim3(1024), dim3(256), 0, st, n_max, bad);
+}
+// (n as a 32-bit count with its double kept beside it, dn + 1 exact: the 64-bit long of
+// the reference converts to double in five instructions a point)
 struct Lsq {
-  double EX = 0, EY = 0, EXX = 0, EXY = 0, VX = 0, CXY = 0, NB = 0;
-  long n = 0;
+  double EX = 0, EY = 0, EXX = 0, EXY = 0, VX = 0, CXY = 0, NB = 0, dn = 0;
+  uint32_t n = 0;
   DEV void add(double x, double y) {
     ++n;
-    const double dn = (double)n;
-    const double rn = __ddiv_rn(1.0, dn);
+    dn = __dadd_rn(dn, 1.0);
+    const double rn = recip_int(dn);
     const double deltaX = __dadd_rn(x, -EX);
     EX = __dadd_rn(EX, div_rcp(deltaX, dn, rn));
     const double ndeltaX = __dadd_rn(x, -EX);
@@ -2070,7 +2098,7 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
 #endif
     err = __dadd_rn(err, fabs(__dadd_rn(__dadd_rn(__dmul_rn(a, (double)p.y), b), -(double)p.x)));
   });
-  if (L.n > 1) R.avg_err = __ddiv_rn(err, (double)L.n);
+  if (L.n > 1) R.avg_err = __ddiv_rn(err, L.dn);
   PROF_T(kc_t3);
   R.rs = first.x;
   R.re = (int32_t)((uint32_t)prev.x + k - 1u);

@@ -26,7 +26,7 @@ STATUS = {0: "OK", 1: "INVALID", 2: "IO", 3: "NOMEM", 4: "DEVICE", 5: "UNSUPPORT
 # every symbol include/pbgpu.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "pbgpu_abi_version", "pbgpu_last_error", "pbgpu_device_count", "pbgpu_device_synchronize",
-    "pbgpu_measure_gather", "pbgpu_measure_gather_shape",
+    "pbgpu_measure_gather", "pbgpu_measure_gather_shape", "pbgpu_check_reciprocal",
     "pbgpu_index_build_fasta", "pbgpu_index_build", "pbgpu_index_free", "pbgpu_index_get_info",
     "pbgpu_index_sr_name", "pbgpu_index_sr_len",
     "pbgpu_align_params_default", "pbgpu_aligner_create", "pbgpu_aligner_free",
@@ -176,6 +176,7 @@ def lib():
         L.pbgpu_device_synchronize.argtypes = [C.c_int]
         L.pbgpu_measure_gather.argtypes = [C.c_int, C.c_uint64, C.POINTER(C.c_double)]
         L.pbgpu_measure_gather_shape.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.POINTER(C.c_double)]
+        L.pbgpu_check_reciprocal.argtypes = [C.c_int, C.c_uint32, C.POINTER(C.c_uint64)]
         L.pbgpu_index_build_fasta.argtypes = [C.POINTER(C.c_char_p), C.c_size_t, C.POINTER(IndexParams), C.POINTER(vp)]
         L.pbgpu_index_build.argtypes = [C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.POINTER(C.c_uint64),
                                         C.c_size_t, C.POINTER(IndexParams), C.POINTER(vp)]
@@ -254,6 +255,13 @@ def measure_gather(device=0, buffer_bytes=64 << 30, unit_bytes=64):
     g = C.c_double()
     _check(lib().pbgpu_measure_gather_shape(device, buffer_bytes, unit_bytes, C.byref(g)))
     return g.value
+
+
+def check_reciprocal(device=0, n_max=1 << 24):
+    """Mismatches of the fit's device reciprocal against __ddiv_rn(1.0, n), n in [1, n_max]."""
+    m = C.c_uint64()
+    _check(lib().pbgpu_check_reciprocal(device, n_max, C.byref(m)))
+    return m.value
 
 
 def _cstrs(items):

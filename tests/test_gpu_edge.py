@@ -170,3 +170,11 @@ def test_long_strands(long_strands, cfg):
     assert max(nb) > 65535 and sum(1 for x in nb if 4095 < x <= 65535) > 10
     got, _ = _gpu(names, seqs, pnames, pseqs, **cfg)
     assert_same_coords(got, exp, f"long strands {cfg}")
+
+
+def test_fit_reciprocal_exact():
+    """The fit divides by the point count n four times a point (least_square_2d.hpp:47-67);
+    the device takes RN(1/n) with a shortened sequence (recip_int): it must equal the
+    correctly rounded 1.0 / n for every n a strand can reach at C1-C5 scale (< 2^24)."""
+    from pacbio_amd import pbgpu
+    assert pbgpu.check_reciprocal(0, 1 << 24) == 0
