@@ -3026,7 +3026,7 @@ DEV uint64_t graph_dkey(double x) {
 // Two tiers by the read's record count (LDS sized to the tier, so the common
 // reads of <= GRAPH_NM_SMALL records run many blocks a CU): NM = GRAPH_NM_SMALL
 // takes those, NM = GRAPH_NMAX the rest.
-constexpr uint32_t GRAPH_SORT_BLOCK = 256, GRAPH_NM_SMALL = 1024;
+constexpr uint32_t GRAPH_SORT_BLOCK = 256, GRAPH_NM_SMALL = 1024, GRAPH_RELAX_MIN = 512;
 template <uint32_t NM>
 DEV bool graph_tier(const GraphDev& G, uint32_t n) {
   if (n == 0 || n > G.nmax || n > GRAPH_NMAX) return false;
@@ -3069,61 +3069,88 @@ __global__ __launch_bounds__(GRAPH_SORT_BLOCK) void k_graph_sort(GraphDev G, uin
 // (k_graph_edges); only the longest-path relaxation and the unions, in the
 // reference's (i, then j) order, are serial per read (k_graph_relax).
 //
-// k_graph_edges: one wave per node i (sorted position), lanes j = i + 1 + lane, ...
-// 64 at a time until the reference's break.  PASS 0 counts each node's edges
-// (ecnt); an exclusive scan gives every node's offset, so the edges of a read are
-// one contiguous stream in (i, j) order; PASS 1 writes them as
-// {j's record index | (unitigs added) << 16, path increment}.
+// k_graph_edges: a block per window of GE_NODES consecutive sorted positions of
+// the batch; the window's nodes and the GE_SLOTS - GE_NODES positions after them
+// (implied span, error, name size, first GRAPH_U unitigs, read bounds) are staged
+// in LDS; a wave per node i, lanes j = i + 1 + lane, ... 64 at a time until the
+// reference's break (positions past the staged ones are read from HBM).  PASS 0
+// counts each node's edges (ecnt); an exclusive scan gives every node's offset,
+// so a read's edges are one contiguous stream in (i, j) order; PASS 1 writes
+// them as {j's record index | (unitigs added) << 16, path increment}.
 constexpr uint32_t GRAPH_U = 8;  // names of at most this many unitigs are matched in registers
 constexpr uint32_t GRAPH_NMAX_K = GRAPH_NMAX;  // reads of more records go to the host (LDS state)
 static_assert(GRAPH_NMAX_K <= 4096, "k_graph_relax matches roots by 12 bits and keeps 16-bit indices");
-constexpr uint32_t GRAPH_EDGE_BLOCK = 256;
+constexpr uint32_t GE_NODES = 64, GE_SLOTS = 384, GE_BLOCK = 256;
 DEV bool graph_on_device(const GraphDev& G, uint32_t n) { return n > 0 && n <= G.nmax && n <= GRAPH_NMAX_K; }
 template <int PASS>
-__global__ __launch_bounds__(GRAPH_EDGE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n_recs) {
+__global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n_recs) {
+  __shared__ double s_is[GE_SLOTS], s_ie[GE_SLOTS], s_er[GE_SLOTS], s_rl[GE_SLOTS];
+  __shared__ uint32_t s_meta[GE_SLOTS], s_lpa[GE_SLOTS], s_end[GE_SLOTS], s_po[GE_SLOTS];
+  __shared__ uint32_t s_u[GRAPH_U * GE_SLOTS];  // [u * GE_SLOTS + slot]
+  const uint64_t q0 = (uint64_t)blockIdx.x * GE_NODES;
+  if (q0 >= n_recs) return;
+  const uint32_t ns = (uint32_t)(n_recs - q0 < GE_SLOTS ? n_recs - q0 : GE_SLOTS);
+  for (uint32_t t = threadIdx.x; t < ns; t += GE_BLOCK) {
+    const uint64_t q = q0 + t;
+    const uint32_t r = G.recs[q].read;  // records are grouped per read
+    const uint64_t e = G.rec_off[r + 1];
+    const uint32_t n = (uint32_t)(e - G.rec_off[r]);
+    const GDesc d = G.desc[q];
+    s_is[t] = d.imp_s; s_ie[t] = d.imp_e; s_er[t] = d.err;
+    s_rl[t] = (double)(G.roff[r + 1] - G.roff[r]);
+    s_meta[t] = d.idx | (d.nsz << 16); s_lpa[t] = d.lp_add; s_po[t] = (uint32_t)d.poff;  // < 2^32 (host check)
+    s_end[t] = graph_on_device(G, n) ? (uint32_t)e : (uint32_t)(q + 1);  // a read left to the host: no scan
+#pragma unroll
+    for (uint32_t u = 0; u < GRAPH_U; ++u) s_u[u * GE_SLOTS + t] = u < d.nsz ? G.ounits[d.poff + u] : 0u;
+  }
+  __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
-  const uint64_t nw = (uint64_t)gridDim.x * (GRAPH_EDGE_BLOCK / 64);
-  for (uint64_t q = (uint64_t)blockIdx.x * (GRAPH_EDGE_BLOCK / 64) + (threadIdx.x >> 6); q < n_recs; q += nw) {
-    const uint32_t r = G.recs[q].read;  // records are grouped per read: q is sorted position q - b of read r
-    const uint64_t b = G.rec_off[r];
-    const uint32_t n = (uint32_t)(G.rec_off[r + 1] - b);
+  const double play = G.play, kd = (double)G.k;
+  const uint32_t km1 = G.k - 1;
+  for (uint32_t ti = threadIdx.x >> 6; ti < GE_NODES && ti < ns; ti += GE_BLOCK / 64) {
+    const uint64_t q = q0 + ti;
+    const uint32_t qe = s_end[ti];
+    const double ie_i = s_ie[ti], err_i = s_er[ti];
     uint32_t cnt = 0;
-    const GDesc di = G.desc[q];
-    const double rl = (double)(G.roff[r + 1] - G.roff[r]);
-    if (graph_on_device(G, n) && !(di.imp_e >= rl)) {  // (imp_e >= rl: hanging off the 3' end)
-      const uint32_t pi = (uint32_t)(q - b);
-      const double ie_i = di.imp_e, err_i = di.err, play = G.play, kd = (double)G.k;
-      const uint32_t km1 = G.k - 1, sa = di.nsz;
-      const uint64_t po_i = di.poff;
+    if ((q + 1 < qe) & !(ie_i >= s_rl[ti])) {  // (imp_e >= rl: hanging off the 3' end)
+      const uint32_t sa = s_meta[ti] >> 16, po_i = s_po[ti];
       uint32_t a[GRAPH_U];
 #pragma unroll
-      for (uint32_t u = 0; u < GRAPH_U; ++u) a[u] = u < sa ? G.ounits[po_i + u] : 0u;
+      for (uint32_t u = 0; u < GRAPH_U; ++u) a[u] = s_u[u * GE_SLOTS + ti];
       auto unit_i = [&](uint32_t t) -> uint32_t { return G.ounits[po_i + t]; };
-      uint64_t* eo = PASS ? &G.eoff[q] : nullptr;
-      const uint64_t e0 = PASS ? *eo : 0;
-      for (uint32_t j0 = pi + 1; j0 < n; j0 += 64) {
-        const uint32_t j = j0 + lane;
-        const bool act = j < n;
-        const GDesc dj = G.desc[b + (act ? j : pi)];
-        const double is_j = dj.imp_s, ie_j = dj.imp_e;
+      const uint64_t e0 = PASS ? G.eoff[q] : 0;
+      for (uint64_t j0 = q + 1; j0 < qe; j0 += 64) {
+        const uint64_t j = j0 + lane;
+        const bool act = j < qe;
+        const uint32_t sj = (uint32_t)((act ? j : q) - q0);
+        // node j: staged, or (a scan past the window) from HBM
+        double is_j, ie_j, er_j;
+        uint32_t mj, lpa_j, po_j, bu[GRAPH_U];
+        if (sj < ns) {
+          is_j = s_is[sj]; ie_j = s_ie[sj]; er_j = s_er[sj]; mj = s_meta[sj]; lpa_j = s_lpa[sj]; po_j = s_po[sj];
+#pragma unroll
+          for (uint32_t u = 0; u < GRAPH_U; ++u) bu[u] = s_u[u * GE_SLOTS + sj];
+        } else {
+          const GDesc dj = G.desc[j];
+          is_j = dj.imp_s; ie_j = dj.imp_e; er_j = dj.err; mj = dj.idx | (dj.nsz << 16); lpa_j = dj.lp_add;
+          po_j = (uint32_t)dj.poff;
+#pragma unroll
+          for (uint32_t u = 0; u < GRAPH_U; ++u) bu[u] = u < dj.nsz ? G.ounits[dj.poff + u] : 0u;
+        }
         const bool skip = (is_j <= 1.0) | (ie_i > __dadd_rn(ie_j, 31.0));  // off the 5' end | not advancing
         const double position_len = __dadd_rn(ie_i, -is_j);
-        const double error = __dmul_rn(G.nb_errors, __dadd_rn(err_i, dj.err));
+        const double error = __dmul_rn(G.nb_errors, __dadd_rn(err_i, er_j));
         const bool brk = act & !skip & (__dadd_rn(__dmul_rn(position_len, play), error) < kd);
         const uint64_t bm = __ballot(brk);
         const uint32_t fb = bm ? (uint32_t)__ffsll((long long)bm) - 1 : 64u;
-        const uint32_t sb = dj.nsz;
+        const uint32_t sb = mj >> 16;
         bool edge = false;
         int32_t nb = 0, common = 0;
         if (act & !skip & (lane < fb) & (sa >= 2) & (sb >= 2)) {
           bool same;
-          uint2 v;
           if ((sa <= GRAPH_U) & (sb <= GRAPH_U)) {
             // super_read_name::overlap (super_read_name.cc:49-72) in registers: the smallest
             // t >= max(sa - sb + 1, 1) with name_i[t..sa) == name_j[0..sa - t)
-            uint32_t bu[GRAPH_U];
-#pragma unroll
-            for (uint32_t u = 0; u < GRAPH_U; ++u) bu[u] = u < sb ? G.ounits[dj.poff + u] : 0u;
             const int t0 = (int)sa - (int)sb + 1;
 #pragma unroll
             for (int t = (int)GRAPH_U - 1; t >= 1; --t) {
@@ -3136,7 +3163,6 @@ __global__ __launch_bounds__(GRAPH_EDGE_BLOCK) void k_graph_edges(GraphDev G, ui
 #pragma unroll
             for (uint32_t u = 0; u < GRAPH_U; ++u) same &= (u >= sa) | (a[u] == bu[u]);
           } else {
-            const uint64_t po_j = dj.poff;
             auto unit_j = [&](uint32_t qq) -> uint32_t { return G.ounits[po_j + qq]; };
             const uint32_t u0 = unit_j(0);
             const int t0 = (int)sa - (int)sb + 1;
@@ -3152,8 +3178,8 @@ __global__ __launch_bounds__(GRAPH_EDGE_BLOCK) void k_graph_edges(GraphDev G, ui
               for (uint32_t u = 0; u < sa && same; ++u) same = unit_i(u) == unit_j(u);
             }
           }
-          v = nb ? G.pp[dj.poff + (uint32_t)nb] : make_uint2(0u, 0u);
           if (nb && !same) {
+            const uint2 v = G.pp[po_j + (uint32_t)nb];
             const int32_t uol = (int32_t)(v.x - (uint32_t)(nb - 1) * km1);
             common = (int32_t)v.y;
             const double duol = (double)uol;
@@ -3166,7 +3192,7 @@ __global__ __launch_bounds__(GRAPH_EDGE_BLOCK) void k_graph_edges(GraphDev G, ui
           const uint32_t at = cnt + (uint32_t)__builtin_popcountll(em & ((1ull << lane) - 1));
           // the edge's path increment (nb_mers or sr_cover of j minus the common k-mers) and
           // the unitigs it adds (overlap_graph.cc:47-53)
-          G.edges[e0 + at] = make_uint2(dj.idx | ((sb - (uint32_t)nb) << 16), dj.lp_add - (uint32_t)common);
+          G.edges[e0 + at] = make_uint2((mj & 0xFFFFu) | ((sb - (uint32_t)nb) << 16), lpa_j - (uint32_t)common);
         }
         cnt += (uint32_t)__builtin_popcountll(em);
         if (bm) break;  // the reference's break
@@ -3176,16 +3202,23 @@ __global__ __launch_bounds__(GRAPH_EDGE_BLOCK) void k_graph_edges(GraphDev G, ui
   }
 }
 
-// k_graph_relax: one wave per read.  The nodes in sorted order; node i's edges
-// (the stream, 64 at a time, the next chunk in flight) update their own node j
-// each (distinct j per lane, as the reference's updates for one i are
-// independent), then are united in j order: the pre-scan roots are found in
-// parallel (path halving; a root never changes by compression, and the roots are
-// what the output needs), a root already met, or i's own, is a no-op, the rest are
-// merged in registers with the reference's rank rule (union_find.cc:13-23).  Node
-// state lives in LDS by record index, sized by the tier (NM records).
+// k_graph_relax: a block of two waves per read, both streaming the read's edges
+// (64 at a time, two chunks in flight) node by node in sorted order.  Wave 0 relaxes
+// the longest paths: node i's edges update their own node j each (distinct j per
+// lane, as the reference's updates for one i are independent).  Wave 1 unites them
+// in j order (union_find.cc:13-23): the pre-scan roots are found in parallel (path
+// halving; a root never changes by compression, and the roots are what the output
+// needs), a root already met, or i's own, is a no-op, the rest are merged in
+// registers with the reference's rank rule.  The unions never read the paths and
+// the paths never read the sets, so the two waves run unsynchronized until the end.
+// Node state lives in LDS by record index; tiers by records a read (NM).
 template <uint32_t NM>
-__global__ __launch_bounds__(64) void k_graph_relax(GraphDev G, uint32_t n_reads) {
+DEV bool graph_relax_tier(const GraphDev& G, uint32_t n) {
+  if (!graph_on_device(G, n)) return false;
+  return (n <= NM && n > NM / 2) || (NM == GRAPH_RELAX_MIN && n <= NM);
+}
+template <uint32_t NM>
+__global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_reads) {
   __shared__ double s_lsi[NM];
   __shared__ int32_t s_lp[NM], s_lun[NM];
   __shared__ int16_t s_lst[NM], s_lpv[NM];
@@ -3193,18 +3226,18 @@ __global__ __launch_bounds__(64) void k_graph_relax(GraphDev G, uint32_t n_reads
   __shared__ uint8_t s_fl[NM], s_rank[NM];
   const uint32_t r = blockIdx.x;
   if (r >= n_reads) return;
-  const uint32_t lane = threadIdx.x;
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint64_t b = G.rec_off[r];
   const uint32_t n = (uint32_t)(G.rec_off[r + 1] - b);
   if (n == 0) return;
   if (!graph_on_device(G, n)) {  // the host traverses this read (marked by the top tier)
     if (NM == GRAPH_NMAX)
-      for (uint32_t i = lane; i < n; i += 64) G.out[b + i] = GraphNode{0, -1, -1, 0, i, GRAPH_HOST};
+      for (uint32_t i = tid; i < n; i += 128) G.out[b + i] = GraphNode{0, -1, -1, 0, i, GRAPH_HOST};
     return;
   }
-  if (!graph_tier<NM>(G, n)) return;
+  if (!graph_relax_tier<NM>(G, n)) return;
   // node_info::reset (overlap_graph.hpp:24-34) of every node
-  for (uint32_t p = lane; p < n; p += 64) {
+  for (uint32_t p = tid; p < n; p += 128) {
     const GDesc d = G.desc[b + p];
     const uint32_t it = d.idx;
     s_idx[p] = (uint16_t)it;
@@ -3214,6 +3247,13 @@ __global__ __launch_bounds__(64) void k_graph_relax(GraphDev G, uint32_t n_reads
     s_par[it] = (uint16_t)it; s_rank[it] = 0;
   }
   __syncthreads();
+  const bool paths = tid < 64;
+  // the read's edge stream: c0 holds [k0, k0 + 64), c1 and c2 the next chunks (in flight)
+  const uint2* E = G.edges + G.eoff[b];
+  const uint32_t ne = (uint32_t)(G.eoff[b + n] - G.eoff[b]);
+  auto ld = [&](uint32_t k) -> uint2 { return k < ne ? E[k] : make_uint2(0u, 0u); };
+  uint2 c0 = ld(lane), c1 = ld(64 + lane), c2 = ld(128 + lane);
+  uint32_t k0 = 0, s = 0;
   auto find = [&](uint32_t q) -> uint32_t {  // union-find root with path halving
     while (s_par[q] != q) {
       const uint32_t g = s_par[s_par[q]];
@@ -3222,76 +3262,74 @@ __global__ __launch_bounds__(64) void k_graph_relax(GraphDev G, uint32_t n_reads
     }
     return q;
   };
-  // the read's edge stream, 64 at a time: cur holds [c0, c0 + 64), nxt the next chunk
-  const uint2* E = G.edges + G.eoff[b];
-  const uint32_t ne = (uint32_t)(G.eoff[b + n] - G.eoff[b]);
-  uint2 cur = lane < ne ? E[lane] : make_uint2(0u, 0u);
-  uint2 nxt = 64 + lane < ne ? E[64 + lane] : make_uint2(0u, 0u);
-  uint32_t c0 = 0, s = 0;
+  uint32_t nx_ec = s_ec[0], nx_it = s_idx[0];
   for (uint32_t p = 0; p < n; ++p) {
-    const uint32_t ec = s_ec[p];
+    const uint32_t ec = nx_ec, it_i = nx_it;
+    if (p + 1 < n) { nx_ec = s_ec[p + 1]; nx_it = s_idx[p + 1]; }
     if (ec == 0) continue;
-    const uint32_t it_i = s_idx[p];
-    const int32_t lp_i = s_lp[it_i], lun_i = s_lun[it_i], lst_i = s_lst[it_i];
-    const double lsi_i = s_lsi[it_i];
     const uint32_t end = s + ec;
+    int32_t lp_i = 0, lun_i = 0, lst_i = 0;
+    double lsi_i = 0;
+    if (paths) { lp_i = s_lp[it_i]; lun_i = s_lun[it_i]; lst_i = s_lst[it_i]; lsi_i = s_lsi[it_i]; }
     while (s < end) {
-      if (s >= c0 + 64) {  // next chunk; the one after it goes in flight
-        cur = nxt;
-        c0 += 64;
-        nxt = c0 + 64 + lane < ne ? E[c0 + 64 + lane] : make_uint2(0u, 0u);
+      if (s >= k0 + 64) {  // next chunk; the one two ahead goes in flight
+        c0 = c1; c1 = c2; k0 += 64;
+        c2 = ld(k0 + 128 + lane);
       }
-      const uint32_t k = c0 + lane;
+      const uint32_t k = k0 + lane;
       const bool edge = (k >= s) & (k < end);
-      const uint32_t it_j = cur.x & 0xFFFFu;
-      if (edge) {  // node_info update (overlap_graph.cc:41-56); this lane owns node j
-        s_fl[it_j] &= (uint8_t)~GRAPH_START;
-        const int32_t nlpath = (int32_t)((uint32_t)lp_i + cur.y);
-        const int32_t lp_j = s_lp[it_j];
-        const bool upd = nlpath > lp_j || (nlpath == lp_j && (s_lst[it_j] == -1 || lsi_i > s_lsi[it_j]));
-        if (upd) {
-          s_lp[it_j] = nlpath;
-          s_lst[it_j] = (int16_t)(lst_i == -1 ? (int32_t)it_i : lst_i);
-          s_lsi[it_j] = lsi_i;
-          s_lpv[it_j] = (int16_t)it_i;
-          s_lun[it_j] = lun_i + (int32_t)(cur.x >> 16);
+      const uint32_t it_j = c0.x & 0xFFFFu;
+      if (paths) {
+        if (edge) {  // node_info update (overlap_graph.cc:41-56); this lane owns node j
+          s_fl[it_j] &= (uint8_t)~GRAPH_START;
+          const int32_t nlpath = (int32_t)((uint32_t)lp_i + c0.y);
+          const int32_t lp_j = s_lp[it_j];
+          const bool upd = nlpath > lp_j || (nlpath == lp_j && (s_lst[it_j] == -1 || lsi_i > s_lsi[it_j]));
+          if (upd) {
+            s_lp[it_j] = nlpath;
+            s_lst[it_j] = (int16_t)(lst_i == -1 ? (int32_t)it_i : lst_i);
+            s_lsi[it_j] = lsi_i;
+            s_lpv[it_j] = (int16_t)it_i;
+            s_lun[it_j] = lun_i + (int32_t)(c0.x >> 16);
+          }
         }
-      }
-      // union_sets(it_i, it_j) for this chunk's edges in j order
-      const uint64_t em = __ballot(edge);
-      const uint32_t r1 = find(it_i);
-      const uint32_t R = edge ? find(it_j) : r1;
-      const uint32_t rk = s_rank[R];
-      // the edge lanes holding the same root: a ballot per bit of R (node indices < 2^12)
-      uint64_t same = em;
+      } else {
+        // union_sets(it_i, it_j) for this chunk's edges in j order
+        const uint64_t em = __ballot(edge);
+        const uint32_t r1 = find(it_i);
+        const uint32_t R = edge ? find(it_j) : r1;
+        const uint32_t rk = s_rank[R];
+        // the edge lanes holding the same root: a ballot per bit of R (node indices < 2^12)
+        uint64_t same = em;
 #pragma unroll
-      for (uint32_t bit = 0; bit < 12; ++bit) {
-        const uint64_t bb = __ballot((R >> bit) & 1u);
-        same &= ((R >> bit) & 1u) ? bb : ~bb;
-      }
-      const bool first = edge & (R != r1) & ((same & ((1ull << lane) - 1)) == 0);
-      uint32_t cr = r1, crank = s_rank[r1];
-      for (uint64_t fm = __ballot(first); fm; fm &= fm - 1) {
-        const uint32_t l = (uint32_t)__ffsll((long long)fm) - 1;
-        const uint32_t vv = (uint32_t)__builtin_amdgcn_readlane((int)R, (int)l);
-        const uint32_t vr = (uint32_t)__builtin_amdgcn_readlane((int)rk, (int)l);
-        if (crank > vr) {
-          if (lane == 0) s_par[vv] = (uint16_t)cr;
-        } else if (crank < vr) {
-          if (lane == 0) s_par[cr] = (uint16_t)vv;
-          cr = vv; crank = vr;
-        } else {
-          ++crank;
-          if (lane == 0) { s_par[vv] = (uint16_t)cr; s_rank[cr] = (uint8_t)crank; }
+        for (uint32_t bit = 0; bit < 12; ++bit) {
+          const uint64_t bb = __ballot((R >> bit) & 1u);
+          same &= ((R >> bit) & 1u) ? bb : ~bb;
+        }
+        const bool first = edge & (R != r1) & ((same & ((1ull << lane) - 1)) == 0);
+        uint32_t cr = r1, crank = s_rank[r1];
+        for (uint64_t fm = __ballot(first); fm; fm &= fm - 1) {
+          const uint32_t l = (uint32_t)__ffsll((long long)fm) - 1;
+          const uint32_t vv = (uint32_t)__builtin_amdgcn_readlane((int)R, (int)l);
+          const uint32_t vr = (uint32_t)__builtin_amdgcn_readlane((int)rk, (int)l);
+          if (crank > vr) {
+            if (lane == 0) s_par[vv] = (uint16_t)cr;
+          } else if (crank < vr) {
+            if (lane == 0) s_par[cr] = (uint16_t)vv;
+            cr = vv; crank = vr;
+          } else {
+            ++crank;
+            if (lane == 0) { s_par[vv] = (uint16_t)cr; s_rank[cr] = (uint8_t)crank; }
+          }
         }
       }
-      s = end < c0 + 64 ? end : c0 + 64;
-      __syncthreads();  // (one wave: this chunk's LDS updates before the next reads)
+      s = end < k0 + 64 ? end : k0 + 64;
+      lds_fence();  // this wave's updates of the chunk before the next reads (the waves run apart)
     }
-    if (lane == 0) s_fl[it_i] &= (uint8_t)~GRAPH_END;
-    __syncthreads();
+    if (paths && lane == 0) s_fl[it_i] &= (uint8_t)~GRAPH_END;
   }
-  for (uint32_t i = lane; i < n; i += 64) {
+  __syncthreads();
+  for (uint32_t i = tid; i < n; i += 128) {
     uint32_t q = i;
     while (s_par[q] != q) q = s_par[q];
     G.out[b + i] = GraphNode{s_lp[i], s_lst[i], s_lpv[i], s_lun[i], q, s_fl[i]};
@@ -3882,8 +3920,8 @@ hipError_t launch_graph(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hi
   hipLaunchKernelGGL(k_graph_sort<GRAPH_NM_SMALL>, dim3(n_reads), dim3(GRAPH_SORT_BLOCK), 0, st, G, n_reads);
   if ((e = hipStreamWaitEvent(st, join, 0)) != hipSuccess) return e;
   // every node's edges: counted, offsets, written
-  const uint32_t eg = (uint32_t)std::min<uint64_t>((n_recs + GRAPH_EDGE_BLOCK / 64 - 1) / (GRAPH_EDGE_BLOCK / 64), 1u << 20);
-  hipLaunchKernelGGL(k_graph_edges<0>, dim3(eg), dim3(GRAPH_EDGE_BLOCK), 0, st, G, n_recs);
+  const uint32_t eg = (uint32_t)((n_recs + GE_NODES - 1) / GE_NODES);
+  hipLaunchKernelGGL(k_graph_edges<0>, dim3(eg), dim3(GE_BLOCK), 0, st, G, n_recs);
   launch_excl_scan(G.ecnt, nullptr, n_recs, G.eoff, scan_scratch, st);
   if ((e = hipMemcpyAsync(n_edges, G.eoff + n_recs, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
   return hipStreamSynchronize(st);
@@ -3891,15 +3929,17 @@ hipError_t launch_graph(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hi
 hipError_t launch_graph_relax(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hipStream_t st, hipStream_t side,
                               hipEvent_t fork, hipEvent_t join) {
   if (!n_recs || !n_reads) return hipSuccess;
-  const uint32_t eg = (uint32_t)std::min<uint64_t>((n_recs + GRAPH_EDGE_BLOCK / 64 - 1) / (GRAPH_EDGE_BLOCK / 64), 1u << 20);
-  hipLaunchKernelGGL(k_graph_edges<1>, dim3(eg), dim3(GRAPH_EDGE_BLOCK), 0, st, G, n_recs);
-  // the long reads' relaxation on the side stream: its waves are the longest
+  const uint32_t eg = (uint32_t)((n_recs + GE_NODES - 1) / GE_NODES);
+  hipLaunchKernelGGL(k_graph_edges<1>, dim3(eg), dim3(GE_BLOCK), 0, st, G, n_recs);
+  // the long reads' relaxation on the side stream: its blocks are the longest
   hipError_t e = hipEventRecord(fork, st);
   if (e == hipSuccess) e = hipStreamWaitEvent(side, fork, 0);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_graph_relax<GRAPH_NMAX>, dim3(n_reads), dim3(64), 0, side, G, n_reads);
+  hipLaunchKernelGGL(k_graph_relax<GRAPH_NMAX>, dim3(n_reads), dim3(128), 0, side, G, n_reads);
+  hipLaunchKernelGGL(k_graph_relax<GRAPH_NMAX / 2>, dim3(n_reads), dim3(128), 0, side, G, n_reads);
   if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_graph_relax<GRAPH_NM_SMALL>, dim3(n_reads), dim3(64), 0, st, G, n_reads);
+  hipLaunchKernelGGL(k_graph_relax<GRAPH_NM_SMALL>, dim3(n_reads), dim3(128), 0, st, G, n_reads);
+  hipLaunchKernelGGL(k_graph_relax<GRAPH_RELAX_MIN>, dim3(n_reads), dim3(128), 0, st, G, n_reads);
   return hipStreamWaitEvent(st, join, 0);
 }
 
