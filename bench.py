@@ -264,6 +264,7 @@ def main():
     # the same for random 512-B runs of 8-B words: the shape of k_group's occurrence-list reads
     b_run = pbgpu.measure_gather(local, 64 << 30, unit_bytes=512) if not args.no_brand else None
 
+    b_filt = b_table = None  # random 64-B gathers over buffers the size of the filter and the table
     k = 21 if args.workload == "C3" else 17
     n_pb = args.reads or PRESETS[args.workload]["n_pb"]
     threads = _cpu_share()
@@ -277,6 +278,9 @@ def main():
     index = pbgpu.Index.from_fasta([sr_fa], k, psa_min=13, device=local)
     t_index = time.time() - t0
     info = index.info()
+    if not args.no_brand:
+        b_filt = pbgpu.measure_gather(local, max(1 << 20, info["filter_bytes"])) if info["filter_bytes"] else None
+        b_table = pbgpu.measure_gather(local, max(1 << 20, info["table_buckets"] * 64))
     akw = dict(k=k, forward=True, unitigs_k=31, unitig_lengths=ds.unitig_lengths, bases_matching=15.0,
                max_count=5000, stretch_cap=10000.0)
     blob, off = ds.pb_blob()
@@ -435,14 +439,27 @@ def main():
                   for kk in kb if kn.get(kk)}
     # k_seed at its access granularity: every presence-filter check and bucket probe is a
     # random access that moves a 64-B sector (the 8-B filter word alone is the algorithmic
-    # minimum above); against B_rand this is the kernel's random-access roofline
+    # minimum above).  The two kinds hit different roofs: the filter (16 MB on C2) lives in
+    # the 256 MB Infinity Cache, the table (GBs) in HBM, so each is priced at the random-64-B
+    # gather rate measured over a buffer of its own size (b_filter_gbs, b_table_gbs), and the
+    # streams (read bases, kept records) at the HBM peak: the mixed roof's time per launch
+    # against the measured one is the kernel's roofline fraction
     if kn.get("k_seed"):
-        sec = (st["n_bases"] + (st["n_filter"] + st["n_probes"]) * 64 + st["n_kept"] * 16) / kn["k_seed"]
-        sgbs = sec / (kms["k_seed"] / kn["k_seed"] * 1e-3) / 1e9
-        per_kernel["k_seed"]["sector_view"] = {
-            "bytes_per_launch": sec, "achieved_gbs": round(sgbs, 1), "frac": round(sgbs / HBM_PEAK_GBS, 4),
-            "frac_of_b_rand": round(sgbs / b_rand, 4) if b_rand else None,
-            "random_accesses_per_launch": (st["n_filter"] + st["n_probes"]) / kn["k_seed"]}
+        nl = kn["k_seed"]
+        sec = (st["n_bases"] + (st["n_filter"] + st["n_probes"]) * 64 + st["n_kept"] * 16) / nl
+        k_ms = kms["k_seed"] / nl
+        sgbs = sec / (k_ms * 1e-3) / 1e9
+        sv = {"bytes_per_launch": sec, "achieved_gbs": round(sgbs, 1), "frac": round(sgbs / HBM_PEAK_GBS, 4),
+              "frac_of_b_rand": round(sgbs / b_rand, 4) if b_rand else None,
+              "random_accesses_per_launch": (st["n_filter"] + st["n_probes"]) / nl}
+        if b_filt and b_table:
+            roof_ms = ((st["n_filter"] / nl) * 64 / (b_filt * 1e9) + (st["n_probes"] / nl) * 64 / (b_table * 1e9) +
+                       ((st["n_bases"] + st["n_kept"] * 16) / nl) / (HBM_PEAK_GBS * 1e9)) * 1e3
+            sv["mixed_roof"] = {"b_filter_gbs": round(b_filt, 1), "filter_bytes": info["filter_bytes"],
+                                "b_table_gbs": round(b_table, 1), "table_bytes": info["table_buckets"] * 64,
+                                "roof_ms": round(roof_ms, 3), "launch_ms": round(k_ms, 3),
+                                "frac": round(roof_ms / k_ms, 4)}
+        per_kernel["k_seed"]["sector_view"] = sv
     # HBM traffic per launch of each kernel from the committed rocprofv3 summary of the
     # same bench (tools/prof_r03.sh, separate FETCH_SIZE / WRITE_SIZE passes over the
     # production device leg): FETCH_SIZE corrected for the kernel's read shape (random

@@ -112,6 +112,7 @@ typedef struct {
   uint64_t device_bytes;    /* resident index footprint */
   double   build_seconds;
   uint64_t sr_begin, sr_end; /* super-reads held on the device (all of them unless sharded) */
+  uint64_t filter_bytes;    /* k_seed's presence filter (0 = none) */
 } pbgpu_index_info;
 pbgpu_status pbgpu_index_get_info(const pbgpu_index* ix, pbgpu_index_info* info);
 /* frag_info.hpp:18-35: fwd name = header line, bwd name = reversed unitigs */

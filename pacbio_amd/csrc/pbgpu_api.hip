@@ -1083,6 +1083,7 @@ pbgpu_status pbgpu_index_get_info(const pbgpu_index* ix, pbgpu_index_info* info)
   info->n_sr = ix->n_sr; info->text_len = ix->n; info->n_kmers = ix->n_kmers; info->n_occurrences = ix->n_occ;
   info->sr_begin = ix->sr_begin; info->sr_end = ix->sr_end;
   info->table_buckets = ix->buckets; info->device_bytes = ix->device_bytes(); info->build_seconds = ix->build_seconds;
+  info->filter_bytes = ix->filt.bytes();
   return PBGPU_OK;
 }
 const char* pbgpu_index_sr_name(const pbgpu_index* ix, uint32_t sr, int bwd) {

@@ -2061,22 +2061,21 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
 #else
   LS.run(O.pts, nl, ps, [&](const int2 p) {
 #endif
-    if (L.n == 0) {
-      first = p;
-    } else {
-      const uint32_t pb_diff = (uint32_t)(p.x - prev.x);
-      R.pb_cons += pb_diff == 1u;
-      R.pb_cover += k < pb_diff ? k : pb_diff;
-      const uint32_t sr_diff = (uint32_t)(p.y - prev.y);
-      R.sr_cons += sr_diff == 1u;
-      R.sr_cover += k < sr_diff ? k : sr_diff;
-    }
+    // consecutive / covered counts against the previous point, branch-free (the first
+    // point adds nothing: its diffs are masked)
+    const bool later = L.n != 0;
+    first = later ? first : p;
+    const uint32_t pb_diff = (uint32_t)(p.x - prev.x), sr_diff = (uint32_t)(p.y - prev.y);
+    R.pb_cons += (later & (pb_diff == 1u)) ? 1u : 0u;
+    R.pb_cover += later ? (k < pb_diff ? k : pb_diff) : 0u;
+    R.sr_cons += (later & (sr_diff == 1u)) ? 1u : 0u;
+    R.sr_cover += later ? (k < sr_diff ? k : sr_diff) : 0u;
 #ifndef PBGPU_EXP_NO_LSQ
     L.add((double)p.y, (double)p.x);
 #else
     ++L.n; L.EX += p.y;
 #endif
-#ifndef PBGPU_EXP_NO_INFO
+#if !defined(PBGPU_EXP_NO_INFO) && !defined(PBGPU_EXP_INFO_PASS2)
     if (info_lds) KI.add(info_pos(p.y));
 #endif
     prev = p;
@@ -2093,6 +2092,10 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
   double err = 0;
 #ifdef PBGPU_EXP_NO_PASS2
   LS.run(O.pts, 0, ps, [&](const int2 p) {
+#elif defined(PBGPU_EXP_INFO_PASS2)
+  // (experiment: kmers_info in the error pass, not beside the fit)
+  LS.run(O.pts, (L.n > 1 || info_lds) ? nl : 0, ps, [&](const int2 p) {
+    if (info_lds) KI.add(info_pos(p.y));
 #else
   LS.run(O.pts, L.n > 1 ? nl : 0, ps, [&](const int2 p) {
 #endif

@@ -58,7 +58,8 @@ class IndexParams(C.Structure):
 class IndexInfo(C.Structure):
     _fields_ = [("n_sr", C.c_uint64), ("text_len", C.c_uint64), ("n_kmers", C.c_uint64),
                 ("n_occurrences", C.c_uint64), ("table_buckets", C.c_uint64), ("device_bytes", C.c_uint64),
-                ("build_seconds", C.c_double), ("sr_begin", C.c_uint64), ("sr_end", C.c_uint64)]
+                ("build_seconds", C.c_double), ("sr_begin", C.c_uint64), ("sr_end", C.c_uint64),
+                ("filter_bytes", C.c_uint64)]
 
 
 class AlignParams(C.Structure):
@@ -176,7 +177,8 @@ def lib():
         L.pbgpu_device_synchronize.argtypes = [C.c_int]
         L.pbgpu_measure_gather.argtypes = [C.c_int, C.c_uint64, C.POINTER(C.c_double)]
         L.pbgpu_measure_gather_shape.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.POINTER(C.c_double)]
-        L.pbgpu_check_reciprocal.argtypes = [C.c_int, C.c_uint32, C.POINTER(C.c_uint64)]
+        if hasattr(L, "pbgpu_check_reciprocal"):  # (absent from older experiment builds)
+            L.pbgpu_check_reciprocal.argtypes = [C.c_int, C.c_uint32, C.POINTER(C.c_uint64)]
         L.pbgpu_index_build_fasta.argtypes = [C.POINTER(C.c_char_p), C.c_size_t, C.POINTER(IndexParams), C.POINTER(vp)]
         L.pbgpu_index_build.argtypes = [C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.POINTER(C.c_uint64),
                                         C.c_size_t, C.POINTER(IndexParams), C.POINTER(vp)]
