@@ -9,6 +9,7 @@ V = {
     "gonly": G,
     "p0": G + ["-DPBGPU_EXP_SKIP_PASS1"],
     "p0notab": G + ["-DPBGPU_EXP_SKIP_PASS1", "-DPBGPU_EXP_P0_NOTABLE"],
+    "nostore": G + ["-DPBGPU_EXP_GROUP_NOSTORE"],
 }
 for n in (sys.argv[1:] or V):
     print(build_pbgpu_variant(n, V[n]))
