@@ -1639,7 +1639,7 @@ static void graph_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   const uint64_t nrec = al->last_records;
   GraphDev G{};
   G.recs = al->recs_sorted.p; G.rec_off = al->rec_off.p; G.roff = rd->off.p;
-  G.noff = al->g_noff.p; G.units = al->g_units.p; G.ul = al->g_ul.p; G.n_ul = al->g_n_ul;
+  G.noff = al->g_names->noff.p; G.units = al->g_names->units.p; G.ul = al->g_names->ul.p; G.n_ul = al->g_names->n_ul;
   G.info_m = al->info_m.p; G.info_b = al->info_b.p;
   G.play = al->g_play; G.nb_errors = al->g_errors; G.k = al->g_k; G.bases = al->g_bases;
   // PBGPU_GRAPH_NMAX (tests): a lower cap on the records of a read traversed on the device
@@ -2149,6 +2149,20 @@ pbgpu_status pbgpu_coords_merge(const pbgpu_coords_batch* const* parts, uint64_t
   API_CATCH
 }
 
+// 64-bit hash of a byte range, a word at a time (the graph arrays' identity)
+static uint64_t hash_words(const void* data, uint64_t bytes, uint64_t h) {
+  const uint8_t* b = (const uint8_t*)data;
+  uint64_t i = 0;
+  for (; i + 8 <= bytes; i += 8) {
+    uint64_t w;
+    memcpy(&w, b + i, 8);
+    h = (h ^ w) * 0x100000001B3ull;
+    h ^= h >> 29;
+  }
+  for (; i < bytes; ++i) h = (h ^ b[i]) * 0x100000001B3ull;
+  return h ^ bytes;
+}
+
 pbgpu_status pbgpu_aligner_set_graph(pbgpu_aligner* al, const pbgpu_graph_params* p) {
   if (!al) return fail(PBGPU_ERR_INVALID, "null argument");
   if (!p) { al->graph = false; return PBGPU_OK; }
@@ -2165,11 +2179,24 @@ pbgpu_status pbgpu_aligner_set_graph(pbgpu_aligner* al, const pbgpu_graph_params
   API_TRY
   HIPCHK(hipSetDevice(al->ix->device));
   const uint64_t nu = p->name_offsets[p->n_sr];
-  al->g_noff.ensure(p->n_sr + 1); al->g_units.ensure(nu + 1); al->g_ul.ensure(p->n_unitigs + 1);
-  HIPCHK(hipMemcpy(al->g_noff.p, p->name_offsets, (p->n_sr + 1) * 8, hipMemcpyHostToDevice));
-  if (nu) HIPCHK(hipMemcpy(al->g_units.p, p->name_units, nu * 4, hipMemcpyHostToDevice));
-  if (p->n_unitigs) HIPCHK(hipMemcpy(al->g_ul.p, p->unitig_lengths, p->n_unitigs * 4, hipMemcpyHostToDevice));
-  al->g_n_ul = p->n_unitigs;
+  {
+    // one device copy per index: an aligner given the same arrays reuses it
+    const uint64_t h = hash_words(p->name_units, nu * 4, hash_words(p->unitig_lengths, p->n_unitigs * 4,
+                                  hash_words(p->name_offsets, (p->n_sr + 1) * 8, 0x9E3779B97F4A7C15ull)));
+    pbgpu_index* ix = const_cast<pbgpu_index*>(al->ix);  // the shared copy is guarded by names_mu
+    std::lock_guard<std::mutex> lk(ix->names_mu);
+    std::shared_ptr<GraphNames> g = ix->graph_names;
+    if (!g || g->hash != h || g->n_sr != p->n_sr || g->n_units != nu || g->n_ul != p->n_unitigs) {
+      g = std::make_shared<GraphNames>();
+      g->hash = h; g->n_sr = p->n_sr; g->n_units = nu; g->n_ul = p->n_unitigs;
+      g->noff.ensure_fixed(p->n_sr + 1); g->units.ensure_fixed(nu + 1); g->ul.ensure_fixed(p->n_unitigs + 1);
+      HIPCHK(hipMemcpy(g->noff.p, p->name_offsets, (p->n_sr + 1) * 8, hipMemcpyHostToDevice));
+      if (nu) HIPCHK(hipMemcpy(g->units.p, p->name_units, nu * 4, hipMemcpyHostToDevice));
+      if (p->n_unitigs) HIPCHK(hipMemcpy(g->ul.p, p->unitig_lengths, p->n_unitigs * 4, hipMemcpyHostToDevice));
+      ix->graph_names = g;
+    }
+    al->g_names = g;
+  }
   al->g_play = p->overlap_play; al->g_errors = p->nb_errors; al->g_k = p->k_len; al->g_bases = p->maximize_bases != 0;
   al->g_mega = p->mega_reads != 0;
   al->g_tiling = p->tiling; al->g_trim = p->trim != 0;

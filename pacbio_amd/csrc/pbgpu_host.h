@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 #include <exception>
+#include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -198,6 +199,16 @@ inline void* temp_storage(dbuf<uint8_t>& t, size_t bytes) {
 }
 
 
+// create_mega_reads' super-read names as unitig lists and the unitig lengths on one
+// device (pbgpu_aligner_set_graph), shared by every aligner of the index that is
+// given the same arrays (content hash): one copy per device, not one per stream
+struct GraphNames {
+  uint64_t hash = 0, n_sr = 0, n_units = 0, n_ul = 0;
+  dbuf<uint64_t> noff;
+  dbuf<uint32_t> units;
+  dbuf<int32_t> ul;
+};
+
 // ------------------------------------------------------------------ index
 struct pbgpu_index {
   int device = 0;
@@ -229,6 +240,8 @@ struct pbgpu_index {
   bool names_ready = false;
   dbuf<char> d_name_fwd, d_name_bwd;
   dbuf<uint64_t> d_name_fwd_off, d_name_bwd_off;
+  // the graph names of this index's aligners (GraphNames), guarded by names_mu
+  std::shared_ptr<GraphNames> graph_names;
   IndexView view() const {
     IndexView v;
     v.text = text.p; v.n = n; v.sr_start = d_sr_start.p; v.n_sr = (uint32_t)(sr_end - sr_begin); v.k = k;
@@ -330,11 +343,10 @@ struct pbgpu_aligner {
   double g_play = 0, g_errors = 0;
   uint32_t g_k = 0;
   int g_bases = 0;
-  uint64_t g_n_ul = 0;
-  dbuf<uint64_t> g_noff, g_poff;
-  dbuf<uint32_t> g_units, g_pre, g_sizes;
+  std::shared_ptr<GraphNames> g_names;  // shared with the index's other aligners
+  dbuf<uint64_t> g_poff;
+  dbuf<uint32_t> g_pre, g_sizes;
   dbuf<GDesc> g_desc;
-  dbuf<int32_t> g_ul;
   dbuf<double2> g_imp;
   dbuf<GraphNode> g_out;
   dbuf<uint32_t> g_ecnt;
