@@ -1820,7 +1820,6 @@ struct KmersInfo {
     }
     pm = pb = om = ob = nm = nb = 0;
   }
-#ifdef PBGPU_EXP_KI2
   // The same steps with no return: a lane whose name failed (!ok) keeps computing on
   // its stale state (its arrays are discarded) but never advances, so every memory
   // update stays inside its own 2 nsz - 1 elements; the advance is entered only when
@@ -1873,56 +1872,6 @@ struct KmersInfo {
     }
     prev_pos = sr_pos;
   }
-#else
-  DEV void add(int32_t sr_pos) {
-    if (!ok) return;
-    const int32_t new_bases = k < sr_pos - prev_pos ? k : sr_pos - prev_pos;
-    while (sr_pos + k > cend + 1) {
-      const bool part = cend >= sr_pos;  // the k-mer starts inside unitig c
-      if (part & (cunitig >= nsz - 1)) { ok = false; return; }
-      const int32_t mx = sr_pos > prev_pos + k ? sr_pos : prev_pos + k;
-      const int32_t nbb = part ? cend - mx + 1 : 0;
-      pb += nbb; ob += nbb;
-      // unitig c is done: write 2c and 2c+1, 2c+2 becomes current
-      acc(mers, 2 * cunitig, pm); acc(bases, 2 * cunitig, pb);
-      if (cunitig + 1 < nsz) { acc(mers, 2 * cunitig + 1, om); acc(bases, 2 * cunitig + 1, ob); }
-      pm = nm; pb = nb; om = ob = nm = nb = 0;
-      const int32_t l = nlen;
-      ++cunitig;
-      if (l == UL_INVALID) { ok = false; return; }
-      cend = (int32_t)((uint32_t)cend + (uint32_t)l - (uint32_t)uk + 1u);
-      nlen = ulen(cunitig + 1);
-    }
-    ++pm;
-    pb += new_bases;
-    // First overlapping unitig (the reference's loop at i = cunitig), branch-free: the
-    // lanes of a wave sit at unrelated places of their super-reads, so a branch here
-    // would run for the whole wave at nearly every point.
-    const bool in_ov = (cunitig < nsz - 1) & ((uint32_t)sr_pos + (uint32_t)k > (uint32_t)cend - (uint32_t)uk + 1u);
-    const int32_t full_mer = (in_ov & (sr_pos + uk > cend + 1)) ? 1 : 0;
-    const int32_t tt0 = sr_pos + k - cend + uk - 2;
-    const int32_t nbb0 = in_ov ? (new_bases < tt0 ? new_bases : tt0) : 0;
-    om += full_mer; nm += full_mer;
-    ob += nbb0; nb += nbb0;
-    // rare: an unusable next length, or the k-mer also reaches the unitig after it
-    int32_t cendi = (int32_t)((uint32_t)cend + (uint32_t)nlen - (uint32_t)uk + 1u);
-    if (in_ov & ((nlen == UL_INVALID) |
-                 ((cunitig + 1 < nsz - 1) & ((uint32_t)sr_pos + (uint32_t)k > (uint32_t)cendi - (uint32_t)uk + 1u)))) {
-      if (nlen == UL_INVALID) { ok = false; return; }
-      for (uint32_t i = cunitig + 1; (i < nsz - 1) && ((uint32_t)sr_pos + (uint32_t)k > (uint32_t)cendi - (uint32_t)uk + 1u); ++i) {
-        const int32_t fm = sr_pos + uk > cendi + 1;
-        acc(mers, 2 * i + 1, fm); acc(mers, 2 * i + 2, fm);
-        const int32_t tt = sr_pos + k - cendi + uk - 2;
-        const int32_t nbb = new_bases < tt ? new_bases : tt;
-        acc(bases, 2 * i + 1, nbb); acc(bases, 2 * i + 2, nbb);
-        const int32_t l = ulen(i + 1);
-        if (l != UL_INVALID) cendi = (int32_t)((uint32_t)cendi + (uint32_t)l - (uint32_t)uk + 1u);
-        else { ok = false; return; }
-      }
-    }
-    prev_pos = sr_pos;
-  }
-#endif
 };
 
 // a / b correctly rounded from y = RN(1 / b): one correction makes q faithful,

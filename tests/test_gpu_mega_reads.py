@@ -271,3 +271,25 @@ def test_no_device_allocation_after_first_batch(tmp_path):
     _run([*base, "--batch-bases", "1000000000", "-o", b], timeout=300)
     ta = open(a).read()
     assert ta.count(">") > 2000 and ta == open(b).read()
+
+
+@pytest.mark.parametrize("tiling", ["greedy", "weighted", "maximal"])
+def test_read_with_many_components(tmp_path, tiling):
+    """One read aligned by 320 super-reads of one unitig each (no name overlaps, so 320
+    single-node components): more than k_mega's 256 in-LDS components, so the tiling keeps
+    its intervals in HBM.  Device graph == host graph, and > 256 mega-reads."""
+    import random
+    rng = random.Random(5)
+    n_sr, seg = 320, 400
+    segs = ["".join(rng.choice("ACGT") for _ in range(seg)) for _ in range(n_sr)]
+    (tmp_path / "sr.fa").write_text("".join(f">{i}F\n{s}\n" for i, s in enumerate(segs)))
+    (tmp_path / "pb.fa").write_text(">read0\n" + "".join(segs) + "\n")
+    (tmp_path / "ul.txt").write_text("".join(f"{seg}\n" for _ in range(n_sr)))
+    base = ["-s", "1M", "-m", "17", "-k", "31", "-l", str(tmp_path / "ul.txt"), "-T", tiling,
+            "-r", str(tmp_path / "sr.fa"), "-p", str(tmp_path / "pb.fa")]
+    a, b = str(tmp_path / "dev"), str(tmp_path / "host")
+    _run([*base, "-o", a])
+    _run([*base, "--host-graph", "-o", b])
+    ta = open(a).read()
+    assert ta == open(b).read()
+    assert ta.count("\n") > 257, ta[:500]  # a header line, then one line per mega-read
