@@ -256,8 +256,9 @@ typedef struct {
   /* overlap graph (pbgpu_aligner_set_graph): device time, records traversed on the device */
   double   ms_graph;
   uint64_t graph_records;
-  /* overlap graph edges found (pairs passing every test of overlap_graph.cc:20-39) */
-  uint64_t graph_edges;
+  /* overlap graph candidate pairs (not skipped, before the break, names of >= 2
+   * unitigs: the traversal's edge capacity, an upper bound on its edges) */
+  uint64_t graph_candidates;
 } pbgpu_stats;
 pbgpu_status pbgpu_aligner_get_stats(const pbgpu_aligner* al, pbgpu_stats* s);
 pbgpu_status pbgpu_aligner_reset_stats(pbgpu_aligner* al);

@@ -1667,7 +1667,7 @@ static void graph_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   G.edges = al->g_edges.p;
   HIPCHK(launch_graph_relax(G, n, nrec, st, al->g_side, al->g_fork, al->g_join));
   HIPCHK(hipGetLastError());
-  al->acc.graph_edges += n_edges;
+  al->acc.graph_candidates += n_edges;
   al->g_mtotal = al->g_munits_used = 0;
   al->g_hosts = 0;
   if (!al->g_mega) return;

@@ -3081,9 +3081,12 @@ __global__ __launch_bounds__(GRAPH_SORT_BLOCK) void k_graph_sort(GraphDev G, uin
 // (implied span, error, name size, first GRAPH_U unitigs, read bounds) are staged
 // in LDS; a wave per node i, lanes j = i + 1 + lane, ... 64 at a time until the
 // reference's break (positions past the staged ones are read from HBM).  PASS 0
-// counts each node's edges (ecnt); an exclusive scan gives every node's offset,
-// so a read's edges are one contiguous stream in (i, j) order; PASS 1 writes
-// them as {j's record index | (unitigs added) << 16, path increment}.
+// counts each node's candidates -- the pairs that are neither skipped nor past the
+// break, with names of two unitigs or more: an upper bound on its edges that needs
+// no name matching -- and an exclusive scan gives every node a region; PASS 1 runs
+// the whole test and writes the node's edges at the start of its region, in j
+// order, as {j's record index | (unitigs added) << 16, path increment}, and the
+// exact count over the capacity (ecnt).
 constexpr uint32_t GRAPH_U = 8;  // names of at most this many unitigs are matched in registers
 constexpr uint32_t GRAPH_NMAX_K = GRAPH_NMAX;  // reads of more records go to the host (LDS state)
 static_assert(GRAPH_NMAX_K <= 4096, "k_graph_relax matches roots by 12 bits and keeps 16-bit indices");
@@ -3151,9 +3154,15 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
         const uint64_t bm = __ballot(brk);
         const uint32_t fb = bm ? (uint32_t)__ffsll((long long)bm) - 1 : 64u;
         const uint32_t sb = mj >> 16;
+        const bool cand = act & !skip & (lane < fb) & (sa >= 2) & (sb >= 2);
+        if (!PASS) {  // the count pass: every pair that may be an edge (an upper bound)
+          cnt += (uint32_t)__builtin_popcountll(__ballot(cand));
+          if (bm) break;
+          continue;
+        }
         bool edge = false;
         int32_t nb = 0, common = 0;
-        if (act & !skip & (lane < fb) & (sa >= 2) & (sb >= 2)) {
+        if (cand) {
           bool same;
           if ((sa <= GRAPH_U) & (sb <= GRAPH_U)) {
             // super_read_name::overlap (super_read_name.cc:49-72) in registers: the smallest
@@ -3195,7 +3204,7 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
           }
         }
         const uint64_t em = __ballot(edge);
-        if (PASS && edge) {
+        if (edge) {
           const uint32_t at = cnt + (uint32_t)__builtin_popcountll(em & ((1ull << lane) - 1));
           // the edge's path increment (nb_mers or sr_cover of j minus the common k-mers) and
           // the unitigs it adds (overlap_graph.cc:47-53)
@@ -3205,7 +3214,7 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
         if (bm) break;  // the reference's break
       }
     }
-    if (!PASS && lane == 0) G.ecnt[q] = cnt;
+    if (lane == 0) G.ecnt[q] = cnt;  // PASS 0: the node's capacity; PASS 1: its edges
   }
 }
 
@@ -3229,6 +3238,7 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
   __shared__ double s_lsi[NM];
   __shared__ int32_t s_lp[NM], s_lun[NM];
   __shared__ int16_t s_lst[NM], s_lpv[NM];
+  __shared__ uint32_t s_es[NM];  // node's edges: start in the read's region
   __shared__ uint16_t s_idx[NM], s_ec[NM], s_par[NM];
   __shared__ uint8_t s_fl[NM], s_rank[NM];
   const uint32_t r = blockIdx.x;
@@ -3249,6 +3259,7 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
     const uint32_t it = d.idx;
     s_idx[p] = (uint16_t)it;
     s_ec[p] = (uint16_t)G.ecnt[b + p];
+    s_es[p] = (uint32_t)(G.eoff[b + p] - G.eoff[b]);
     s_lp[it] = (int32_t)d.lp_add; s_lun[it] = (int32_t)d.nsz; s_lst[it] = -1; s_lpv[it] = -1;
     s_lsi[it] = d.imp_s; s_fl[it] = (uint8_t)(GRAPH_START | GRAPH_END);
     s_par[it] = (uint16_t)it; s_rank[it] = 0;
@@ -3260,7 +3271,7 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
   const uint32_t ne = (uint32_t)(G.eoff[b + n] - G.eoff[b]);
   auto ld = [&](uint32_t k) -> uint2 { return k < ne ? E[k] : make_uint2(0u, 0u); };
   uint2 c0 = ld(lane), c1 = ld(64 + lane), c2 = ld(128 + lane);
-  uint32_t k0 = 0, s = 0;
+  uint32_t k0 = 0;
   auto find = [&](uint32_t q) -> uint32_t {  // union-find root with path halving
     while (s_par[q] != q) {
       const uint32_t g = s_par[s_par[q]];
@@ -3269,17 +3280,18 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
     }
     return q;
   };
-  uint32_t nx_ec = s_ec[0], nx_it = s_idx[0];
+  uint32_t nx_ec = s_ec[0], nx_it = s_idx[0], nx_es = s_es[0];
   for (uint32_t p = 0; p < n; ++p) {
     const uint32_t ec = nx_ec, it_i = nx_it;
-    if (p + 1 < n) { nx_ec = s_ec[p + 1]; nx_it = s_idx[p + 1]; }
+    uint32_t s = nx_es;
+    if (p + 1 < n) { nx_ec = s_ec[p + 1]; nx_it = s_idx[p + 1]; nx_es = s_es[p + 1]; }
     if (ec == 0) continue;
     const uint32_t end = s + ec;
     int32_t lp_i = 0, lun_i = 0, lst_i = 0;
     double lsi_i = 0;
     if (paths) { lp_i = s_lp[it_i]; lun_i = s_lun[it_i]; lst_i = s_lst[it_i]; lsi_i = s_lsi[it_i]; }
     while (s < end) {
-      if (s >= k0 + 64) {  // next chunk; the one two ahead goes in flight
+      while (s >= k0 + 64) {  // next chunk (past the unused end of a region); two ahead in flight
         c0 = c1; c1 = c2; k0 += 64;
         c2 = ld(k0 + 128 + lane);
       }
@@ -3302,20 +3314,24 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
         }
       } else {
         // union_sets(it_i, it_j) for this chunk's edges in j order
-        const uint64_t em = __ballot(edge);
         const uint32_t r1 = find(it_i);
         const uint32_t R = edge ? find(it_j) : r1;
-        const uint32_t rk = s_rank[R];
-        // the edge lanes holding the same root: a ballot per bit of R (node indices < 2^12)
-        uint64_t same = em;
+        // most edges join nodes already in i's set: nothing to merge then
+        const uint64_t fo = __ballot(edge & (R != r1));
+        uint64_t fm = fo;
+        if (fo & (fo - 1)) {  // two or more foreign edges: the first lane of each root
+          // the edge lanes holding the same root: a ballot per bit of R (node indices < 2^12)
+          uint64_t same = fo;
 #pragma unroll
-        for (uint32_t bit = 0; bit < 12; ++bit) {
-          const uint64_t bb = __ballot((R >> bit) & 1u);
-          same &= ((R >> bit) & 1u) ? bb : ~bb;
+          for (uint32_t bit = 0; bit < 12; ++bit) {
+            const uint64_t bb = __ballot((R >> bit) & 1u);
+            same &= ((R >> bit) & 1u) ? bb : ~bb;
+          }
+          fm = __ballot(((fo >> lane) & 1) && (same & ((1ull << lane) - 1)) == 0);
         }
-        const bool first = edge & (R != r1) & ((same & ((1ull << lane) - 1)) == 0);
-        uint32_t cr = r1, crank = s_rank[r1];
-        for (uint64_t fm = __ballot(first); fm; fm &= fm - 1) {
+        const uint32_t rk = fm ? s_rank[R] : 0u;
+        uint32_t cr = r1, crank = fm ? s_rank[r1] : 0u;
+        for (; fm; fm &= fm - 1) {
           const uint32_t l = (uint32_t)__ffsll((long long)fm) - 1;
           const uint32_t vv = (uint32_t)__builtin_amdgcn_readlane((int)R, (int)l);
           const uint32_t vr = (uint32_t)__builtin_amdgcn_readlane((int)rk, (int)l);
