@@ -29,7 +29,7 @@ namespace pbgpu {
 // Optional phase profiling of k_lis (build with -DPBGPU_PROF; tools/prof_lis.py):
 // per-wave s_memtime deltas summed into g_prof.
 #ifdef PBGPU_PROF
-constexpr int PROF_SLOTS = 96;
+constexpr int PROF_SLOTS = 112;
 __device__ unsigned long long g_prof[PROF_SLOTS];
 #define PROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define PROF_ADD(slot, v) do { if (lane_id() == 0) atomicAdd(&g_prof[slot], (unsigned long long)(v)); } while (0)
@@ -2056,7 +2056,7 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
     const int32_t pos = fwd_align ? so : (int32_t)(R.ql + (uint32_t)so - k + 2u);
     return pos < 0 ? -pos : pos;
   };
-  // pass 1: cons / cover, the least-squares fit (pb_aligner.cc:19-47), kmers_info (LDS case)
+  // pass 1: cons / cover and the least-squares fit (pb_aligner.cc:19-47)
   Lsq L;
   int2 prev = make_int2(0, 0), first = make_int2(0, 0);
   PROF_T(kc_t1);
@@ -2079,12 +2079,9 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
 #else
     ++L.n; L.EX += p.y;
 #endif
-#if !defined(PBGPU_EXP_NO_INFO) && !defined(PBGPU_EXP_INFO_PASS2)
-    if (info_lds) KI.add(info_pos(p.y));
-#endif
     prev = p;
   });
-  // pass 2: average error of the fit (least_square_2d.hpp:70-80 + pb_aligner.cc:49-60)
+  // pass 2: average error of the fit (least_square_2d.hpp:70-80 + pb_aligner.cc:49-60) and kmers_info
   PROF_T(kc_t2);
   double a = 0, b = 0;
   if (L.n == 1) {
@@ -2094,14 +2091,15 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
     R.stretch = a; R.offset = b;
   }
   double err = 0;
+  // kmers_info (LDS case) rides this pass, not the fit's: the fit's registers are dead
+  // here, and the pass then also runs for single-point chains (-0.6 ms, r04b)
 #ifdef PBGPU_EXP_NO_PASS2
   LS.run(O.pts, 0, ps, [&](const int2 p) {
-#elif defined(PBGPU_EXP_INFO_PASS2)
-  // (experiment: kmers_info in the error pass, not beside the fit)
-  LS.run(O.pts, (L.n > 1 || info_lds) ? nl : 0, ps, [&](const int2 p) {
-    if (info_lds) KI.add(info_pos(p.y));
 #else
-  LS.run(O.pts, L.n > 1 ? nl : 0, ps, [&](const int2 p) {
+  LS.run(O.pts, (L.n > 1 || info_lds) ? nl : 0, ps, [&](const int2 p) {
+#endif
+#ifndef PBGPU_EXP_NO_INFO
+    if (info_lds) KI.add(info_pos(p.y));
 #endif
     err = __dadd_rn(err, fabs(__dadd_rn(__dadd_rn(__dmul_rn(a, (double)p.y), b), -(double)p.x)));
   });
@@ -3280,6 +3278,10 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
     }
     return q;
   };
+#ifdef PBGPU_PROF
+  uint64_t pr_find = 0, pr_merge = 0, pr_paths = 0, pr_chunks = 0;
+  const uint64_t pr0 = __builtin_amdgcn_s_memtime();
+#endif
   uint32_t nx_ec = s_ec[0], nx_it = s_idx[0], nx_es = s_es[0];
   for (uint32_t p = 0; p < n; ++p) {
     const uint32_t ec = nx_ec, it_i = nx_it;
@@ -3298,6 +3300,10 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
       const uint32_t k = k0 + lane;
       const bool edge = (k >= s) & (k < end);
       const uint32_t it_j = c0.x & 0xFFFFu;
+      PROF_T(pa);
+#ifdef PBGPU_PROF
+      ++pr_chunks;
+#endif
       if (paths) {
         if (edge) {  // node_info update (overlap_graph.cc:41-56); this lane owns node j
           s_fl[it_j] &= (uint8_t)~GRAPH_START;
@@ -3312,12 +3318,20 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
             s_lun[it_j] = lun_i + (int32_t)(c0.x >> 16);
           }
         }
+#ifdef PBGPU_PROF
+        lds_fence();
+        pr_paths += __builtin_amdgcn_s_memtime() - pa;
+#endif
       } else {
         // union_sets(it_i, it_j) for this chunk's edges in j order
         const uint32_t r1 = find(it_i);
         const uint32_t R = edge ? find(it_j) : r1;
         // most edges join nodes already in i's set: nothing to merge then
         const uint64_t fo = __ballot(edge & (R != r1));
+        PROF_T(pb);
+#ifdef PBGPU_PROF
+        pr_find += pb - pa;
+#endif
         uint64_t fm = fo;
         if (fo & (fo - 1)) {  // two or more foreign edges: the first lane of each root
           // the edge lanes holding the same root: a ballot per bit of R (node indices < 2^12)
@@ -3345,12 +3359,26 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
             if (lane == 0) { s_par[vv] = (uint16_t)cr; s_rank[cr] = (uint8_t)crank; }
           }
         }
+#ifdef PBGPU_PROF
+        lds_fence();
+        pr_merge += __builtin_amdgcn_s_memtime() - pb;
+#endif
       }
       s = end < k0 + 64 ? end : k0 + 64;
       lds_fence();  // this wave's updates of the chunk before the next reads (the waves run apart)
     }
     if (paths && lane == 0) s_fl[it_i] &= (uint8_t)~GRAPH_END;
   }
+#ifdef PBGPU_PROF
+  // slots 80..: [paths wave] chunk ticks, chunks, total; [union wave] find ticks, merge ticks,
+  // total; nodes; blocks (NM = 4096 / 2048 tiers at +16)
+  {
+    const uint32_t sl = 80 + (NM > GRAPH_NM_SMALL ? 16 : 0);
+    const uint64_t tot = __builtin_amdgcn_s_memtime() - pr0;
+    if (paths) { PROF_ADD(sl + 0, pr_paths); PROF_ADD(sl + 1, pr_chunks); PROF_ADD(sl + 2, tot); PROF_ADD(sl + 6, n); PROF_ADD(sl + 7, 1); }
+    else { PROF_ADD(sl + 3, pr_find); PROF_ADD(sl + 4, pr_merge); PROF_ADD(sl + 5, tot); }
+  }
+#endif
   __syncthreads();
   for (uint32_t i = tid; i < n; i += 128) {
     uint32_t q = i;

@@ -29,10 +29,10 @@ def main():
     al.align_resident(rr)
     L = pbgpu.lib()
     f = getattr(L, "pbgpu_debug_prof", None)
-    buf = (C.c_ulonglong * 96)()
+    buf = (C.c_ulonglong * 112)()
     if f is not None:
         f.argtypes = [C.POINTER(C.c_ulonglong), C.c_int, C.c_int]
-        f(buf, 96, 1)
+        f(buf, 112, 1)
     al.reset_stats()
     t = time.time()
     al.align_resident(rr)
@@ -41,13 +41,13 @@ def main():
     st = al.stats()
     print(f"align_resident {wall * 1e3:.1f} ms, graph {st['ms_graph']:.2f} ms over {st['graph_records']} records")
     if f is not None:
-        f(buf, 96, 1)
-        v = list(buf)[80:88]
-        tot = max(1, v[6])
-        print(f"k_graph: waves {v[7]}, nodes {v[5]}, chunks {v[4]} ({v[4] / max(1, v[5]):.2f} a node), "
-              f"ticks a node {v[6] / max(1, v[5]):.0f}")
-        for nm, x in zip(["chunk scan", "names + sums", "node updates", "unions"], v[:4]):
-            print(f"  {nm:14s} {x / max(1, v[5]):8.0f} ticks a node ({100.0 * x / tot:5.1f}%)")
+        f(buf, 112, 1)
+        for tier, base in (("<= 1024 records", 80), ("> 1024 records", 96)):
+            v = list(buf)[base:base + 8]
+            nn, nb = max(1, v[6]), max(1, v[7])
+            print(f"k_graph_relax {tier}: blocks {v[7]}, nodes {v[6]}, chunks {v[1]} ({v[1] / nn:.2f} a node); "
+                  f"ticks a node: paths wave {v[2] / nn:.0f} (chunk work {v[0] / nn:.0f}), "
+                  f"union wave {v[5] / nn:.0f} (finds {v[3] / nn:.0f}, merges {v[4] / nn:.0f})")
         w = list(buf)[88:96]
         nw = max(1, w[5])
         print(f"k_mega: waves {w[5]}, candidates {w[7] >> 32}, components {w[7] & 0xffffffff}, "
