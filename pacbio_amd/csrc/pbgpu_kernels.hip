@@ -3093,7 +3093,7 @@ DEV bool graph_on_device(const GraphDev& G, uint32_t n) { return n > 0 && n <= G
 template <int PASS>
 __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n_recs) {
   __shared__ double s_is[GE_SLOTS], s_ie[GE_SLOTS], s_er[GE_SLOTS], s_rl[GE_SLOTS];
-  __shared__ uint32_t s_meta[GE_SLOTS], s_lpa[GE_SLOTS], s_end[GE_SLOTS], s_po[GE_SLOTS];
+  __shared__ uint32_t s_meta[GE_SLOTS], s_lpa[GE_SLOTS], s_end[GE_SLOTS], s_po[GE_SLOTS], s_rb[GE_SLOTS];
   __shared__ uint32_t s_u[GRAPH_U * GE_SLOTS];  // [u * GE_SLOTS + slot]
   const uint64_t q0 = (uint64_t)blockIdx.x * GE_NODES;
   if (q0 >= n_recs) return;
@@ -3101,13 +3101,14 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
   for (uint32_t t = threadIdx.x; t < ns; t += GE_BLOCK) {
     const uint64_t q = q0 + t;
     const uint32_t r = G.recs[q].read;  // records are grouped per read
-    const uint64_t e = G.rec_off[r + 1];
-    const uint32_t n = (uint32_t)(e - G.rec_off[r]);
+    const uint64_t e = G.rec_off[r + 1], rb = G.rec_off[r];
+    const uint32_t n = (uint32_t)(e - rb);
     const GDesc d = G.desc[q];
     s_is[t] = d.imp_s; s_ie[t] = d.imp_e; s_er[t] = d.err;
     s_rl[t] = (double)(G.roff[r + 1] - G.roff[r]);
     s_meta[t] = d.idx | (d.nsz << 16); s_lpa[t] = d.lp_add; s_po[t] = (uint32_t)d.poff;  // < 2^32 (host check)
     s_end[t] = graph_on_device(G, n) ? (uint32_t)e : (uint32_t)(q + 1);  // a read left to the host: no scan
+    s_rb[t] = (uint32_t)rb;
 #pragma unroll
     for (uint32_t u = 0; u < GRAPH_U; ++u) s_u[u * GE_SLOTS + t] = u < d.nsz ? G.ounits[d.poff + u] : 0u;
   }
@@ -3207,6 +3208,7 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
           // the edge's path increment (nb_mers or sr_cover of j minus the common k-mers) and
           // the unitigs it adds (overlap_graph.cc:47-53)
           G.edges[e0 + at] = make_uint2((mj & 0xFFFFu) | ((sb - (uint32_t)nb) << 16), lpa_j - (uint32_t)common);
+          G.inc[s_rb[ti] + (mj & 0xFFFFu)] = 1;  // j has an edge into it: not a start node
         }
         cnt += (uint32_t)__builtin_popcountll(em);
         if (bm) break;  // the reference's break
@@ -3237,8 +3239,8 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
   __shared__ int32_t s_lp[NM], s_lun[NM];
   __shared__ int16_t s_lst[NM], s_lpv[NM];
   __shared__ uint32_t s_es[NM];  // node's edges: start in the read's region
-  __shared__ uint16_t s_idx[NM], s_ec[NM], s_par[NM];
-  __shared__ uint8_t s_fl[NM], s_rank[NM];
+  __shared__ uint16_t s_idx[NM], s_ec[NM], s_par[NM], s_pos[NM];
+  __shared__ uint8_t s_rank[NM];
   const uint32_t r = blockIdx.x;
   if (r >= n_reads) return;
   const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -3256,10 +3258,11 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
     const GDesc d = G.desc[b + p];
     const uint32_t it = d.idx;
     s_idx[p] = (uint16_t)it;
+    s_pos[it] = (uint16_t)p;
     s_ec[p] = (uint16_t)G.ecnt[b + p];
     s_es[p] = (uint32_t)(G.eoff[b + p] - G.eoff[b]);
     s_lp[it] = (int32_t)d.lp_add; s_lun[it] = (int32_t)d.nsz; s_lst[it] = -1; s_lpv[it] = -1;
-    s_lsi[it] = d.imp_s; s_fl[it] = (uint8_t)(GRAPH_START | GRAPH_END);
+    s_lsi[it] = d.imp_s;
     s_par[it] = (uint16_t)it; s_rank[it] = 0;
   }
   __syncthreads();
@@ -3270,14 +3273,7 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
   auto ld = [&](uint32_t k) -> uint2 { return k < ne ? E[k] : make_uint2(0u, 0u); };
   uint2 c0 = ld(lane), c1 = ld(64 + lane), c2 = ld(128 + lane);
   uint32_t k0 = 0;
-  auto find = [&](uint32_t q) -> uint32_t {  // union-find root with path halving
-    while (s_par[q] != q) {
-      const uint32_t g = s_par[s_par[q]];
-      s_par[q] = (uint16_t)g;
-      q = g;
-    }
-    return q;
-  };
+
 #ifdef PBGPU_PROF
   uint64_t pr_find = 0, pr_merge = 0, pr_paths = 0, pr_chunks = 0;
   const uint64_t pr0 = __builtin_amdgcn_s_memtime();
@@ -3306,7 +3302,6 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
 #endif
       if (paths) {
         if (edge) {  // node_info update (overlap_graph.cc:41-56); this lane owns node j
-          s_fl[it_j] &= (uint8_t)~GRAPH_START;
           const int32_t nlpath = (int32_t)((uint32_t)lp_i + c0.y);
           const int32_t lp_j = s_lp[it_j];
           const bool upd = nlpath > lp_j || (nlpath == lp_j && (s_lst[it_j] == -1 || lsi_i > s_lsi[it_j]));
@@ -3324,8 +3319,17 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
 #endif
       } else {
         // union_sets(it_i, it_j) for this chunk's edges in j order
-        const uint32_t r1 = find(it_i);
-        const uint32_t R = edge ? find(it_j) : r1;
+        // both roots in one walk (path halving on each): the two chains' LDS round trips
+        // overlap instead of following one another
+        uint32_t r1 = it_i, R = edge ? it_j : it_i;
+        for (;;) {
+          const uint32_t p1 = s_par[r1], p2 = s_par[R];
+          if ((p1 == r1) & (p2 == R)) break;
+          const uint32_t g1 = s_par[p1], g2 = s_par[p2];
+          if (p1 != r1) { s_par[r1] = (uint16_t)g1; r1 = g1; }
+          if (p2 != R) { s_par[R] = (uint16_t)g2; R = g2; }
+        }
+        if (!edge) R = r1;
         // most edges join nodes already in i's set: nothing to merge then
         const uint64_t fo = __ballot(edge & (R != r1));
         PROF_T(pb);
@@ -3365,9 +3369,11 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
 #endif
       }
       s = end < k0 + 64 ? end : k0 + 64;
-      lds_fence();  // this wave's updates of the chunk before the next reads (the waves run apart)
+      // a wave's LDS operations execute in order, so the next chunk's reads see this one's
+      // writes; the fence keeps the compiler from moving memory operations across
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
     }
-    if (paths && lane == 0) s_fl[it_i] &= (uint8_t)~GRAPH_END;
   }
 #ifdef PBGPU_PROF
   // slots 80..: [paths wave] chunk ticks, chunks, total; [union wave] find ticks, merge ticks,
@@ -3383,7 +3389,9 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
   for (uint32_t i = tid; i < n; i += 128) {
     uint32_t q = i;
     while (s_par[q] != q) q = s_par[q];
-    G.out[b + i] = GraphNode{s_lp[i], s_lst[i], s_lpv[i], s_lun[i], q, s_fl[i]};
+    // start node: no edge into it (marked by k_graph_edges); end node: no edge out of it
+    const uint32_t fl = (G.inc[b + i] ? 0u : GRAPH_START) | (s_ec[s_pos[i]] ? 0u : GRAPH_END);
+    G.out[b + i] = GraphNode{s_lp[i], s_lst[i], s_lpv[i], s_lun[i], q, fl};
   }
 }
 // ====================================================== mega-reads (device)
