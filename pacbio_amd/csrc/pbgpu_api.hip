@@ -1657,9 +1657,8 @@ static void graph_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   al->g_pre.ensure(3 * tot + 3); al->g_imp.ensure(nrec + 1); al->g_desc.ensure(nrec + 1); al->g_out.ensure(nrec + 1);
   G.pp = (uint2*)al->g_pre.p; G.ounits = al->g_pre.p + 2 * (tot + 1);
   G.imp = al->g_imp.p; G.desc = al->g_desc.p; G.out = al->g_out.p;
-  al->g_ecnt.ensure(nrec + 1); al->g_eoff.ensure(nrec + 1); al->g_inc.ensure(nrec + 1);
-  G.ecnt = al->g_ecnt.p; G.eoff = al->g_eoff.p; G.inc = al->g_inc.p;
-  HIPCHK(hipMemsetAsync(al->g_inc.p, 0, nrec + 1, st));
+  al->g_ecnt.ensure(nrec + 1); al->g_eoff.ensure(nrec + 1);
+  G.ecnt = al->g_ecnt.p; G.eoff = al->g_eoff.p;
   uint64_t n_edges = 0;
   HIPCHK(launch_graph(G, n, nrec, st, al->g_side, al->g_fork, al->g_join,
                       (uint64_t*)temp_storage(al->tmp, excl_scan_scratch_words(nrec) * 8), &n_edges));

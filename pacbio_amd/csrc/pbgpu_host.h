@@ -352,7 +352,6 @@ struct pbgpu_aligner {
   dbuf<uint32_t> g_ecnt;
   dbuf<uint64_t> g_eoff;
   dbuf<uint2> g_edges;
-  dbuf<uint8_t> g_inc;
   // mega-reads on the device (pbgpu_graph_params.mega_reads)
   bool g_mega = false;
   int g_tiling = 0, g_trim = 0;

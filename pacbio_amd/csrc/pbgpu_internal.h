@@ -231,7 +231,6 @@ struct GraphDev {
   uint32_t* ecnt;
   uint64_t* eoff;
   uint2* edges;
-  uint8_t* inc;  // per record (read order): 1 = some edge goes into it (zeroed per batch)
   // mega-reads on the device (pbgpu_graph_params.mega_reads)
   int mega, tiling, trim;
   double min_density, min_len;

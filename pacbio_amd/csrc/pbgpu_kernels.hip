@@ -3093,7 +3093,7 @@ DEV bool graph_on_device(const GraphDev& G, uint32_t n) { return n > 0 && n <= G
 template <int PASS>
 __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n_recs) {
   __shared__ double s_is[GE_SLOTS], s_ie[GE_SLOTS], s_er[GE_SLOTS], s_rl[GE_SLOTS];
-  __shared__ uint32_t s_meta[GE_SLOTS], s_lpa[GE_SLOTS], s_end[GE_SLOTS], s_po[GE_SLOTS], s_rb[GE_SLOTS];
+  __shared__ uint32_t s_meta[GE_SLOTS], s_lpa[GE_SLOTS], s_end[GE_SLOTS], s_po[GE_SLOTS];
   __shared__ uint32_t s_u[GRAPH_U * GE_SLOTS];  // [u * GE_SLOTS + slot]
   const uint64_t q0 = (uint64_t)blockIdx.x * GE_NODES;
   if (q0 >= n_recs) return;
@@ -3101,14 +3101,13 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
   for (uint32_t t = threadIdx.x; t < ns; t += GE_BLOCK) {
     const uint64_t q = q0 + t;
     const uint32_t r = G.recs[q].read;  // records are grouped per read
-    const uint64_t e = G.rec_off[r + 1], rb = G.rec_off[r];
-    const uint32_t n = (uint32_t)(e - rb);
+    const uint64_t e = G.rec_off[r + 1];
+    const uint32_t n = (uint32_t)(e - G.rec_off[r]);
     const GDesc d = G.desc[q];
     s_is[t] = d.imp_s; s_ie[t] = d.imp_e; s_er[t] = d.err;
     s_rl[t] = (double)(G.roff[r + 1] - G.roff[r]);
     s_meta[t] = d.idx | (d.nsz << 16); s_lpa[t] = d.lp_add; s_po[t] = (uint32_t)d.poff;  // < 2^32 (host check)
     s_end[t] = graph_on_device(G, n) ? (uint32_t)e : (uint32_t)(q + 1);  // a read left to the host: no scan
-    s_rb[t] = (uint32_t)rb;
 #pragma unroll
     for (uint32_t u = 0; u < GRAPH_U; ++u) s_u[u * GE_SLOTS + t] = u < d.nsz ? G.ounits[d.poff + u] : 0u;
   }
@@ -3208,7 +3207,6 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
           // the edge's path increment (nb_mers or sr_cover of j minus the common k-mers) and
           // the unitigs it adds (overlap_graph.cc:47-53)
           G.edges[e0 + at] = make_uint2((mj & 0xFFFFu) | ((sb - (uint32_t)nb) << 16), lpa_j - (uint32_t)common);
-          G.inc[s_rb[ti] + (mj & 0xFFFFu)] = 1;  // j has an edge into it: not a start node
         }
         cnt += (uint32_t)__builtin_popcountll(em);
         if (bm) break;  // the reference's break
@@ -3240,7 +3238,7 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
   __shared__ int16_t s_lst[NM], s_lpv[NM];
   __shared__ uint32_t s_es[NM];  // node's edges: start in the read's region
   __shared__ uint16_t s_idx[NM], s_ec[NM], s_par[NM], s_pos[NM];
-  __shared__ uint8_t s_rank[NM];
+  __shared__ uint8_t s_rank[NM], s_in[NM];
   const uint32_t r = blockIdx.x;
   if (r >= n_reads) return;
   const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -3262,7 +3260,7 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
     s_ec[p] = (uint16_t)G.ecnt[b + p];
     s_es[p] = (uint32_t)(G.eoff[b + p] - G.eoff[b]);
     s_lp[it] = (int32_t)d.lp_add; s_lun[it] = (int32_t)d.nsz; s_lst[it] = -1; s_lpv[it] = -1;
-    s_lsi[it] = d.imp_s;
+    s_lsi[it] = d.imp_s; s_in[it] = 0;
     s_par[it] = (uint16_t)it; s_rank[it] = 0;
   }
   __syncthreads();
@@ -3302,6 +3300,7 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
 #endif
       if (paths) {
         if (edge) {  // node_info update (overlap_graph.cc:41-56); this lane owns node j
+          s_in[it_j] = 1;  // an edge into j: not a start node
           const int32_t nlpath = (int32_t)((uint32_t)lp_i + c0.y);
           const int32_t lp_j = s_lp[it_j];
           const bool upd = nlpath > lp_j || (nlpath == lp_j && (s_lst[it_j] == -1 || lsi_i > s_lsi[it_j]));
@@ -3389,8 +3388,8 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
   for (uint32_t i = tid; i < n; i += 128) {
     uint32_t q = i;
     while (s_par[q] != q) q = s_par[q];
-    // start node: no edge into it (marked by k_graph_edges); end node: no edge out of it
-    const uint32_t fl = (G.inc[b + i] ? 0u : GRAPH_START) | (s_ec[s_pos[i]] ? 0u : GRAPH_END);
+    // start node: no edge into it; end node: no edge out of it
+    const uint32_t fl = (s_in[i] ? 0u : GRAPH_START) | (s_ec[s_pos[i]] ? 0u : GRAPH_END);
     G.out[b + i] = GraphNode{s_lp[i], s_lst[i], s_lpv[i], s_lun[i], q, fl};
   }
 }
