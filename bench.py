@@ -610,6 +610,7 @@ def main():
                                                      ("seed", "group", "lis", "fit", "records")},
                                "kernel_ms_per_launch": {kk: round(kms[kk] / max(1, kn[kk]), 3) for kk in kms},
                                "kernel_launches": dict(kn),
+                               "host_order_ms_per_step": round(st["ms_host_order"] / args.device_steps, 3),
                                "counters_per_step": {n: st[n] // args.device_steps for n in
                                                      ("n_kmers", "n_probes", "n_kept", "n_hits", "n_chains",
                                                       "n_lis_tests", "n_records")},

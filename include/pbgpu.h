@@ -259,6 +259,8 @@ typedef struct {
   /* overlap graph candidate pairs (not skipped, before the break, names of >= 2
    * unitigs: the traversal's edge capacity, an upper bound on its edges) */
   uint64_t graph_candidates;
+  /* host time ordering a batch's reads for the group stage (the GPU waits for it) */
+  double   ms_host_order;
 } pbgpu_stats;
 pbgpu_status pbgpu_aligner_get_stats(const pbgpu_aligner* al, pbgpu_stats* s);
 pbgpu_status pbgpu_aligner_reset_stats(pbgpu_aligner* al);

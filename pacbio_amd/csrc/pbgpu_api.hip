@@ -1750,7 +1750,8 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
   HIPCHK(hipEventRecord(al->ev[1], st));
   launch_excl_scan(nullptr, al->nhits.p, n, al->hit_off.p,
                    (uint64_t*)temp_storage(al->tmp, excl_scan_scratch_words(n) * 8), st);
-  std::vector<uint64_t> hoff(n + 1);
+  std::vector<uint64_t>& hoff = al->h_hoff;
+  hoff.resize(n + 1);
   HIPCHK(hipMemcpyAsync(hoff.data(), al->hit_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   // ------------------------------------- sub-batches: group -> chains (retry)
@@ -1787,16 +1788,31 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
     // only costs time: an overflowing read resumes in the next tier.
     uint32_t n_small = 0, n_bigr = 0;
     {
-      std::vector<uint32_t> rl(nr), rs, rb;
-      std::vector<uint8_t> parts(nr);
-      for (uint32_t i = 0; i < nr; ++i) rl[i] = r0 + i;
-      std::stable_sort(rl.begin(), rl.end(), [&](uint32_t a, uint32_t b) {
-        return hoff[a + 1] - hoff[a] > hoff[b + 1] - hoff[b];
-      });
+      const auto th0 = std::chrono::steady_clock::now();
+      // Longest first by a counting sort over hit-count classes (exact below 128 hits, 16
+      // classes per octave above; stable within a class): the order only schedules the
+      // reads, so classes are as good as an exact sort, and O(n) where std::stable_sort
+      // took milliseconds of host time while the GPU waited
+      constexpr uint32_t NCL = 128 + 16 * 58;
+      auto cls = [](uint64_t h) -> uint32_t {
+        if (h < 128) return (uint32_t)h;
+        const uint32_t l = 63u - (uint32_t)__builtin_clzll(h);
+        return 128u + 16u * (l - 7u) + (uint32_t)((h >> (l - 4u)) & 15u);
+      };
+      std::vector<uint32_t>& rl = al->h_order;
+      std::vector<uint32_t>& cnt = al->h_class;
+      std::vector<uint8_t>& parts = al->h_parts;
+      rl.resize(nr); parts.resize(nr); cnt.assign(NCL + 1, 0);
+      for (uint32_t r = r0; r < r1; ++r) ++cnt[NCL - 1 - cls(hoff[r + 1] - hoff[r])];
+      for (uint32_t c = 0, acc = 0; c <= NCL; ++c) { const uint32_t v = cnt[c]; cnt[c] = acc; acc += v; }
+      for (uint32_t r = r0; r < r1; ++r) rl[cnt[NCL - 1 - cls(hoff[r + 1] - hoff[r])]++] = r;
       const double fill_small = 0.95 * (double)((1u << hcap_log2) - (1u << hcap_log2) / 4);
       // tests: PBGPU_GROUP_PRED_SCALE=0 routes every read to the smallest table (all overflow paths)
       const double pred_scale = getenv("PBGPU_GROUP_PRED_SCALE") ? atof(getenv("PBGPU_GROUP_PRED_SCALE")) : 1.0;
       const double fill_big = 0.95 * (double)((1u << kGroupLdsMaxLog2) - (1u << kGroupLdsMaxLog2) / 4);
+      std::vector<uint32_t>& rs = al->h_small;
+      std::vector<uint32_t>& rb = al->h_big;
+      rs.clear(); rb.clear();
       for (uint32_t r : rl) {
         const double pred = (double)(hoff[r + 1] - hoff[r]) * al->chains_per_hit * pred_scale;
         parts[r - r0] = (uint8_t)std::min(255.0, std::max(1.0, std::ceil(pred / fill_big)));
@@ -1804,6 +1820,7 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
       }
       n_small = (uint32_t)rs.size(); n_bigr = (uint32_t)rb.size();
       rs.insert(rs.end(), rb.begin(), rb.end());
+      al->acc.ms_host_order += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count();
       al->read_list.ensure(nr);
       al->nparts.ensure(n);
       al->prog.ensure(n);

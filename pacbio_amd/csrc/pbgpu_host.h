@@ -314,6 +314,9 @@ struct pbgpu_aligner {
   uint64_t hit_budget = 4000000000ull, rec_hint = 0, info_per_chain = 32;
   double chains_per_hit = 1.0 / 80;  // k_group tier estimate (C2: 1.1 x 1/90), refined after every batch
   dbuf<uint32_t> ovf_list, read_list;
+  std::vector<uint32_t> h_order, h_class, h_small, h_big;  // host scratch of the group stage's read order
+  std::vector<uint8_t> h_parts;
+  std::vector<uint64_t> h_hoff;
   dbuf<uint8_t> nparts;
   dbuf<uint2> prog;
   // sharded index: per-base k-mer counts of the current batch (SEED_COUNTS, then summed)
