@@ -1254,6 +1254,9 @@ pbgpu_status pbgpu_aligner_free(pbgpu_aligner* al) {
   if (al->g_fork) (void)hipEventDestroy(al->g_fork);
   if (al->g_join) (void)hipEventDestroy(al->g_join);
   if (al->g_side) (void)hipStreamDestroy(al->g_side);
+  if (al->grp_fork) (void)hipEventDestroy(al->grp_fork);
+  if (al->grp_join) (void)hipEventDestroy(al->grp_join);
+  if (al->grp_side) (void)hipStreamDestroy(al->grp_side);
   if (al->st) (void)hipStreamDestroy(al->st);
   delete al;
   return PBGPU_OK;
@@ -1835,14 +1838,34 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
       static_assert(ST_LIS_TESTS == ST_CHAINS + 1, "per-attempt stat slots are adjacent");
       HIPCHK(hipMemsetAsync(al->stats.p + ST_CHAINS, 0, 16, st));  // redone on a retry: counted per attempt
       O.resume = 0;
+      // PBGPU_GROUP_OVERLAP=1 (experiment): the 16-wave tier's reads -- the longest -- on a side
+      // stream, started first, beside the 4-wave tier
+      static const bool overlap = getenv("PBGPU_GROUP_OVERLAP") && atoi(getenv("PBGPU_GROUP_OVERLAP"));
+      if (overlap && n_bigr) {
+        if (!al->grp_side) {
+          HIPCHK(hipStreamCreateWithFlags(&al->grp_side, hipStreamNonBlocking));
+          HIPCHK(hipEventCreateWithFlags(&al->grp_fork, hipEventDisableTiming));
+          HIPCHK(hipEventCreateWithFlags(&al->grp_join, hipEventDisableTiming));
+        }
+        HIPCHK(hipEventRecord(al->grp_fork, st));
+        HIPCHK(hipStreamWaitEvent(al->grp_side, al->grp_fork, 0));
+        launch_group(v, al->krec.p, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0,
+                     al->read_list.p + n_small, n_bigr, kGroupLdsMaxLog2, nullptr, O, al->stats.p, al->grp_side);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(al->grp_join, al->grp_side));
+      }
       HIPCHK(hipEventRecord(al->ev[8], st));
       launch_group(v, al->krec.p, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0, al->read_list.p, n_small,
                    hcap_log2, nullptr, O, al->stats.p, st);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(al->ev[9], st));
-      launch_group(v, al->krec.p, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0,
-                   al->read_list.p + n_small, n_bigr, kGroupLdsMaxLog2, nullptr, O, al->stats.p, st);
-      HIPCHK(hipGetLastError());
+      if (overlap && n_bigr) {
+        HIPCHK(hipStreamWaitEvent(st, al->grp_join, 0));
+      } else {
+        launch_group(v, al->krec.p, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0,
+                     al->read_list.p + n_small, n_bigr, kGroupLdsMaxLog2, nullptr, O, al->stats.p, st);
+        HIPCHK(hipGetLastError());
+      }
       O.resume = 1;
       uint32_t cnt[4];
       HIPCHK(hipMemcpyAsync(cnt, al->counters.p, 16, hipMemcpyDeviceToHost, st));

@@ -311,6 +311,8 @@ struct pbgpu_aligner {
   hipEvent_t ev[20]{};
   hipStream_t g_side = nullptr;  // the overlap graph's long-read tier (set_graph)
   hipEvent_t g_fork = nullptr, g_join = nullptr;
+  hipStream_t grp_side = nullptr;  // the group stage's 16-wave tier (PBGPU_GROUP_OVERLAP)
+  hipEvent_t grp_fork = nullptr, grp_join = nullptr;
   uint64_t hit_budget = 4000000000ull, rec_hint = 0, info_per_chain = 32;
   double chains_per_hit = 1.0 / 80;  // k_group tier estimate (C2: 1.1 x 1/90), refined after every batch
   dbuf<uint32_t> ovf_list, read_list;

@@ -1,12 +1,11 @@
 #!/bin/bash
-# Per-kernel ms (tools/exp/kernel_ms.py, 25k C2 reads) of the product library under
-# environment settings, interleaved twice: bash tools/exp/ab_env.sh "" "PBGPU_OCC_SR=1" ...
+# device-leg A/B of an environment switch: bash tools/exp/ab_env.sh "VAR=val" ...  ("" = none)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-for rep in 1 2; do
-  for e in "$@"; do
-    env $e timeout -k 10 300 python -u tools/exp/kernel_ms.py --reads 25000 > gpurun_out/abenv.txt 2>&1 || { cat gpurun_out/abenv.txt; exit 1; }
-    echo "[$e] $(tail -1 gpurun_out/abenv.txt)"
-  done
+for e in "$@"; do
+  env $e timeout -k 10 400 python bench.py --steps 1 --warmup 0 --device-steps 3 --parts 0 --cmr-steps 0 --no-cpu-baseline --skip-default-leg --no-brand > gpurun_out/abe.json 2> gpurun_out/abe.err || { tail -5 gpurun_out/abe.err; exit 1; }
+  python3 -c "
+import json; d=json.load(open('gpurun_out/abe.json')); c=d['config']['device_leg']
+print('$e', round(d['value_device']/1e9,3), round(c['ms_per_step'],2), c['stage_ms_per_step'])"
 done
