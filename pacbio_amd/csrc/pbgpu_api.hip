@@ -1254,6 +1254,8 @@ pbgpu_status pbgpu_aligner_free(pbgpu_aligner* al) {
   if (al->g_fork) (void)hipEventDestroy(al->g_fork);
   if (al->g_join) (void)hipEventDestroy(al->g_join);
   if (al->g_side) (void)hipStreamDestroy(al->g_side);
+  if (al->g_join2) (void)hipEventDestroy(al->g_join2);
+  if (al->g_side2) (void)hipStreamDestroy(al->g_side2);
   if (al->grp_fork) (void)hipEventDestroy(al->grp_fork);
   if (al->grp_join) (void)hipEventDestroy(al->grp_join);
   if (al->grp_side) (void)hipStreamDestroy(al->grp_side);
@@ -1668,7 +1670,7 @@ static void graph_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   HIPCHK(hipGetLastError());
   al->g_edges.ensure(n_edges + 1);
   G.edges = al->g_edges.p;
-  HIPCHK(launch_graph_relax(G, n, nrec, st, al->g_side, al->g_fork, al->g_join));
+  HIPCHK(launch_graph_relax(G, n, nrec, st, al->g_side, al->g_side2, al->g_fork, al->g_join, al->g_join2));
   HIPCHK(hipGetLastError());
   al->acc.graph_candidates += n_edges;
   al->g_mtotal = al->g_munits_used = 0;
@@ -2243,8 +2245,10 @@ pbgpu_status pbgpu_aligner_set_graph(pbgpu_aligner* al, const pbgpu_graph_params
   al->g_min_density = p->min_density; al->g_min_len = p->min_len;
   if (!al->g_side) {
     HIPCHK(hipStreamCreateWithFlags(&al->g_side, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&al->g_side2, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&al->g_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&al->g_join, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&al->g_join2, hipEventDisableTiming));
   }
   al->graph = true;
   return PBGPU_OK;

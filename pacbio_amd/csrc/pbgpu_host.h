@@ -310,7 +310,8 @@ struct pbgpu_aligner {
   pbgpu_stats acc{};
   hipEvent_t ev[20]{};
   hipStream_t g_side = nullptr;  // the overlap graph's long-read tier (set_graph)
-  hipEvent_t g_fork = nullptr, g_join = nullptr;
+  hipEvent_t g_fork = nullptr, g_join = nullptr, g_join2 = nullptr;
+  hipStream_t g_side2 = nullptr;  // the overlap graph's 1025-2048-record tier
   hipStream_t grp_side = nullptr;  // the group stage's 16-wave tier (PBGPU_GROUP_OVERLAP)
   hipEvent_t grp_fork = nullptr, grp_join = nullptr;
   uint64_t hit_budget = 4000000000ull, rec_hint = 0, info_per_chain = 32;

@@ -282,6 +282,6 @@ void launch_graph_sizes(const GraphDev& G, uint64_t n_recs, uint32_t* sizes, uin
 hipError_t launch_graph(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hipStream_t st, hipStream_t side,
                         hipEvent_t fork, hipEvent_t join, uint64_t* scan_scratch, uint64_t* n_edges);
 hipError_t launch_graph_relax(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hipStream_t st, hipStream_t side,
-                              hipEvent_t fork, hipEvent_t join);
+                              hipStream_t side2, hipEvent_t fork, hipEvent_t join, hipEvent_t join2);
 
 }  // namespace pbgpu

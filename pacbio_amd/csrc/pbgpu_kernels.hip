@@ -3986,20 +3986,24 @@ hipError_t launch_graph(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hi
   return hipStreamSynchronize(st);
 }
 hipError_t launch_graph_relax(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hipStream_t st, hipStream_t side,
-                              hipEvent_t fork, hipEvent_t join) {
+                              hipStream_t side2, hipEvent_t fork, hipEvent_t join, hipEvent_t join2) {
   if (!n_recs || !n_reads) return hipSuccess;
   const uint32_t eg = (uint32_t)((n_recs + GE_NODES - 1) / GE_NODES);
   hipLaunchKernelGGL(k_graph_edges<1>, dim3(eg), dim3(GE_BLOCK), 0, st, G, n_recs);
-  // the long reads' relaxation on the side stream: its blocks are the longest
+  // the long reads' relaxations each on a side stream of their own (their blocks are the
+  // longest: > 2048 records, then > 1024), beside the short reads' on st
   hipError_t e = hipEventRecord(fork, st);
   if (e == hipSuccess) e = hipStreamWaitEvent(side, fork, 0);
+  if (e == hipSuccess) e = hipStreamWaitEvent(side2, fork, 0);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_graph_relax<GRAPH_NMAX>, dim3(n_reads), dim3(128), 0, side, G, n_reads);
-  hipLaunchKernelGGL(k_graph_relax<GRAPH_NMAX / 2>, dim3(n_reads), dim3(128), 0, side, G, n_reads);
+  hipLaunchKernelGGL(k_graph_relax<GRAPH_NMAX / 2>, dim3(n_reads), dim3(128), 0, side2, G, n_reads);
   if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
+  if ((e = hipEventRecord(join2, side2)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_graph_relax<GRAPH_NM_SMALL>, dim3(n_reads), dim3(128), 0, st, G, n_reads);
   hipLaunchKernelGGL(k_graph_relax<GRAPH_RELAX_MIN>, dim3(n_reads), dim3(128), 0, st, G, n_reads);
-  return hipStreamWaitEvent(st, join, 0);
+  if ((e = hipStreamWaitEvent(st, join, 0)) != hipSuccess) return e;
+  return hipStreamWaitEvent(st, join2, 0);
 }
 
 }  // namespace pbgpu
