@@ -397,7 +397,7 @@ def main():
     # ---- create_mega_reads (row f3, the aligner's production caller): the CLI over the
     # same files, overlap graph / tiling on the GPU; its own clock (--timing wall_s: first
     # batch read -> mega-reads file closed; the index build is before it), one warm-up run
-    el_cmr, cmr_t, worst_cmr = None, None, None
+    el_cmr, cmr_t, worst_cmr, cmr_runs = None, None, None, None
     if args.cmr_steps > 0:
         import json as _json
         import subprocess
@@ -405,7 +405,7 @@ def main():
         cflags = ["-s", "1M", "-m", str(k), "--psa-min", "13", "-k", "31", "-l", ul_txt, "-B", "15", "--max-count",
                   "5000", "--stretch-cap", "10000", "-t", str(threads), "-r", sr_fa, "-p", pb_fa, "--timing",
                   "--devices", str(local), "-o", os.path.join(wd, "mega_reads")]
-        walls = []
+        walls, cmr_runs = [], []
         for i in range(args.cmr_steps + 1):
             r = subprocess.run([cmr, *cflags], capture_output=True, text=True)
             if r.returncode:
@@ -413,6 +413,7 @@ def main():
             cmr_t = _json.loads(r.stderr.strip().splitlines()[-1])
             if i:
                 walls.append(cmr_t["wall_s"])
+                cmr_runs.append(cmr_t)
         # the median run, the worst beside it (every run's wall is listed too)
         el_cmr = comm.max(sorted(walls)[len(walls) // 2])
         worst_cmr = comm.max(max(walls))
@@ -574,6 +575,8 @@ def main():
                                                                      "output_bytes")} if cmr_t else None),
             "create_mega_reads_walls_s": walls if args.cmr_steps > 0 else None,
             "create_mega_reads_worst_wall_s": worst_cmr,
+            # every timed run's own --timing stages (a slow run shows which stage it lost time in)
+            "create_mega_reads_runs": cmr_runs if args.cmr_steps > 0 else None,
             "create_mega_reads_allocs": ({kk: cmr_t.get(kk) for kk in ("device_allocs", "device_allocs_late",
                                                                        "pinned_allocs", "pinned_allocs_late")}
                                          if cmr_t else None),

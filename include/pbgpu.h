@@ -256,9 +256,9 @@ typedef struct {
   /* overlap graph (pbgpu_aligner_set_graph): device time, records traversed on the device */
   double   ms_graph;
   uint64_t graph_records;
-  /* overlap graph candidate pairs (not skipped, before the break, names of >= 2
-   * unitigs: the traversal's edge capacity, an upper bound on its edges) */
-  uint64_t graph_candidates;
+  /* overlap graph nodes of more than 64 edges (the rest past their block, written
+   * by a second pass over those nodes) */
+  uint64_t graph_ovf_nodes;
   /* host time ordering a batch's reads for the group stage (the GPU waits for it) */
   double   ms_host_order;
 } pbgpu_stats;

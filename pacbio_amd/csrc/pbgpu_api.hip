@@ -1662,17 +1662,18 @@ static void graph_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   al->g_pre.ensure(3 * tot + 3); al->g_imp.ensure(nrec + 1); al->g_desc.ensure(nrec + 1); al->g_out.ensure(nrec + 1);
   G.pp = (uint2*)al->g_pre.p; G.ounits = al->g_pre.p + 2 * (tot + 1);
   G.imp = al->g_imp.p; G.desc = al->g_desc.p; G.out = al->g_out.p;
-  al->g_ecnt.ensure(nrec + 1); al->g_eoff.ensure(nrec + 1);
-  G.ecnt = al->g_ecnt.p; G.eoff = al->g_eoff.p;
-  uint64_t n_edges = 0;
-  HIPCHK(launch_graph(G, n, nrec, st, al->g_side, al->g_fork, al->g_join,
-                      (uint64_t*)temp_storage(al->tmp, excl_scan_scratch_words(nrec) * 8), &n_edges));
+  al->g_ecnt.ensure(nrec + 1); al->g_eoff.ensure(nrec + 1); al->g_ovf_list.ensure(nrec + 1); al->g_ovf.ensure(2);
+  al->g_edges.ensure(nrec * GRAPH_EBLK);
+  G.ecnt = al->g_ecnt.p; G.eoff = al->g_eoff.p; G.edges = al->g_edges.p;
+  G.ovf = al->g_ovf.p; G.ovf_list = al->g_ovf_list.p;
+  uint64_t ovf[2];
+  HIPCHK(launch_graph(G, n, nrec, st, al->g_side, al->g_fork, al->g_join, ovf));
   HIPCHK(hipGetLastError());
-  al->g_edges.ensure(n_edges + 1);
-  G.edges = al->g_edges.p;
-  HIPCHK(launch_graph_relax(G, n, nrec, st, al->g_side, al->g_side2, al->g_fork, al->g_join, al->g_join2));
+  al->g_eovf.ensure(std::max<uint64_t>(ovf[1], nrec) + 1);  // (a floor: the next batches rarely grow it)
+  G.eovf = al->g_eovf.p;
+  HIPCHK(launch_graph_relax(G, n, nrec, ovf[0], st, al->g_side, al->g_side2, al->g_fork, al->g_join, al->g_join2));
   HIPCHK(hipGetLastError());
-  al->acc.graph_candidates += n_edges;
+  al->acc.graph_ovf_nodes += ovf[0];
   al->g_mtotal = al->g_munits_used = 0;
   al->g_hosts = 0;
   if (!al->g_mega) return;

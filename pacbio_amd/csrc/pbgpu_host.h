@@ -357,7 +357,8 @@ struct pbgpu_aligner {
   dbuf<GraphNode> g_out;
   dbuf<uint32_t> g_ecnt;
   dbuf<uint64_t> g_eoff;
-  dbuf<uint2> g_edges;
+  dbuf<uint2> g_edges, g_eovf;
+  dbuf<uint64_t> g_ovf, g_ovf_list;
   // mega-reads on the device (pbgpu_graph_params.mega_reads)
   bool g_mega = false;
   int g_tiling = 0, g_trim = 0;

@@ -225,12 +225,16 @@ struct GraphDev {
   uint32_t* ounits;           // the name's unitigs in the record's orientation (at poff)
   GDesc* desc;                // per read, in sorted order
   GraphNode* out;
-  // the traversal's edges (k_graph_edges): per node in sorted order its count and its
-  // offset into the edge stream; an edge is {j's record index | unitigs added << 16,
-  // path increment}
+  // the traversal's edges (k_graph_edges): per node in sorted order its count, its
+  // first GRAPH_EBLK edges in a block of its own (edges + q * GRAPH_EBLK) and, past
+  // them, the rest at eovf + eoff[q]; an edge is {j's record index | unitigs added
+  // << 16, path increment}.  ovf: {nodes listed in ovf_list, overflow edges}
   uint32_t* ecnt;
   uint64_t* eoff;
   uint2* edges;
+  uint2* eovf;
+  uint64_t* ovf;
+  uint64_t* ovf_list;
   // mega-reads on the device (pbgpu_graph_params.mega_reads)
   int mega, tiling, trim;
   double min_density, min_len;
@@ -273,15 +277,17 @@ void launch_host_pack(const GraphDev& G, uint32_t n_reads, const uint64_t* hroff
                       GraphNode* hgraph, int32_t* hinfo_m, int32_t* hinfo_b, hipStream_t st);
 // G.poff from the records' name sizes (then the caller sizes pul / pco by poff[n_recs])
 void launch_graph_sizes(const GraphDev& G, uint64_t n_recs, uint32_t* sizes, uint64_t* scan_scratch, hipStream_t st);
-// implied positions and prefix sums, the per-read sort, each node's edge count and
-// offset (G.ecnt / G.eoff; *n_edges = their total, the stream synchronized);
-// then, with G.edges sized for them, launch_graph_relax writes the edges and
-// traverses -> G.out.  side: a second stream for the reads of more than
-// GRAPH_NM_SMALL records (their sort and relaxation run beside the others');
-// fork / join: events ordering it with st
+// implied positions and prefix sums, the per-read sort, every node's edges (G.ecnt,
+// the first GRAPH_EBLK of each in G.edges, sized n_recs * GRAPH_EBLK; the nodes with
+// more listed: ovf[2] = {nodes, edges past their blocks}, the stream synchronized);
+// then, with G.eovf sized for them, launch_graph_relax writes those and traverses
+// -> G.out.  side / side2: streams for the reads of more than GRAPH_NM_SMALL records
+// (their sort and relaxation run beside the others'); fork / join / join2: events
+// ordering them with st
+constexpr uint32_t GRAPH_EBLK = 64;
 hipError_t launch_graph(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hipStream_t st, hipStream_t side,
-                        hipEvent_t fork, hipEvent_t join, uint64_t* scan_scratch, uint64_t* n_edges);
-hipError_t launch_graph_relax(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hipStream_t st, hipStream_t side,
-                              hipStream_t side2, hipEvent_t fork, hipEvent_t join, hipEvent_t join2);
+                        hipEvent_t fork, hipEvent_t join, uint64_t* ovf);
+hipError_t launch_graph_relax(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, uint64_t n_ovf, hipStream_t st,
+                              hipStream_t side, hipStream_t side2, hipEvent_t fork, hipEvent_t join, hipEvent_t join2);
 
 }  // namespace pbgpu

@@ -3032,7 +3032,8 @@ DEV uint64_t graph_dkey(double x) {
 // Two tiers by the read's record count (LDS sized to the tier, so the common
 // reads of <= GRAPH_NM_SMALL records run many blocks a CU): NM = GRAPH_NM_SMALL
 // takes those, NM = GRAPH_NMAX the rest.
-constexpr uint32_t GRAPH_SORT_BLOCK = 256, GRAPH_NM_SMALL = 1024, GRAPH_RELAX_MIN = 512;
+constexpr uint32_t GRAPH_SORT_BLOCK = 256, GRAPH_NM_SMALL = 1024, GRAPH_RELAX_MIN = 512, GRAPH_RELAX_PF = 6;
+static_assert(GRAPH_EBLK == 64, "k_graph_relax takes a node's block as one 64-lane load");
 template <uint32_t NM>
 DEV bool graph_tier(const GraphDev& G, uint32_t n) {
   if (n == 0 || n > G.nmax || n > GRAPH_NMAX) return false;
@@ -3079,28 +3080,30 @@ __global__ __launch_bounds__(GRAPH_SORT_BLOCK) void k_graph_sort(GraphDev G, uin
 // the batch; the window's nodes and the GE_SLOTS - GE_NODES positions after them
 // (implied span, error, name size, first GRAPH_U unitigs, read bounds) are staged
 // in LDS; a wave per node i, lanes j = i + 1 + lane, ... 64 at a time until the
-// reference's break (positions past the staged ones are read from HBM).  PASS 0
-// counts each node's candidates -- the pairs that are neither skipped nor past the
-// break, with names of two unitigs or more: an upper bound on its edges that needs
-// no name matching -- and an exclusive scan gives every node a region; PASS 1 runs
-// the whole test and writes the node's edges at the start of its region, in j
-// order, as {j's record index | (unitigs added) << 16, path increment}, and the
-// exact count over the capacity (ecnt).
+// reference's break (positions past the staged ones are read from HBM).  Each node
+// writes its first GRAPH_EBLK edges, in j order, as {j's record index | (unitigs
+// added) << 16, path increment} into a block of its own, and its exact count
+// (ecnt); a node with more (a few in a hundred) is listed, with its region past the
+// block.  OVF: a wave per listed node runs its scan again (from HBM) and writes the
+// edges past its block there.
 constexpr uint32_t GRAPH_U = 8;  // names of at most this many unitigs are matched in registers
 constexpr uint32_t GRAPH_NMAX_K = GRAPH_NMAX;  // reads of more records go to the host (LDS state)
 static_assert(GRAPH_NMAX_K <= 4096, "k_graph_relax matches roots by 12 bits and keeps 16-bit indices");
 constexpr uint32_t GE_NODES = 64, GE_SLOTS = 384, GE_BLOCK = 256;
 DEV bool graph_on_device(const GraphDev& G, uint32_t n) { return n > 0 && n <= G.nmax && n <= GRAPH_NMAX_K; }
-template <int PASS>
-__global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n_recs) {
+template <bool OVF>
+__global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n_recs, uint64_t n_ovf) {
   __shared__ double s_is[GE_SLOTS], s_ie[GE_SLOTS], s_er[GE_SLOTS], s_rl[GE_SLOTS];
   __shared__ uint32_t s_meta[GE_SLOTS], s_lpa[GE_SLOTS], s_end[GE_SLOTS], s_po[GE_SLOTS];
   __shared__ uint32_t s_u[GRAPH_U * GE_SLOTS];  // [u * GE_SLOTS + slot]
-  const uint64_t q0 = (uint64_t)blockIdx.x * GE_NODES;
-  if (q0 >= n_recs) return;
-  const uint32_t ns = (uint32_t)(n_recs - q0 < GE_SLOTS ? n_recs - q0 : GE_SLOTS);
+  constexpr uint32_t WAVES = GE_BLOCK / 64;
+  // OVF: slot t holds listed node blockIdx.x * WAVES + t; nothing else is staged
+  const uint64_t q0 = (uint64_t)blockIdx.x * (OVF ? WAVES : GE_NODES);
+  if (q0 >= (OVF ? n_ovf : n_recs)) return;
+  const uint64_t lim = OVF ? n_ovf : n_recs;
+  const uint32_t ns = (uint32_t)(lim - q0 < (OVF ? WAVES : GE_SLOTS) ? lim - q0 : (OVF ? WAVES : GE_SLOTS));
   for (uint32_t t = threadIdx.x; t < ns; t += GE_BLOCK) {
-    const uint64_t q = q0 + t;
+    const uint64_t q = OVF ? G.ovf_list[q0 + t] : q0 + t;
     const uint32_t r = G.recs[q].read;  // records are grouped per read
     const uint64_t e = G.rec_off[r + 1];
     const uint32_t n = (uint32_t)(e - G.rec_off[r]);
@@ -3116,8 +3119,8 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
   const uint32_t lane = threadIdx.x & 63;
   const double play = G.play, kd = (double)G.k;
   const uint32_t km1 = G.k - 1;
-  for (uint32_t ti = threadIdx.x >> 6; ti < GE_NODES && ti < ns; ti += GE_BLOCK / 64) {
-    const uint64_t q = q0 + ti;
+  for (uint32_t ti = threadIdx.x >> 6; ti < (OVF ? WAVES : GE_NODES) && ti < ns; ti += WAVES) {
+    const uint64_t q = OVF ? G.ovf_list[q0 + ti] : q0 + ti;
     const uint32_t qe = s_end[ti];
     const double ie_i = s_ie[ti], err_i = s_er[ti];
     uint32_t cnt = 0;
@@ -3127,7 +3130,8 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
 #pragma unroll
       for (uint32_t u = 0; u < GRAPH_U; ++u) a[u] = s_u[u * GE_SLOTS + ti];
       auto unit_i = [&](uint32_t t) -> uint32_t { return G.ounits[po_i + t]; };
-      const uint64_t e0 = PASS ? G.eoff[q] : 0;
+      uint2* const out = OVF ? G.eovf : G.edges;
+      const uint64_t ob = OVF ? G.eoff[q] - GRAPH_EBLK : q * GRAPH_EBLK;  // (mod 2^64)
       for (uint64_t j0 = q + 1; j0 < qe; j0 += 64) {
         const uint64_t j = j0 + lane;
         const bool act = j < qe;
@@ -3135,12 +3139,12 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
         // node j: staged, or (a scan past the window) from HBM
         double is_j, ie_j, er_j;
         uint32_t mj, lpa_j, po_j, bu[GRAPH_U];
-        if (sj < ns) {
+        if (!OVF && sj < ns) {
           is_j = s_is[sj]; ie_j = s_ie[sj]; er_j = s_er[sj]; mj = s_meta[sj]; lpa_j = s_lpa[sj]; po_j = s_po[sj];
 #pragma unroll
           for (uint32_t u = 0; u < GRAPH_U; ++u) bu[u] = s_u[u * GE_SLOTS + sj];
         } else {
-          const GDesc dj = G.desc[j];
+          const GDesc dj = G.desc[act ? j : q];
           is_j = dj.imp_s; ie_j = dj.imp_e; er_j = dj.err; mj = dj.idx | (dj.nsz << 16); lpa_j = dj.lp_add;
           po_j = (uint32_t)dj.poff;
 #pragma unroll
@@ -3154,11 +3158,6 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
         const uint32_t fb = bm ? (uint32_t)__ffsll((long long)bm) - 1 : 64u;
         const uint32_t sb = mj >> 16;
         const bool cand = act & !skip & (lane < fb) & (sa >= 2) & (sb >= 2);
-        if (!PASS) {  // the count pass: every pair that may be an edge (an upper bound)
-          cnt += (uint32_t)__builtin_popcountll(__ballot(cand));
-          if (bm) break;
-          continue;
-        }
         bool edge = false;
         int32_t nb = 0, common = 0;
         if (cand) {
@@ -3203,22 +3202,29 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
           }
         }
         const uint64_t em = __ballot(edge);
-        if (edge) {
-          const uint32_t at = cnt + (uint32_t)__builtin_popcountll(em & ((1ull << lane) - 1));
+        const uint32_t at = cnt + (uint32_t)__builtin_popcountll(em & ((1ull << lane) - 1));
+        if (edge & (OVF ? at >= GRAPH_EBLK : at < GRAPH_EBLK)) {
           // the edge's path increment (nb_mers or sr_cover of j minus the common k-mers) and
           // the unitigs it adds (overlap_graph.cc:47-53)
-          G.edges[e0 + at] = make_uint2((mj & 0xFFFFu) | ((sb - (uint32_t)nb) << 16), lpa_j - (uint32_t)common);
+          out[ob + at] = make_uint2((mj & 0xFFFFu) | ((sb - (uint32_t)nb) << 16), lpa_j - (uint32_t)common);
         }
         cnt += (uint32_t)__builtin_popcountll(em);
         if (bm) break;  // the reference's break
       }
     }
-    if (lane == 0) G.ecnt[q] = cnt;  // PASS 0: the node's capacity; PASS 1: its edges
+    if (!OVF && lane == 0) {
+      G.ecnt[q] = cnt;
+      if (cnt > GRAPH_EBLK) {  // its region past the block, and listed
+        G.eoff[q] = atomicAdd((unsigned long long*)&G.ovf[1], (unsigned long long)(cnt - GRAPH_EBLK));
+        G.ovf_list[atomicAdd((unsigned long long*)&G.ovf[0], 1ull)] = q;
+      }
+    }
   }
 }
 
 // k_graph_relax: a block of two waves per read, both streaming the read's edges
-// (64 at a time, two chunks in flight) node by node in sorted order.  Wave 0 relaxes
+// node by node in sorted order (each node's block, GRAPH_RELAX_PF nodes ahead in
+// flight; the rare edges past a block as they come).  Wave 0 relaxes
 // the longest paths: node i's edges update their own node j each (distinct j per
 // lane, as the reference's updates for one i are independent).  Wave 1 unites them
 // in j order (union_find.cc:13-23): the pre-scan roots are found in parallel (path
@@ -3237,7 +3243,6 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
   __shared__ double s_lsi[NM];
   __shared__ int32_t s_lp[NM], s_lun[NM];
   __shared__ int16_t s_lst[NM], s_lpv[NM];
-  __shared__ uint32_t s_es[NM];  // node's edges: start in the read's region
   __shared__ uint16_t s_idx[NM], s_ec[NM], s_par[NM], s_pos[NM];
   __shared__ uint8_t s_rank[NM], s_in[NM];
   const uint32_t r = blockIdx.x;
@@ -3259,41 +3264,42 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
     s_idx[p] = (uint16_t)it;
     s_pos[it] = (uint16_t)p;
     s_ec[p] = (uint16_t)G.ecnt[b + p];
-    s_es[p] = (uint32_t)(G.eoff[b + p] - G.eoff[b]);
     s_lp[it] = (int32_t)d.lp_add; s_lun[it] = (int32_t)d.nsz; s_lst[it] = -1; s_lpv[it] = -1;
     s_lsi[it] = d.imp_s; s_in[it] = 0;
     s_par[it] = (uint16_t)it; s_rank[it] = 0;
   }
   __syncthreads();
   const bool paths = tid < 64;
-  // the read's edge stream: c0 holds [k0, k0 + 64), c1 and c2 the next chunks (in flight)
-  const uint2* E = G.edges + G.eoff[b];
-  const uint32_t ne = (uint32_t)(G.eoff[b + n] - G.eoff[b]);
-  auto ld = [&](uint32_t k) -> uint2 { return k < ne ? E[k] : make_uint2(0u, 0u); };
-  uint2 c0 = ld(lane), c1 = ld(64 + lane), c2 = ld(128 + lane);
-  uint32_t k0 = 0;
+  // the nodes' edge blocks: pf[d] holds node p + d's (lanes past its count zero)
+  const uint2* EB = G.edges + b * GRAPH_EBLK;
+  auto ldb = [&](uint32_t p) -> uint2 {
+    const uint32_t ec = p < n ? s_ec[p] : 0u;
+    return lane < ec ? EB[(uint64_t)p * GRAPH_EBLK + lane] : make_uint2(0u, 0u);
+  };
+  uint2 pf[GRAPH_RELAX_PF];
+#pragma unroll
+  for (uint32_t d = 0; d < GRAPH_RELAX_PF; ++d) pf[d] = ldb(d);
 
 #ifdef PBGPU_PROF
   uint64_t pr_find = 0, pr_merge = 0, pr_paths = 0, pr_chunks = 0;
   const uint64_t pr0 = __builtin_amdgcn_s_memtime();
 #endif
-  uint32_t nx_ec = s_ec[0], nx_it = s_idx[0], nx_es = s_es[0];
+  uint32_t nx_ec = s_ec[0], nx_it = s_idx[0];
   for (uint32_t p = 0; p < n; ++p) {
     const uint32_t ec = nx_ec, it_i = nx_it;
-    uint32_t s = nx_es;
-    if (p + 1 < n) { nx_ec = s_ec[p + 1]; nx_it = s_idx[p + 1]; nx_es = s_es[p + 1]; }
+    if (p + 1 < n) { nx_ec = s_ec[p + 1]; nx_it = s_idx[p + 1]; }
+    const uint2 blk = pf[0];
+#pragma unroll
+    for (uint32_t d = 0; d + 1 < GRAPH_RELAX_PF; ++d) pf[d] = pf[d + 1];
+    pf[GRAPH_RELAX_PF - 1] = ldb(p + GRAPH_RELAX_PF);
     if (ec == 0) continue;
-    const uint32_t end = s + ec;
     int32_t lp_i = 0, lun_i = 0, lst_i = 0;
     double lsi_i = 0;
     if (paths) { lp_i = s_lp[it_i]; lun_i = s_lun[it_i]; lst_i = s_lst[it_i]; lsi_i = s_lsi[it_i]; }
-    while (s < end) {
-      while (s >= k0 + 64) {  // next chunk (past the unused end of a region); two ahead in flight
-        c0 = c1; c1 = c2; k0 += 64;
-        c2 = ld(k0 + 128 + lane);
-      }
-      const uint32_t k = k0 + lane;
-      const bool edge = (k >= s) & (k < end);
+    for (uint32_t k0 = 0; k0 < ec; k0 += 64) {
+      const bool edge = k0 + lane < ec;
+      // past the block: the node's overflow region (G.eoff)
+      const uint2 c0 = k0 == 0 ? blk : (edge ? G.eovf[G.eoff[b + p] + (k0 - GRAPH_EBLK) + lane] : make_uint2(0u, 0u));
       const uint32_t it_j = c0.x & 0xFFFFu;
       PROF_T(pa);
 #ifdef PBGPU_PROF
@@ -3368,7 +3374,6 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
         pr_merge += __builtin_amdgcn_s_memtime() - pb;
 #endif
       }
-      s = end < k0 + 64 ? end : k0 + 64;
       // a wave's LDS operations execute in order, so the next chunk's reads see this one's
       // writes; the fence keeps the compiler from moving memory operations across
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -3963,33 +3968,34 @@ void launch_graph_sizes(const GraphDev& G, uint64_t n_recs, uint32_t* sizes, uin
   launch_excl_scan(sizes, nullptr, n_recs, G.poff, scan_scratch, st);
 }
 hipError_t launch_graph(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hipStream_t st, hipStream_t side,
-                        hipEvent_t fork, hipEvent_t join, uint64_t* scan_scratch, uint64_t* n_edges) {
-  *n_edges = 0;
+                        hipEvent_t fork, hipEvent_t join, uint64_t* ovf) {
+  ovf[0] = ovf[1] = 0;
   if (!n_recs || !n_reads) return hipSuccess;
+  hipError_t e = hipMemsetAsync(G.ovf, 0, 16, st);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_graph_prep, dim3((uint32_t)std::min<uint64_t>((n_recs + 255) / 256, 65535)), dim3(256), 0, st,
                      G, n_recs);
   // the per-read sorts: the long reads' tier on the side stream, beside the short one.  A
   // failed fork or join would let a kernel read what the other stream still writes, so
   // each is checked (the caller raises)
-  hipError_t e = hipEventRecord(fork, st);
-  if (e == hipSuccess) e = hipStreamWaitEvent(side, fork, 0);
+  if ((e = hipEventRecord(fork, st)) == hipSuccess) e = hipStreamWaitEvent(side, fork, 0);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_graph_sort<GRAPH_NMAX>, dim3(n_reads), dim3(GRAPH_SORT_BLOCK), 0, side, G, n_reads);
   if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_graph_sort<GRAPH_NM_SMALL>, dim3(n_reads), dim3(GRAPH_SORT_BLOCK), 0, st, G, n_reads);
   if ((e = hipStreamWaitEvent(st, join, 0)) != hipSuccess) return e;
-  // every node's edges: counted, offsets, written
+  // every node's edges (its first GRAPH_EBLK) and the nodes with more
   const uint32_t eg = (uint32_t)((n_recs + GE_NODES - 1) / GE_NODES);
-  hipLaunchKernelGGL(k_graph_edges<0>, dim3(eg), dim3(GE_BLOCK), 0, st, G, n_recs);
-  launch_excl_scan(G.ecnt, nullptr, n_recs, G.eoff, scan_scratch, st);
-  if ((e = hipMemcpyAsync(n_edges, G.eoff + n_recs, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_graph_edges<false>, dim3(eg), dim3(GE_BLOCK), 0, st, G, n_recs, 0ull);
+  if ((e = hipMemcpyAsync(ovf, G.ovf, 16, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
   return hipStreamSynchronize(st);
 }
-hipError_t launch_graph_relax(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hipStream_t st, hipStream_t side,
-                              hipStream_t side2, hipEvent_t fork, hipEvent_t join, hipEvent_t join2) {
+hipError_t launch_graph_relax(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, uint64_t n_ovf, hipStream_t st,
+                              hipStream_t side, hipStream_t side2, hipEvent_t fork, hipEvent_t join, hipEvent_t join2) {
   if (!n_recs || !n_reads) return hipSuccess;
-  const uint32_t eg = (uint32_t)((n_recs + GE_NODES - 1) / GE_NODES);
-  hipLaunchKernelGGL(k_graph_edges<1>, dim3(eg), dim3(GE_BLOCK), 0, st, G, n_recs);
+  constexpr uint32_t W = GE_BLOCK / 64;
+  if (n_ovf) hipLaunchKernelGGL(k_graph_edges<true>, dim3((uint32_t)((n_ovf + W - 1) / W)), dim3(GE_BLOCK), 0, st, G,
+                                n_recs, n_ovf);
   // the long reads' relaxations each on a side stream of their own (their blocks are the
   // longest: > 2048 records, then > 1024), beside the short reads' on st
   hipError_t e = hipEventRecord(fork, st);

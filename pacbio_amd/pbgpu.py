@@ -148,7 +148,7 @@ class Stats(C.Structure):
                [(n, C.c_uint64) for n in ("g0_kept", "g0_hits", "g0_chains", "l0_hits", "l0_strands",
                                           "n_fine_hits", "n_fine_windows")] + [("ms_fine", C.c_double)] + \
                [(n, C.c_uint64) for n in ("fit_chains", "fit_points", "n_filter", "l0_points")] + \
-               [("ms_graph", C.c_double), ("graph_records", C.c_uint64), ("graph_candidates", C.c_uint64),
+               [("ms_graph", C.c_double), ("graph_records", C.c_uint64), ("graph_ovf_nodes", C.c_uint64),
                                                                     ("ms_host_order", C.c_double)]
 
     def as_dict(self):
