@@ -259,11 +259,6 @@ def main():
     if ndev > 0:
         local %= ndev
 
-    # B_rand (SURVEY 8(d)): random 64-B sector gathers over a 64 GB buffer, this GPU, this run
-    b_rand = pbgpu.measure_gather(local, 64 << 30) if not args.no_brand else None
-    # the same for random 512-B runs of 8-B words: the shape of k_group's occurrence-list reads
-    b_run = pbgpu.measure_gather(local, 64 << 30, unit_bytes=512) if not args.no_brand else None
-
     b_filt = b_table = None  # random 64-B gathers over buffers the size of the filter and the table
     k = 21 if args.workload == "C3" else 17
     n_pb = args.reads or PRESETS[args.workload]["n_pb"]
@@ -274,6 +269,41 @@ def main():
     ds.write(wd)
     t_gen = time.time() - t0
     sr_fa, pb_fa, ul_txt = (os.path.join(wd, f) for f in ("sr.fa", "pb.fa", "ul.txt"))
+    # ---- create_mega_reads (row f3, the aligner's production caller): the CLI over the
+    # same files, overlap graph / tiling on the GPU; its own clock (--timing wall_s: first
+    # batch read -> mega-reads file closed; the index build is before it), one warm-up run.
+    # First, before this process allocates on the GPU: with another process on the card
+    # that has made and freed tens of GB (the 64 GB gathers below), a run's hipMalloc now
+    # and then blocks for ~4 s (PBGPU_DEBUG_STALL reports); the CLI
+    # runs alone in production.
+    el_cmr, cmr_t, worst_cmr, cmr_runs = None, None, None, None
+    if args.cmr_steps > 0:
+        import json as _json
+        import subprocess
+        cmr = os.path.join(ROOT, "pacbio_amd", "bin", "create_mega_reads")
+        cflags = ["-s", "1M", "-m", str(k), "--psa-min", "13", "-k", "31", "-l", ul_txt, "-B", "15", "--max-count",
+                  "5000", "--stretch-cap", "10000", "-t", str(threads), "-r", sr_fa, "-p", pb_fa, "--timing",
+                  "--devices", str(local), "-o", os.path.join(wd, "mega_reads")]
+        walls, cmr_runs = [], []
+        for i in range(args.cmr_steps + 1):
+            # PBGPU_DEBUG_STALL=1: the library names any HIP call that blocked > 0.5 s (kept per run)
+            r = subprocess.run([cmr, *cflags], capture_output=True, text=True,
+                               env=dict(os.environ, PBGPU_DEBUG_STALL="1"))
+            if r.returncode:
+                raise RuntimeError(f"create_mega_reads failed: {r.stderr[-2000:]}")
+            cmr_t = _json.loads(r.stderr.strip().splitlines()[-1])
+            cmr_t["stalls"] = [ln for ln in r.stderr.splitlines() if ln.startswith("pbgpu stall")]
+            if i:
+                walls.append(cmr_t["wall_s"])
+                cmr_runs.append(cmr_t)
+        # the median run, the worst beside it (every run's wall is listed too)
+        el_cmr = comm.max(sorted(walls)[len(walls) // 2])
+        worst_cmr = comm.max(max(walls))
+    # B_rand (SURVEY 8(d)): random 64-B sector gathers over a 64 GB buffer, this GPU, this run
+    b_rand = pbgpu.measure_gather(local, 64 << 30) if not args.no_brand else None
+    # the same for random 512-B runs of 8-B words: the shape of k_group's occurrence-list reads
+    b_run = pbgpu.measure_gather(local, 64 << 30, unit_bytes=512) if not args.no_brand else None
+
     t0 = time.time()
     index = pbgpu.Index.from_fasta([sr_fa], k, psa_min=13, device=local)
     t_index = time.time() - t0
@@ -394,29 +424,6 @@ def main():
         _rm_parts(pouts[-1])
         prunner.close()
 
-    # ---- create_mega_reads (row f3, the aligner's production caller): the CLI over the
-    # same files, overlap graph / tiling on the GPU; its own clock (--timing wall_s: first
-    # batch read -> mega-reads file closed; the index build is before it), one warm-up run
-    el_cmr, cmr_t, worst_cmr, cmr_runs = None, None, None, None
-    if args.cmr_steps > 0:
-        import json as _json
-        import subprocess
-        cmr = os.path.join(ROOT, "pacbio_amd", "bin", "create_mega_reads")
-        cflags = ["-s", "1M", "-m", str(k), "--psa-min", "13", "-k", "31", "-l", ul_txt, "-B", "15", "--max-count",
-                  "5000", "--stretch-cap", "10000", "-t", str(threads), "-r", sr_fa, "-p", pb_fa, "--timing",
-                  "--devices", str(local), "-o", os.path.join(wd, "mega_reads")]
-        walls, cmr_runs = [], []
-        for i in range(args.cmr_steps + 1):
-            r = subprocess.run([cmr, *cflags], capture_output=True, text=True)
-            if r.returncode:
-                raise RuntimeError(f"create_mega_reads failed: {r.stderr[-2000:]}")
-            cmr_t = _json.loads(r.stderr.strip().splitlines()[-1])
-            if i:
-                walls.append(cmr_t["wall_s"])
-                cmr_runs.append(cmr_t)
-        # the median run, the worst beside it (every run's wall is listed too)
-        el_cmr = comm.max(sorted(walls)[len(walls) // 2])
-        worst_cmr = comm.max(max(walls))
     value_cmr = comm.sum(bases_rank) / el_cmr if el_cmr else None
 
     total_bases = comm.sum(bases_rank) * args.steps

@@ -1700,6 +1700,7 @@ static void graph_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   al->g_mtotal = cnt[0];
   al->g_munits_used = std::min<uint64_t>(cnt[1], tot);
   al->g_hosts = cnt[2];
+  al->acc.graph_host_reads += cnt[2];
   al->g_mc.ensure(cnt[0] + 1);
   launch_mega_pack(G, n, al->g_moff.p, al->g_mc.p, st);
   HIPCHK(hipGetLastError());

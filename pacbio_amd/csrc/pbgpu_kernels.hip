@@ -3083,7 +3083,7 @@ __global__ __launch_bounds__(GRAPH_SORT_BLOCK) void k_graph_sort(GraphDev G, uin
 // reference's break (positions past the staged ones are read from HBM).  Each node
 // writes its first GRAPH_EBLK edges, in j order, as {j's record index | (unitigs
 // added) << 16, path increment} into a block of its own, and its exact count
-// (ecnt); a node with more (a few in a hundred) is listed, with its region past the
+// (ecnt); a node with more (2 in 28k on C2) is listed, with its region past the
 // block.  OVF: a wave per listed node runs its scan again (from HBM) and writes the
 // edges past its block there.
 constexpr uint32_t GRAPH_U = 8;  // names of at most this many unitigs are matched in registers
@@ -3232,7 +3232,12 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
 // needs), a root already met, or i's own, is a no-op, the rest are merged in
 // registers with the reference's rank rule.  The unions never read the paths and
 // the paths never read the sets, so the two waves run unsynchronized until the end.
-// Node state lives in LDS by record index; tiers by records a read (NM).
+// Node state lives in LDS by record index, 18 B a node (four blocks a CU at NM =
+// 2048); tiers by records a read (NM).  Each node's record index and edge count come
+// from HBM, 64 positions a load, one load ahead.  The start node's implied start
+// (lstart_imp_s), which the reference compares as a double, is kept as its rank key:
+// the first sorted position of its imp_s value (the nodes are sorted by imp_s, so
+// a > b exactly when their keys are), NaN as RANK_NAN, which compares false.
 template <uint32_t NM>
 DEV bool graph_relax_tier(const GraphDev& G, uint32_t n) {
   if (!graph_on_device(G, n)) return false;
@@ -3240,11 +3245,12 @@ DEV bool graph_relax_tier(const GraphDev& G, uint32_t n) {
 }
 template <uint32_t NM>
 __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_reads) {
-  __shared__ double s_lsi[NM];
   __shared__ int32_t s_lp[NM], s_lun[NM];
   __shared__ int16_t s_lst[NM], s_lpv[NM];
-  __shared__ uint16_t s_idx[NM], s_ec[NM], s_par[NM], s_pos[NM];
-  __shared__ uint8_t s_rank[NM], s_in[NM];
+  __shared__ uint16_t s_lsk[NM], s_par[NM];
+  __shared__ uint8_t s_rank[NM], s_fl[NM];  // s_fl: 1 an edge into it, 2 an edge out of it
+  __shared__ uint64_t s_head[NM / 64];       // sorted positions starting an imp_s value
+  constexpr uint32_t RANK_NAN = 0xFFFFu;
   const uint32_t r = blockIdx.x;
   if (r >= n_reads) return;
   const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -3257,66 +3263,93 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
     return;
   }
   if (!graph_relax_tier<NM>(G, n)) return;
-  // node_info::reset (overlap_graph.hpp:24-34) of every node
-  for (uint32_t p = tid; p < n; p += 128) {
+  // node_info::reset (overlap_graph.hpp:24-34) of every node; the imp_s value heads
+  for (uint32_t p0 = 0; p0 < n; p0 += 128) {
+    const uint32_t p = p0 + tid;
+    bool head = false;
+    if (p < n) {
+      const GDesc d = G.desc[b + p];
+      const uint32_t it = d.idx;
+      head = p == 0 || !(G.desc[b + p - 1].imp_s == d.imp_s);  // (-0 == +0; a NaN heads its own)
+      s_lp[it] = (int32_t)d.lp_add; s_lun[it] = (int32_t)d.nsz; s_lst[it] = -1; s_lpv[it] = -1;
+      s_fl[it] = G.ecnt[b + p] ? 2 : 0;
+      s_par[it] = (uint16_t)it; s_rank[it] = 0;
+    }
+    const uint64_t hm = __ballot(head);
+    if (lane == 0 && p < NM) s_head[p >> 6] = hm;
+  }
+  __syncthreads();
+  for (uint32_t p = tid; p < n; p += 128) {  // rank key: the last head at or before p
     const GDesc d = G.desc[b + p];
-    const uint32_t it = d.idx;
-    s_idx[p] = (uint16_t)it;
-    s_pos[it] = (uint16_t)p;
-    s_ec[p] = (uint16_t)G.ecnt[b + p];
-    s_lp[it] = (int32_t)d.lp_add; s_lun[it] = (int32_t)d.nsz; s_lst[it] = -1; s_lpv[it] = -1;
-    s_lsi[it] = d.imp_s; s_in[it] = 0;
-    s_par[it] = (uint16_t)it; s_rank[it] = 0;
+    uint32_t w = p >> 6;
+    uint64_t m = s_head[w] & (~0ull >> (63 - (p & 63)));
+    while (!m) m = s_head[--w];  // position 0 is a head
+    s_lsk[d.idx] = d.imp_s != d.imp_s ? RANK_NAN : w * 64 + 63 - (uint32_t)__builtin_clzll(m);
   }
   __syncthreads();
   const bool paths = tid < 64;
+  // per sorted position: record index | edge count << 16; cur holds [c0, c0 + 64), nxt the
+  // next 64 (in flight)
+  auto ldw = [&](uint32_t p) -> uint32_t {
+    return p < n ? (G.desc[b + p].idx | (G.ecnt[b + p] << 16)) : 0u;
+  };
+  uint32_t c0 = 0, cur = ldw(lane), nxt = ldw(64 + lane);
+  auto wd = [&](uint32_t x) -> uint32_t {  // x wave-uniform, in [c0, c0 + 128)
+    const uint32_t o = x - c0;
+    return (uint32_t)__builtin_amdgcn_readlane((int)(o < 64 ? cur : nxt), (int)(o & 63));
+  };
   // the nodes' edge blocks: pf[d] holds node p + d's (lanes past its count zero)
   const uint2* EB = G.edges + b * GRAPH_EBLK;
-  auto ldb = [&](uint32_t p) -> uint2 {
-    const uint32_t ec = p < n ? s_ec[p] : 0u;
+  auto ldb = [&](uint32_t p, uint32_t ec) -> uint2 {
     return lane < ec ? EB[(uint64_t)p * GRAPH_EBLK + lane] : make_uint2(0u, 0u);
   };
   uint2 pf[GRAPH_RELAX_PF];
 #pragma unroll
-  for (uint32_t d = 0; d < GRAPH_RELAX_PF; ++d) pf[d] = ldb(d);
+  for (uint32_t d = 0; d < GRAPH_RELAX_PF; ++d) pf[d] = ldb(d, wd(d) >> 16);
 
 #ifdef PBGPU_PROF
   uint64_t pr_find = 0, pr_merge = 0, pr_paths = 0, pr_chunks = 0;
   const uint64_t pr0 = __builtin_amdgcn_s_memtime();
 #endif
-  uint32_t nx_ec = s_ec[0], nx_it = s_idx[0];
   for (uint32_t p = 0; p < n; ++p) {
-    const uint32_t ec = nx_ec, it_i = nx_it;
-    if (p + 1 < n) { nx_ec = s_ec[p + 1]; nx_it = s_idx[p + 1]; }
+    if (p - c0 == 64) {
+      c0 += 64; cur = nxt;
+      nxt = ldw(c0 + 64 + lane);
+    }
+    const uint32_t w = wd(p), ec = w >> 16, it_i = w & 0xFFFFu;
     const uint2 blk = pf[0];
 #pragma unroll
     for (uint32_t d = 0; d + 1 < GRAPH_RELAX_PF; ++d) pf[d] = pf[d + 1];
-    pf[GRAPH_RELAX_PF - 1] = ldb(p + GRAPH_RELAX_PF);
+    pf[GRAPH_RELAX_PF - 1] = ldb(p + GRAPH_RELAX_PF, wd(p + GRAPH_RELAX_PF) >> 16);
     if (ec == 0) continue;
     int32_t lp_i = 0, lun_i = 0, lst_i = 0;
-    double lsi_i = 0;
-    if (paths) { lp_i = s_lp[it_i]; lun_i = s_lun[it_i]; lst_i = s_lst[it_i]; lsi_i = s_lsi[it_i]; }
+    uint32_t lsk_i = 0;
+    if (paths) { lp_i = s_lp[it_i]; lun_i = s_lun[it_i]; lst_i = s_lst[it_i]; lsk_i = s_lsk[it_i]; }
     for (uint32_t k0 = 0; k0 < ec; k0 += 64) {
       const bool edge = k0 + lane < ec;
       // past the block: the node's overflow region (G.eoff)
-      const uint2 c0 = k0 == 0 ? blk : (edge ? G.eovf[G.eoff[b + p] + (k0 - GRAPH_EBLK) + lane] : make_uint2(0u, 0u));
-      const uint32_t it_j = c0.x & 0xFFFFu;
+      const uint2 ce = k0 == 0 ? blk : (edge ? G.eovf[G.eoff[b + p] + (k0 - GRAPH_EBLK) + lane] : make_uint2(0u, 0u));
+      const uint32_t it_j = ce.x & 0xFFFFu;
       PROF_T(pa);
 #ifdef PBGPU_PROF
       ++pr_chunks;
 #endif
       if (paths) {
         if (edge) {  // node_info update (overlap_graph.cc:41-56); this lane owns node j
-          s_in[it_j] = 1;  // an edge into j: not a start node
-          const int32_t nlpath = (int32_t)((uint32_t)lp_i + c0.y);
+          s_fl[it_j] |= 1;  // an edge into j: not a start node
+          const int32_t nlpath = (int32_t)((uint32_t)lp_i + ce.y);
           const int32_t lp_j = s_lp[it_j];
-          const bool upd = nlpath > lp_j || (nlpath == lp_j && (s_lst[it_j] == -1 || lsi_i > s_lsi[it_j]));
+          bool upd = nlpath > lp_j;
+          if (!upd && nlpath == lp_j) {  // (lstart_imp_s: lsk_i > lsk_j, neither NaN)
+            const uint32_t lsk_j = s_lsk[it_j];
+            upd = s_lst[it_j] == -1 || ((lsk_i != RANK_NAN) & (lsk_j != RANK_NAN) & (lsk_i > lsk_j));
+          }
           if (upd) {
             s_lp[it_j] = nlpath;
             s_lst[it_j] = (int16_t)(lst_i == -1 ? (int32_t)it_i : lst_i);
-            s_lsi[it_j] = lsi_i;
+            s_lsk[it_j] = (uint16_t)lsk_i;
             s_lpv[it_j] = (int16_t)it_i;
-            s_lun[it_j] = lun_i + (int32_t)(c0.x >> 16);
+            s_lun[it_j] = lun_i + (int32_t)(ce.x >> 16);
           }
         }
 #ifdef PBGPU_PROF
@@ -3395,7 +3428,7 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
     uint32_t q = i;
     while (s_par[q] != q) q = s_par[q];
     // start node: no edge into it; end node: no edge out of it
-    const uint32_t fl = (s_in[i] ? 0u : GRAPH_START) | (s_ec[s_pos[i]] ? 0u : GRAPH_END);
+    const uint32_t fl = (s_fl[i] & 1 ? 0u : GRAPH_START) | (s_fl[i] & 2 ? 0u : GRAPH_END);
     G.out[b + i] = GraphNode{s_lp[i], s_lst[i], s_lpv[i], s_lun[i], q, fl};
   }
 }

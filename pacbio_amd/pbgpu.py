@@ -149,7 +149,8 @@ class Stats(C.Structure):
                                           "n_fine_hits", "n_fine_windows")] + [("ms_fine", C.c_double)] + \
                [(n, C.c_uint64) for n in ("fit_chains", "fit_points", "n_filter", "l0_points")] + \
                [("ms_graph", C.c_double), ("graph_records", C.c_uint64), ("graph_ovf_nodes", C.c_uint64),
-                                                                    ("ms_host_order", C.c_double)]
+                                                                    ("ms_host_order", C.c_double),
+                                                                    ("graph_host_reads", C.c_uint64)]
 
     def as_dict(self):
         d = {n: getattr(self, n) for n, _ in self._fields_ if not n.startswith("kernel_")}

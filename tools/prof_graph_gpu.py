@@ -14,10 +14,11 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reads", type=int, default=10000)
+    ap.add_argument("--workload", default="C2", help="a tools/synth.py preset (C4r: C4's repeat model and read lengths)")
     a = ap.parse_args()
     from pacbio_amd import pbgpu
     from tools.synth import Dataset
-    ds = Dataset("C2", seed=42, threads=16, n_pb=a.reads)
+    ds = Dataset(a.workload, seed=42, threads=16, n_pb=a.reads)
     names = [n.decode() for n in ds.sr_names()]
     ix = pbgpu.Index.from_records(ds.sr_names(), ds.sr_seqs(), 17)
     ul = [int(x) for x in ds.unitig_lengths]
@@ -39,7 +40,11 @@ def main():
     pbgpu.device_synchronize(0)
     wall = time.time() - t
     st = al.stats()
-    print(f"align_resident {wall * 1e3:.1f} ms, graph {st['ms_graph']:.2f} ms over {st['graph_records']} records")
+    print(f"align_resident {wall * 1e3:.1f} ms, graph {st['ms_graph']:.2f} ms over {st['graph_records']} records, "
+          f"{st['graph_ovf_nodes']} nodes of more than 64 edges")
+    print(f"{a.workload}: {a.reads} reads, {st['graph_records'] / max(1, a.reads):.0f} records a read, "
+          f"{st['graph_host_reads']} left to the host graph (> 4096 records): "
+          f"{100.0 * st['graph_host_reads'] / max(1, a.reads):.3f}%")
     if f is not None:
         f(buf, 112, 1)
         for tier, base in (("<= 1024 records", 80), ("> 1024 records", 96)):
