@@ -78,6 +78,17 @@ def _spawn_ranks(n, argv):
     return rc
 
 
+def _device_count():
+    """GPUs visible, counted in a child process: this one makes no HIP call before its
+    create_mega_reads leg (see there)."""
+    import subprocess
+    code = f"import sys; sys.path.insert(0, {ROOT!r}); from pacbio_amd import pbgpu; print(pbgpu.lib().pbgpu_device_count())"
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True)
+    if r.returncode:
+        raise RuntimeError(f"counting GPUs failed: {r.stderr[-2000:]}")
+    return int(r.stdout.split()[-1])
+
+
 def _check_world(gpus):
     """`--gpus N` and the launcher's WORLD_SIZE must agree.  Returns True when this
     process is a rank (launched by torchrun, by _spawn_ranks, or N == 1) and False
@@ -255,7 +266,7 @@ def main():
     from tools.synth import Dataset, PRESETS
 
     # more ranks than visible GPUs (a rehearsal of the N>1 launch on a 1-GPU box): ranks share
-    ndev = pbgpu.lib().pbgpu_device_count()
+    ndev = _device_count()
     if ndev > 0:
         local %= ndev
 
@@ -272,10 +283,9 @@ def main():
     # ---- create_mega_reads (row f3, the aligner's production caller): the CLI over the
     # same files, overlap graph / tiling on the GPU; its own clock (--timing wall_s: first
     # batch read -> mega-reads file closed; the index build is before it), one warm-up run.
-    # First, before this process allocates on the GPU: with another process on the card
-    # that has made and freed tens of GB (the 64 GB gathers below), a run's hipMalloc now
-    # and then blocks for ~4 s (PBGPU_DEBUG_STALL reports); the CLI
-    # runs alone in production.
+    # First, before this process makes any HIP call: with another process holding a HIP
+    # context on the card, a run's hipMalloc now and then blocks for ~4 s
+    # (PBGPU_DEBUG_STALL reports); the CLI runs alone in production.
     el_cmr, cmr_t, worst_cmr, cmr_runs = None, None, None, None
     if args.cmr_steps > 0:
         import json as _json

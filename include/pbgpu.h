@@ -515,6 +515,10 @@ typedef struct {
    * so these are 0 unless a batch needs more than 2x the first's density) */
   uint64_t n_device_allocs, n_device_allocs_late;
   uint64_t n_pinned_allocs, n_pinned_allocs_late;
+  /* bytes of those device allocations, and the seconds the workers spent in
+   * hipMalloc / hipFree (a call that blocks shows here) */
+  uint64_t device_alloc_bytes;
+  double   alloc_seconds;
 } pbgpu_run_stats;
 
 pbgpu_status pbgpu_run(pbgpu_index* const* indexes, size_t n_indexes, const pbgpu_align_params* params,

@@ -144,7 +144,9 @@ void run_parallel(int threads, F&& work) {
 // a per-batch buffer that must grow is then sized for a full batch with 2x
 // headroom (a ramped first batch holds few reads, so its hit and record
 // densities vary), and the full batches that follow allocate nothing.
-inline thread_local uint64_t tl_dev_allocs = 0, tl_pinned_allocs = 0;
+inline thread_local uint64_t tl_dev_allocs = 0, tl_pinned_allocs = 0, tl_dev_bytes = 0;
+inline thread_local double tl_alloc_s = 0;  // seconds in hipMalloc / hipFree of dbufs
+inline double mono_s() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 inline thread_local double tl_grow_scale = 1.0;
 inline size_t grow_target(size_t cnt) {
   const double s = tl_grow_scale;
@@ -158,13 +160,22 @@ struct dbuf {
   dbuf(const dbuf&) = delete;
   dbuf& operator=(const dbuf&) = delete;
   ~dbuf() { release(); }
-  void release() { if (p) HIPFREE(hipFree(p)); p = nullptr; n = 0; }
+  void release() {
+    if (p) {
+      const double t = mono_s();
+      HIPFREE(hipFree(p));
+      tl_alloc_s += mono_s() - t;
+    }
+    p = nullptr; n = 0;
+  }
   __attribute__((noinline)) void alloc(size_t cnt) {
     release();
     if (cnt) {
       if (stall_debug_allocs()) alloc_note(cnt * sizeof(T), __builtin_return_address(0));
+      const double t = mono_s();
       HIPCHK(hipMalloc((void**)&p, cnt * sizeof(T)));
-      ++tl_dev_allocs;
+      tl_alloc_s += mono_s() - t;
+      ++tl_dev_allocs; tl_dev_bytes += cnt * sizeof(T);
       n = cnt;
     }
   }
@@ -180,8 +191,10 @@ struct dbuf {
     T* q = nullptr;
     const size_t nn = std::max(tl_grow_scale > 1.0 ? grow_target(cnt) : cnt, n + n / 2);
     if (stall_debug_allocs()) alloc_note(nn * sizeof(T), __builtin_return_address(0));
+    const double t = mono_s();
     HIPCHK(hipMalloc((void**)&q, nn * sizeof(T)));
-    ++tl_dev_allocs;
+    tl_alloc_s += mono_s() - t;
+    ++tl_dev_allocs; tl_dev_bytes += nn * sizeof(T);
     if (p && keep) HIPCHK(hipMemcpyAsync(q, p, keep * sizeof(T), hipMemcpyDeviceToDevice, st));
     HIPCHK(hipStreamSynchronize(st));
     release();

@@ -653,7 +653,8 @@ static void run_part(pbgpu_runner* R, RunPart& part, const pbgpu_run_params* run
         pbgpu_read_batch rb{b->n(), b->seq.p, b->off.data(), b->names.data(), b->name_off.data()};
         // buffers that grow in this batch are sized for a full batch (pbgpu_host.h)
         tl_grow_scale = std::min(64.0, std::max(1.0, b->grow_scale));
-        const uint64_t a0 = tl_dev_allocs, p0 = tl_pinned_allocs;
+        const uint64_t a0 = tl_dev_allocs, p0 = tl_pinned_allocs, by0 = tl_dev_bytes;
+        const double as0 = tl_alloc_s;
         const double t0 = now_s();
         upload_reads_into(al, &rb, rd);
         const double t1 = now_s();
@@ -720,6 +721,8 @@ static void run_part(pbgpu_runner* R, RunPart& part, const pbgpu_run_params* run
           S.n_records += al->last_records;
           S.n_device_allocs += tl_dev_allocs - a0;
           S.n_pinned_allocs += tl_pinned_allocs - p0;
+          S.device_alloc_bytes += tl_dev_bytes - by0;
+          S.alloc_seconds += tl_alloc_s - as0;
           if (!first) {
             S.n_device_allocs_late += tl_dev_allocs - a0;
             S.n_pinned_allocs_late += tl_pinned_allocs - p0;
@@ -892,6 +895,7 @@ static void runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_s
     S.writer_idle_seconds += x.writer_idle_seconds;
     S.n_device_allocs += x.n_device_allocs; S.n_device_allocs_late += x.n_device_allocs_late;
     S.n_pinned_allocs += x.n_pinned_allocs; S.n_pinned_allocs_late += x.n_pinned_allocs_late;
+    S.device_alloc_bytes += x.device_alloc_bytes; S.alloc_seconds += x.alloc_seconds;
   }
   S.open_seconds = t_open;
   const double tc = now_s();

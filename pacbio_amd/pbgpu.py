@@ -91,7 +91,8 @@ class RunStats(C.Structure):
                                           "d2h_seconds", "write_seconds", "writer_idle_seconds", "open_seconds",
                                           "close_seconds")] + \
                [(n, C.c_uint64) for n in ("n_device_allocs", "n_device_allocs_late", "n_pinned_allocs",
-                                          "n_pinned_allocs_late")]
+                                          "n_pinned_allocs_late", "device_alloc_bytes")] + \
+               [("alloc_seconds", C.c_double)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

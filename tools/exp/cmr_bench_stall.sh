@@ -8,4 +8,4 @@ timeout -k 10 500 python -u bench.py --steps 1 --warmup 0 --device-steps 1 --par
 python3 -c "
 import json; d=json.load(open('gpurun_out/cmr_stall_$TAG.json'))
 print('cmr', d['value_create_mega_reads']/1e9, d['create_mega_reads_walls_s'])
-for r in d['create_mega_reads_runs']: print(r['wall_s'], r['align_s'], r['stalls'])"
+for r in d['create_mega_reads_runs']: print(r['wall_s'], r['align_s'], r.get('alloc_s'), r.get('device_alloc_bytes'), r.get('device_allocs'), r['stalls'])"
