@@ -261,7 +261,7 @@ typedef struct {
   uint64_t graph_ovf_nodes;
   /* host time ordering a batch's reads for the group stage (the GPU waits for it) */
   double   ms_host_order;
-  /* overlap graph: reads left to the host graph (more than 4096 records) */
+  /* overlap graph: reads left to the host graph (more than 8192 records) */
   uint64_t graph_host_reads;
 } pbgpu_stats;
 pbgpu_status pbgpu_aligner_get_stats(const pbgpu_aligner* al, pbgpu_stats* s);

@@ -113,6 +113,10 @@ bool stall_debug_allocs() {
   static const bool on = getenv("PBGPU_DEBUG_STALL") && atoi(getenv("PBGPU_DEBUG_STALL")) >= 2;
   return on;
 }
+double stall_threshold_s() {
+  static const double t = getenv("PBGPU_DEBUG_STALL_MS") ? atof(getenv("PBGPU_DEBUG_STALL_MS")) * 1e-3 : 0.5;
+  return t;
+}
 void stall_report(double seconds, const char* call, const char* file, int line) {
   fprintf(stderr, "pbgpu stall: %.3f s in %s (%s:%d)\n", seconds, call, file, line);
 }

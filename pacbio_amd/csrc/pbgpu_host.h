@@ -43,6 +43,7 @@ struct hip_error : std::runtime_error {
 // (file:line and the call), to find where a slow run waits
 bool stall_debug();
 bool stall_debug_allocs();  // PBGPU_DEBUG_STALL=2: also every device allocation
+double stall_threshold_s();  // PBGPU_DEBUG_STALL_MS: the report threshold (default 500 ms)
 void stall_report(double seconds, const char* call, const char* file, int line);
 // PBGPU_DEBUG_STALL=2: one line per device allocation with its size and the caller's
 // offset in libpbgpu.so (nm -C maps it to the function that grew the buffer)
@@ -54,7 +55,7 @@ void alloc_note(size_t bytes, const void* caller);
     hipError_t _e = (x);                                                                               \
     if (_dbg) {                                                                                        \
       const double _dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - _t0).count(); \
-      if (_dt > 0.5) stall_report(_dt, #x, __FILE__, __LINE__);                                        \
+      if (_dt > stall_threshold_s()) stall_report(_dt, #x, __FILE__, __LINE__);                                        \
     }                                                                                                  \
     if (_e != hipSuccess) {                                                                            \
       char _b[512];                                                                                    \
@@ -70,7 +71,7 @@ void alloc_note(size_t bytes, const void* caller);
     (void)(x);                                                                                         \
     if (_dbg) {                                                                                        \
       const double _dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - _t0).count(); \
-      if (_dt > 0.5) stall_report(_dt, #x, __FILE__, __LINE__);                                        \
+      if (_dt > stall_threshold_s()) stall_report(_dt, #x, __FILE__, __LINE__);                                        \
     }                                                                                                  \
   } while (0)
 struct bad_input : std::runtime_error { using std::runtime_error::runtime_error; };
@@ -145,7 +146,8 @@ void run_parallel(int threads, F&& work) {
 // headroom (a ramped first batch holds few reads, so its hit and record
 // densities vary), and the full batches that follow allocate nothing.
 inline thread_local uint64_t tl_dev_allocs = 0, tl_pinned_allocs = 0, tl_dev_bytes = 0;
-inline thread_local double tl_alloc_s = 0;  // seconds in hipMalloc / hipFree of dbufs
+inline thread_local double tl_alloc_s = 0;   // seconds in hipMalloc / hipFree of dbufs
+inline thread_local double tl_pinned_s = 0;  // seconds in the run path's hipHostMalloc / hipHostFree
 inline double mono_s() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 inline thread_local double tl_grow_scale = 1.0;
 inline size_t grow_target(size_t cnt) {

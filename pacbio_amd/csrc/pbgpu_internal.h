@@ -198,7 +198,7 @@ struct GraphNode {
 };
 static_assert(sizeof(GraphNode) == 24, "GraphNode layout must match pbgpu_graph_node");
 constexpr uint32_t GRAPH_START = 1u, GRAPH_END = 2u, GRAPH_HOST = 1u << 31;  // flags
-constexpr uint32_t GRAPH_NMAX = 4096;  // records of a read traversed on the device (more: GRAPH_HOST)
+constexpr uint32_t GRAPH_NMAX = 8192;  // records of a read traversed on the device (more: GRAPH_HOST)
 // a record in the per-read sorted order (k_graph's ring of sorted positions)
 struct GDesc {
   double imp_s, imp_e, err;

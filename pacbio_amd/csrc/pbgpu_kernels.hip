@@ -3029,15 +3029,16 @@ DEV uint64_t graph_dkey(double x) {
 }
 // per read: records by (imp_s, imp_e), ties in record order (the host's stable_sort of
 // sort_nodes), written out as descriptors in that order
-// Two tiers by the read's record count (LDS sized to the tier, so the common
+// Three tiers by the read's record count (LDS sized to the tier, so the common
 // reads of <= GRAPH_NM_SMALL records run many blocks a CU): NM = GRAPH_NM_SMALL
-// takes those, NM = GRAPH_NMAX the rest.
-constexpr uint32_t GRAPH_SORT_BLOCK = 256, GRAPH_NM_SMALL = 1024, GRAPH_RELAX_MIN = 512, GRAPH_RELAX_PF = 6;
+// takes those, NM = GRAPH_NM_MID the reads up to it, NM = GRAPH_NMAX the rest.
+constexpr uint32_t GRAPH_SORT_BLOCK = 256, GRAPH_NM_SMALL = 1024, GRAPH_NM_MID = 4096, GRAPH_RELAX_MIN = 512,
+                   GRAPH_RELAX_PF = 6;
 static_assert(GRAPH_EBLK == 64, "k_graph_relax takes a node's block as one 64-lane load");
 template <uint32_t NM>
 DEV bool graph_tier(const GraphDev& G, uint32_t n) {
   if (n == 0 || n > G.nmax || n > GRAPH_NMAX) return false;
-  return n <= NM && (NM == GRAPH_NM_SMALL || n > GRAPH_NM_SMALL);
+  return n <= NM && (NM == GRAPH_NM_SMALL || n > (NM == GRAPH_NM_MID ? GRAPH_NM_SMALL : GRAPH_NM_MID));
 }
 template <uint32_t NM>
 __global__ __launch_bounds__(GRAPH_SORT_BLOCK) void k_graph_sort(GraphDev G, uint32_t n_reads) {
@@ -3088,7 +3089,9 @@ __global__ __launch_bounds__(GRAPH_SORT_BLOCK) void k_graph_sort(GraphDev G, uin
 // edges past its block there.
 constexpr uint32_t GRAPH_U = 8;  // names of at most this many unitigs are matched in registers
 constexpr uint32_t GRAPH_NMAX_K = GRAPH_NMAX;  // reads of more records go to the host (LDS state)
-static_assert(GRAPH_NMAX_K <= 4096, "k_graph_relax matches roots by 12 bits and keeps 16-bit indices");
+constexpr uint32_t GRAPH_ROOT_BITS = 13;  // k_graph_relax matches roots by this many bits
+static_assert(GRAPH_NMAX_K <= (1u << GRAPH_ROOT_BITS) && GRAPH_NMAX_K < 0x8000u,
+              "k_graph_relax matches roots by GRAPH_ROOT_BITS and keeps 15-bit indices");
 constexpr uint32_t GE_NODES = 64, GE_SLOTS = 384, GE_BLOCK = 256;
 DEV bool graph_on_device(const GraphDev& G, uint32_t n) { return n > 0 && n <= G.nmax && n <= GRAPH_NMAX_K; }
 template <bool OVF>
@@ -3377,10 +3380,10 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
 #endif
         uint64_t fm = fo;
         if (fo & (fo - 1)) {  // two or more foreign edges: the first lane of each root
-          // the edge lanes holding the same root: a ballot per bit of R (node indices < 2^12)
+          // the edge lanes holding the same root: a ballot per bit of R (node indices < 2^13)
           uint64_t same = fo;
 #pragma unroll
-          for (uint32_t bit = 0; bit < 12; ++bit) {
+          for (uint32_t bit = 0; bit < GRAPH_ROOT_BITS; ++bit) {
             const uint64_t bb = __ballot((R >> bit) & 1u);
             same &= ((R >> bit) & 1u) ? bb : ~bb;
           }
@@ -3569,10 +3572,12 @@ __global__ __launch_bounds__(64) void k_mega(GraphDev G, uint32_t n_reads) {
   }
   const bool serial = __ballot(odd) != 0;
   if (!serial) {
+    constexpr uint32_t RW = GRAPH_NMAX / 64 / 64;  // root words a lane: lane * RW ...
+    static_assert(GRAPH_NMAX == 64 * 64 * RW, "whole root words a lane");
     __shared__ uint64_t s_roots[GRAPH_NMAX / 64];  // the winners' roots (node indices)
     __shared__ uint32_t s_rpre[GRAPH_NMAX / 64];
-    static_assert(GRAPH_NMAX == 64 * 64, "one root word a lane");
-    s_roots[lane] = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < RW; ++t) s_roots[lane * RW + t] = 0;
     __syncthreads();
     // a candidate wins its root if no candidate of the root has a larger (lpath,
     // density) and none before it an equal one: where the reference's fold (replace on
@@ -3605,14 +3610,16 @@ __global__ __launch_bounds__(64) void k_mega(GraphDev G, uint32_t n_reads) {
     __threadfence_block();
     __syncthreads();
     // a winner's component index = its root's rank among the winners' roots
-    const uint32_t pc = (uint32_t)__builtin_popcountll(s_roots[lane]);
+    uint32_t pcw[RW], pc = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < RW; ++t) { pcw[t] = (uint32_t)__builtin_popcountll(s_roots[lane * RW + t]); pc += pcw[t]; }
     uint32_t incl = pc;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t v = __shfl_up(incl, o, 64);
       if (lane >= (uint32_t)o) incl += v;
     }
-    s_rpre[lane] = incl - pc;
+    for (uint32_t t = 0, acc = incl - pc; t < RW; ++t) { s_rpre[lane * RW + t] = acc; acc += pcw[t]; }
     m = (uint32_t)__shfl(incl, 63, 64);
     __syncthreads();
     for (uint32_t c = lane; c < nc; c += 64)
@@ -4008,12 +4015,13 @@ hipError_t launch_graph(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hi
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_graph_prep, dim3((uint32_t)std::min<uint64_t>((n_recs + 255) / 256, 65535)), dim3(256), 0, st,
                      G, n_recs);
-  // the per-read sorts: the long reads' tier on the side stream, beside the short one.  A
+  // the per-read sorts: the long reads' tiers on the side stream, beside the short one.  A
   // failed fork or join would let a kernel read what the other stream still writes, so
   // each is checked (the caller raises)
   if ((e = hipEventRecord(fork, st)) == hipSuccess) e = hipStreamWaitEvent(side, fork, 0);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_graph_sort<GRAPH_NMAX>, dim3(n_reads), dim3(GRAPH_SORT_BLOCK), 0, side, G, n_reads);
+  hipLaunchKernelGGL(k_graph_sort<GRAPH_NM_MID>, dim3(n_reads), dim3(GRAPH_SORT_BLOCK), 0, side, G, n_reads);
   if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_graph_sort<GRAPH_NM_SMALL>, dim3(n_reads), dim3(GRAPH_SORT_BLOCK), 0, st, G, n_reads);
   if ((e = hipStreamWaitEvent(st, join, 0)) != hipSuccess) return e;
@@ -4029,14 +4037,15 @@ hipError_t launch_graph_relax(const GraphDev& G, uint32_t n_reads, uint64_t n_re
   constexpr uint32_t W = GE_BLOCK / 64;
   if (n_ovf) hipLaunchKernelGGL(k_graph_edges<true>, dim3((uint32_t)((n_ovf + W - 1) / W)), dim3(GE_BLOCK), 0, st, G,
                                 n_recs, n_ovf);
-  // the long reads' relaxations each on a side stream of their own (their blocks are the
-  // longest: > 2048 records, then > 1024), beside the short reads' on st
+  // the long reads' relaxations on side streams (their blocks are the longest: > 4096
+  // records then > 2048 on one, > 1024 on the other), beside the short reads' on st
   hipError_t e = hipEventRecord(fork, st);
   if (e == hipSuccess) e = hipStreamWaitEvent(side, fork, 0);
   if (e == hipSuccess) e = hipStreamWaitEvent(side2, fork, 0);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_graph_relax<GRAPH_NMAX>, dim3(n_reads), dim3(128), 0, side, G, n_reads);
-  hipLaunchKernelGGL(k_graph_relax<GRAPH_NMAX / 2>, dim3(n_reads), dim3(128), 0, side2, G, n_reads);
+  hipLaunchKernelGGL(k_graph_relax<GRAPH_NMAX / 2>, dim3(n_reads), dim3(128), 0, side, G, n_reads);
+  hipLaunchKernelGGL(k_graph_relax<GRAPH_NMAX / 4>, dim3(n_reads), dim3(128), 0, side2, G, n_reads);
   if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
   if ((e = hipEventRecord(join2, side2)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_graph_relax<GRAPH_NM_SMALL>, dim3(n_reads), dim3(128), 0, st, G, n_reads);

@@ -36,6 +36,13 @@
 
 namespace {
 
+// PBGPU_TIMELINE=1: one stderr line per batch and stage (seconds since the run began), to
+// see where a run's wall goes (fill, first-batch allocations, tail)
+static bool timeline() {
+  static const bool on = getenv("PBGPU_TIMELINE") && atoi(getenv("PBGPU_TIMELINE"));
+  return on;
+}
+static double g_tl0 = 0;
 double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -101,10 +108,12 @@ struct PinnedVec {  // growable pinned byte buffer (H2D at full PCIe rate, no st
     if (c <= cap) return;
     const size_t nc = std::max(c, cap + cap / 2);
     char* q = nullptr;
+    const double t0 = mono_s();
     HIPCHK(hipHostMalloc((void**)&q, nc, hipHostMallocDefault));
     ++tl_pinned_allocs;
     if (n) memcpy(q, p, n);
     if (p) HIPFREE(hipHostFree(p));
+    tl_pinned_s += mono_s() - t0;
     p = q;
     cap = nc;
   }
@@ -400,7 +409,9 @@ class TextPool {
       out.cap = 0;
       const size_t cap = grow_target(need);
       hipError_t e = hipSuccess;
+      const double t0 = mono_s();
       HIPFREE(e = hipHostMalloc((void**)&out.p, cap, hipHostMallocDefault));
+      tl_pinned_s += mono_s() - t0;
       if (e != hipSuccess) { put(Pinned{}, false); HIPCHK(e); }
       ++tl_pinned_allocs;
       out.cap = cap;
@@ -504,6 +515,9 @@ struct RecordsView {
   static void room(PinnedVec& v, uint64_t bytes) {
     if (v.cap < bytes) v.reserve(std::max<uint64_t>(grow_target(std::max<uint64_t>(bytes, 1)), 2 * bytes));
   }
+  static void room_fixed(PinnedVec& v, uint64_t bytes) {  // (not scaled with the batch)
+    if (v.cap < bytes) v.reserve(std::max<uint64_t>(bytes + bytes / 4, 2 * v.cap));
+  }
   void download(pbgpu_aligner* al) {
     const uint64_t n = al->last_reads;
     static_assert(sizeof(pbgpu_record) == sizeof(Rec), "record layout");
@@ -519,18 +533,27 @@ struct RecordsView {
     room(off, (n + 1) * 8);
     if (!dev_mega || al->g_hosts) HIPCHK(hipMemcpyAsync(off.p, d_off, (n + 1) * 8, hipMemcpyDeviceToHost, al->st));
     else memset(off.p, 0, (n + 1) * 8);
-    // (with device mega-reads only the reads left to the host come down: a batch's first
-    // such read must not grow the buffers, so they hold an eighth of its records at least)
-    const uint64_t nr_room = dev_mega ? std::max<uint64_t>(nr, al->last_records / 8 + 4096) : nr;
-    const uint64_t ni_room = dev_mega ? std::max<uint64_t>(ni, al->last_info / 8 + 4096) : ni;
-    room(recs, nr_room * sizeof(Rec)); room(km, ni_room * 4); room(kb, ni_room * 4);
+    // (with device mega-reads only the reads left to the host come down, reads of more than
+    // GRAPH_NMAX records: room for four such reads from the start, not scaled with the
+    // batch -- sized by the batch it was a few hundred MB of pinned memory, ~50 ms of the
+    // first batch's critical path -- and grown if a batch has more)
+    const uint64_t host_room = 4 * (uint64_t)(GRAPH_NMAX + 1);
+    const uint64_t nr_room = dev_mega ? std::max<uint64_t>(nr, host_room) : nr;
+    const uint64_t ni_room =
+        dev_mega ? std::max<uint64_t>(ni, host_room * (al->last_info / std::max<uint64_t>(1, al->last_records) + 2)) : ni;
+    if (dev_mega) {
+      room_fixed(recs, nr_room * sizeof(Rec)); room_fixed(km, ni_room * 4); room_fixed(kb, ni_room * 4);
+    } else {
+      room(recs, nr_room * sizeof(Rec)); room(km, ni_room * 4); room(kb, ni_room * 4);
+    }
     if (nr) HIPCHK(hipMemcpyAsync(recs.p, d_rec, nr * sizeof(Rec), hipMemcpyDeviceToHost, al->st));
     if (ni) {
       HIPCHK(hipMemcpyAsync(km.p, d_km, ni * 4, hipMemcpyDeviceToHost, al->st));
       HIPCHK(hipMemcpyAsync(kb.p, d_kb, ni * 4, hipMemcpyDeviceToHost, al->st));
     }
     if (al->graph) {
-      room(graph, nr_room * sizeof(GraphNode));
+      if (dev_mega) room_fixed(graph, nr_room * sizeof(GraphNode));
+      else room(graph, nr_room * sizeof(GraphNode));
       if (nr) HIPCHK(hipMemcpyAsync(graph.p, d_graph, nr * sizeof(GraphNode), hipMemcpyDeviceToHost, al->st));
     }
     if (dev_mega) {
@@ -633,6 +656,9 @@ static void run_part(pbgpu_runner* R, RunPart& part, const pbgpu_run_params* run
           dcv.notify_all();
           break;
         }
+        if (timeline())
+          fprintf(stderr, "pbgpu tl read %llu bases %llu %.4f %.4f\n", (unsigned long long)id,
+                  (unsigned long long)b->seq.n, t0 - g_tl0, now_s() - g_tl0);
         if (!inq.push(b)) break;
       }
     } catch (...) {
@@ -654,7 +680,7 @@ static void run_part(pbgpu_runner* R, RunPart& part, const pbgpu_run_params* run
         // buffers that grow in this batch are sized for a full batch (pbgpu_host.h)
         tl_grow_scale = std::min(64.0, std::max(1.0, b->grow_scale));
         const uint64_t a0 = tl_dev_allocs, p0 = tl_pinned_allocs, by0 = tl_dev_bytes;
-        const double as0 = tl_alloc_s;
+        const double as0 = tl_alloc_s, ps0 = tl_pinned_s;
         const double t0 = now_s();
         upload_reads_into(al, &rb, rd);
         const double t1 = now_s();
@@ -708,6 +734,11 @@ static void run_part(pbgpu_runner* R, RunPart& part, const pbgpu_run_params* run
           pbgpu_free_text(txt);
         }
         const uint64_t id = b->id, nreads = b->n(), nbases = b->seq.n;
+        if (timeline())
+          fprintf(stderr, "pbgpu tl work %llu aligner %zu allocs %llu (%.4f s) pinned %llu (%.4f s) %.4f %.4f %.4f %.4f %.4f\n",
+                  (unsigned long long)id, wi, (unsigned long long)(tl_dev_allocs - a0), tl_alloc_s - as0,
+                  (unsigned long long)(tl_pinned_allocs - p0), tl_pinned_s - ps0, t0 - g_tl0, t1 - g_tl0, t2 - g_tl0,
+                  t3 - g_tl0, t5 - g_tl0);
         freeq.push(b);  // the batch's host buffers are free again
         {
           std::lock_guard<std::mutex> lk(smu);
@@ -778,6 +809,7 @@ static void run_part(pbgpu_runner* R, RunPart& part, const pbgpu_run_params* run
           S.coords_bytes += d.len;
           S.details_bytes += d.details.size();
         }
+        if (timeline()) fprintf(stderr, "pbgpu tl write %llu %.4f %.4f\n", (unsigned long long)next, t1 - g_tl0, now_s() - g_tl0);
         if (d.mtext) {
           free(d.mtext);
           part.texts->advance();
@@ -816,6 +848,7 @@ static void run_part(pbgpu_runner* R, RunPart& part, const pbgpu_run_params* run
 static void runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_stats* stats) {
   std::lock_guard<std::mutex> run_lock(R->run_mu);
   const double t_start = now_s();
+  g_tl0 = t_start;
   const size_t P = R->parts.size();
   // outputs first (early error reporting, jf_aligner.cc:170-178); part p writes
   // <path>.p when there are several parts

@@ -293,3 +293,40 @@ def test_read_with_many_components(tmp_path, tiling):
     ta = open(a).read()
     assert ta == open(b).read()
     assert ta.count("\n") > 257, ta[:500]  # a header line, then one line per mega-read
+
+
+def test_device_graph_long_reads_c4r(tmp_path):
+    """C4r (C4's repeat model and 15-kb-N50 reads, ~1300 records a read, ~9% of the reads
+    over 4096): 300 reads.  Reads of 4097-8192 records are traversed on the device (the top
+    sort and relax tiers), longer ones on the host; the device graph gives the host
+    graph's bytes, and the C ABI's host flags are exactly the reads over 8192 records."""
+    import numpy as np
+    from pacbio_amd import pbgpu
+    from tools.synth import Dataset
+    ds = Dataset("C4r", seed=42, threads=16, n_pb=300)
+    ds.write(str(tmp_path))
+    names = [n.decode() for n in ds.sr_names()]
+    ul = [int(x) for x in ds.unitig_lengths]
+    blob, off = ds.pb_blob()  # (views into the dataset: closed at the end)
+    base = ["-s", "1M", "-m", "17", "--psa-min", "13", "-k", "31", "-l", str(tmp_path / "ul.txt"), "-B", "15",
+            "--max-count", "5000", "--stretch-cap", "10000", "-t", "16",
+            "-r", str(tmp_path / "sr.fa"), "-p", str(tmp_path / "pb.fa")]
+    a, b = str(tmp_path / "dev"), str(tmp_path / "host")
+    _run([*base, "-o", a], timeout=300)
+    _run([*base, "--host-graph", "-o", b], timeout=300)
+    ta = open(a).read()
+    assert ta.count(">") > 200 and ta == open(b).read()
+    ix = pbgpu.Index.from_fasta([str(tmp_path / "sr.fa")], 17, psa_min=13)
+    kw = dict(k=17, forward=True, unitigs_k=31, unitig_lengths=ul, bases_matching=15.0, max_count=5000,
+              stretch_cap=10000.0)
+    al0 = pbgpu.Aligner(ix, **kw)  # the records (graph nodes) a read
+    al0.align_resident(al0.upload(blob=blob, offsets=off))
+    nrec = np.diff(al0.download().read_offsets.astype(np.int64))
+    al = pbgpu.Aligner(ix, **kw)
+    al.set_graph([pbgpu.parse_unitigs(n) for n in names], ul, 31, mega_reads=True)
+    al.align_resident(al.upload(blob=blob, offsets=off))
+    host = al.download().mega[3].astype(bool)
+    assert ((nrec > 4096) & (nrec <= 8192)).sum() >= 5, np.sort(nrec)[-40:]
+    assert (host == (nrec > 8192)).all()
+    assert al.stats()["graph_host_reads"] == int((nrec > 8192).sum())
+    ds.close()
