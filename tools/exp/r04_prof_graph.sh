@@ -4,7 +4,7 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 TAG=${1:-g}; N=${2:-50000}
 D=gpurun_out/profg_$TAG; mkdir -p $D
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o run -- python3 tools/prof_graph_gpu.py --reads $N > $D/run.log 2>&1 || { tail -20 $D/run.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o run -- python3 tools/prof_graph_gpu.py --reads $N --workload ${WL:-C2} > $D/run.log 2>&1 || { tail -20 $D/run.log; exit 1; }
 tail -3 $D/run.log
 f=$(find $D -name "*kernel_stats.csv" | head -1)
 python3 - "$f" <<'PY'

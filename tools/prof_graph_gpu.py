@@ -43,7 +43,7 @@ def main():
     print(f"align_resident {wall * 1e3:.1f} ms, graph {st['ms_graph']:.2f} ms over {st['graph_records']} records, "
           f"{st['graph_ovf_nodes']} nodes of more than 64 edges")
     print(f"{a.workload}: {a.reads} reads, {st['graph_records'] / max(1, a.reads):.0f} records a read, "
-          f"{st['graph_host_reads']} left to the host graph (> 4096 records): "
+          f"{st['graph_host_reads']} left to the host graph (> 8192 records): "
           f"{100.0 * st['graph_host_reads'] / max(1, a.reads):.3f}%")
     if f is not None:
         f(buf, 112, 1)
