@@ -518,6 +518,19 @@ struct RecordsView {
   static void room_fixed(PinnedVec& v, uint64_t bytes) {  // (not scaled with the batch)
     if (v.cap < bytes) v.reserve(std::max<uint64_t>(bytes + bytes / 4, 2 * v.cap));
   }
+  // With device mega-reads, everything a batch downloads is small and nearly fixed in
+  // size: reserved when the runner is made, so that the first batches' pinned
+  // allocations (a few ms each, serialized across the workers) do not stall the
+  // pipeline.  Reads a batch: at most batch_bases / 1000 + 4096 (reads of 1 kb on
+  // average), 4 mega-reads a read of 16 unitigs each; records and info of four reads
+  // left to the host, 32 info entries a record.  A batch that needs more grows them.
+  void reserve_mega(uint64_t batch_bases) {
+    const uint64_t reads = batch_bases / 1000 + 4096, host_room = 4 * (uint64_t)(GRAPH_NMAX + 1);
+    off.reserve((reads + 1) * 8); moff.reserve((reads + 1) * 8); mhost.reserve(reads + 1);
+    mega.reserve(4 * reads * sizeof(MegaOut)); munits.reserve(64 * reads * 4);
+    recs.reserve(host_room * sizeof(Rec)); graph.reserve(host_room * sizeof(GraphNode));
+    km.reserve(host_room * 32 * 4); kb.reserve(host_room * 32 * 4);
+  }
   void download(pbgpu_aligner* al) {
     const uint64_t n = al->last_reads;
     static_assert(sizeof(pbgpu_record) == sizeof(Rec), "record layout");
@@ -981,6 +994,21 @@ pbgpu_status pbgpu_runner_create(pbgpu_index* const* indexes, size_t n_indexes, 
       R->al.push_back(a);
       R->rd.emplace_back(new pbgpu_reads);
       R->views.emplace_back(new RecordsView);
+      if (run->records_fn && run->graph && run->graph->mega_reads) {
+        RecordsView& V = *R->views.back();
+        V.reserve_mega(R->batch_bases);
+        // the first device -> pinned copy on a stream blocked for 7-8 ms inside
+        // hipMemcpyAsync (the copy path's first use) in each worker's first batch:
+        // taken here, once, with a small and a large copy each way
+        HIPCHK(hipSetDevice(a->device));
+        dbuf<char> w;
+        w.alloc(1 << 20);
+        HIPCHK(hipMemcpyAsync(V.mega.p, w.p, 8, hipMemcpyDeviceToHost, a->st));
+        HIPCHK(hipMemcpyAsync(V.mega.p, w.p, 1 << 20, hipMemcpyDeviceToHost, a->st));
+        HIPCHK(hipMemcpyAsync(w.p, V.mega.p, 8, hipMemcpyHostToDevice, a->st));
+        HIPCHK(hipMemcpyAsync(w.p, V.mega.p, 1 << 20, hipMemcpyHostToDevice, a->st));
+        HIPCHK(hipStreamSynchronize(a->st));
+      }
       if (R->details) pbgpu_aligner_set_details(a, 1);
       if (run->records_fn && run->graph) {
         const pbgpu_status g = pbgpu_aligner_set_graph(a, run->graph);
