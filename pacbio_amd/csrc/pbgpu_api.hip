@@ -1654,12 +1654,15 @@ static void graph_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   // PBGPU_GRAPH_NMAX (tests): a lower cap on the records of a read traversed on the device
   G.nmax = GRAPH_NMAX;
   if (const char* e = getenv("PBGPU_GRAPH_NMAX")) G.nmax = (uint32_t)std::min<long>(GRAPH_NMAX, std::max(0l, atol(e)));
-  al->g_poff.ensure(nrec + 1); al->g_sizes.ensure(nrec + 1);
-  G.poff = al->g_poff.p;
-  launch_graph_sizes(G, nrec, al->g_sizes.p, (uint64_t*)temp_storage(al->tmp, excl_scan_scratch_words(nrec) * 8), st);
+  al->g_poff.ensure(nrec + 1); al->g_sizes.ensure(nrec + 1); al->g_maxn.ensure(1);
+  G.poff = al->g_poff.p; G.max_n = al->g_maxn.p;
+  HIPCHK(hipMemsetAsync(al->g_maxn.p, 0, 4, st));
+  launch_graph_sizes(G, n, nrec, al->g_sizes.p, (uint64_t*)temp_storage(al->tmp, excl_scan_scratch_words(nrec) * 8), st);
   HIPCHK(hipGetLastError());
   uint64_t tot = 0;
+  uint32_t max_n = 0;
   HIPCHK(hipMemcpyAsync(&tot, al->g_poff.p + nrec, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&max_n, al->g_maxn.p, 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   // k_graph keeps name offsets as 32 bits (a batch of 2^32 unitigs would be 48 GB of names)
   if (tot >= (1ull << 32)) throw bad_input("more than 2^32 name unitigs in one batch's records");
@@ -1671,11 +1674,12 @@ static void graph_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   G.ecnt = al->g_ecnt.p; G.eoff = al->g_eoff.p; G.edges = al->g_edges.p;
   G.ovf = al->g_ovf.p; G.ovf_list = al->g_ovf_list.p;
   uint64_t ovf[2];
-  HIPCHK(launch_graph(G, n, nrec, st, al->g_side, al->g_fork, al->g_join, ovf));
+  HIPCHK(launch_graph(G, n, nrec, max_n, st, al->g_side, al->g_fork, al->g_join, ovf));
   HIPCHK(hipGetLastError());
   al->g_eovf.ensure(std::max<uint64_t>(ovf[1], nrec) + 1);  // (a floor: the next batches rarely grow it)
   G.eovf = al->g_eovf.p;
-  HIPCHK(launch_graph_relax(G, n, nrec, ovf[0], st, al->g_side, al->g_side2, al->g_fork, al->g_join, al->g_join2));
+  HIPCHK(launch_graph_relax(G, n, nrec, max_n, ovf[0], st, al->g_side, al->g_side2, al->g_fork, al->g_join,
+                            al->g_join2));
   HIPCHK(hipGetLastError());
   al->acc.graph_ovf_nodes += ovf[0];
   al->g_mtotal = al->g_munits_used = 0;

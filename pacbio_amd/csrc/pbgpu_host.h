@@ -373,6 +373,7 @@ struct pbgpu_aligner {
   dbuf<uint32_t> g_ecnt;
   dbuf<uint64_t> g_eoff;
   dbuf<uint2> g_edges, g_eovf;
+  dbuf<uint32_t> g_maxn;
   dbuf<uint64_t> g_ovf, g_ovf_list;
   // mega-reads on the device (pbgpu_graph_params.mega_reads)
   bool g_mega = false;

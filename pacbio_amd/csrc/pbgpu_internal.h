@@ -229,6 +229,7 @@ struct GraphDev {
   // first GRAPH_EBLK edges in a block of its own (edges + q * GRAPH_EBLK) and, past
   // them, the rest at eovf + eoff[q]; an edge is {j's record index | unitigs added
   // << 16, path increment}.  ovf: {nodes listed in ovf_list, overflow edges}
+  uint32_t* max_n;  // the most records of a read in the batch (k_graph_sizes; gates the tiers)
   uint32_t* ecnt;
   uint64_t* eoff;
   uint2* edges;
@@ -276,7 +277,9 @@ void launch_host_sizes(const GraphDev& G, uint32_t n_reads, uint32_t* rsize, uin
 void launch_host_pack(const GraphDev& G, uint32_t n_reads, const uint64_t* hroff, const uint64_t* hioff, Rec* hrec,
                       GraphNode* hgraph, int32_t* hinfo_m, int32_t* hinfo_b, hipStream_t st);
 // G.poff from the records' name sizes (then the caller sizes pul / pco by poff[n_recs])
-void launch_graph_sizes(const GraphDev& G, uint64_t n_recs, uint32_t* sizes, uint64_t* scan_scratch, hipStream_t st);
+// (and *G.max_n: the most records of a read, for the tiers' launches)
+void launch_graph_sizes(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, uint32_t* sizes, uint64_t* scan_scratch,
+                        hipStream_t st);
 // implied positions and prefix sums, the per-read sort, every node's edges (G.ecnt,
 // the first GRAPH_EBLK of each in G.edges, sized n_recs * GRAPH_EBLK; the nodes with
 // more listed: ovf[2] = {nodes, edges past their blocks}, the stream synchronized);
@@ -285,9 +288,11 @@ void launch_graph_sizes(const GraphDev& G, uint64_t n_recs, uint32_t* sizes, uin
 // (their sort and relaxation run beside the others'); fork / join / join2: events
 // ordering them with st
 constexpr uint32_t GRAPH_EBLK = 64;
-hipError_t launch_graph(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hipStream_t st, hipStream_t side,
-                        hipEvent_t fork, hipEvent_t join, uint64_t* ovf);
-hipError_t launch_graph_relax(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, uint64_t n_ovf, hipStream_t st,
-                              hipStream_t side, hipStream_t side2, hipEvent_t fork, hipEvent_t join, hipEvent_t join2);
+// (max_n: *G.max_n as k_graph_sizes left it; tiers above it are not launched)
+hipError_t launch_graph(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, uint32_t max_n, hipStream_t st,
+                        hipStream_t side, hipEvent_t fork, hipEvent_t join, uint64_t* ovf);
+hipError_t launch_graph_relax(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, uint32_t max_n, uint64_t n_ovf,
+                              hipStream_t st, hipStream_t side, hipStream_t side2, hipEvent_t fork, hipEvent_t join,
+                              hipEvent_t join2);
 
 }  // namespace pbgpu

@@ -2993,32 +2993,80 @@ DEV uint32_t graph_unit(const GraphDev& G, uint32_t sr, uint32_t nsz, bool rev, 
   return rev ? G.units[o + nsz - 1 - u] ^ 1u : G.units[o + u];
 }
 DEV uint32_t graph_nsz(const GraphDev& G, uint32_t sr) { return (uint32_t)(G.noff[sr + 1] - G.noff[sr]); }
+constexpr uint32_t GRAPH_PREP_U = 8;  // names of at most this many unitigs: loads batched in registers
 __global__ void k_graph_sizes(GraphDev G, uint64_t n, uint32_t* sizes) {
   for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < n; q += (uint64_t)gridDim.x * blockDim.x)
     sizes[q] = graph_nsz(G, G.recs[q].sr) + 1;
+}
+// the most records of a read in the batch (a wave's max, one atomic a wave)
+__global__ void k_graph_max_n(GraphDev G, uint32_t n_reads) {
+  uint32_t mx = 0;
+  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n_reads; r += gridDim.x * blockDim.x) {
+    const uint32_t nr = (uint32_t)(G.rec_off[r + 1] - G.rec_off[r]);
+    mx = nr > mx ? nr : mx;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t v = (uint32_t)__shfl_xor((int)mx, o, 64);
+    mx = v > mx ? v : mx;
+  }
+  if ((threadIdx.x & 63) == 0 && mx) atomicMax(G.max_n, mx);
 }
 // per record: implied start / end (overlap_graph.hpp:24-34), its name's unitigs in
 // its orientation, and the prefix sums over them of the unitig lengths (ulen: 0 past
 // the lengths, as the host's) and of info[2u] - info[2u - 1] (kmers_info, or
 // bases_info with -b; 0 past n_info)
 __global__ void k_graph_prep(GraphDev G, uint64_t n) {
+  const uint32_t* __restrict__ units = G.units;
+  const int32_t* __restrict__ ul = G.ul;
+  uint32_t* __restrict__ ounits = G.ounits;
+  uint2* __restrict__ pp = G.pp;
   for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < n; q += (uint64_t)gridDim.x * blockDim.x) {
     const Rec R = G.recs[q];
     G.imp[q] = make_double2(__dadd_rn(R.stretch, R.offset), __dadd_rn(__dmul_rn(R.stretch, (double)R.ql), R.offset));
-    const uint32_t nsz = graph_nsz(G, R.sr);
+    const uint64_t o = G.noff[R.sr];
+    const uint32_t nsz = (uint32_t)(G.noff[R.sr + 1] - o);
     const bool rev = (R.flags & 2u) != 0;
-    const int32_t* info = G.bases ? G.info_b : G.info_m;
-    auto info_at = [&](uint32_t i) -> uint32_t { return i < R.n_info ? (uint32_t)info[R.info_off + i] : 0u; };
+    const int32_t* __restrict__ info = (G.bases ? G.info_b : G.info_m) + R.info_off;
+    const uint32_t ni = R.n_info;
+    auto info_at = [&](uint32_t i) -> uint32_t { return i < ni ? (uint32_t)info[i] : 0u; };
     const uint64_t po = G.poff[q];
+    pp[po] = make_uint2(0u, 0u);
+    if (nsz <= GRAPH_PREP_U) {
+      // the name's unitigs, their lengths and info words as independent loads issued
+      // together (the loop below waits for each unitig's id before its length, and
+      // for its stores before the next loads)
+      uint32_t un[GRAPH_PREP_U], len[GRAPH_PREP_U], ia[GRAPH_PREP_U], ib[GRAPH_PREP_U];
+#pragma unroll
+      for (uint32_t u = 0; u < GRAPH_PREP_U; ++u)
+        un[u] = u < nsz ? (rev ? units[o + nsz - 1 - u] ^ 1u : units[o + u]) : 0u;
+#pragma unroll
+      for (uint32_t u = 0; u < GRAPH_PREP_U; ++u) {
+        const uint32_t id = un[u] >> 1;
+        len[u] = (u < nsz && id < G.n_ul) ? (uint32_t)ul[id] : 0u;
+        ia[u] = u < nsz ? info_at(2 * u) : 0u;
+        ib[u] = (u < nsz && u > 0) ? info_at(2 * u - 1) : 0u;
+      }
+      uint32_t a = 0, c = 0;
+#pragma unroll
+      for (uint32_t u = 0; u < GRAPH_PREP_U; ++u) {
+        if (u < nsz) {
+          a += len[u];
+          c += ia[u] - ib[u];
+          ounits[po + u] = un[u];
+          pp[po + u + 1] = make_uint2(a, c);
+        }
+      }
+      continue;
+    }
     uint32_t a = 0, c = 0;
-    G.pp[po] = make_uint2(0u, 0u);
     for (uint32_t u = 0; u < nsz; ++u) {
-      const uint32_t un = graph_unit(G, R.sr, nsz, rev, u);
-      G.ounits[po + u] = un;
+      const uint32_t un = rev ? units[o + nsz - 1 - u] ^ 1u : units[o + u];
+      ounits[po + u] = un;
       const uint32_t id = un >> 1;
-      a += id < G.n_ul ? (uint32_t)G.ul[id] : 0u;
+      a += id < G.n_ul ? (uint32_t)ul[id] : 0u;
       c += info_at(2 * u) - (u > 0 ? info_at(2 * u - 1) : 0u);
-      G.pp[po + u + 1] = make_uint2(a, c);
+      pp[po + u + 1] = make_uint2(a, c);
     }
   }
 }
@@ -4002,13 +4050,16 @@ void launch_mega_pack(const GraphDev& G, uint32_t n_reads, const uint64_t* moff,
   if (!n_reads) return;
   hipLaunchKernelGGL(k_mega_pack, dim3(n_reads), dim3(64), 0, st, G, n_reads, moff, mc);
 }
-void launch_graph_sizes(const GraphDev& G, uint64_t n_recs, uint32_t* sizes, uint64_t* scan_scratch, hipStream_t st) {
+void launch_graph_sizes(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, uint32_t* sizes, uint64_t* scan_scratch,
+                        hipStream_t st) {
+  if (n_reads)
+    hipLaunchKernelGGL(k_graph_max_n, dim3(std::min<uint32_t>((n_reads + 255) / 256, 1024)), dim3(256), 0, st, G, n_reads);
   if (n_recs) hipLaunchKernelGGL(k_graph_sizes, dim3((uint32_t)std::min<uint64_t>((n_recs + 255) / 256, 65535)), dim3(256),
                                  0, st, G, n_recs, sizes);
   launch_excl_scan(sizes, nullptr, n_recs, G.poff, scan_scratch, st);
 }
-hipError_t launch_graph(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hipStream_t st, hipStream_t side,
-                        hipEvent_t fork, hipEvent_t join, uint64_t* ovf) {
+hipError_t launch_graph(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, uint32_t max_n, hipStream_t st,
+                        hipStream_t side, hipEvent_t fork, hipEvent_t join, uint64_t* ovf) {
   ovf[0] = ovf[1] = 0;
   if (!n_recs || !n_reads) return hipSuccess;
   hipError_t e = hipMemsetAsync(G.ovf, 0, 16, st);
@@ -4020,8 +4071,12 @@ hipError_t launch_graph(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hi
   // each is checked (the caller raises)
   if ((e = hipEventRecord(fork, st)) == hipSuccess) e = hipStreamWaitEvent(side, fork, 0);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_graph_sort<GRAPH_NMAX>, dim3(n_reads), dim3(GRAPH_SORT_BLOCK), 0, side, G, n_reads);
-  hipLaunchKernelGGL(k_graph_sort<GRAPH_NM_MID>, dim3(n_reads), dim3(GRAPH_SORT_BLOCK), 0, side, G, n_reads);
+  // (a tier above the batch's longest read is not launched: an empty 8192-record block
+  // still takes a CU's LDS while it starts and exits, 1.4 ms a launch of 50k of them)
+  if (max_n > GRAPH_NM_MID)
+    hipLaunchKernelGGL(k_graph_sort<GRAPH_NMAX>, dim3(n_reads), dim3(GRAPH_SORT_BLOCK), 0, side, G, n_reads);
+  if (max_n > GRAPH_NM_SMALL)
+    hipLaunchKernelGGL(k_graph_sort<GRAPH_NM_MID>, dim3(n_reads), dim3(GRAPH_SORT_BLOCK), 0, side, G, n_reads);
   if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_graph_sort<GRAPH_NM_SMALL>, dim3(n_reads), dim3(GRAPH_SORT_BLOCK), 0, st, G, n_reads);
   if ((e = hipStreamWaitEvent(st, join, 0)) != hipSuccess) return e;
@@ -4031,8 +4086,9 @@ hipError_t launch_graph(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, hi
   if ((e = hipMemcpyAsync(ovf, G.ovf, 16, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
   return hipStreamSynchronize(st);
 }
-hipError_t launch_graph_relax(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, uint64_t n_ovf, hipStream_t st,
-                              hipStream_t side, hipStream_t side2, hipEvent_t fork, hipEvent_t join, hipEvent_t join2) {
+hipError_t launch_graph_relax(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, uint32_t max_n, uint64_t n_ovf,
+                              hipStream_t st, hipStream_t side, hipStream_t side2, hipEvent_t fork, hipEvent_t join,
+                              hipEvent_t join2) {
   if (!n_recs || !n_reads) return hipSuccess;
   constexpr uint32_t W = GE_BLOCK / 64;
   if (n_ovf) hipLaunchKernelGGL(k_graph_edges<true>, dim3((uint32_t)((n_ovf + W - 1) / W)), dim3(GE_BLOCK), 0, st, G,
@@ -4043,12 +4099,18 @@ hipError_t launch_graph_relax(const GraphDev& G, uint32_t n_reads, uint64_t n_re
   if (e == hipSuccess) e = hipStreamWaitEvent(side, fork, 0);
   if (e == hipSuccess) e = hipStreamWaitEvent(side2, fork, 0);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_graph_relax<GRAPH_NMAX>, dim3(n_reads), dim3(128), 0, side, G, n_reads);
-  hipLaunchKernelGGL(k_graph_relax<GRAPH_NMAX / 2>, dim3(n_reads), dim3(128), 0, side, G, n_reads);
-  hipLaunchKernelGGL(k_graph_relax<GRAPH_NMAX / 4>, dim3(n_reads), dim3(128), 0, side2, G, n_reads);
+  // (tiers above the longest read are not launched; the top one also marks the reads
+  // left to the host, so it runs whenever a read is past the device cap)
+  if (max_n > GRAPH_NMAX / 2 || max_n > G.nmax)
+    hipLaunchKernelGGL(k_graph_relax<GRAPH_NMAX>, dim3(n_reads), dim3(128), 0, side, G, n_reads);
+  if (max_n > GRAPH_NMAX / 4)
+    hipLaunchKernelGGL(k_graph_relax<GRAPH_NMAX / 2>, dim3(n_reads), dim3(128), 0, side, G, n_reads);
+  if (max_n > GRAPH_NMAX / 8)
+    hipLaunchKernelGGL(k_graph_relax<GRAPH_NMAX / 4>, dim3(n_reads), dim3(128), 0, side2, G, n_reads);
   if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
   if ((e = hipEventRecord(join2, side2)) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_graph_relax<GRAPH_NM_SMALL>, dim3(n_reads), dim3(128), 0, st, G, n_reads);
+  if (max_n > GRAPH_RELAX_MIN)
+    hipLaunchKernelGGL(k_graph_relax<GRAPH_NM_SMALL>, dim3(n_reads), dim3(128), 0, st, G, n_reads);
   hipLaunchKernelGGL(k_graph_relax<GRAPH_RELAX_MIN>, dim3(n_reads), dim3(128), 0, st, G, n_reads);
   if ((e = hipStreamWaitEvent(st, join, 0)) != hipSuccess) return e;
   return hipStreamWaitEvent(st, join2, 0);
