@@ -96,6 +96,9 @@ void launch_fine_empty(IndexView ix, uint32_t k, const ChainDesc* chains, uint32
 void launch_rec_hist(const uint32_t* rec_read, uint32_t n, uint32_t* per_read, hipStream_t st);
 void launch_rec_scatter(const uint32_t* rec_read, uint32_t n, const uint64_t* rec_off, uint32_t* cursor, uint32_t* order,
                         hipStream_t st);
+// order[rec_off[rec_read[i]] + rec_slot[i]] = i (the slots counted at emission)
+void launch_rec_place(const uint32_t* rec_read, const uint32_t* rec_slot, uint32_t n, const uint64_t* rec_off,
+                      uint32_t* order, hipStream_t st);
 int rec_sort_lcap();
 void launch_rec_sort(const Rec* recs, const uint64_t* rec_off, const uint32_t* order, uint64_t* gscratch,
                      uint32_t n_reads, Rec* out, hipStream_t st);
@@ -1510,18 +1513,22 @@ static uint32_t lis_stage(pbgpu_aligner* al, uint32_t nch, uint64_t Hs, const Li
 
 // Records grouped per read and sorted by (rs, re, ql, sr, emit): al->recs[0..nrec)
 // -> al->recs_sorted, al->rec_off.  timed: event around the sort kernel.
-static void records_stage(pbgpu_aligner* al, uint32_t n, uint32_t nrec, bool timed) {
+// counted: every record's read count and slot were taken at emission (ChainOut.per_read)
+static void records_stage(pbgpu_aligner* al, uint32_t n, uint32_t nrec, bool timed, bool counted = false) {
   hipStream_t st = al->st;
   al->rec_per_read.ensure(n); al->rec_cursor.ensure(n);
-  HIPCHK(hipMemsetAsync(al->rec_per_read.p, 0, n * 4, st));
-  HIPCHK(hipMemsetAsync(al->rec_cursor.p, 0, n * 4, st));
-  launch_rec_hist(al->rec_read.p, nrec, al->rec_per_read.p, st);
+  if (!counted) {
+    HIPCHK(hipMemsetAsync(al->rec_per_read.p, 0, n * 4, st));
+    HIPCHK(hipMemsetAsync(al->rec_cursor.p, 0, n * 4, st));
+    launch_rec_hist(al->rec_read.p, nrec, al->rec_per_read.p, st);
+  }
   launch_excl_scan(al->rec_per_read.p, nullptr, n, al->rec_off.p,
                    (uint64_t*)temp_storage(al->tmp, excl_scan_scratch_words(n) * 8), st);
   al->order.ensure(nrec + 1);
   al->sort_scratch.ensure(6ull * nrec + 6);
   al->recs_sorted.ensure(nrec + 1);
-  launch_rec_scatter(al->rec_read.p, nrec, al->rec_off.p, al->rec_cursor.p, al->order.p, st);
+  if (counted) launch_rec_place(al->rec_read.p, al->rec_slot.p, nrec, al->rec_off.p, al->order.p, st);
+  else launch_rec_scatter(al->rec_read.p, nrec, al->rec_off.p, al->rec_cursor.p, al->order.p, st);
   if (timed) HIPCHK(hipEventRecord(al->ev[15], st));
   launch_rec_sort(al->recs.p, al->rec_off.p, al->order.p, al->sort_scratch.p, n, al->recs_sorted.p, st);
   HIPCHK(hipGetLastError());
@@ -1775,6 +1782,12 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
   al->ovf_reads.ensure(n);
   al->ovf_list.ensure(n);  // (used only by batches with reads past the first group tier)
   uint64_t rec_done = 0, info_done = 0;
+  // records counted per read as they are emitted (ChainOut.per_read), unless --max-match
+  // re-emits or a sub-batch is redone after a record overflow: then records_stage counts
+  static const bool rec_hist = getenv("PBGPU_REC_HIST") != nullptr;  // (A/B: always count afterwards)
+  bool counted = !al->P.max_match && !rec_hist;
+  al->rec_per_read.ensure(n);
+  if (counted) HIPCHK(hipMemsetAsync(al->rec_per_read.p, 0, (size_t)n * 4, st));
   double ms_group = 0, ms_lis = 0, ms_fit = 0;
   double k_ms[PBGPU_KERNEL_N] = {};
   uint64_t k_n[PBGPU_KERNEL_N] = {};
@@ -1937,6 +1950,7 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
       const uint64_t rec_need = rec_done + (uint64_t)nch * (al->P.max_match ? 2 : 1) + 1024 * (attempt + 1);
       al->recs.grow_keep(std::max<uint64_t>(rec_need, al->rec_hint), rec_done, st);
       al->rec_read.grow_keep(al->recs.n, rec_done, st);
+      al->rec_slot.grow_keep(al->recs.n, rec_done, st);
       if (al->P.unitigs_k) {
         const uint64_t info_need = info_done + (uint64_t)nch * al->info_per_chain + 4096;
         al->info_m.grow_keep(info_need, info_done, st);
@@ -1960,6 +1974,8 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
       CO.info_m = al->info_m.p; CO.info_b = al->info_b.p; CO.info_count = al->info_count.p; CO.info_cap = al->info_m.n;
       CO.stats = al->stats.p;
       CO.emit_of = nullptr;  // coarse: the round index is the emission index
+      CO.per_read = counted ? al->rec_per_read.p : nullptr;
+      CO.rec_slot = al->rec_slot.p;
       HIPCHK(hipEventRecord(al->ev[13], st));
       launch_coords(v, al->P, al->chains.p, al->perm.p, n_fit, rd->off.p, 0, CO, st);
       HIPCHK(hipGetLastError());
@@ -2017,6 +2033,7 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
         break;
       }
       if (attempt > 8) throw std::runtime_error("record buffer growth did not converge");
+      counted = false;  // this attempt's emitted records were counted: records_stage recounts
       // grow (keeping the records of earlier sub-batches) and redo this sub-batch from the group pass
       al->rec_hint = std::max<uint64_t>(al->rec_hint, (uint64_t)nrec + 4096);
       al->info_per_chain = al->info_per_chain * 2 + 16;
@@ -2027,7 +2044,7 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
   al->last_info = info_done;
   HIPCHK(hipEventRecord(al->ev[3], st));
   const uint32_t nrec = (uint32_t)al->last_records;
-  records_stage(al, n, nrec, true);
+  records_stage(al, n, nrec, true, counted);
   HIPCHK(hipEventRecord(al->ev[4], st));
   if (al->fine) {
     HIPCHK(hipEventRecord(al->ev[16], st));

@@ -314,6 +314,7 @@ struct pbgpu_aligner {
   dbuf<uint32_t> redo[3];
   dbuf<Rec> recs, recs_sorted;
   dbuf<uint32_t> rec_read;  // the read of every record of recs (written with it)
+  dbuf<uint32_t> rec_slot;  // its rank among its read's records (ChainOut.rec_slot)
   dbuf<int32_t> info_m, info_b;
   dbuf<uint8_t> tmp;
   dbuf<uint32_t> gtable;

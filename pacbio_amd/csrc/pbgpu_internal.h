@@ -178,6 +178,11 @@ struct ChainOut {
   uint64_t info_cap;
   unsigned long long* stats;
   const uint32_t* emit_of;  // fine pass: per chain, the emission index of its coarse record (else null)
+  // (coarse pass without --max-match) per read its record count, and per record its
+  // rank among its read's (the counter's old value): records_stage then places the
+  // records with neither a histogram nor a scatter of atomics.  Null: not counted.
+  uint32_t* per_read;
+  uint32_t* rec_slot;
 };
 
 // Exclusive scan of n counts (u32 or u64, exactly one of in32 / in64 non-null) into

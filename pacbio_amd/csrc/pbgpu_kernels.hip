@@ -2138,8 +2138,12 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
   PROF_T(kc_t5);
   if (keep) {
     const uint32_t ri = atomicAdd(O.rec_count, 1u);
-    if (ri < O.rec_cap && info_ok) { O.recs[ri] = R; O.rec_read[ri] = R.read; }
-    else atomicAdd(&O.stats[ST_REC_OVERFLOW], 1ull);
+    if (ri < O.rec_cap && info_ok) {
+      O.recs[ri] = R; O.rec_read[ri] = R.read;
+      if (O.per_read) O.rec_slot[ri] = atomicAdd(&O.per_read[R.read], 1u);
+    } else {
+      atomicAdd(&O.stats[ST_REC_OVERFLOW], 1ull);
+    }
     if (P.max_match) O.redo[atomicAdd(O.n_redo, 1u)] = c;
   }
 #ifdef PBGPU_PROF
@@ -2399,6 +2403,11 @@ __global__ void k_fine_empty(IndexView ix, uint32_t k, const ChainDesc* __restri
 __global__ void k_rec_hist(const uint32_t* rec_read, uint32_t n, uint32_t* per_read) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
     atomicAdd(&per_read[rec_read[i]], 1u);
+}
+__global__ void k_rec_place(const uint32_t* __restrict__ rec_read, const uint32_t* __restrict__ rec_slot, uint32_t n,
+                            const uint64_t* __restrict__ rec_off, uint32_t* __restrict__ order) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    order[rec_off[rec_read[i]] + rec_slot[i]] = i;
 }
 __global__ void k_rec_scatter(const uint32_t* rec_read, uint32_t n, const uint64_t* rec_off, uint32_t* cursor,
                               uint32_t* order) {
@@ -2734,6 +2743,12 @@ uint32_t big_bucket() {  // first length class whose items all exceed LIS_U16_MA
 void launch_rec_hist(const uint32_t* rec_read, uint32_t n, uint32_t* per_read, hipStream_t st) {
   if (!n) return;
   hipLaunchKernelGGL(k_rec_hist, dim3(1024), dim3(256), 0, st, rec_read, n, per_read);
+}
+void launch_rec_place(const uint32_t* rec_read, const uint32_t* rec_slot, uint32_t n, const uint64_t* rec_off,
+                      uint32_t* order, hipStream_t st) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_rec_place, dim3(std::min<uint32_t>((n + 255) / 256, 16384)), dim3(256), 0, st, rec_read, rec_slot,
+                     n, rec_off, order);
 }
 void launch_rec_scatter(const uint32_t* rec_read, uint32_t n, const uint64_t* rec_off, uint32_t* cursor, uint32_t* order,
                         hipStream_t st) {
