@@ -225,7 +225,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="C2", choices=["C1", "C2", "C3"])
+    ap.add_argument("--workload", default="C2", choices=["C1", "C2", "C3", "C4r"])
     ap.add_argument("--reads", type=int, default=0, help="override reads per GPU")
     ap.add_argument("--cpu-sample-reads", type=int, default=0, help="CPU baseline sample (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")

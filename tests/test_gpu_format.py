@@ -241,3 +241,18 @@ def test_cli_bad_input_exits_1(small_dir):
                         "/dev/null"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 1
     assert "neither FASTA nor FASTQ" in r.stderr
+
+
+def test_cli_records_counted_at_emission(small_dir):
+    """The records stage's two paths give the same bytes: per-read counts and slots taken
+    by k_coords as it emits (the default) and the count + scatter afterwards
+    (PBGPU_REC_HIST=1, the path of --max-match and of record-overflow retries); many
+    small batches over two aligners."""
+    base = [CLI, "-s", "1", "-m", "17", "-r", os.path.join(small_dir, "sr.fa"), "-l", os.path.join(small_dir, "ul.txt"),
+            "-k", "31", "-f", "-B", "15", "--batch-bases", "30k", "--coords", "/dev/stdout",
+            "-p", os.path.join(small_dir, "pb.fa")]
+    r1 = subprocess.run(base, capture_output=True, text=True, timeout=300)
+    r2 = subprocess.run(base, capture_output=True, text=True, timeout=300, env=dict(os.environ, PBGPU_REC_HIST="1"))
+    assert r1.returncode == 0, r1.stderr
+    assert r2.returncode == 0, r2.stderr
+    assert r1.stdout.count("\n") > 50 and r1.stdout == r2.stdout
