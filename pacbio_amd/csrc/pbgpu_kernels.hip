@@ -3155,12 +3155,17 @@ constexpr uint32_t GRAPH_NMAX_K = GRAPH_NMAX;  // reads of more records go to th
 constexpr uint32_t GRAPH_ROOT_BITS = 13;  // k_graph_relax matches roots by this many bits
 static_assert(GRAPH_NMAX_K <= (1u << GRAPH_ROOT_BITS) && GRAPH_NMAX_K < 0x8000u,
               "k_graph_relax matches roots by GRAPH_ROOT_BITS and keeps 15-bit indices");
-constexpr uint32_t GE_NODES = 64, GE_SLOTS = 384, GE_BLOCK = 256;
+#ifndef PBGPU_GE_SLOTS
+#define PBGPU_GE_SLOTS 384
+#endif
+constexpr uint32_t GE_NODES = 64, GE_SLOTS = PBGPU_GE_SLOTS, GE_BLOCK = 256;
 DEV bool graph_on_device(const GraphDev& G, uint32_t n) { return n > 0 && n <= G.nmax && n <= GRAPH_NMAX_K; }
 template <bool OVF>
 __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n_recs, uint64_t n_ovf) {
-  __shared__ double s_is[GE_SLOTS], s_ie[GE_SLOTS], s_er[GE_SLOTS], s_rl[GE_SLOTS];
-  __shared__ uint32_t s_meta[GE_SLOTS], s_lpa[GE_SLOTS], s_end[GE_SLOTS], s_po[GE_SLOTS];
+  __shared__ double s_is[GE_SLOTS], s_ie[GE_SLOTS], s_er[GE_SLOTS];
+  __shared__ uint32_t s_meta[GE_SLOTS], s_lpa[GE_SLOTS], s_po[GE_SLOTS];
+  __shared__ double s_rl[GE_NODES];    // node i's read length and scan end: the window's
+  __shared__ uint32_t s_end[GE_NODES];  // nodes only (OVF: WAVES <= GE_NODES slots)
   __shared__ uint32_t s_u[GRAPH_U * GE_SLOTS];  // [u * GE_SLOTS + slot]
   constexpr uint32_t WAVES = GE_BLOCK / 64;
   // OVF: slot t holds listed node blockIdx.x * WAVES + t; nothing else is staged
@@ -3175,9 +3180,11 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
     const uint32_t n = (uint32_t)(e - G.rec_off[r]);
     const GDesc d = G.desc[q];
     s_is[t] = d.imp_s; s_ie[t] = d.imp_e; s_er[t] = d.err;
-    s_rl[t] = (double)(G.roff[r + 1] - G.roff[r]);
     s_meta[t] = d.idx | (d.nsz << 16); s_lpa[t] = d.lp_add; s_po[t] = (uint32_t)d.poff;  // < 2^32 (host check)
-    s_end[t] = graph_on_device(G, n) ? (uint32_t)e : (uint32_t)(q + 1);  // a read left to the host: no scan
+    if (t < GE_NODES) {
+      s_rl[t] = (double)(G.roff[r + 1] - G.roff[r]);
+      s_end[t] = graph_on_device(G, n) ? (uint32_t)e : (uint32_t)(q + 1);  // a read left to the host: no scan
+    }
 #pragma unroll
     for (uint32_t u = 0; u < GRAPH_U; ++u) s_u[u * GE_SLOTS + t] = u < d.nsz ? G.ounits[d.poff + u] : 0u;
   }
