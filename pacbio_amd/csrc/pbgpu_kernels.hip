@@ -2548,7 +2548,10 @@ void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const ui
                   uint32_t hcap_log2, uint32_t* gtable, GroupOut O, unsigned long long* stats, hipStream_t st) {
   if (!n_list) return;
   if (!gtable) {  // LDS table: hcap_log2 <= 13; the 8192-slot table gets a 16-wave block
-    const size_t lds = ((size_t)3 << hcap_log2) * sizeof(uint32_t);
+    // PBGPU_GROUP_LDS_PAD (experiment): extra dynamic LDS for the 4-wave tier, so fewer of
+    // its blocks share a CU (fewer reads' lists open at once)
+    static const size_t pad = getenv("PBGPU_GROUP_LDS_PAD") ? (size_t)atol(getenv("PBGPU_GROUP_LDS_PAD")) : 0;
+    const size_t lds = ((size_t)3 << hcap_log2) * sizeof(uint32_t) + (hcap_log2 < 13 ? pad : 0);
     // the 96 KiB dynamic-LDS attribute, set once per device (function attributes are per device)
     static std::atomic<uint64_t> attr_done(0);
     int dev = 0;
