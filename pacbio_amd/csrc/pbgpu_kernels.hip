@@ -3098,8 +3098,11 @@ DEV uint64_t graph_dkey(double x) {
 // Three tiers by the read's record count (LDS sized to the tier, so the common
 // reads of <= GRAPH_NM_SMALL records run many blocks a CU): NM = GRAPH_NM_SMALL
 // takes those, NM = GRAPH_NM_MID the reads up to it, NM = GRAPH_NMAX the rest.
+#ifndef PBGPU_RELAX_PF
+#define PBGPU_RELAX_PF 6
+#endif
 constexpr uint32_t GRAPH_SORT_BLOCK = 256, GRAPH_NM_SMALL = 1024, GRAPH_NM_MID = 4096, GRAPH_RELAX_MIN = 512,
-                   GRAPH_RELAX_PF = 6;
+                   GRAPH_RELAX_PF = PBGPU_RELAX_PF;
 static_assert(GRAPH_EBLK == 64, "k_graph_relax takes a node's block as one 64-lane load");
 template <uint32_t NM>
 DEV bool graph_tier(const GraphDev& G, uint32_t n) {
