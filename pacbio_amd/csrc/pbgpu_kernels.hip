@@ -3166,6 +3166,25 @@ static_assert(GRAPH_NMAX_K <= (1u << GRAPH_ROOT_BITS) && GRAPH_NMAX_K < 0x8000u,
 #endif
 constexpr uint32_t GE_NODES = 64, GE_SLOTS = PBGPU_GE_SLOTS, GE_BLOCK = 256;
 DEV bool graph_on_device(const GraphDev& G, uint32_t n) { return n > 0 && n <= G.nmax && n <= GRAPH_NMAX_K; }
+// super_read_name::overlap (super_read_name.cc:49-72) in registers for a name i of SA
+// unitigs (wave-uniform: the wave's node): the smallest t >= max(SA - sb + 1, 1) with
+// name_i[t..SA) == name_j[0..SA - t) (0: none), and whether the names are the same
+template <int SA>
+DEV void name_overlap_reg(const uint32_t (&a)[GRAPH_U], const uint32_t (&bu)[GRAPH_U], uint32_t sb, int32_t& nb,
+                          bool& same) {
+  const int t0 = SA - (int)sb + 1;
+  nb = 0;
+#pragma unroll
+  for (int t = SA - 1; t >= 1; --t) {
+    bool m = (t >= t0) & (a[t] == bu[0]);
+#pragma unroll
+    for (int qq = t + 1; qq < SA; ++qq) m &= a[qq] == bu[qq - t];
+    nb = m ? SA - t : nb;
+  }
+  same = sb == (uint32_t)SA;
+#pragma unroll
+  for (int u = 0; u < SA; ++u) same &= a[u] == bu[u];
+}
 template <bool OVF>
 __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n_recs, uint64_t n_ovf) {
   __shared__ double s_is[GE_SLOTS], s_ie[GE_SLOTS], s_er[GE_SLOTS];
@@ -3205,6 +3224,7 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
     uint32_t cnt = 0;
     if ((q + 1 < qe) & !(ie_i >= s_rl[ti])) {  // (imp_e >= rl: hanging off the 3' end)
       const uint32_t sa = s_meta[ti] >> 16, po_i = s_po[ti];
+      const uint32_t sa_u = (uint32_t)__builtin_amdgcn_readfirstlane((int)sa);  // (uniform: the wave's node i)
       uint32_t a[GRAPH_U];
 #pragma unroll
       for (uint32_t u = 0; u < GRAPH_U; ++u) a[u] = s_u[u * GE_SLOTS + ti];
@@ -3242,19 +3262,17 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
         if (cand) {
           bool same;
           if ((sa <= GRAPH_U) & (sb <= GRAPH_U)) {
-            // super_read_name::overlap (super_read_name.cc:49-72) in registers: the smallest
-            // t >= max(sa - sb + 1, 1) with name_i[t..sa) == name_j[0..sa - t)
-            const int t0 = (int)sa - (int)sb + 1;
-#pragma unroll
-            for (int t = (int)GRAPH_U - 1; t >= 1; --t) {
-              bool m = (t < (int)sa) & (t >= t0) & (a[t] == bu[0]);
-#pragma unroll
-              for (int qq = t + 1; qq < (int)GRAPH_U; ++qq) m &= (qq >= (int)sa) | (a[qq] == bu[qq - t]);
-              nb = m ? (int32_t)sa - t : nb;
+            // specialized by the wave-uniform name size of node i: the compare network
+            // of SA unitigs, not of GRAPH_U (names are mostly 2-5 unitigs)
+            switch (sa_u) {
+              case 2: name_overlap_reg<2>(a, bu, sb, nb, same); break;
+              case 3: name_overlap_reg<3>(a, bu, sb, nb, same); break;
+              case 4: name_overlap_reg<4>(a, bu, sb, nb, same); break;
+              case 5: name_overlap_reg<5>(a, bu, sb, nb, same); break;
+              case 6: name_overlap_reg<6>(a, bu, sb, nb, same); break;
+              case 7: name_overlap_reg<7>(a, bu, sb, nb, same); break;
+              default: name_overlap_reg<8>(a, bu, sb, nb, same); break;
             }
-            same = sb == sa;
-#pragma unroll
-            for (uint32_t u = 0; u < GRAPH_U; ++u) same &= (u >= sa) | (a[u] == bu[u]);
           } else {
             auto unit_j = [&](uint32_t qq) -> uint32_t { return G.ounits[po_j + qq]; };
             const uint32_t u0 = unit_j(0);
