@@ -238,6 +238,9 @@ def main():
     ap.add_argument("--device-streams", type=int, default=1,
                     help="aligners of the device-only leg: 1 = every launch runs alone, so the per-launch event times "
                          "(the roofline) measure the kernel, not two overlapping launches")
+    ap.add_argument("--device-chunk-bases", type=float, default=1.5e9,
+                    help="the device leg aligns its resident reads in chunks of at most this many bases (C2's "
+                         "617 Mbases are one; C3's 3.6 Gbases in one call need more than 288 GB of working buffers)")
     ap.add_argument("--parts", type=int, default=2,
                     help="part files of the extra coords-out leg (value_parts; 0 = no such leg)")
     ap.add_argument("--cmr-steps", type=int, default=3,
@@ -327,38 +330,61 @@ def main():
     bases_rank = int(off[-1])
 
     # ---- device-only leg (value_device): reads resident in HBM, records left in HBM
+    # (in chunks of at most --device-chunk-bases: every chunk resident before the clock)
+    cuts = [0]
+    for r in range(1, len(off)):
+        if int(off[r]) - int(off[cuts[-1]]) > args.device_chunk_bases and r - 1 > cuts[-1]:
+            cuts.append(r - 1)
+    cuts.append(len(off) - 1)
+
+    def upload_chunks(a):
+        out = []
+        for r0, r1 in zip(cuts[:-1], cuts[1:]):
+            if r0 == 0 and r1 == len(off) - 1:
+                out.append(a.upload(blob=blob, offsets=off))
+            else:
+                b0, b1 = int(off[r0]), int(off[r1])
+                out.append(a.upload(blob=bytes(blob[b0:b1]), offsets=off[r0:r1 + 1] - off[r0]))
+        return out
+
     al = pbgpu.StreamAligner(index, streams=args.device_streams, **akw)
-    reads = al.upload(blob=blob, offsets=off)
-    al.align_resident(reads)
+    chunks = upload_chunks(al)
+    for c in chunks:
+        al.align_resident(c)
     al.reset_stats()
     pbgpu.device_synchronize(local)
     comm.barrier()
     td = time.perf_counter()
     for _ in range(args.device_steps):
-        al.align_resident(reads)
+        for c in chunks:
+            al.align_resident(c)
     pbgpu.device_synchronize(local)
     comm.barrier()
     el_dev = comm.max(time.perf_counter() - td)
     st = al.stats()
-    al.free(reads)
+    for c in chunks:
+        al.free(c)
     al.close()
 
     # SURVEY 8(d)'s second flag set: the defaults, without -l / -f (device leg only)
     el_dev2, st2 = None, None
     if not args.skip_default_leg:
         al2 = pbgpu.StreamAligner(index, streams=args.device_streams, k=k)
-        reads = al2.upload(blob=blob, offsets=off)
-        al2.align_resident(reads)
+        chunks = upload_chunks(al2)
+        for c in chunks:
+            al2.align_resident(c)
         pbgpu.device_synchronize(local)
         comm.barrier()
         td = time.perf_counter()
         for _ in range(args.device_steps):
-            al2.align_resident(reads)
+            for c in chunks:
+                al2.align_resident(c)
         pbgpu.device_synchronize(local)
         comm.barrier()
         el_dev2 = comm.max(time.perf_counter() - td)
         st2 = al2.stats()
-        al2.free(reads)
+        for c in chunks:
+            al2.free(c)
         al2.close()
 
     # ---- end to end (value): PacBio FASTA -> coords file, pbgpu_run
@@ -626,6 +652,7 @@ def main():
                 "allocs_in_timed_steps": {n: sum(r[n] for r in rstats) for n in
                                           ("n_device_allocs", "n_pinned_allocs")},
                 "device_leg": {"ms_per_step": el_dev / args.device_steps * 1e3, "streams": args.device_streams,
+                               "chunks": len(cuts) - 1,
                                "stage_ms_per_step": {s: round(st["ms_" + s] / args.device_steps, 3) for s in
                                                      ("seed", "group", "lis", "fit", "records")},
                                "kernel_ms_per_launch": {kk: round(kms[kk] / max(1, kn[kk]), 3) for kk in kms},
