@@ -1451,11 +1451,14 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
   constexpr uint32_t NONE = 0xFFFFu;
   constexpr int PF = (SMAX + 63) / 64;  // prefetch registers per lane
   __shared__ int2 s_x[WPB][SMAX];
-  __shared__ uint16_t s_nxt[WPB][SMAX], s_len[WPB][SMAX], s_P[WPB][SMAX], s_root[WPB][SMAX], s_rs[WPB][SMAX];
+  // s_ord: the list L (lis_align.hpp:146) as an array in reverse order -- after i
+  // elements, s_ord[i - 1] is the head and the node the reference's walk reaches after s
+  // steps is s_ord[i - 1 - s] (every element is inserted, so the list holds all of them)
+  __shared__ uint16_t s_ord[WPB][SMAX], s_len[WPB][SMAX], s_P[WPB][SMAX], s_root[WPB][SMAX], s_rs[WPB][SMAX];
   const int lane = lane_id();
   const uint32_t wv = threadIdx.x >> 6;
   int2* sx = s_x[wv];
-  uint16_t *snxt = s_nxt[wv], *sln = s_len[wv], *sP = s_P[wv], *sroot = s_root[wv], *srs = s_rs[wv];
+  uint16_t *sord = s_ord[wv], *sln = s_len[wv], *sP = s_P[wv], *sroot = s_root[wv], *srs = s_rs[wv];
   const uint32_t nwaves = gridDim.x * WPB;
   const bool fast = lp.W == 1 && !lp.mer_all;
   uint64_t tests = 0, my_hits = 0, my_strands = 0, my_points = 0;
@@ -1585,6 +1588,10 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
       for (uint32_t j = lane; j < n; j += 64) sx[j] = X[base + j];
     }
     lds_fence();
+#ifdef PBGPU_PROF
+    const uint64_t pw_t0 = __builtin_amdgcn_s_memtime();
+    uint64_t pw_rounds = 0;
+#endif
     // ---- list order: k_group leaves each 256-hit step's run of a list unordered.
     // Odd-even transposition in LDS until a round swaps nothing (an ordered strand
     // costs one compare per element); written back to X when anything moved, for
@@ -1603,10 +1610,16 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
         }
         if (!__ballot(sw)) break;
         moved = true;
+#ifdef PBGPU_PROF
+        ++pw_rounds;
+#endif
       }
       if (moved)
         for (uint32_t j = lane; j < n; j += 64) X[base + j] = sx[j];
     }
+#ifdef PBGPU_PROF
+    const uint64_t pw_t1 = __builtin_amdgcn_s_memtime();
+#endif
     // ---- forward pass (compute_L_P)
     uint32_t head = NONE, longest = 0, longest_ind = 0;
     uint32_t cur = 0;
@@ -1639,7 +1652,7 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
           if ((uint32_t)lane < m) {
             const uint32_t elen = hl + 1 + lane;
             const uint32_t P = lane == 0 ? head : i - 1;
-            snxt[i] = (uint16_t)P; sln[i] = (uint16_t)elen; sP[i] = (uint16_t)P; sroot[i] = (uint16_t)hr;
+            sord[i] = (uint16_t)i; sln[i] = (uint16_t)elen; sP[i] = (uint16_t)P; sroot[i] = (uint16_t)hr;
             srs[i] = (uint16_t)(P + 1 == i ? rsr : i);
             cand = (elen > longest) &
                    ((lp.seq_all != 0) | linear_ok(lp.a, (double)(xi.x - hrx.x), (double)(xi.y - hrx.y)));
@@ -1658,43 +1671,76 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
         }
       }
       if (cur < pend) {
-        // ---- literal step for element cur (wave-uniform)
+        // ---- literal step for element cur (wave-uniform): the reference's walk down L
+        // (lis_align.hpp:156-171) evaluated 64 nodes at a time.  Lane l of chunk c0 holds
+        // the node at walk step s = c0 + l; the node that takes i is the first set lane of
+        // a ballot, and `prev` (the first node of the smallest length met before it: the
+        // last strict decrease of the walk's running minimum) is a min-reduction of
+        // (len, s) over the nodes before it.  On repeat-rich strands the walks are long
+        // (C4r: 76 nodes a step on average), which a serial pointer chase paid node by node.
         const uint32_t i = cur;
         const int2 xi = sx[i];
-        uint32_t prev = NONE, prev_len = 0, prev_nxt = NONE, found = NONE;
+        uint32_t found = NONE, found_s = 0, best = 0xFFFFFFFFu;  // best: len << 16 | s (lane-local)
+        bool hit = false;
 #ifdef PBGPU_PROF
         PROF_ADD(20, 1);
 #endif
-        for (uint32_t it = head; it != NONE;) {
-          ++tests;
-          PROF_ADD(23, 1);
-          const uint32_t lj = sln[it];
-          const int2 xj = sx[it];
-          if (xi.y > xj.y) {
-            bool ok;
-            if (lp.mer_all) ok = true;
-            else if (lp.W == 1) ok = affine_ok(lp.a, lp.b, lp.C, (double)(xi.x - xj.x), (double)(xi.y - xj.y));
-            else if (lp.W == 0 || lj < lp.W) ok = true;  // !will_be_filled()
-            else {
-              uint32_t anc = it;
-              for (uint32_t q = 1; q < lp.W; ++q) anc = sP[anc];
-              const int2 xa = sx[anc];
-              ok = affine_ok(lp.a, lp.b, lp.C, (double)(xi.x - xa.x), (double)(xi.y - xa.y));
-            }
-            if (ok) { found = it; break; }
+        for (uint32_t c0 = 0; c0 < i; c0 += 64) {
+          const uint32_t s = c0 + lane;
+          const bool valid = s < i;
+          const uint32_t j = sord[valid ? i - 1 - s : 0];
+          const uint32_t lj = sln[j];
+          const int2 xj = sx[j];
+          bool ok = valid & (xi.y > xj.y);
+          if (lp.mer_all) {
+          } else if (lp.W == 1) {
+            ok &= affine_ok(lp.a, lp.b, lp.C, (double)(xi.x - xj.x), (double)(xi.y - xj.y));
+          } else if (lp.W == 0) {
+          } else if (ok & (lj >= lp.W)) {  // will_be_filled(): the window's oldest add
+            uint32_t anc = j;
+            for (uint32_t q = 1; q < lp.W; ++q) anc = sP[anc];
+            const int2 xa = sx[anc];
+            ok = affine_ok(lp.a, lp.b, lp.C, (double)(xi.x - xa.x), (double)(xi.y - xa.y));
           }
-          const uint32_t nx = snxt[it];
-          if (prev == NONE || lj < prev_len) { prev = it; prev_len = lj; prev_nxt = nx; }
-          it = nx;
+          const uint64_t fb = __ballot(ok);
+          const uint32_t lim = fb ? (uint32_t)__ffsll((unsigned long long)fb) - 1 : 64u;
+          const uint32_t key = lj << 16 | s;
+          if (valid & (lane < lim) & (key < best)) best = key;
+#ifdef PBGPU_PROF
+          PROF_ADD(23, 1);
+#endif
+          if (fb) {
+            found_s = c0 + lim; hit = true;
+            found = (uint32_t)__builtin_amdgcn_readlane((int)j, (int)lim);
+            break;
+          }
+        }
+        tests += hit ? found_s + 1 : i;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          const uint32_t y = (uint32_t)__shfl_xor((int)best, o, 64);
+          best = y < best ? y : best;
         }
         uint32_t elen, eroot, P;
-        if (found != NONE) { elen = sln[found] + 1u; eroot = sroot[found]; P = found; }
+        if (hit) { elen = sln[found] + 1u; eroot = sroot[found]; P = found; }
         else { elen = 1; eroot = i; P = NONE; }
-        uint32_t enxt;
-        if (prev == NONE) { enxt = head; head = i; }
-        else { enxt = prev_nxt; if (lane == 0) snxt[prev] = (uint16_t)i; }
+        if (best == 0xFFFFFFFFu) {  // nothing met before the taker: insert at the head
+          if (lane == 0) sord[i] = (uint16_t)i;
+          head = i;
+        } else {  // insert after prev (walk step ps): shift positions [a, i) up by one
+          const uint32_t a = i - 1 - (best & 0xFFFFu);
+          for (int32_t t0 = (int32_t)i - 1; t0 >= (int32_t)a; t0 -= 64) {
+            const int32_t q = t0 - lane;
+            const bool mv = q >= (int32_t)a;
+            const uint16_t v = sord[mv ? q : 0];
+            if (mv) sord[q + 1] = v;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+          }
+          if (lane == 0) sord[a] = (uint16_t)i;
+        }
         if (lane == 0) {
-          snxt[i] = (uint16_t)enxt; sln[i] = (uint16_t)elen; sP[i] = (uint16_t)P; sroot[i] = (uint16_t)eroot;
+          sln[i] = (uint16_t)elen; sP[i] = (uint16_t)P; sroot[i] = (uint16_t)eroot;
           srs[i] = (uint16_t)(P + 1 == i ? srs[i - 1] : i);
         }
         if (elen > longest) {
@@ -1707,6 +1753,9 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
         lds_fence();
       }
     }
+#ifdef PBGPU_PROF
+    const uint64_t pw_t2 = __builtin_amdgcn_s_memtime();
+#endif
     // ---- backtracking (indices): whole P(e) = e-1 runs at a time, lis points in ascending order
     // compact layout unless a point lies too far from the last one: then once
     // more in the wide layout (rare: spans beyond 64 kb)
@@ -1736,6 +1785,16 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
     if (lane == 0) lisl[item] = longest;
     my_points += longest;
     lds_fence();  // LDS reads of this strand done before the next strand's commit
+#ifdef PBGPU_PROF
+    {  // per tier (255: slots 24.., 511: 28..): order ticks, order rounds, forward ticks, strand ticks
+      const uint64_t pw_t3 = __builtin_amdgcn_s_memtime();
+      const int sb = SMAX == 255 ? 24 : 28;
+      if (SMAX == 255 || SMAX == 511) {
+        PROF_ADD(sb + 0, pw_t1 - pw_t0); PROF_ADD(sb + 1, pw_rounds); PROF_ADD(sb + 2, pw_t2 - pw_t1);
+        PROF_ADD(sb + 3, pw_t3 - pw_t0);
+      }
+    }
+#endif
   }
   tests = lane == 0 ? tests : 0;
   tests = wave_sum_u64(tests);
@@ -3203,15 +3262,20 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
     const uint32_t r = G.recs[q].read;  // records are grouped per read
     const uint64_t e = G.rec_off[r + 1];
     const uint32_t n = (uint32_t)(e - G.rec_off[r]);
-    const GDesc d = G.desc[q];
+    // a read left to the host has no descriptors (k_graph_sort skipped it: G.desc holds an
+    // earlier batch's words there), so nothing of it is read; its slots are never a j of a
+    // device read's scan (scans stop at their read's end) and its nodes scan nothing
+    const bool dev = graph_on_device(G, n);
+    GDesc d{0.0, 0.0, 0.0, 0u, 0u, 0u, 0u, 0u};
+    if (dev) d = G.desc[q];
     s_is[t] = d.imp_s; s_ie[t] = d.imp_e; s_er[t] = d.err;
     s_meta[t] = d.idx | (d.nsz << 16); s_lpa[t] = d.lp_add; s_po[t] = (uint32_t)d.poff;  // < 2^32 (host check)
     if (t < GE_NODES) {
       s_rl[t] = (double)(G.roff[r + 1] - G.roff[r]);
-      s_end[t] = graph_on_device(G, n) ? (uint32_t)e : (uint32_t)(q + 1);  // a read left to the host: no scan
+      s_end[t] = dev ? (uint32_t)e : (uint32_t)(q + 1);  // a read left to the host: no scan
     }
 #pragma unroll
-    for (uint32_t u = 0; u < GRAPH_U; ++u) s_u[u * GE_SLOTS + t] = u < d.nsz ? G.ounits[d.poff + u] : 0u;
+    for (uint32_t u = 0; u < GRAPH_U; ++u) s_u[u * GE_SLOTS + t] = (dev & (u < d.nsz)) ? G.ounits[d.poff + u] : 0u;
   }
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63;

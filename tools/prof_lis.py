@@ -51,6 +51,14 @@ def main():
         print(f"  {n:16s} {x / waves:12.0f} ticks/wave  ({100.0 * x / max(1, v[5]):5.1f}%)")
     g = list(buf)
     print(f"k_lis_w: literal steps={g[20]} (scan iterations {g[23]}), clean runs={g[21]} covering {g[22]} elements")
+    for label, sb in (("k_lis_w<255>", 24), ("k_lis_w<511>", 28)):
+        tot = max(1, g[sb + 3])
+        print(f"  {label}: order {100.0 * g[sb] / tot:5.1f}% ({g[sb + 1]} rounds), forward {100.0 * g[sb + 2] / tot:5.1f}%, "
+              f"backtrack+rest {100.0 * (tot - g[sb] - g[sb + 2]) / tot:5.1f}%, strand ticks {g[sb + 3]}")
+    print(f"stages ms: seed {st['ms_seed']:.1f} group {st['ms_group']:.1f} lis {st['ms_lis']:.1f} fit {st['ms_fit']:.1f} "
+          f"records {st['ms_records']:.1f}")
+    print(f"counters: hits {st['n_hits']}, lis tests {st['n_lis_tests']}, chains {st.get('n_chains')}, "
+          f"records {st.get('n_records')}, bases {sum(len(s) for s in ds.pb_seqs()) if a.reads <= 20000 else 'n/a'}")
     for label, sb in (("k_group 2048-slot tier", 8), ("k_group 8192-slot tier", 14)):
         blocks = max(1, g[sb + 5])
         print(f"{label}: blocks={g[sb + 5]} (ms: tier0 {st['kernel_ms']['k_group']:.2f})")
