@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PBGPU_ABI_VERSION 6
+#define PBGPU_ABI_VERSION 7
 
 typedef enum pbgpu_status {
   PBGPU_OK = 0,
@@ -261,8 +261,12 @@ typedef struct {
   uint64_t graph_ovf_nodes;
   /* host time ordering a batch's reads for the group stage (the GPU waits for it) */
   double   ms_host_order;
-  /* overlap graph: reads left to the host graph (more than 8192 records) */
+  /* overlap graph: reads left to the host graph (more than 65535 records; 8192 before ABI 7) */
   uint64_t graph_host_reads;
+  /* ABI 7: group-stage rounds that doubled the hash partitions of the reads
+   * overflowing the 8192-slot table (instead of an HBM table), and reads grouped
+   * in HBM tables */
+  uint64_t group_refines, group_hbm_reads;
 } pbgpu_stats;
 pbgpu_status pbgpu_aligner_get_stats(const pbgpu_aligner* al, pbgpu_stats* s);
 pbgpu_status pbgpu_aligner_reset_stats(pbgpu_aligner* al);
@@ -519,6 +523,11 @@ typedef struct {
    * hipMalloc / hipFree (a call that blocks shows here) */
   uint64_t device_alloc_bytes;
   double   alloc_seconds;
+  /* ABI 7: the device working set -- the workers' largest live device bytes (each
+   * worker's aligner buffers at their high-water mark), summed over the workers --
+   * and, with records_fn and a device graph, the reads whose graph the host finished */
+  uint64_t device_peak_bytes;
+  uint64_t graph_host_reads;
 } pbgpu_run_stats;
 
 pbgpu_status pbgpu_run(pbgpu_index* const* indexes, size_t n_indexes, const pbgpu_align_params* params,

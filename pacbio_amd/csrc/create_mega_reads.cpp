@@ -10,7 +10,7 @@
 // GPU after each batch's records are sorted (k_graph*, k_mega; ABI 5,
 // pbgpu_aligner_set_graph); the host only writes the text, on -t threads.  The
 // host restatement (overlap_graph.cpp) runs --dot, --host-graph and the reads
-// the device leaves to it (more than 4,096 records).  The mega-reads of each
+// the device leaves to it (more than GRAPH_NMAX_BIG = 65,535 records; round 5).  The mega-reads of each
 // batch are written in input order (the reference's output with -t 1).
 // GPU options as in jf_aligner: --devices, --streams, --batch-bases, --timing
 // (stage times as JSON on stderr).
@@ -382,13 +382,14 @@ int main(int argc, char** argv) {
             "\"output_bytes\": %llu, \"read_s\": %.6f, \"upload_s\": %.6f, \"align_s\": %.6f, "
             "\"download_s\": %.6f, \"graph_s\": %.6f, \"write_s\": %.6f, \"writer_idle_s\": %.6f, "
             "\"device_allocs\": %llu, \"device_allocs_late\": %llu, \"pinned_allocs\": %llu, "
-            "\"pinned_allocs_late\": %llu, \"device_alloc_bytes\": %llu, \"alloc_s\": %.6f}\n",
+            "\"pinned_allocs_late\": %llu, \"device_alloc_bytes\": %llu, \"alloc_s\": %.6f, "
+            "\"device_peak_bytes\": %llu, \"graph_host_reads\": %llu}\n",
             st.wall_seconds, (unsigned long long)st.n_batches, (unsigned long long)st.n_reads,
             (unsigned long long)st.n_bases, (unsigned long long)st.n_records, (unsigned long long)st.coords_bytes,
             st.read_seconds, st.upload_seconds, st.align_seconds, st.format_seconds, st.d2h_seconds, st.write_seconds,
             st.writer_idle_seconds, (unsigned long long)st.n_device_allocs,
             (unsigned long long)st.n_device_allocs_late, (unsigned long long)st.n_pinned_allocs,
             (unsigned long long)st.n_pinned_allocs_late, (unsigned long long)st.device_alloc_bytes,
-            st.alloc_seconds);
+            st.alloc_seconds, (unsigned long long)st.device_peak_bytes, (unsigned long long)st.graph_host_reads);
   return 0;
 }

@@ -225,13 +225,14 @@ int main(int argc, char** argv) {
             "\"coords_bytes\": %llu, \"read_s\": %.6f, \"upload_s\": %.6f, \"align_s\": %.6f, \"format_s\": %.6f, "
             "\"d2h_s\": %.6f, \"write_s\": %.6f, \"writer_idle_s\": %.6f, "
             "\"device_allocs\": %llu, \"device_allocs_late\": %llu, \"pinned_allocs\": %llu, "
-            "\"pinned_allocs_late\": %llu, \"device_alloc_bytes\": %llu, \"alloc_s\": %.6f}\n",
+            "\"pinned_allocs_late\": %llu, \"device_alloc_bytes\": %llu, \"alloc_s\": %.6f, "
+            "\"device_peak_bytes\": %llu}\n",
             st.wall_seconds, (unsigned long long)st.n_batches, (unsigned long long)st.n_reads,
             (unsigned long long)st.n_bases, (unsigned long long)st.n_records, (unsigned long long)st.coords_bytes,
             st.read_seconds, st.upload_seconds, st.align_seconds, st.format_seconds, st.d2h_seconds, st.write_seconds,
             st.writer_idle_seconds, (unsigned long long)st.n_device_allocs,
             (unsigned long long)st.n_device_allocs_late, (unsigned long long)st.n_pinned_allocs,
             (unsigned long long)st.n_pinned_allocs_late, (unsigned long long)st.device_alloc_bytes,
-            st.alloc_seconds);
+            st.alloc_seconds, (unsigned long long)st.device_peak_bytes);
   return 0;
 }

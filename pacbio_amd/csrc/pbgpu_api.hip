@@ -49,10 +49,14 @@ void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const ui
                   const uint64_t* hit_off, uint64_t node_base, uint32_t r0, const uint32_t* read_list, uint32_t n_list,
                   uint32_t hcap_log2, uint32_t* gtable, GroupOut O, unsigned long long* stats, hipStream_t st);
 uint64_t group_table_words(uint32_t hcap_log2);
+void launch_group_refine(const uint32_t* list, uint32_t n, uint2* prog, hipStream_t st);
 void launch_sr_ul(const uint32_t* ids, uint64_t n, const int32_t* ul, uint64_t n_ul, int32_t* out, hipStream_t st);
 void launch_counts_pack16(bool unpack, const uint32_t* src, uint64_t n, uint32_t* dst, hipStream_t st);
 void launch_occ_sr(const uint64_t* occ, uint64_t n, uint32_t* out, hipStream_t st);
-constexpr uint32_t kGroupLdsMaxLog2 = 13;  // 8192-slot table, 96 KiB of LDS
+#ifndef PBGPU_GROUP_BIG_LOG2
+#define PBGPU_GROUP_BIG_LOG2 13
+#endif
+constexpr uint32_t kGroupLdsMaxLog2 = PBGPU_GROUP_BIG_LOG2;  // 8192-slot table, 96 KiB of LDS
 void launch_init_slen(const ChainDesc* chains, uint32_t n_chains, uint32_t* slen, hipStream_t st);
 void launch_strand_order(const uint32_t* slen, uint32_t n_items, uint32_t* hist, uint32_t* cursor, uint32_t* perm,
                          int phase, hipStream_t st);
@@ -1254,8 +1258,112 @@ pbgpu_status pbgpu_aligner_create(const pbgpu_index* ix, const pbgpu_align_param
   API_CATCH
 }
 
+// PBGPU_DEBUG_BUFFERS=1: each aligner's device buffers at its free, largest first (the
+// working set by buffer; pbgpu_run_stats.device_peak_bytes is the device-wide figure)
+static void buffer_report(const pbgpu_aligner* al) {
+  std::vector<std::pair<const char*, size_t>> v = {
+      {"ul", al->ul.bytes()},
+      {"sr_ul", al->sr_ul.bytes()},
+      {"krec", al->krec.bytes()},
+      {"n_kept", al->n_kept.bytes()},
+      {"thr", al->thr.bytes()},
+      {"rec_per_read", al->rec_per_read.bytes()},
+      {"rec_cursor", al->rec_cursor.bytes()},
+      {"order", al->order.bytes()},
+      {"ovf_reads", al->ovf_reads.bytes()},
+      {"counters", al->counters.bytes()},
+      {"sort_scratch", al->sort_scratch.bytes()},
+      {"nhits", al->nhits.bytes()},
+      {"hit_off", al->hit_off.bytes()},
+      {"rec_off", al->rec_off.bytes()},
+      {"huge_elems", al->huge_elems.bytes()},
+      {"hits", al->hits.bytes()},
+      {"chains", al->chains.bytes()},
+      {"perm", al->perm.bytes()},
+      {"X", al->X.bytes()},
+      {"pts", al->pts.bytes()},
+      {"nodes", al->nodes.bytes()},
+      {"nodes32", al->nodes32.bytes()},
+      {"lisl", al->lisl.bytes()},
+      {"hist", al->hist.bytes()},
+      {"slen", al->slen.bytes()},
+      {"recs", al->recs.bytes()},
+      {"recs_sorted", al->recs_sorted.bytes()},
+      {"rec_read", al->rec_read.bytes()},
+      {"rec_slot", al->rec_slot.bytes()},
+      {"info_m", al->info_m.bytes()},
+      {"info_b", al->info_b.bytes()},
+      {"tmp", al->tmp.bytes()},
+      {"gtable", al->gtable.bytes()},
+      {"stats", al->stats.bytes()},
+      {"info_count", al->info_count.bytes()},
+      {"ovf_list", al->ovf_list.bytes()},
+      {"read_list", al->read_list.bytes()},
+      {"nparts", al->nparts.bytes()},
+      {"prog", al->prog.bytes()},
+      {"gcount", al->gcount.bytes()},
+      {"gcount16", al->gcount16.bytes()},
+      {"fwin", al->fwin.bytes()},
+      {"fread_hits", al->fread_hits.bytes()},
+      {"lstart", al->lstart.bytes()},
+      {"lend", al->lend.bytes()},
+      {"emit_of", al->emit_of.bytes()},
+      {"X2", al->X2.bytes()},
+      {"g_poff", al->g_poff.bytes()},
+      {"g_pre", al->g_pre.bytes()},
+      {"g_sizes", al->g_sizes.bytes()},
+      {"g_desc", al->g_desc.bytes()},
+      {"g_imp", al->g_imp.bytes()},
+      {"g_out", al->g_out.bytes()},
+      {"g_ecnt", al->g_ecnt.bytes()},
+      {"g_eoff", al->g_eoff.bytes()},
+      {"g_edges", al->g_edges.bytes()},
+      {"g_eovf", al->g_eovf.bytes()},
+      {"g_maxn", al->g_maxn.bytes()},
+      {"g_ovf", al->g_ovf.bytes()},
+      {"g_ovf_list", al->g_ovf_list.bytes()},
+      {"g_cand", al->g_cand.bytes()},
+      {"g_ord", al->g_ord.bytes()},
+      {"g_ivs", al->g_ivs.bytes()},
+      {"g_mo", al->g_mo.bytes()},
+      {"g_mc", al->g_mc.bytes()},
+      {"g_mcount", al->g_mcount.bytes()},
+      {"g_munits", al->g_munits.bytes()},
+      {"g_nhost", al->g_nhost.bytes()},
+      {"g_mhost", al->g_mhost.bytes()},
+      {"g_moff", al->g_moff.bytes()},
+      {"g_uused", al->g_uused.bytes()},
+      {"g_rsize", al->g_rsize.bytes()},
+      {"g_isize", al->g_isize.bytes()},
+      {"g_hroff", al->g_hroff.bytes()},
+      {"g_hioff", al->g_hioff.bytes()},
+      {"g_hrec", al->g_hrec.bytes()},
+      {"g_hgraph", al->g_hgraph.bytes()},
+      {"g_hinfo", al->g_hinfo.bytes()},
+      {"fmt_len", al->fmt_len.bytes()},
+      {"fmt_pos", al->fmt_pos.bytes()},
+      {"text", al->text.bytes()},
+      {"redo[0]", al->redo[0].bytes()},
+      {"redo[1]", al->redo[1].bytes()},
+      {"redo[2]", al->redo[2].bytes()},
+      {"fwk[0]", al->fwk[0].bytes()},
+      {"fwk[1]", al->fwk[1].bytes()},
+      {"fwi[0]", al->fwi[0].bytes()},
+      {"fwi[1]", al->fwi[1].bytes()},
+      {"fkeys[0]", al->fkeys[0].bytes()},
+      {"fkeys[1]", al->fkeys[1].bytes()}};
+  std::sort(v.begin(), v.end(), [](const auto& a, const auto& b) { return a.second > b.second; });
+  size_t tot = 0;
+  for (const auto& e : v) tot += e.second;
+  fprintf(stderr, "pbgpu buffers: aligner %p device %d: %.3f GB in all;", (const void*)al, al->device, tot * 1e-9);
+  for (const auto& e : v)
+    if (e.second >= (16u << 20)) fprintf(stderr, " %s %.3f", e.first, e.second * 1e-9);
+  fprintf(stderr, "\n");
+}
+
 pbgpu_status pbgpu_aligner_free(pbgpu_aligner* al) {
   if (!al) return PBGPU_OK;
+  if (getenv("PBGPU_DEBUG_BUFFERS")) buffer_report(al);
   (void)hipSetDevice(al->device);  // not al->ix: the index may be freed first
   for (auto& e : al->ev) if (e) (void)hipEventDestroy(e);
   if (al->g_fork) (void)hipEventDestroy(al->g_fork);
@@ -1659,8 +1767,12 @@ static void graph_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   G.info_m = al->info_m.p; G.info_b = al->info_b.p;
   G.play = al->g_play; G.nb_errors = al->g_errors; G.k = al->g_k; G.bases = al->g_bases;
   // PBGPU_GRAPH_NMAX (tests): a lower cap on the records of a read traversed on the device
-  G.nmax = GRAPH_NMAX;
-  if (const char* e = getenv("PBGPU_GRAPH_NMAX")) G.nmax = (uint32_t)std::min<long>(GRAPH_NMAX, std::max(0l, atol(e)));
+  G.nmax = GRAPH_NMAX_BIG;
+  if (const char* e = getenv("PBGPU_GRAPH_NMAX")) G.nmax = (uint32_t)std::min<long>(GRAPH_NMAX_BIG, std::max(0l, atol(e)));
+  // reads past GRAPH_NMAX records keep their sort keys and node state here (6 words a
+  // record, the records stage's sort scratch: sized for this batch's records already)
+  al->sort_scratch.ensure(6ull * nrec + 6);
+  G.scratch = al->sort_scratch.p;
   al->g_poff.ensure(nrec + 1); al->g_sizes.ensure(nrec + 1); al->g_maxn.ensure(1);
   G.poff = al->g_poff.p; G.max_n = al->g_maxn.p;
   HIPCHK(hipMemsetAsync(al->g_maxn.p, 0, 4, st));
@@ -1800,7 +1912,11 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
     while (r1 < n && hoff[r1] - hoff[r0] < target && hoff[r1 + 1] - hoff[r0] <= budget) ++r1;
     const uint64_t Hs = hoff[r1] - hoff[r0];
     const uint32_t nr = r1 - r0;
-    al->X.ensure(Hs + 1 + GROUP_SINKS); al->pts.ensure(Hs + 9); al->nodes.ensure((Hs + 1) * 8);  // pts: + one 64-byte row (k_coords row loads)
+    // per-hit buffers: at most the hit budget's (a read past it forms a sub-batch of its own)
+    const uint64_t hcap = std::max<uint64_t>(Hs, std::min<uint64_t>(budget, 1ull << 40)) + 64;
+    al->X.ensure_capped(Hs + 1 + GROUP_SINKS, hcap + GROUP_SINKS);
+    al->pts.ensure_capped(Hs + 9, hcap);  // pts: + one 64-byte row (k_coords row loads)
+    al->nodes.ensure_capped((Hs + 1) * 8, hcap * 8);
     al->chains.ensure(std::min<uint64_t>(Hs, (uint64_t)nr << 10) + 1);  // grown below if a batch needs more
     GroupOut O;
     O.X = al->X.p; O.chains = al->chains.p;
@@ -1904,19 +2020,38 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
         HIPCHK(hipMemcpy(ovf.data(), al->ovf_reads.p, n_ovf * 4, hipMemcpyDeviceToHost));
         uint64_t mx = 0;
         for (uint32_t r : ovf) mx = std::max(mx, hoff[r + 1] - hoff[r]);
-        // next tier: the 8192-slot LDS table, then HBM tables x4 each round (a read
-        // from the 8192 tier may retry it once; results do not depend on the tier)
-        lg = lg < kGroupLdsMaxLog2 ? kGroupLdsMaxLog2 : lg + 2;
+        // next tier: the 8192-slot LDS table; a read that overflows it again stays there
+        // with twice its hash partitions (k_group_refine: the placed partitions keep their
+        // lists, the rest split in two), while every read's count fits the u8; past that,
+        // HBM tables x4 each round (results do not depend on the tier).  On C4r reads the
+        // HBM tier took 75 ms a launch (r04h) for what refined LDS passes do in a fraction.
+        const bool refine_off = getenv("PBGPU_GROUP_REFINE") && !atoi(getenv("PBGPU_GROUP_REFINE"));  // (tests)
+        bool refine = false;
+        if (lg == kGroupLdsMaxLog2 && !refine_off) {
+          refine = true;
+          for (uint32_t r : ovf) refine &= al->h_parts[r - r0] <= 127;
+        }
+        if (refine) {
+          for (uint32_t r : ovf) al->h_parts[r - r0] *= 2;
+          ++al->acc.group_refines;
+        } else {
+          lg = lg < kGroupLdsMaxLog2 ? kGroupLdsMaxLog2 : lg + 2;
+        }
         if (lg > kGroupLdsMaxLog2 && (1ull << (lg - 2)) > 2 * mx + 256)
           throw std::runtime_error("group table growth did not converge");
         al->ovf_list.ensure(n_ovf);
         HIPCHK(hipMemcpyAsync(al->ovf_list.p, ovf.data(), n_ovf * 4, hipMemcpyHostToDevice, st));
         HIPCHK(hipMemsetAsync(al->counters.p + 3, 0, 4, st));
+        if (refine) {
+          HIPCHK(hipMemcpyAsync(al->nparts.p + r0, al->h_parts.data(), nr, hipMemcpyHostToDevice, st));
+          launch_group_refine(al->ovf_list.p, n_ovf, al->prog.p, st);
+        }
         if (lg <= kGroupLdsMaxLog2) {
           launch_group(v, al->krec.p, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0,
                        al->ovf_list.p, n_ovf, lg, nullptr, O, al->stats.p, st);
           HIPCHK(hipGetLastError());
         } else {
+          al->acc.group_hbm_reads += n_ovf;
           const uint64_t words = group_table_words(lg);
           const uint32_t grp = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_ovf, (1ull << 28) / words));
           al->gtable.ensure_fixed((uint64_t)grp * words);

@@ -142,17 +142,24 @@ void run_parallel(int threads, F&& work) {
 // target when the batch is a ramped one filled to its target (the first
 // batches of a run are 1/8 .. 1/2 of a full batch; a batch cut short by the
 // end of the input has no full batches after it and keeps 1):
-// a per-batch buffer that must grow is then sized for a full batch with 2x
+// a per-batch buffer that must grow is then sized for a full batch with 1.5x
 // headroom (a ramped first batch holds few reads, so its hit and record
-// densities vary), and the full batches that follow allocate nothing.
+// densities vary), and the full batches that follow allocate nothing.  Round 5:
+// 1.5x, not 2x (a cold C2 create_mega_reads run held 63 GB of buffers); the
+// per-hit buffers are also capped by the aligner's hit budget (ensure_capped),
+// which pbgpu_run sets per aligner, so they never follow the ramp's estimate
+// past it.
 inline thread_local uint64_t tl_dev_allocs = 0, tl_pinned_allocs = 0, tl_dev_bytes = 0;
+// device bytes held by this thread's allocations and their high-water mark (a worker's
+// aligner: its working set; pbgpu_run_stats.device_peak_bytes sums the workers' peaks)
+inline thread_local int64_t tl_dev_live = 0, tl_dev_peak = 0;
 inline thread_local double tl_alloc_s = 0;   // seconds in hipMalloc / hipFree of dbufs
 inline thread_local double tl_pinned_s = 0;  // seconds in the run path's hipHostMalloc / hipHostFree
 inline double mono_s() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 inline thread_local double tl_grow_scale = 1.0;
 inline size_t grow_target(size_t cnt) {
   const double s = tl_grow_scale;
-  return s > 1.0 ? (size_t)((double)cnt * s * 2.0) + 1 : cnt + cnt / 4;
+  return s > 1.0 ? (size_t)((double)cnt * s * 1.5) + 1 : cnt + cnt / 4;
 }
 template <typename T>
 struct dbuf {
@@ -167,6 +174,7 @@ struct dbuf {
       const double t = mono_s();
       HIPFREE(hipFree(p));
       tl_alloc_s += mono_s() - t;
+      tl_dev_live -= (int64_t)(n * sizeof(T));
     }
     p = nullptr; n = 0;
   }
@@ -178,13 +186,19 @@ struct dbuf {
       HIPCHK(hipMalloc((void**)&p, cnt * sizeof(T)));
       tl_alloc_s += mono_s() - t;
       ++tl_dev_allocs; tl_dev_bytes += cnt * sizeof(T);
+      tl_dev_live += (int64_t)(cnt * sizeof(T)); tl_dev_peak = std::max(tl_dev_peak, tl_dev_live);
       n = cnt;
     }
   }
   // A per-batch buffer grows to at least twice its size (first: grow_target of the
   // request): a run's batches vary, and every reallocation is a device-wide hipFree
   // plus a hipMalloc, which now and then blocks for seconds (PBGPU_DEBUG_STALL)
-  void ensure(size_t cnt) { if (cnt > n) alloc(std::max(grow_target(cnt), 2 * n)); }
+  void ensure(size_t cnt) { if (cnt > n) alloc(std::max(grow_target(cnt), n + n / 2)); }
+  // the same, never sized past cap (a buffer whose need is bounded: the per-hit buffers
+  // by the hit budget of a sub-batch) unless cnt itself is
+  void ensure_capped(size_t cnt, size_t cap) {
+    if (cnt > n) alloc(std::max(cnt, std::min(std::max(grow_target(cnt), n + n / 2), cap)));
+  }
   // a buffer whose size does not follow the batch's (never scaled by tl_grow_scale)
   void ensure_fixed(size_t cnt) { if (cnt > n) alloc(std::max(cnt + cnt / 4, 2 * n)); }
   // grow keeping the first `keep` elements (stream-ordered copy)
@@ -197,6 +211,7 @@ struct dbuf {
     HIPCHK(hipMalloc((void**)&q, nn * sizeof(T)));
     tl_alloc_s += mono_s() - t;
     ++tl_dev_allocs; tl_dev_bytes += nn * sizeof(T);
+    tl_dev_live += (int64_t)(nn * sizeof(T)); tl_dev_peak = std::max(tl_dev_peak, tl_dev_live);
     if (p && keep) HIPCHK(hipMemcpyAsync(q, p, keep * sizeof(T), hipMemcpyDeviceToDevice, st));
     HIPCHK(hipStreamSynchronize(st));
     release();

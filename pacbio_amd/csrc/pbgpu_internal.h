@@ -203,7 +203,11 @@ struct GraphNode {
 };
 static_assert(sizeof(GraphNode) == 24, "GraphNode layout must match pbgpu_graph_node");
 constexpr uint32_t GRAPH_START = 1u, GRAPH_END = 2u, GRAPH_HOST = 1u << 31;  // flags
-constexpr uint32_t GRAPH_NMAX = 8192;  // records of a read traversed on the device (more: GRAPH_HOST)
+constexpr uint32_t GRAPH_NMAX = 8192;  // records of a read traversed with its node state in LDS
+// records of a read traversed on the device at all (more: GRAPH_HOST): past GRAPH_NMAX the
+// sort keys and the node state live in the read's region of GraphDev::scratch; an edge
+// names its node j in 16 bits
+constexpr uint32_t GRAPH_NMAX_BIG = 65535;
 // a record in the per-read sorted order (k_graph's ring of sorted positions)
 struct GDesc {
   double imp_s, imp_e, err;
@@ -223,7 +227,7 @@ struct GraphDev {
   double play, nb_errors;     // -O, -e
   uint32_t k;                 // -k
   int bases;                  // -b
-  uint32_t nmax;              // reads with more records go to the host (<= GRAPH_NMAX; tests lower it)
+  uint32_t nmax;              // reads with more records go to the host (<= GRAPH_NMAX_BIG; tests lower it)
   double2* imp;               // per record: implied start, end
   uint64_t* poff;             // per record: its prefix sums' offset (nsz + 1 each)
   uint2* pp;                  // prefix sums along the name: {unitig lengths, info[2u] - info[2u - 1]}
@@ -255,6 +259,10 @@ struct GraphDev {
   uint64_t units_cap;
   uint64_t n_recs;
   uint32_t* n_host;           // reads left to the host
+  // 6 words per record (the records stage's sort scratch, free by then): reads of more
+  // than GRAPH_NMAX records keep their sort keys, then their node state, then k_mega's
+  // root bitmap in their region [6 rec_off[r], 6 rec_off[r + 1])
+  uint64_t* scratch;
 };
 // mega_read_info (overlap_graph.hpp:48-58) of a candidate, with its node's lpath and root
 struct MegaTmp {
@@ -292,7 +300,10 @@ void launch_graph_sizes(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, ui
 // -> G.out.  side / side2: streams for the reads of more than GRAPH_NM_SMALL records
 // (their sort and relaxation run beside the others'); fork / join / join2: events
 // ordering them with st
-constexpr uint32_t GRAPH_EBLK = 64;
+#ifndef PBGPU_GRAPH_EBLK
+#define PBGPU_GRAPH_EBLK 64
+#endif
+constexpr uint32_t GRAPH_EBLK = PBGPU_GRAPH_EBLK;
 // (max_n: *G.max_n as k_graph_sizes left it; tiers above it are not launched)
 hipError_t launch_graph(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, uint32_t max_n, hipStream_t st,
                         hipStream_t side, hipEvent_t fork, hipEvent_t join, uint64_t* ovf);

@@ -1815,6 +1815,8 @@ __global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict_
 // array must not be reached through a flat pointer, whose accesses wait for
 // every outstanding global load (the row prefetch).
 typedef __attribute__((address_space(3))) int32_t lds_i32;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
 // kmers_info of names with at most INFO_LDS_UNITIGS unitigs is accumulated in LDS (k_coords)
 constexpr uint32_t INFO_LDS_UNITIGS = 8, INFO_LDS = 2 * INFO_LDS_UNITIGS - 1;
 template <typename T>
@@ -2610,7 +2612,10 @@ void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const ui
     // PBGPU_GROUP_LDS_PAD (experiment): extra dynamic LDS for the 4-wave tier, so fewer of
     // its blocks share a CU (fewer reads' lists open at once)
     static const size_t pad = getenv("PBGPU_GROUP_LDS_PAD") ? (size_t)atol(getenv("PBGPU_GROUP_LDS_PAD")) : 0;
-    const size_t lds = ((size_t)3 << hcap_log2) * sizeof(uint32_t) + (hcap_log2 < 13 ? pad : 0);
+#ifndef PBGPU_GROUP_BIG_LOG2
+#define PBGPU_GROUP_BIG_LOG2 13
+#endif
+    const size_t lds = ((size_t)3 << hcap_log2) * sizeof(uint32_t) + (hcap_log2 < PBGPU_GROUP_BIG_LOG2 ? pad : 0);
     // the 96 KiB dynamic-LDS attribute, set once per device (function attributes are per device)
     static std::atomic<uint64_t> attr_done(0);
     int dev = 0;
@@ -2623,7 +2628,7 @@ void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const ui
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
       attr_done.fetch_or(bit, std::memory_order_acq_rel);
     }
-    if (hcap_log2 >= 13)
+    if (hcap_log2 >= PBGPU_GROUP_BIG_LOG2)
       hipLaunchKernelGGL((k_group<false, GROUP_BLOCK_BIG>), dim3(n_list), dim3(GROUP_BLOCK_BIG), lds, st, ix, krec, roff,
                          n_kept, thr, hit_off, node_base, r0, read_list, n_list, hcap_log2, gtable, O, stats);
     else
@@ -2664,6 +2669,17 @@ void launch_sr_ul(const uint32_t* ids, uint64_t n, const int32_t* ul, uint64_t n
   if (n) hipLaunchKernelGGL(k_sr_ul, dim3(1024), dim3(256), 0, st, ids, n, ul, n_ul, out);
 }
 uint64_t group_table_words(uint32_t hcap_log2) { return (uint64_t)3 << hcap_log2; }
+// A read that overflowed the 8192-slot table in partition p of P resumes with 2P
+// partitions from partition 2p.  part_of() maps a super-read to a hash range
+// floor(h * P / 2^32), so partition p of P is exactly partitions 2p and 2p + 1 of 2P:
+// the partitions already placed keep their lists, and the rest split in two.
+__global__ void k_group_refine(const uint32_t* __restrict__ list, uint32_t n, uint2* prog) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) { const uint32_t r = list[t]; prog[r].x *= 2; }
+}
+void launch_group_refine(const uint32_t* list, uint32_t n, uint2* prog, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_group_refine, dim3((n + 255) / 256), dim3(256), 0, st, list, n, prog);
+}
 
 static uint32_t grid_for(uint32_t n, uint32_t block, uint32_t cap = 65536) {
   uint64_t g = ((uint64_t)n + block - 1) / block;
@@ -3162,7 +3178,7 @@ DEV uint64_t graph_dkey(double x) {
 #endif
 constexpr uint32_t GRAPH_SORT_BLOCK = 256, GRAPH_NM_SMALL = 1024, GRAPH_NM_MID = 4096, GRAPH_RELAX_MIN = 512,
                    GRAPH_RELAX_PF = PBGPU_RELAX_PF;
-static_assert(GRAPH_EBLK == 64, "k_graph_relax takes a node's block as one 64-lane load");
+static_assert(GRAPH_EBLK >= 1 && GRAPH_EBLK <= 64, "k_graph_relax takes a node's block with one 64-lane load");
 template <uint32_t NM>
 DEV bool graph_tier(const GraphDev& G, uint32_t n) {
   if (n == 0 || n > G.nmax || n > GRAPH_NMAX) return false;
@@ -3216,15 +3232,16 @@ __global__ __launch_bounds__(GRAPH_SORT_BLOCK) void k_graph_sort(GraphDev G, uin
 // block.  OVF: a wave per listed node runs its scan again (from HBM) and writes the
 // edges past its block there.
 constexpr uint32_t GRAPH_U = 8;  // names of at most this many unitigs are matched in registers
-constexpr uint32_t GRAPH_NMAX_K = GRAPH_NMAX;  // reads of more records go to the host (LDS state)
+constexpr uint32_t GRAPH_NMAX_K = GRAPH_NMAX;  // reads of more records: k_graph_relax_big (state in HBM)
 constexpr uint32_t GRAPH_ROOT_BITS = 13;  // k_graph_relax matches roots by this many bits
 static_assert(GRAPH_NMAX_K <= (1u << GRAPH_ROOT_BITS) && GRAPH_NMAX_K < 0x8000u,
               "k_graph_relax matches roots by GRAPH_ROOT_BITS and keeps 15-bit indices");
+static_assert(GRAPH_NMAX_BIG <= 0xFFFFu, "an edge holds its node j in 16 bits");
 #ifndef PBGPU_GE_SLOTS
 #define PBGPU_GE_SLOTS 384
 #endif
 constexpr uint32_t GE_NODES = 64, GE_SLOTS = PBGPU_GE_SLOTS, GE_BLOCK = 256;
-DEV bool graph_on_device(const GraphDev& G, uint32_t n) { return n > 0 && n <= G.nmax && n <= GRAPH_NMAX_K; }
+DEV bool graph_on_device(const GraphDev& G, uint32_t n) { return n > 0 && n <= G.nmax && n <= GRAPH_NMAX_BIG; }
 // super_read_name::overlap (super_read_name.cc:49-72) in registers for a name i of SA
 // unitigs (wave-uniform: the wave's node): the smallest t >= max(SA - sb + 1, 1) with
 // name_i[t..SA) == name_j[0..SA - t) (0: none), and whether the names are the same
@@ -3462,7 +3479,7 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
   // the nodes' edge blocks: pf[d] holds node p + d's (lanes past its count zero)
   const uint2* EB = G.edges + b * GRAPH_EBLK;
   auto ldb = [&](uint32_t p, uint32_t ec) -> uint2 {
-    return lane < ec ? EB[(uint64_t)p * GRAPH_EBLK + lane] : make_uint2(0u, 0u);
+    return lane < (ec < GRAPH_EBLK ? ec : GRAPH_EBLK) ? EB[(uint64_t)p * GRAPH_EBLK + lane] : make_uint2(0u, 0u);
   };
   uint2 pf[GRAPH_RELAX_PF];
 #pragma unroll
@@ -3489,7 +3506,9 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
     for (uint32_t k0 = 0; k0 < ec; k0 += 64) {
       const bool edge = k0 + lane < ec;
       // past the block: the node's overflow region (G.eoff)
-      const uint2 ce = k0 == 0 ? blk : (edge ? G.eovf[G.eoff[b + p] + (k0 - GRAPH_EBLK) + lane] : make_uint2(0u, 0u));
+      // the first GRAPH_EBLK edges from the node's block (prefetched), the rest from its region past it
+      const uint2 ce = k0 + lane < GRAPH_EBLK ? blk
+                                              : (edge ? G.eovf[G.eoff[b + p] + (k0 + lane - GRAPH_EBLK)] : make_uint2(0u, 0u));
       const uint32_t it_j = ce.x & 0xFFFFu;
       PROF_T(pa);
 #ifdef PBGPU_PROF
@@ -3589,6 +3608,196 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
     uint32_t q = i;
     while (s_par[q] != q) q = s_par[q];
     // start node: no edge into it; end node: no edge out of it
+    const uint32_t fl = (s_fl[i] & 1 ? 0u : GRAPH_START) | (s_fl[i] & 2 ? 0u : GRAPH_END);
+    G.out[b + i] = GraphNode{s_lp[i], s_lst[i], s_lpv[i], s_lun[i], q, fl};
+  }
+}
+// Reads of more than GRAPH_NMAX records (up to GRAPH_NMAX_BIG; on C4r-shaped reads 1.8%
+// of the reads, round 4 left them to the host graph at ~10 ms of a core each): the same
+// two steps with their keys and node state in the read's region of G.scratch (6 words a
+// record) instead of LDS, one block per such read.
+constexpr uint32_t GRAPH_BIG_BLOCK = 1024;
+DEV bool graph_big(const GraphDev& G, uint32_t n) { return n > GRAPH_NMAX && graph_on_device(G, n); }
+// k_graph_sort for one big read: the bitonic network over np2 <= 2n entries of {hi, lo, ex}
+__global__ __launch_bounds__(GRAPH_BIG_BLOCK) void k_graph_sort_big(GraphDev G, uint32_t n_reads) {
+  const uint32_t r = blockIdx.x;
+  if (r >= n_reads) return;
+  const uint64_t b = G.rec_off[r];
+  const uint32_t n = (uint32_t)(G.rec_off[r + 1] - b);
+  if (!graph_big(G, n)) return;
+  uint32_t np2 = 1;
+  while (np2 < n) np2 <<= 1;
+  uint64_t* hi = G.scratch + 6 * b;
+  uint64_t* lo = hi + np2;
+  uint64_t* ex = lo + np2;
+  for (uint32_t i = threadIdx.x; i < np2; i += GRAPH_BIG_BLOCK) {
+    if (i < n) {
+      const double2 m = G.imp[b + i];
+      hi[i] = graph_dkey(m.x); lo[i] = graph_dkey(m.y); ex[i] = i;
+    } else {
+      hi[i] = ~0ull; lo[i] = ~0ull; ex[i] = ~0ull;
+    }
+  }
+  __syncthreads();
+  bitonic_keys<GRAPH_BIG_BLOCK>(hi, lo, ex, np2);
+  for (uint32_t p = threadIdx.x; p < n; p += GRAPH_BIG_BLOCK) {
+    const uint32_t i = (uint32_t)ex[p];
+    const Rec& R = G.recs[b + i];
+    const double2 m = G.imp[b + i];
+    G.desc[b + p] = GDesc{m.x, m.y, R.avg_err, G.poff[b + i], i, graph_nsz(G, R.sr),
+                          G.bases ? R.sr_cover : (uint32_t)R.nb_mers, 0u};
+  }
+}
+// k_graph_relax for one big read, node state in HBM (8 u32 arrays of n, then the imp_s
+// head bitmap): the same two waves, the same order of updates and unions.  The state is
+// this block's alone and both waves run on one CU, so plain loads and stores with a
+// workgroup fence after each chunk (its stores complete before the next chunk's loads)
+// order it as the LDS kernel's in-order LDS does.
+__global__ __launch_bounds__(128) void k_graph_relax_big(GraphDev G, uint32_t n_reads) {
+  constexpr uint32_t RANK_NAN = 0xFFFFFFFFu, NONE = 0xFFFFFFFFu;
+  const uint32_t r = blockIdx.x;
+  if (r >= n_reads) return;
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint64_t b = G.rec_off[r];
+  const uint32_t n = (uint32_t)(G.rec_off[r + 1] - b);
+  if (!graph_big(G, n)) return;
+  int32_t* s_lp = reinterpret_cast<int32_t*>(G.scratch + 6 * b);
+  int32_t* s_lun = s_lp + n;
+  int32_t* s_lst = s_lun + n;
+  int32_t* s_lpv = s_lst + n;
+  uint32_t* s_lsk = reinterpret_cast<uint32_t*>(s_lpv + n);
+  uint32_t* s_par = s_lsk + n;
+  uint32_t* s_rank = s_par + n;
+  uint32_t* s_fl = s_rank + n;                                  // 1 an edge into it, 2 an edge out of it
+  uint64_t* s_head = G.scratch + 6 * b + 4 * (uint64_t)n;     // (n + 63) / 64 words: within 6n
+  for (uint32_t p0 = 0; p0 < n; p0 += 128) {
+    const uint32_t p = p0 + tid;
+    bool head = false;
+    if (p < n) {
+      const GDesc d = G.desc[b + p];
+      const uint32_t it = d.idx;
+      head = p == 0 || !(G.desc[b + p - 1].imp_s == d.imp_s);  // (-0 == +0; a NaN heads its own)
+      s_lp[it] = (int32_t)d.lp_add; s_lun[it] = (int32_t)d.nsz; s_lst[it] = -1; s_lpv[it] = -1;
+      s_fl[it] = G.ecnt[b + p] ? 2 : 0;
+      s_par[it] = it; s_rank[it] = 0;
+    }
+    const uint64_t hm = __ballot(head);
+    if (lane == 0 && p < n) s_head[p >> 6] = hm;
+  }
+  __syncthreads();
+  for (uint32_t p = tid; p < n; p += 128) {  // rank key: the last head at or before p
+    const GDesc d = G.desc[b + p];
+    uint32_t w = p >> 6;
+    uint64_t m = s_head[w] & (~0ull >> (63 - (p & 63)));
+    while (!m) m = s_head[--w];  // position 0 is a head
+    s_lsk[d.idx] = d.imp_s != d.imp_s ? RANK_NAN : w * 64 + 63 - (uint32_t)__builtin_clzll(m);
+  }
+  __syncthreads();
+  const bool paths = tid < 64;
+  auto ldw = [&](uint32_t p) -> uint32_t {
+    return p < n ? (G.desc[b + p].idx | (G.ecnt[b + p] << 16)) : 0u;
+  };
+  // edge counts past 65535 do not fit the packed word: a node's count comes from ecnt
+  uint32_t c0 = 0, cur = ldw(lane), nxt = ldw(64 + lane);
+  auto wd = [&](uint32_t x) -> uint32_t {
+    const uint32_t o = x - c0;
+    return (uint32_t)__builtin_amdgcn_readlane((int)(o < 64 ? cur : nxt), (int)(o & 63));
+  };
+  const uint2* EB = G.edges + b * GRAPH_EBLK;
+  auto ldb = [&](uint32_t p, uint32_t ec) -> uint2 {
+    return lane < (ec < GRAPH_EBLK ? ec : GRAPH_EBLK) ? EB[(uint64_t)p * GRAPH_EBLK + lane] : make_uint2(0u, 0u);
+  };
+  uint2 pf[GRAPH_RELAX_PF];
+#pragma unroll
+  for (uint32_t d = 0; d < GRAPH_RELAX_PF; ++d) pf[d] = ldb(d, wd(d) >> 16);
+  for (uint32_t p = 0; p < n; ++p) {
+    if (p - c0 == 64) {
+      c0 += 64; cur = nxt;
+      nxt = ldw(c0 + 64 + lane);
+    }
+    const uint32_t w = wd(p), it_i = w & 0xFFFFu;
+    const uint32_t ec = G.ecnt[b + p];  // (wave-uniform load; the packed count is 16 bits)
+    const uint2 blk = pf[0];
+#pragma unroll
+    for (uint32_t d = 0; d + 1 < GRAPH_RELAX_PF; ++d) pf[d] = pf[d + 1];
+    pf[GRAPH_RELAX_PF - 1] = ldb(p + GRAPH_RELAX_PF, wd(p + GRAPH_RELAX_PF) >> 16);
+    if (ec == 0) continue;
+    int32_t lp_i = 0, lun_i = 0, lst_i = 0;
+    uint32_t lsk_i = 0;
+    if (paths) { lp_i = s_lp[it_i]; lun_i = s_lun[it_i]; lst_i = s_lst[it_i]; lsk_i = s_lsk[it_i]; }
+    for (uint32_t k0 = 0; k0 < ec; k0 += 64) {
+      const bool edge = k0 + lane < ec;
+      // the first GRAPH_EBLK edges from the node's block (prefetched), the rest from its region past it
+      const uint2 ce = k0 + lane < GRAPH_EBLK ? blk
+                                              : (edge ? G.eovf[G.eoff[b + p] + (k0 + lane - GRAPH_EBLK)] : make_uint2(0u, 0u));
+      const uint32_t it_j = ce.x & 0xFFFFu;
+      if (paths) {
+        if (edge) {  // node_info update (overlap_graph.cc:41-56); this lane owns node j
+          s_fl[it_j] |= 1;
+          const int32_t nlpath = (int32_t)((uint32_t)lp_i + ce.y);
+          const int32_t lp_j = s_lp[it_j];
+          bool upd = nlpath > lp_j;
+          if (!upd && nlpath == lp_j) {  // (lstart_imp_s: lsk_i > lsk_j, neither NaN)
+            const uint32_t lsk_j = s_lsk[it_j];
+            upd = s_lst[it_j] == -1 || ((lsk_i != RANK_NAN) & (lsk_j != RANK_NAN) & (lsk_i > lsk_j));
+          }
+          if (upd) {
+            s_lp[it_j] = nlpath;
+            s_lst[it_j] = lst_i == -1 ? (int32_t)it_i : lst_i;
+            s_lsk[it_j] = lsk_i;
+            s_lpv[it_j] = (int32_t)it_i;
+            s_lun[it_j] = lun_i + (int32_t)(ce.x >> 16);
+          }
+        }
+      } else {
+        // union_sets(it_i, it_j) for this chunk's edges in j order (union_find.cc:13-23)
+        uint32_t r1 = it_i, R = edge ? it_j : it_i;
+        for (;;) {
+          const uint32_t p1 = s_par[r1], p2 = s_par[R];
+          if ((p1 == r1) & (p2 == R)) break;
+          const uint32_t g1 = s_par[p1], g2 = s_par[p2];
+          if (p1 != r1) { s_par[r1] = g1; r1 = g1; }
+          if (p2 != R) { s_par[R] = g2; R = g2; }
+        }
+        if (!edge) R = r1;
+        const uint64_t fo = __ballot(edge & (R != r1));
+        uint64_t fm = fo;
+        if (fo & (fo - 1)) {  // the first lane of each foreign root: a ballot per bit of R (< 2^16)
+          uint64_t same = fo;
+#pragma unroll
+          for (uint32_t bit = 0; bit < 16; ++bit) {
+            const uint64_t bb = __ballot((R >> bit) & 1u);
+            same &= ((R >> bit) & 1u) ? bb : ~bb;
+          }
+          fm = __ballot(((fo >> lane) & 1) && (same & ((1ull << lane) - 1)) == 0);
+        }
+        const uint32_t rk = fm ? s_rank[R] : 0u;
+        uint32_t cr = r1, crank = fm ? s_rank[r1] : 0u;
+        for (; fm; fm &= fm - 1) {
+          const uint32_t l = (uint32_t)__ffsll((long long)fm) - 1;
+          const uint32_t vv = (uint32_t)__builtin_amdgcn_readlane((int)R, (int)l);
+          const uint32_t vr = (uint32_t)__builtin_amdgcn_readlane((int)rk, (int)l);
+          if (crank > vr) {
+            if (lane == 0) s_par[vv] = cr;
+          } else if (crank < vr) {
+            if (lane == 0) s_par[cr] = vv;
+            cr = vv; crank = vr;
+          } else {
+            ++crank;
+            if (lane == 0) { s_par[vv] = cr; s_rank[cr] = crank; }
+          }
+        }
+      }
+      // this chunk's stores complete before the next chunk's (or node's) loads
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  (void)NONE;
+  __syncthreads();
+  for (uint32_t i = tid; i < n; i += 128) {
+    uint32_t q = i;
+    while (s_par[q] != q) q = s_par[q];
     const uint32_t fl = (s_fl[i] & 1 ? 0u : GRAPH_START) | (s_fl[i] & 2 ? 0u : GRAPH_END);
     G.out[b + i] = GraphNode{s_lp[i], s_lst[i], s_lpv[i], s_lun[i], q, fl};
   }
@@ -3734,8 +3943,11 @@ __global__ __launch_bounds__(64) void k_mega(GraphDev G, uint32_t n_reads) {
     static_assert(GRAPH_NMAX == 64 * 64 * RW, "whole root words a lane");
     __shared__ uint64_t s_roots[GRAPH_NMAX / 64];  // the winners' roots (node indices)
     __shared__ uint32_t s_rpre[GRAPH_NMAX / 64];
-#pragma unroll
-    for (uint32_t t = 0; t < RW; ++t) s_roots[lane * RW + t] = 0;
+    // the root bitmap and its prefix counts: in LDS, or for a read of more than GRAPH_NMAX
+    // records in its region of G.scratch (free after the relaxation)
+    auto components = [&](auto* roots, auto* rpre, uint32_t rw) {
+    for (uint32_t t = 0; t < rw; ++t) roots[lane * rw + t] = 0;
+    __threadfence_block();
     __syncthreads();
     // a candidate wins its root if no candidate of the root has a larger (lpath,
     // density) and none before it an equal one: where the reference's fold (replace on
@@ -3762,31 +3974,43 @@ __global__ __launch_bounds__(64) void k_mega(GraphDev G, uint32_t n_reads) {
           win &= !((r2 == rt) & (better | tie_before));
         }
       }
-      if (win) atomicOr((unsigned long long*)&s_roots[rt >> 6], 1ull << (rt & 63));
+      if (win) __atomic_fetch_or(&roots[rt >> 6], 1ull << (rt & 63), __ATOMIC_RELAXED);
       if (ok) tiled[c] = win ? 1 : 0;  // (scratch until the tiling)
     }
     __threadfence_block();
     __syncthreads();
     // a winner's component index = its root's rank among the winners' roots
-    uint32_t pcw[RW], pc = 0;
-#pragma unroll
-    for (uint32_t t = 0; t < RW; ++t) { pcw[t] = (uint32_t)__builtin_popcountll(s_roots[lane * RW + t]); pc += pcw[t]; }
+    uint32_t pc = 0;
+    for (uint32_t t = 0; t < rw; ++t) pc += (uint32_t)__builtin_popcountll(__atomic_load_n(&roots[lane * rw + t], __ATOMIC_RELAXED));
     uint32_t incl = pc;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t v = __shfl_up(incl, o, 64);
       if (lane >= (uint32_t)o) incl += v;
     }
-    for (uint32_t t = 0, acc = incl - pc; t < RW; ++t) { s_rpre[lane * RW + t] = acc; acc += pcw[t]; }
+    for (uint32_t t = 0, acc = incl - pc; t < rw; ++t) {
+      rpre[lane * rw + t] = acc;
+      acc += (uint32_t)__builtin_popcountll(__atomic_load_n(&roots[lane * rw + t], __ATOMIC_RELAXED));
+    }
     m = (uint32_t)__shfl(incl, 63, 64);
+    __threadfence_block();
     __syncthreads();
     for (uint32_t c = lane; c < nc; c += 64)
       if (tiled[c]) {
         const uint32_t rt = cand[c].root;
-        comp[s_rpre[rt >> 6] + (uint32_t)__builtin_popcountll(s_roots[rt >> 6] & ((1ull << (rt & 63)) - 1))] = (int32_t)c;
+        comp[rpre[rt >> 6] + (uint32_t)__builtin_popcountll(__atomic_load_n(&roots[rt >> 6], __ATOMIC_RELAXED) &
+                                                           ((1ull << (rt & 63)) - 1))] = (int32_t)c;
       }
     __threadfence_block();
     __syncthreads();
+    };
+    if (n > GRAPH_NMAX) {
+      const uint32_t rwb = (n + 4095) / 4096;  // n <= GRAPH_NMAX_BIG: 64 * rwb words of each
+      uint64_t* groots = G.scratch + 6 * b;
+      components(groots, reinterpret_cast<uint32_t*>(groots + 64 * rwb), rwb);
+    } else {
+      components((lds_u64*)s_roots, (lds_u32*)s_rpre, RW);
+    }
     // the tiling order, the reference's stable insertion sorts as ranks: lpath
     // descending (greedy), weight descending (weighted), tiling_end ascending
     // (maximal); none keeps component order.  key: ascending, exact (negation).
@@ -4183,6 +4407,8 @@ hipError_t launch_graph(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, ui
   if (e != hipSuccess) return e;
   // (a tier above the batch's longest read is not launched: an empty 8192-record block
   // still takes a CU's LDS while it starts and exits, 1.4 ms a launch of 50k of them)
+  if (max_n > GRAPH_NMAX)
+    hipLaunchKernelGGL(k_graph_sort_big, dim3(n_reads), dim3(GRAPH_BIG_BLOCK), 0, side, G, n_reads);
   if (max_n > GRAPH_NM_MID)
     hipLaunchKernelGGL(k_graph_sort<GRAPH_NMAX>, dim3(n_reads), dim3(GRAPH_SORT_BLOCK), 0, side, G, n_reads);
   if (max_n > GRAPH_NM_SMALL)
@@ -4211,6 +4437,8 @@ hipError_t launch_graph_relax(const GraphDev& G, uint32_t n_reads, uint64_t n_re
   if (e != hipSuccess) return e;
   // (tiers above the longest read are not launched; the top one also marks the reads
   // left to the host, so it runs whenever a read is past the device cap)
+  if (max_n > GRAPH_NMAX && G.nmax > GRAPH_NMAX)
+    hipLaunchKernelGGL(k_graph_relax_big, dim3(n_reads), dim3(128), 0, side, G, n_reads);
   if (max_n > GRAPH_NMAX / 2 || max_n > G.nmax)
     hipLaunchKernelGGL(k_graph_relax<GRAPH_NMAX>, dim3(n_reads), dim3(128), 0, side, G, n_reads);
   if (max_n > GRAPH_NMAX / 4)

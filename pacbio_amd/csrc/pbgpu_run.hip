@@ -546,8 +546,9 @@ struct RecordsView {
     room(off, (n + 1) * 8);
     if (!dev_mega || al->g_hosts) HIPCHK(hipMemcpyAsync(off.p, d_off, (n + 1) * 8, hipMemcpyDeviceToHost, al->st));
     else memset(off.p, 0, (n + 1) * 8);
-    // (with device mega-reads only the reads left to the host come down, reads of more than
-    // GRAPH_NMAX records: room for four such reads from the start, not scaled with the
+    // (with device mega-reads only the reads left to the host come down -- since round 5
+    // only reads of more than GRAPH_NMAX_BIG records, or past PBGPU_GRAPH_NMAX in tests --:
+    // room for four reads of GRAPH_NMAX records from the start, not scaled with the
     // batch -- sized by the batch it was a few hundred MB of pinned memory, ~50 ms of the
     // first batch's critical path -- and grown if a batch has more)
     const uint64_t host_room = 4 * (uint64_t)(GRAPH_NMAX + 1);
@@ -611,6 +612,18 @@ struct pbgpu_runner {
   uint64_t batch_bases = 0;
   std::vector<RunPart> parts;  // one, or n_parts (part files)
   std::mutex run_mu;           // one run at a time
+  // device working set (pbgpu_run_stats.device_peak_bytes): per device its used bytes
+  // (hipMemGetInfo) before the aligners were made, and the most seen after any batch
+  static constexpr int kMaxDev = 64;
+  uint64_t dev_base[kMaxDev] = {};
+  std::atomic<uint64_t> dev_peak[kMaxDev] = {};
+  void note_device_use(int d) {
+    size_t fr = 0, tot = 0;
+    if (d < 0 || d >= kMaxDev || hipMemGetInfo(&fr, &tot) != hipSuccess) return;
+    const uint64_t used = (uint64_t)(tot - fr);
+    uint64_t cur = dev_peak[d].load();
+    while (used > cur && !dev_peak[d].compare_exchange_weak(cur, used)) {}
+  }
   ~pbgpu_runner() {
     rd.clear();
     for (auto* a : al) pbgpu_aligner_free(a);
@@ -763,6 +776,7 @@ static void run_part(pbgpu_runner* R, RunPart& part, const pbgpu_run_params* run
           S.n_reads += nreads;
           S.n_bases += nbases;
           S.n_records += al->last_records;
+          if (al->graph && al->g_mega) S.graph_host_reads += al->g_hosts;
           S.n_device_allocs += tl_dev_allocs - a0;
           S.n_pinned_allocs += tl_pinned_allocs - p0;
           S.device_alloc_bytes += tl_dev_bytes - by0;
@@ -773,6 +787,7 @@ static void run_part(pbgpu_runner* R, RunPart& part, const pbgpu_run_params* run
           }
         }
         first = false;
+        R->note_device_use(al->device);
         {
           std::lock_guard<std::mutex> lk(dmu);
           done.emplace(id, std::move(d));
@@ -942,7 +957,10 @@ static void runner_run(pbgpu_runner* R, const pbgpu_run_params* run, pbgpu_run_s
     S.n_device_allocs += x.n_device_allocs; S.n_device_allocs_late += x.n_device_allocs_late;
     S.n_pinned_allocs += x.n_pinned_allocs; S.n_pinned_allocs_late += x.n_pinned_allocs_late;
     S.device_alloc_bytes += x.device_alloc_bytes; S.alloc_seconds += x.alloc_seconds;
+    S.graph_host_reads += x.graph_host_reads;
   }
+  for (int d = 0; d < pbgpu_runner::kMaxDev; ++d)
+    if (R->dev_base[d]) S.device_peak_bytes += R->dev_peak[d].load() - R->dev_base[d];
   S.open_seconds = t_open;
   const double tc = now_s();
   for (size_t i = 0; i < P; ++i) {
@@ -973,6 +991,12 @@ pbgpu_status pbgpu_host_free(void* p) {
   return PBGPU_OK;
 }
 
+static uint64_t run_hit_budget() {
+  const char* e = getenv("PBGPU_RUN_HIT_BUDGET");
+  const uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
+  return v ? v : 256ull << 20;
+}
+
 pbgpu_status pbgpu_runner_create(pbgpu_index* const* indexes, size_t n_indexes, const pbgpu_align_params* params,
                                  const pbgpu_run_params* run, pbgpu_runner** out) {
   if (!indexes || !n_indexes || !params || !run || !out) return fail(PBGPU_ERR_INVALID, "null argument");
@@ -982,6 +1006,15 @@ pbgpu_status pbgpu_runner_create(pbgpu_index* const* indexes, size_t n_indexes, 
   }
   API_TRY
   std::unique_ptr<pbgpu_runner> R(new pbgpu_runner);
+  for (size_t i = 0; i < n_indexes; ++i) {  // the devices' use before the aligners (the indexes, other work)
+    const int d = indexes[i]->device;
+    if (d < 0 || d >= pbgpu_runner::kMaxDev || R->dev_base[d]) continue;
+    size_t fr = 0, tot = 0;
+    HIPCHK(hipSetDevice(d));
+    HIPCHK(hipMemGetInfo(&fr, &tot));
+    R->dev_base[d] = (uint64_t)(tot - fr);
+    R->dev_peak[d] = R->dev_base[d];
+  }
   const uint32_t per_dev = run->aligners_per_device ? run->aligners_per_device : 2;
   R->batch_bases = run->batch_bases ? run->batch_bases : (64ull << 20);
   R->details = run->details_path != nullptr && run->records_fn == nullptr;  // --details coords output
@@ -991,6 +1024,12 @@ pbgpu_status pbgpu_runner_create(pbgpu_index* const* indexes, size_t n_indexes, 
       pbgpu_aligner* a = nullptr;
       const pbgpu_status s = pbgpu_aligner_create(indexes[i], params, &a);
       if (s != PBGPU_OK) return s;
+      // the run path's hit budget: a batch's sub-batches hold at most this many hits, so
+      // the per-hit buffers (24 B a hit) stay at ~6 GB an aligner whatever the batch
+      // (a 64-Mbase batch: ~370 M hits on C2, ~750 M on C4r-shaped reads; round 4 sized
+      // them for the whole batch with 2x headroom, 63 GB for a cold C2 run).
+      // PBGPU_RUN_HIT_BUDGET overrides it.
+      a->hit_budget = run_hit_budget();
       R->al.push_back(a);
       R->rd.emplace_back(new pbgpu_reads);
       R->views.emplace_back(new RecordsView);

@@ -92,7 +92,7 @@ class RunStats(C.Structure):
                                           "close_seconds")] + \
                [(n, C.c_uint64) for n in ("n_device_allocs", "n_device_allocs_late", "n_pinned_allocs",
                                           "n_pinned_allocs_late", "device_alloc_bytes")] + \
-               [("alloc_seconds", C.c_double)]
+               [("alloc_seconds", C.c_double), ("device_peak_bytes", C.c_uint64), ("graph_host_reads", C.c_uint64)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -151,7 +151,9 @@ class Stats(C.Structure):
                [(n, C.c_uint64) for n in ("fit_chains", "fit_points", "n_filter", "l0_points")] + \
                [("ms_graph", C.c_double), ("graph_records", C.c_uint64), ("graph_ovf_nodes", C.c_uint64),
                                                                     ("ms_host_order", C.c_double),
-                                                                    ("graph_host_reads", C.c_uint64)]
+                                                                    ("graph_host_reads", C.c_uint64),
+                                                                    ("group_refines", C.c_uint64),
+                                                                    ("group_hbm_reads", C.c_uint64)]
 
     def as_dict(self):
         d = {n: getattr(self, n) for n, _ in self._fields_ if not n.startswith("kernel_")}

@@ -116,18 +116,27 @@ def test_dense_group_overflow(dense, cfg):
     assert_same_coords(got, exp, f"dense {cfg}")
 
 
+@pytest.mark.parametrize("refine", ["1", "0"], ids=["refine", "hbm"])
 @pytest.mark.parametrize("data", ["dense", "small"])
-def test_group_all_overflow(data, dense, small, monkeypatch):
+def test_group_all_overflow(data, refine, dense, small, monkeypatch):
     """Every read predicted to fit the smallest (2048-slot) table: reads touching
     more super-reads abandon it mid k-mer group and resume in the 8192-slot LDS
-    tier and the HBM tables; a full table must never trap a thread."""
+    tier, then either with their hash partitions doubled (the default: the
+    partitions already placed keep their lists) or in HBM tables
+    (PBGPU_GROUP_REFINE=0); a full table must never trap a thread."""
     ds = dense if data == "dense" else small
     monkeypatch.setenv("PBGPU_GROUP_PRED_SCALE", "0")
+    monkeypatch.setenv("PBGPU_GROUP_REFINE", refine)
     names, seqs = ds.sr_names(), ds.sr_seqs()
     pnames, pseqs = ds.pb_names(), ds.pb_seqs()
     exp = _oracle(names, seqs, pnames, pseqs, ul=ds.unitig_lengths, forward=True, unitigs_k=31)
-    got, _ = _gpu(names, seqs, pnames, pseqs, ul=ds.unitig_lengths, forward=True, unitigs_k=31)
-    assert_same_coords(got, exp, f"all-overflow {data}")
+    got, st = _gpu(names, seqs, pnames, pseqs, ul=ds.unitig_lengths, forward=True, unitigs_k=31)
+    assert_same_coords(got, exp, f"all-overflow {data} refine={refine}")
+    if data == "dense":
+        if refine == "1":
+            assert st["group_refines"] > 0 and st["group_hbm_reads"] == 0, st
+        else:
+            assert st["group_refines"] == 0 and st["group_hbm_reads"] > 0, st
 
 
 def test_repeats_threshold():

@@ -297,9 +297,11 @@ def test_read_with_many_components(tmp_path, tiling):
 
 def test_device_graph_long_reads_c4r(tmp_path):
     """C4r (C4's repeat model and 15-kb-N50 reads, ~1300 records a read, ~9% of the reads
-    over 4096): 300 reads.  Reads of 4097-8192 records are traversed on the device (the top
-    sort and relax tiers), longer ones on the host; the device graph gives the host
-    graph's bytes, and the C ABI's host flags are exactly the reads over 8192 records."""
+    over 4096 and ~2% over 8192): 300 reads.  Every read is traversed on the device -- up to
+    8192 records in the LDS tiers, past that with its sort keys and node state in HBM
+    (k_graph_sort_big / k_graph_relax_big, round 5) -- and the output equals the host
+    graph's bytes, and those of a run that leaves the reads over 8192 records to the host
+    (PBGPU_GRAPH_NMAX=8192, round 4's cap).  The C ABI flags no read for the host."""
     import numpy as np
     from pacbio_amd import pbgpu
     from tools.synth import Dataset
@@ -311,11 +313,14 @@ def test_device_graph_long_reads_c4r(tmp_path):
     base = ["-s", "1M", "-m", "17", "--psa-min", "13", "-k", "31", "-l", str(tmp_path / "ul.txt"), "-B", "15",
             "--max-count", "5000", "--stretch-cap", "10000", "-t", "16",
             "-r", str(tmp_path / "sr.fa"), "-p", str(tmp_path / "pb.fa")]
-    a, b = str(tmp_path / "dev"), str(tmp_path / "host")
-    _run([*base, "-o", a], timeout=300)
-    _run([*base, "--host-graph", "-o", b], timeout=300)
-    ta = open(a).read()
-    assert ta.count(">") > 200 and ta == open(b).read()
+    outs = []
+    for extra, env in (([], None), (["--host-graph"], None), ([], {"PBGPU_GRAPH_NMAX": "8192"})):
+        o = str(tmp_path / f"mr{len(outs)}")
+        r = subprocess.run([CMR, *base, *extra, "-o", o], capture_output=True, text=True, timeout=300,
+                           env=dict(os.environ, **(env or {})))
+        assert r.returncode == 0, r.stderr
+        outs.append(open(o).read())
+    assert outs[0].count(">") > 200 and outs[0] == outs[1] == outs[2]
     ix = pbgpu.Index.from_fasta([str(tmp_path / "sr.fa")], 17, psa_min=13)
     kw = dict(k=17, forward=True, unitigs_k=31, unitig_lengths=ul, bases_matching=15.0, max_count=5000,
               stretch_cap=10000.0)
@@ -327,6 +332,6 @@ def test_device_graph_long_reads_c4r(tmp_path):
     al.align_resident(al.upload(blob=blob, offsets=off))
     host = al.download().mega[3].astype(bool)
     assert ((nrec > 4096) & (nrec <= 8192)).sum() >= 5, np.sort(nrec)[-40:]
-    assert (host == (nrec > 8192)).all()
-    assert al.stats()["graph_host_reads"] == int((nrec > 8192).sum())
+    assert (nrec > 8192).sum() >= 2, np.sort(nrec)[-40:]
+    assert not host.any() and al.stats()["graph_host_reads"] == 0
     ds.close()

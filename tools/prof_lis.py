@@ -34,6 +34,8 @@ def main():
         pbgpu.device_synchronize(0)
         st = al.stats()
         print(f"k_group tier0: {st['kernel_ms']['k_group']:.2f} ms, k_lis: {st['kernel_ms']['k_lis']:.2f} ms")
+        print(f"stages ms: seed {st['ms_seed']:.1f} group {st['ms_group']:.1f} lis {st['ms_lis']:.1f} fit {st['ms_fit']:.1f} "
+              f"records {st['ms_records']:.1f}; group refines {st['group_refines']}, HBM-table reads {st['group_hbm_reads']}")
         return
     f.argtypes = [C.POINTER(C.c_ulonglong), C.c_int, C.c_int]
     f(buf, 32, 1)
