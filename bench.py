@@ -220,6 +220,22 @@ def _cpu_share():
         return os.cpu_count() or 1
 
 
+def _cmr_runs(cmr, flags, steps):
+    """bin/create_mega_reads `steps` + 1 times (the first untimed): the runs' own --timing
+    JSON (with PBGPU_DEBUG_STALL=1: any HIP call that blocked > 0.5 s, kept per run)"""
+    import subprocess
+    runs = []
+    for i in range(steps + 1):
+        r = subprocess.run([cmr, *flags], capture_output=True, text=True, env=dict(os.environ, PBGPU_DEBUG_STALL="1"))
+        if r.returncode:
+            raise RuntimeError(f"create_mega_reads failed: {r.stderr[-2000:]}")
+        t = json.loads(r.stderr.strip().splitlines()[-1])
+        t["stalls"] = [ln for ln in r.stderr.splitlines() if ln.startswith("pbgpu stall")]
+        if i:
+            runs.append(t)
+    return runs
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -250,6 +266,11 @@ def main():
                          "production leg's)")
     ap.add_argument("--workdir", default=os.environ.get("PBGPU_BENCH_DIR", "/tmp"),
                     help="where the input FASTA and the coords output are written")
+    ap.add_argument("--c4r-reads", type=int, default=20000,
+                    help="reads of the C4r leg (C4's repeat model and 15-kb-N50 reads; 0 = no such leg): device path, "
+                         "create_mega_reads and the CPU oracle on the same reads, reported under c4r")
+    ap.add_argument("--c4r-cmr-steps", type=int, default=2, help="timed create_mega_reads runs of the C4r leg")
+    ap.add_argument("--c4r-cpu-seconds", type=float, default=8.0, help="target C4r CPU-oracle sample duration")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU work: the ranks meet at the barrier and rank 0 prints n_gpus (launch rehearsal)")
     args = ap.parse_args()
@@ -312,6 +333,31 @@ def main():
         # the median run, the worst beside it (every run's wall is listed too)
         el_cmr = comm.max(sorted(walls)[len(walls) // 2])
         worst_cmr = comm.max(max(walls))
+    # ---- the C4r leg's inputs and its create_mega_reads runs (before any HIP call here too):
+    # C4's repeat model (2% of the genome in 5-50-copy repeats) and read lengths (15 kb N50)
+    # on a 16 Mbp genome, the shape of BASELINE's chr1 / whole-human configs at a size one
+    # GPU and the CPU oracle both run (such reads ran >10x slower per base)
+    c4 = None
+    if args.c4r_reads > 0:
+        c4 = {"n_pb": args.c4r_reads}
+        t0 = time.time()
+        ds4 = Dataset("C4r", seed=42, threads=min(threads, 16), n_pb=args.c4r_reads,
+                      pb_index_base=rank * args.c4r_reads)
+        c4["wd"] = tempfile.mkdtemp(prefix=f"pbgpu_bench_c4r_r{rank}_", dir=wd)
+        ds4.write(c4["wd"])
+        c4["gen_s"] = time.time() - t0
+        c4["ds"] = ds4
+        sr4, pb4, ul4 = (os.path.join(c4["wd"], f) for f in ("sr.fa", "pb.fa", "ul.txt"))
+        if args.c4r_cmr_steps > 0:
+            cmr = os.path.join(ROOT, "pacbio_amd", "bin", "create_mega_reads")
+            c4["cmr_runs"] = _cmr_runs(cmr, ["-s", "1M", "-m", "17", "--psa-min", "13", "-k", "31", "-l", ul4, "-B",
+                                             "15", "--max-count", "5000", "--stretch-cap", "10000", "-t",
+                                             str(threads), "-r", sr4, "-p", pb4, "--timing", "--devices",
+                                             str(local), "-o", os.path.join(c4["wd"], "mega_reads")],
+                                       args.c4r_cmr_steps)
+            walls4 = [t["wall_s"] for t in c4["cmr_runs"]]
+            c4["cmr_wall"] = comm.max(sorted(walls4)[len(walls4) // 2])
+            c4["cmr_worst"] = comm.max(max(walls4))
     # B_rand: random 64-B sector gathers over a 64 GB buffer, this GPU, this run
     b_rand = pbgpu.measure_gather(local, 64 << 30) if not args.no_brand else None
     # the same for random 512-B runs of 8-B words: the shape of k_group's occurrence-list reads
@@ -386,6 +432,30 @@ def main():
         for c in chunks:
             al2.free(c)
         al2.close()
+
+    # ---- the C4r leg on the device: its reads resident, production flags, one aligner
+    if c4 is not None:
+        ds4 = c4["ds"]
+        ix4 = pbgpu.Index.from_fasta([os.path.join(c4["wd"], "sr.fa")], 17, psa_min=13, device=local)
+        akw4 = dict(akw, k=17, unitig_lengths=ds4.unitig_lengths)
+        al4 = pbgpu.StreamAligner(ix4, streams=1, **akw4)
+        blob4, off4 = ds4.pb_blob()
+        c4["bases"] = int(off4[-1])
+        rr4 = al4.upload(blob=blob4, offsets=off4)
+        al4.align_resident(rr4)
+        al4.reset_stats()
+        pbgpu.device_synchronize(local)
+        comm.barrier()
+        td = time.perf_counter()
+        for _ in range(args.device_steps):
+            al4.align_resident(rr4)
+        pbgpu.device_synchronize(local)
+        comm.barrier()
+        c4["el_dev"] = comm.max(time.perf_counter() - td)
+        c4["st"] = al4.stats()
+        al4.free(rr4)
+        al4.close()
+        c4["ix"] = ix4
 
     # ---- end to end (value): PacBio FASTA -> coords file, pbgpu_run
     # (a pbgpu_runner keeps its aligners and pinned buffers across steps: a service
@@ -578,6 +648,76 @@ def main():
                          f"formatting, {cthreads} threads (the job's CPU share of the box), {sec:.2f} s",
                "gpu_parity_reads_checked": len(oe), "gpu_parity_reads_differing": mism}
 
+    # ---- the C4r leg's figures (collectives on every rank) and its CPU oracle (rank 0, N = 1)
+    c4_out = None
+    if c4 is not None:
+        bases4 = comm.sum(c4["bases"])
+        st4, dsteps4 = c4["st"], max(1, args.device_steps)
+        cpu4 = None
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            from oracle.oracle import OracleIndex, params
+            from tests._compare import split_reads
+            cthreads = args.cpu_threads or threads
+            ds4 = c4["ds"]
+            oix4 = OracleIndex.from_fasta([os.path.join(c4["wd"], "sr.fa")], 17, threads=cthreads)
+            p4 = params(**dict(akw, k=17, unitig_lengths=ds4.unitig_lengths))
+            allp4, alln4 = ds4.pb_seqs(), ds4.pb_names()
+            npil = max(1, min(len(allp4), 2 * cthreads))
+            tp = time.perf_counter()
+            oix4.align_format(p4, alln4[:npil], allp4[:npil], threads=cthreads)
+            rate = sum(len(x) for x in allp4[:npil]) / max(time.perf_counter() - tp, 1e-6)
+            want, nsamp, acc = rate * args.c4r_cpu_seconds, 0, 0
+            while nsamp < len(allp4) and acc < want:
+                acc += len(allp4[nsamp])
+                nsamp += 1
+            nsamp = max(nsamp, npil)
+            ps4, pn4 = allp4[:nsamp], alln4[:nsamp]
+            tc = time.perf_counter()
+            exp4 = oix4.align_format(p4, pn4, ps4, threads=cthreads)
+            sec4 = time.perf_counter() - tc
+            sb4 = sum(len(x) for x in ps4)
+            oix4.close()
+            g4 = pbgpu.Aligner(c4["ix"], **dict(akw, k=17, unitig_lengths=ds4.unitig_lengths))
+            rr = g4.upload(ps4, names=pn4)
+            g4.align_resident(rr)
+            got4 = g4.format_device(rr)
+            rr.close()
+            g4.close()
+            og, rg = split_reads(got4)
+            oe, re_ = split_reads(exp4)
+            mism4 = sum(1 for h in set(og) | set(oe) if sorted(rg.get(h, [])) != sorted(re_.get(h, [])))
+            cpu4 = {"value": sb4 / sec4, "unit": "bases/s", "cores": cthreads, "kind": "port",
+                    "sample": f"first {nsamp} C4r reads ({sb4} bases, {exp4.count(chr(10))} text lines), oracle/ C "
+                              f"restatement, align + coords text, {cthreads} threads, {sec4:.2f} s",
+                    "gpu_parity_reads_checked": len(oe), "gpu_parity_reads_differing": mism4}
+        per_base = {n: st4[n] / max(1, st4["n_bases"]) for n in
+                    ("n_kmers", "n_probes", "n_kept", "n_hits", "n_chains", "n_lis_tests", "n_records")}
+        value_dev4 = bases4 * dsteps4 / c4["el_dev"]
+        runs4 = c4.get("cmr_runs") or []
+        c4_out = {
+            "workload": "C4r: C4's repeat model (2% of a 16 Mbp genome in 5-50-copy repeats of 1-6 kb, 1% "
+                        "substitutions) and read lengths (lognormal mean 12.5 kb, sigma 0.6: 15 kb N50), 800k "
+                        f"super-reads, {args.c4r_reads} reads per GPU, production flags",
+            "bases_per_gpu": c4["bases"],
+            "value_device": value_dev4,
+            "value_device_note": "reads resident in HBM, device path to sorted records in HBM, one aligner",
+            "ms_per_step": c4["el_dev"] / dsteps4 * 1e3,
+            "stage_ms_per_step": {s: round(st4["ms_" + s] / dsteps4, 3) for s in
+                                  ("seed", "group", "lis", "fit", "records")},
+            "counters_per_base": per_base,
+            "group_refines_per_step": st4["group_refines"] / dsteps4,
+            "value_create_mega_reads": bases4 / c4["cmr_wall"] if c4.get("cmr_wall") else None,
+            "create_mega_reads_walls_s": [t["wall_s"] for t in runs4],
+            "create_mega_reads_worst_wall_s": c4.get("cmr_worst"),
+            "create_mega_reads_runs": runs4,
+            "cpu_oracle": cpu4,
+            "gpu_device_over_cpu": (value_dev4 / cpu4["value"]) if cpu4 else None,
+            "generate_s": round(c4["gen_s"], 3),
+        }
+        c4["ix"].close()
+        c4["ds"].close()
+        shutil.rmtree(c4["wd"], ignore_errors=True)
+
     # SURVEY 8(d)'s whole-path algorithmic bytes of the device leg: 2-bit read stream,
     # 64-B index probes, occurrences enumerated (8 B), hits grouped (write + read, 16 B),
     # LIS predecessor tests (16 B), records out (96 B)
@@ -633,7 +773,9 @@ def main():
             "config": {
                 "workload": {"C1": "C1: 100 PB x 10 kb vs 1k SRs, k=17",
                              "C2": "C2 E. coli-scale: 50k PB (lognormal mean 12 kb, CLR 13%) per GPU vs 200k SRs, k=17",
-                             "C3": "C3 yeast-scale: PB (mean 12 kb) vs 1M SRs, k=21"}[args.workload],
+                             "C3": "C3 yeast-scale: PB (mean 12 kb) vs 1M SRs, k=21",
+                             "C4r": "C4r: C4's repeat model and 15-kb-N50 reads on a 16 Mbp genome vs 800k SRs, k=17"}[
+                                 args.workload],
                 "flags": f"-m {k} --psa-min 13 -l ul.txt -k 31 -f -B 15 --max-count 5000 --stretch-cap 10000",
                 "step": "pbgpu_run: pb.fa -> coords file (parse, upload, align, device format, D2H, write)",
                 "reads_per_gpu": len(off) - 1,
@@ -682,6 +824,7 @@ def main():
                          "b_run512_gbs": b_run, "frac_of_b_run512": (achieved / b_run) if b_run else None,
                          "by_kernel": per_kernel},
             "cpu_baseline": cpu,
+            "c4r": c4_out,
         }
         print(json.dumps(out), flush=True)
     index.close()

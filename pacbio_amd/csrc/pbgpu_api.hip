@@ -1619,6 +1619,30 @@ static uint32_t lis_stage(pbgpu_aligner* al, uint32_t nch, uint64_t Hs, const Li
   return n_fit;
 }
 
+// Bump allocation over the batch's per-hit buffers (X, pts, nodes), which are dead once the
+// records are out: the graph stage's temporaries (and the records sort's keys) are carved
+// from them instead of holding buffers of their own (round 5: the two working sets are
+// disjoint in time, so an aligner holds their maximum, not their sum).  A request that
+// does not fit falls back to the buffer given.
+struct DeadHits {
+  struct Region { uint8_t* p; size_t n, used; };
+  Region r[3];
+  explicit DeadHits(pbgpu_aligner* al)
+      : r{{(uint8_t*)al->X.p, al->X.bytes(), 0}, {(uint8_t*)al->pts.p, al->pts.bytes(), 0},
+          {(uint8_t*)al->nodes.p, al->nodes.bytes(), 0}} {}
+  template <typename T>
+  T* take(dbuf<T>& own, size_t cnt) {
+    const size_t bytes = cnt * sizeof(T);
+    if (!getenv("PBGPU_NO_CARVE"))
+      for (auto& x : r) {
+        const size_t a = (x.used + 255) & ~(size_t)255;
+        if (x.p && a + bytes <= x.n) { x.used = a + bytes; return reinterpret_cast<T*>(x.p + a); }
+      }
+    own.ensure(cnt);
+    return own.p;
+  }
+};
+
 // Records grouped per read and sorted by (rs, re, ql, sr, emit): al->recs[0..nrec)
 // -> al->recs_sorted, al->rec_off.  timed: event around the sort kernel.
 // counted: every record's read count and slot were taken at emission (ChainOut.per_read)
@@ -1633,12 +1657,13 @@ static void records_stage(pbgpu_aligner* al, uint32_t n, uint32_t nrec, bool tim
   launch_excl_scan(al->rec_per_read.p, nullptr, n, al->rec_off.p,
                    (uint64_t*)temp_storage(al->tmp, excl_scan_scratch_words(n) * 8), st);
   al->order.ensure(nrec + 1);
-  al->sort_scratch.ensure(6ull * nrec + 6);
+  DeadHits dead(al);  // (every sub-batch's hits are done with)
+  uint64_t* sort_keys = dead.take(al->sort_scratch, 6ull * nrec + 6);
   al->recs_sorted.ensure(nrec + 1);
   if (counted) launch_rec_place(al->rec_read.p, al->rec_slot.p, nrec, al->rec_off.p, al->order.p, st);
   else launch_rec_scatter(al->rec_read.p, nrec, al->rec_off.p, al->rec_cursor.p, al->order.p, st);
   if (timed) HIPCHK(hipEventRecord(al->ev[15], st));
-  launch_rec_sort(al->recs.p, al->rec_off.p, al->order.p, al->sort_scratch.p, n, al->recs_sorted.p, st);
+  launch_rec_sort(al->recs.p, al->rec_off.p, al->order.p, sort_keys, n, al->recs_sorted.p, st);
   HIPCHK(hipGetLastError());
 }
 
@@ -1658,8 +1683,9 @@ static void fine_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   HIPCHK(hipMemcpyAsync(woff.data(), al->rec_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, st));
   // windows sorted by (read, super-read) (the lookup side of prime_frags_pos's std::map)
   al->fwin.ensure(nwin + 1); al->fwi[0].ensure(nwin + 1);
-  al->sort_scratch.ensure(6ull * nwin + 6);
-  launch_fine_win_sort(al->recs_sorted.p, al->rec_off.p, n, al->sort_scratch.p, al->fwi[0].p, st);
+  DeadHits dead(al);  // (the coarse hits are done with; the fine ones come after the windows)
+  launch_fine_win_sort(al->recs_sorted.p, al->rec_off.p, n, dead.take(al->sort_scratch, 6ull * nwin + 6), al->fwi[0].p,
+                       st);
   launch_fine_windows(al->recs_sorted.p, nwin, nullptr, al->fwi[0].p, 1, rd->off.p, al->PF.k, al->fwin.p, st);
   HIPCHK(hipGetLastError());
   // windowed hits per read
@@ -1759,6 +1785,7 @@ static void fine_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
 // implied positions and name prefix sums per record, the per-read sort, the traversal.
 static void graph_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   hipStream_t st = al->st;
+  DeadHits dead(al);
   const uint32_t n = (uint32_t)rd->n_reads;
   const uint64_t nrec = al->last_records;
   GraphDev G{};
@@ -1769,34 +1796,36 @@ static void graph_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   // PBGPU_GRAPH_NMAX (tests): a lower cap on the records of a read traversed on the device
   G.nmax = GRAPH_NMAX_BIG;
   if (const char* e = getenv("PBGPU_GRAPH_NMAX")) G.nmax = (uint32_t)std::min<long>(GRAPH_NMAX_BIG, std::max(0l, atol(e)));
-  // reads past GRAPH_NMAX records keep their sort keys and node state here (6 words a
-  // record, the records stage's sort scratch: sized for this batch's records already)
-  al->sort_scratch.ensure(6ull * nrec + 6);
-  G.scratch = al->sort_scratch.p;
-  al->g_poff.ensure(nrec + 1); al->g_sizes.ensure(nrec + 1); al->g_maxn.ensure(1);
-  G.poff = al->g_poff.p; G.max_n = al->g_maxn.p;
+  // reads past GRAPH_NMAX records keep their sort keys and node state here (6 words a record)
+  G.scratch = dead.take(al->sort_scratch, 6ull * nrec + 6);
+  al->g_maxn.ensure(1);
+  G.poff = dead.take(al->g_poff, nrec + 1); G.max_n = al->g_maxn.p;
+  uint32_t* g_sizes = dead.take(al->g_sizes, nrec + 1);
   HIPCHK(hipMemsetAsync(al->g_maxn.p, 0, 4, st));
-  launch_graph_sizes(G, n, nrec, al->g_sizes.p, (uint64_t*)temp_storage(al->tmp, excl_scan_scratch_words(nrec) * 8), st);
+  launch_graph_sizes(G, n, nrec, g_sizes, (uint64_t*)temp_storage(al->tmp, excl_scan_scratch_words(nrec) * 8), st);
   HIPCHK(hipGetLastError());
   uint64_t tot = 0;
   uint32_t max_n = 0;
-  HIPCHK(hipMemcpyAsync(&tot, al->g_poff.p + nrec, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&tot, G.poff + nrec, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(&max_n, al->g_maxn.p, 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   // k_graph keeps name offsets as 32 bits (a batch of 2^32 unitigs would be 48 GB of names)
   if (tot >= (1ull << 32)) throw bad_input("more than 2^32 name unitigs in one batch's records");
-  al->g_pre.ensure(3 * tot + 3); al->g_imp.ensure(nrec + 1); al->g_desc.ensure(nrec + 1); al->g_out.ensure(nrec + 1);
-  G.pp = (uint2*)al->g_pre.p; G.ounits = al->g_pre.p + 2 * (tot + 1);
-  G.imp = al->g_imp.p; G.desc = al->g_desc.p; G.out = al->g_out.p;
-  al->g_ecnt.ensure(nrec + 1); al->g_eoff.ensure(nrec + 1); al->g_ovf_list.ensure(nrec + 1); al->g_ovf.ensure(2);
-  al->g_edges.ensure(nrec * GRAPH_EBLK);
-  G.ecnt = al->g_ecnt.p; G.eoff = al->g_eoff.p; G.edges = al->g_edges.p;
-  G.ovf = al->g_ovf.p; G.ovf_list = al->g_ovf_list.p;
+  // (with device mega-reads the nodes are temporaries too: only the host reads' come down)
+  uint32_t* g_pre = dead.take(al->g_pre, 3 * tot + 3);
+  G.pp = (uint2*)g_pre; G.ounits = g_pre + 2 * (tot + 1);
+  G.imp = dead.take(al->g_imp, nrec + 1); G.desc = dead.take(al->g_desc, nrec + 1);
+  if (al->g_mega) G.out = dead.take(al->g_out, nrec + 1);
+  else { al->g_out.ensure(nrec + 1); G.out = al->g_out.p; }
+  al->g_ovf.ensure(2);
+  G.ecnt = dead.take(al->g_ecnt, nrec + 1); G.eoff = dead.take(al->g_eoff, nrec + 1);
+  G.ovf_list = dead.take(al->g_ovf_list, nrec + 1);
+  G.edges = dead.take(al->g_edges, nrec * GRAPH_EBLK);
+  G.ovf = al->g_ovf.p;
   uint64_t ovf[2];
   HIPCHK(launch_graph(G, n, nrec, max_n, st, al->g_side, al->g_fork, al->g_join, ovf));
   HIPCHK(hipGetLastError());
-  al->g_eovf.ensure(std::max<uint64_t>(ovf[1], nrec) + 1);  // (a floor: the next batches rarely grow it)
-  G.eovf = al->g_eovf.p;
+  G.eovf = dead.take(al->g_eovf, std::max<uint64_t>(ovf[1], nrec) + 1);  // (a floor: the next batches rarely grow it)
   HIPCHK(launch_graph_relax(G, n, nrec, max_n, ovf[0], st, al->g_side, al->g_side2, al->g_fork, al->g_join,
                             al->g_join2));
   HIPCHK(hipGetLastError());
@@ -1807,10 +1836,10 @@ static void graph_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   // components, tiling and the printed mega-reads' paths on the device
   G.mega = 1; G.tiling = al->g_tiling; G.trim = al->g_trim;
   G.min_density = al->g_min_density; G.min_len = al->g_min_len;
-  al->g_cand.ensure(nrec + 1); al->g_ord.ensure(3 * nrec + 3); al->g_ivs.ensure(2 * nrec + 2);
-  al->g_mo.ensure(nrec + 1); al->g_mcount.ensure(n + 1); al->g_mhost.ensure(n + 1); al->g_moff.ensure(n + 1);
+  G.cand = dead.take(al->g_cand, nrec + 1); G.ord = dead.take(al->g_ord, 3 * nrec + 3);
+  G.ivs = dead.take(al->g_ivs, 2 * nrec + 2); G.mo = dead.take(al->g_mo, nrec + 1);
+  al->g_mcount.ensure(n + 1); al->g_mhost.ensure(n + 1); al->g_moff.ensure(n + 1);
   al->g_munits.ensure(tot + 1); al->g_uused.ensure(1); al->g_nhost.ensure(1);
-  G.cand = al->g_cand.p; G.ord = al->g_ord.p; G.ivs = al->g_ivs.p; G.mo = al->g_mo.p;
   G.mcount = al->g_mcount.p; G.mhost = al->g_mhost.p; G.munits = al->g_munits.p; G.units_used = al->g_uused.p;
   G.units_cap = tot; G.n_recs = nrec; G.n_host = al->g_nhost.p;
   HIPCHK(hipMemsetAsync(al->g_uused.p, 0, 8, st));
@@ -1832,25 +1861,30 @@ static void graph_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   launch_mega_pack(G, n, al->g_moff.p, al->g_mc.p, st);
   HIPCHK(hipGetLastError());
   al->g_hrecs = al->g_hinfos = 0;
-  // the reads left to the host (few, long): their packing buffers are sized with every
-  // batch, not only when a batch first has such a read (no allocation after the first)
-  al->g_rsize.ensure(n + 1); al->g_isize.ensure(nrec + 1); al->g_hroff.ensure(n + 1); al->g_hioff.ensure(nrec + 1);
-  al->g_hrec.ensure(nrec / 8 + 4096); al->g_hgraph.ensure(nrec / 8 + 4096);
-  al->g_hinfo.ensure(2 * (al->last_info / 8 + 4096));
+  // the reads left to the host (since round 5 only reads past GRAPH_NMAX_BIG records, or
+  // past PBGPU_GRAPH_NMAX in tests): their packing buffers hold four reads of
+  // GRAPH_NMAX records from the first batch on (no allocation after it unless a batch
+  // has more), the per-record sizes and offsets are temporaries
+  constexpr uint64_t host_room = 4 * (uint64_t)(GRAPH_NMAX + 1);
+  al->g_rsize.ensure(n + 1); al->g_hroff.ensure(n + 1);
+  al->g_hrec.ensure(host_room); al->g_hgraph.ensure(host_room);
+  al->g_hinfo.ensure(2 * host_room * (al->last_info / std::max<uint64_t>(1, nrec) + 2));
   if (!al->g_hosts) return;
   // the reads left to the host: their records, nodes and info packed (a small download)
-  launch_host_sizes(G, n, al->g_rsize.p, al->g_isize.p, st);
+  uint32_t* g_isize = dead.take(al->g_isize, nrec + 1);
+  uint64_t* g_hioff = dead.take(al->g_hioff, nrec + 1);
+  launch_host_sizes(G, n, al->g_rsize.p, g_isize, st);
   launch_excl_scan(al->g_rsize.p, nullptr, n, al->g_hroff.p,
                    (uint64_t*)temp_storage(al->tmp, excl_scan_scratch_words(n) * 8), st);
-  launch_excl_scan(al->g_isize.p, nullptr, nrec, al->g_hioff.p,
-                   (uint64_t*)temp_storage(al->tmp, excl_scan_scratch_words(nrec) * 8), st);
+  launch_excl_scan(g_isize, nullptr, nrec, g_hioff, (uint64_t*)temp_storage(al->tmp, excl_scan_scratch_words(nrec) * 8),
+                   st);
   uint64_t hc[2] = {0, 0};
   HIPCHK(hipMemcpyAsync(&hc[0], al->g_hroff.p + n, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(&hc[1], al->g_hioff.p + nrec, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&hc[1], g_hioff + nrec, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   al->g_hrecs = hc[0]; al->g_hinfos = hc[1];
   al->g_hrec.ensure(hc[0] + 1); al->g_hgraph.ensure(hc[0] + 1); al->g_hinfo.ensure(2 * hc[1] + 2);
-  launch_host_pack(G, n, al->g_hroff.p, al->g_hioff.p, al->g_hrec.p, al->g_hgraph.p, al->g_hinfo.p,
+  launch_host_pack(G, n, al->g_hroff.p, g_hioff, al->g_hrec.p, al->g_hgraph.p, al->g_hinfo.p,
                    al->g_hinfo.p + hc[1] + 1, st);
   HIPCHK(hipGetLastError());
 }
@@ -1874,23 +1908,28 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
     return;
   }
   HIPCHK(hipMemsetAsync(al->stats.p, 0, ST_N * 8, st));
-  // ---------------------------------------------------------------- seed
-  al->krec.ensure(rd->n_bases + 1);
+  // The batch in chunks of reads of at most chunk_bases bases: per chunk its seeding
+  // (KRec, 16 B a base) and its sub-batches, the records appended.  One chunk unless the
+  // batch is larger than the device holds (round 4: one 3.6-Gbase C3 call ran out of HBM;
+  // the caller had to cut it).  The hit budget is likewise held to the free memory.
+  size_t mem_free = 0, mem_tot = 0;
+  HIPCHK(hipMemGetInfo(&mem_free, &mem_tot));
+  const uint64_t mem_avail = (uint64_t)mem_free + al->krec.bytes() + al->X.bytes() + al->pts.bytes() + al->nodes.bytes();
+  uint64_t chunk_bases = std::max<uint64_t>(1ull << 26, mem_avail / 16 / 8);
+  if (const char* e = getenv("PBGPU_CHUNK_BASES")) chunk_bases = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
+  const uint64_t budget = std::max<uint64_t>(1ull << 20, std::min<uint64_t>(al->hit_budget, mem_avail / 24 / 3));
+  const uint32_t hcap_log2 = 11;
+  std::vector<uint64_t> h_roff;  // host copy of the read offsets (the chunk cuts)
+  if (rd->h_off.size() == (size_t)n + 1) {
+    h_roff = rd->h_off;
+  } else {
+    h_roff.resize(n + 1);
+    HIPCHK(hipMemcpyAsync(h_roff.data(), rd->off.p, (n + 1) * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
   al->n_kept.ensure(n); al->thr.ensure(n); al->nhits.ensure(n); al->hit_off.ensure(n + 1);
-  HIPCHK(hipEventRecord(al->ev[0], st));
-  launch_seed(seed_mode, v, rd->seq.p, rd->off.p, n, al->P, al->krec.p, al->n_kept.p, al->thr.p, al->nhits.p,
-              al->stats.p, gcount, ix->null_ptr, st);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(al->ev[1], st));
-  launch_excl_scan(nullptr, al->nhits.p, n, al->hit_off.p,
-                   (uint64_t*)temp_storage(al->tmp, excl_scan_scratch_words(n) * 8), st);
   std::vector<uint64_t>& hoff = al->h_hoff;
   hoff.resize(n + 1);
-  HIPCHK(hipMemcpyAsync(hoff.data(), al->hit_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  // ------------------------------------- sub-batches: group -> chains (retry)
-  const uint64_t budget = al->hit_budget;
-  const uint32_t hcap_log2 = 11;
   al->ovf_reads.ensure(n);
   al->ovf_list.ensure(n);  // (used only by batches with reads past the first group tier)
   uint64_t rec_done = 0, info_done = 0;
@@ -1900,16 +1939,39 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
   bool counted = !al->P.max_match && !rec_hist;
   al->rec_per_read.ensure(n);
   if (counted) HIPCHK(hipMemsetAsync(al->rec_per_read.p, 0, (size_t)n * 4, st));
-  double ms_group = 0, ms_lis = 0, ms_fit = 0;
+  double ms_group = 0, ms_lis = 0, ms_fit = 0, ms_seed = 0;
   double k_ms[PBGPU_KERNEL_N] = {};
   uint64_t k_n[PBGPU_KERNEL_N] = {};
   uint64_t n_chains = 0, n_tests = 0;
+  for (uint32_t c0 = 0; c0 < n;) {
+  uint32_t c1 = c0 + 1;
+  while (c1 < n && h_roff[c1 + 1] - h_roff[c0] <= chunk_bases) ++c1;
+  const uint32_t ncr = c1 - c0;
+  const uint64_t cb0 = h_roff[c0];
+  // ---------------------------------------------------------------- seed
+  // KRec of the chunk's bases: the kernels index it by absolute base offset (roff), so the
+  // pointer handed to them is shifted back by the chunk's first base
+  al->krec.ensure_capped(h_roff[c1] - cb0 + 1, al->base_cap ? al->base_cap + 1 : ~(size_t)0);
+  KRec* const krec = al->krec.p - cb0;
+  HIPCHK(hipEventRecord(al->ev[0], st));
+  launch_seed(seed_mode, v, rd->seq.p, rd->off.p + c0, ncr, al->P, krec, al->n_kept.p + c0, al->thr.p + c0,
+              al->nhits.p + c0, al->stats.p, gcount, ix->null_ptr, st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(al->ev[1], st));
+  // hit offsets relative to the chunk's first read
+  launch_excl_scan(nullptr, al->nhits.p + c0, ncr, al->hit_off.p + c0,
+                   (uint64_t*)temp_storage(al->tmp, excl_scan_scratch_words(ncr) * 8), st);
+  HIPCHK(hipMemcpyAsync(hoff.data() + c0, al->hit_off.p + c0, (size_t)(ncr + 1) * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  ms_seed += ev_ms(al->ev[0], al->ev[1]);
+  k_ms[PBGPU_KERNEL_SEED] += ev_ms(al->ev[0], al->ev[1]); k_n[PBGPU_KERNEL_SEED]++;
+  // ------------------------------------- sub-batches: group -> chains (retry)
   // sub-batches of about equal hits (ceil(total / budget) of them), each <= budget
-  const uint64_t n_sub = (hoff[n] + budget - 1) / budget;
-  const uint64_t target = n_sub ? (hoff[n] + n_sub - 1) / n_sub : 0;
-  for (uint32_t r0 = 0; r0 < n;) {
+  const uint64_t n_sub = (hoff[c1] + budget - 1) / budget;
+  const uint64_t target = n_sub ? (hoff[c1] + n_sub - 1) / n_sub : 0;
+  for (uint32_t r0 = c0; r0 < c1;) {
     uint32_t r1 = r0 + 1;
-    while (r1 < n && hoff[r1] - hoff[r0] < target && hoff[r1 + 1] - hoff[r0] <= budget) ++r1;
+    while (r1 < c1 && hoff[r1] - hoff[r0] < target && hoff[r1 + 1] - hoff[r0] <= budget) ++r1;
     const uint64_t Hs = hoff[r1] - hoff[r0];
     const uint32_t nr = r1 - r0;
     // per-hit buffers: at most the hit budget's (a read past it forms a sub-batch of its own)
@@ -1990,20 +2052,20 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
         }
         HIPCHK(hipEventRecord(al->grp_fork, st));
         HIPCHK(hipStreamWaitEvent(al->grp_side, al->grp_fork, 0));
-        launch_group(v, al->krec.p, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0,
+        launch_group(v, krec, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0,
                      al->read_list.p + n_small, n_bigr, kGroupLdsMaxLog2, nullptr, O, al->stats.p, al->grp_side);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(al->grp_join, al->grp_side));
       }
       HIPCHK(hipEventRecord(al->ev[8], st));
-      launch_group(v, al->krec.p, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0, al->read_list.p, n_small,
+      launch_group(v, krec, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0, al->read_list.p, n_small,
                    hcap_log2, nullptr, O, al->stats.p, st);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(al->ev[9], st));
       if (overlap && n_bigr) {
         HIPCHK(hipStreamWaitEvent(st, al->grp_join, 0));
       } else {
-        launch_group(v, al->krec.p, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0,
+        launch_group(v, krec, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0,
                      al->read_list.p + n_small, n_bigr, kGroupLdsMaxLog2, nullptr, O, al->stats.p, st);
         HIPCHK(hipGetLastError());
       }
@@ -2047,7 +2109,7 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
           launch_group_refine(al->ovf_list.p, n_ovf, al->prog.p, st);
         }
         if (lg <= kGroupLdsMaxLog2) {
-          launch_group(v, al->krec.p, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0,
+          launch_group(v, krec, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0,
                        al->ovf_list.p, n_ovf, lg, nullptr, O, al->stats.p, st);
           HIPCHK(hipGetLastError());
         } else {
@@ -2058,7 +2120,7 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
           for (uint32_t s0 = 0; s0 < n_ovf; s0 += grp) {
             const uint32_t m = std::min(grp, n_ovf - s0);
             HIPCHK(hipMemsetAsync(al->gtable.p, 0, (size_t)m * words * 4, st));
-            launch_group(v, al->krec.p, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0,
+            launch_group(v, krec, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0,
                          al->ovf_list.p + s0, m, lg, al->gtable.p, O, al->stats.p, st);
             HIPCHK(hipGetLastError());
           }
@@ -2175,6 +2237,8 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
     }
     r0 = r1;
   }
+  c0 = c1;
+  }  // chunks
   al->last_records = rec_done;
   al->last_info = info_done;
   HIPCHK(hipEventRecord(al->ev[3], st));
@@ -2211,12 +2275,11 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
     al->acc.ms_graph += ev_ms(al->ev[18], al->ev[19]);
     al->acc.graph_records += al->last_records;
   }
-  al->acc.ms_seed += ev_ms(al->ev[0], al->ev[1]);
+  al->acc.ms_seed += ms_seed;
   al->acc.ms_group += ms_group;
   al->acc.ms_lis += ms_lis;
   al->acc.ms_fit += ms_fit;
   al->acc.ms_records += ev_ms(al->ev[3], al->ev[4]);
-  k_ms[PBGPU_KERNEL_SEED] += ev_ms(al->ev[0], al->ev[1]); k_n[PBGPU_KERNEL_SEED]++;
   k_ms[PBGPU_KERNEL_REC_SORT] += ev_ms(al->ev[15], al->ev[4]); k_n[PBGPU_KERNEL_REC_SORT]++;
   for (int i = 0; i < PBGPU_KERNEL_N; ++i) { al->acc.kernel_ms[i] += k_ms[i]; al->acc.kernel_launches[i] += k_n[i]; }
   al->have_result = true;

@@ -346,6 +346,8 @@ struct pbgpu_aligner {
   hipStream_t grp_side = nullptr;  // the group stage's 16-wave tier (PBGPU_GROUP_OVERLAP)
   hipEvent_t grp_fork = nullptr, grp_join = nullptr;
   uint64_t hit_budget = 4000000000ull, rec_hint = 0, info_per_chain = 32;
+  // pbgpu_run: the most bases a batch holds (0 = unknown): the per-base buffers never grow past it
+  uint64_t base_cap = 0;
   double chains_per_hit = 1.0 / 80;  // k_group tier estimate (C2: 1.1 x 1/90), refined after every batch
   dbuf<uint32_t> ovf_list, read_list;
   std::vector<uint32_t> h_order, h_class, h_small, h_big;  // host scratch of the group stage's read order

@@ -3945,37 +3945,50 @@ __global__ __launch_bounds__(64) void k_mega(GraphDev G, uint32_t n_reads) {
     __shared__ uint32_t s_rpre[GRAPH_NMAX / 64];
     // the root bitmap and its prefix counts: in LDS, or for a read of more than GRAPH_NMAX
     // records in its region of G.scratch (free after the relaxation)
-    auto components = [&](auto* roots, auto* rpre, uint32_t rw) {
+    auto components = [&](auto* roots, auto* rpre, uint32_t rw, uint64_t* ra) {
     for (uint32_t t = 0; t < rw; ++t) roots[lane * rw + t] = 0;
+    // A candidate wins its root if no candidate of the root has a larger (lpath, density)
+    // and none before it an equal one: where the reference's fold (replace on strictly
+    // better, in candidate order) ends.  Per root, three atomic passes in the read's
+    // scratch (ra: lpath max, density key max, index min; a root is a node index < n):
+    // the best lpath, then the best density among those, then the first candidate
+    // among those.  (Round 4 compared every pair of candidates: O(nc^2) readlanes, the
+    // whole k_mega time on C4r reads with thousands of candidates.)  No NaN density here
+    // (those reads take the serial path), so the key order is the double order, and
+    // graph_dkey maps -0 and +0 to one key, as == sees them.
+    int32_t* lpmax = reinterpret_cast<int32_t*>(ra);
+    uint32_t* imin = reinterpret_cast<uint32_t*>(ra) + n;
+    unsigned long long* dmax = reinterpret_cast<unsigned long long*>(ra) + n;
+    for (uint32_t c = lane; c < nc; c += 64) {
+      const uint32_t rt = cand[c].root;
+      lpmax[rt] = INT32_MIN; imin[rt] = 0xFFFFFFFFu; dmax[rt] = 0ull;
+    }
     __threadfence_block();
     __syncthreads();
-    // a candidate wins its root if no candidate of the root has a larger (lpath,
-    // density) and none before it an equal one: where the reference's fold (replace on
-    // strictly better, in candidate order) ends
-    for (uint32_t c0 = 0; c0 < nc; c0 += 64) {
-      const uint32_t c = c0 + lane;
-      const bool ok = c < nc;
-      const uint32_t rt = ok ? cand[c].root : 0xFFFFFFFFu;
-      const int32_t lp = ok ? cand[c].lpath : 0;
-      const double d = ok ? cand[c].density : 0.0;
-      bool win = ok;
-      for (uint32_t e0 = 0; e0 < nc; e0 += 64) {
-        const uint32_t e = e0 + lane;
-        const uint32_t rte = e < nc ? cand[e].root : 0xFFFFFFFEu;
-        const int32_t lpe = e < nc ? cand[e].lpath : 0;
-        const double de = e < nc ? cand[e].density : 0.0;
-        const uint32_t cnt = nc - e0 < 64 ? nc - e0 : 64;
-        for (uint32_t x = 0; x < cnt; ++x) {
-          const uint32_t r2 = rl_u32(rte, x);
-          const int32_t lp2 = (int32_t)rl_u32((uint32_t)lpe, x);
-          const double d2 = rl_f64(de, x);
-          const bool better = (lp2 > lp) | ((lp2 == lp) & (d2 > d));
-          const bool tie_before = (lp2 == lp) & (d2 == d) & (e0 + x < c);
-          win &= !((r2 == rt) & (better | tie_before));
-        }
-      }
+    for (uint32_t c = lane; c < nc; c += 64) atomicMax(&lpmax[cand[c].root], cand[c].lpath);
+    __threadfence_block();
+    __syncthreads();
+    for (uint32_t c = lane; c < nc; c += 64) {
+      const uint32_t rt = cand[c].root;
+      if (cand[c].lpath == __hip_atomic_load(&lpmax[rt], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMax(&dmax[rt], (unsigned long long)graph_dkey(cand[c].density));
+    }
+    __threadfence_block();
+    __syncthreads();
+    for (uint32_t c = lane; c < nc; c += 64) {
+      const uint32_t rt = cand[c].root;
+      if (cand[c].lpath == __hip_atomic_load(&lpmax[rt], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &&
+          (unsigned long long)graph_dkey(cand[c].density) ==
+              __hip_atomic_load(&dmax[rt], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMin(&imin[rt], c);
+    }
+    __threadfence_block();
+    __syncthreads();
+    for (uint32_t c = lane; c < nc; c += 64) {
+      const uint32_t rt = cand[c].root;
+      const bool win = __hip_atomic_load(&imin[rt], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == c;
       if (win) __atomic_fetch_or(&roots[rt >> 6], 1ull << (rt & 63), __ATOMIC_RELAXED);
-      if (ok) tiled[c] = win ? 1 : 0;  // (scratch until the tiling)
+      tiled[c] = win ? 1 : 0;  // (scratch until the tiling)
     }
     __threadfence_block();
     __syncthreads();
@@ -4004,12 +4017,14 @@ __global__ __launch_bounds__(64) void k_mega(GraphDev G, uint32_t n_reads) {
     __threadfence_block();
     __syncthreads();
     };
+    // the read's region of G.scratch, 6 words a record: [the root bitmap and its prefix
+    // counts (reads past GRAPH_NMAX records)], then the per-root arrays (2 words a node)
     if (n > GRAPH_NMAX) {
       const uint32_t rwb = (n + 4095) / 4096;  // n <= GRAPH_NMAX_BIG: 64 * rwb words of each
       uint64_t* groots = G.scratch + 6 * b;
-      components(groots, reinterpret_cast<uint32_t*>(groots + 64 * rwb), rwb);
+      components(groots, reinterpret_cast<uint32_t*>(groots + 64 * rwb), rwb, groots + 128 * rwb);
     } else {
-      components((lds_u64*)s_roots, (lds_u32*)s_rpre, RW);
+      components((lds_u64*)s_roots, (lds_u32*)s_rpre, RW, G.scratch + 6 * b);
     }
     // the tiling order, the reference's stable insertion sorts as ranks: lpath
     // descending (greedy), weight descending (weighted), tiling_end ascending
@@ -4247,10 +4262,45 @@ __global__ __launch_bounds__(64) void k_mega(GraphDev G, uint32_t n_reads) {
   m = (uint32_t)__shfl((int)m, 0, 64);
   nt = (uint32_t)__shfl((int)nt, 0, 64);
   PROF_T(km3);
-  if (G.tiling != PBGPU_TILING_NONE && lane == 0)
-    stable_sort(tiled, nt, [&](int32_t x, int32_t y) {
-      return M(x).imp_s < M(y).imp_s || (M(x).imp_s == M(y).imp_s && M(x).imp_e < M(y).imp_e);
-    });
+  // the tiled mega-reads in print order: the reference's stable sort by (imp_s, imp_e)
+  // (overlap_graph.cc:254-260).  As ranks over every lane -- #{smaller} + #{equal, earlier}
+  // -- written into `order`, which the tiling has consumed; lane 0's insertion sort took
+  // ~nt^2 / 4 dependent HBM compares, tens of ms for a C4r read with hundreds of tiles.
+  // A NaN key makes the comparison chain order-dependent: then the serial sort, as before.
+  const int32_t* tiled_sorted = tiled;
+  if (G.tiling != PBGPU_TILING_NONE && nt > 1) {
+    bool nan_key = false;
+    for (uint32_t t = lane; t < nt; t += 64) {
+      const MegaTmp& q = M(tiled[t]);
+      nan_key |= isnan(q.imp_s) | isnan(q.imp_e);
+    }
+    if (__ballot(nan_key)) {
+      if (lane == 0)
+        stable_sort(tiled, nt, [&](int32_t x, int32_t y) {
+          return M(x).imp_s < M(y).imp_s || (M(x).imp_s == M(y).imp_s && M(x).imp_e < M(y).imp_e);
+        });
+    } else {
+      for (uint32_t t0 = 0; t0 < nt; t0 += 64) {
+        const uint32_t t = t0 + lane;
+        const bool ok = t < nt;
+        const int32_t it = ok ? tiled[t] : 0;
+        const double ks = ok ? M(it).imp_s : 0.0, ke = ok ? M(it).imp_e : 0.0;
+        uint32_t rank = 0;
+        for (uint32_t u0 = 0; u0 < nt; u0 += 64) {
+          const bool uk = u0 + lane < nt;
+          const int32_t iu = uk ? tiled[u0 + lane] : 0;
+          const double us = uk ? M(iu).imp_s : 0.0, ue = uk ? M(iu).imp_e : 0.0;
+          const uint32_t cnt = nt - u0 < 64 ? nt - u0 : 64;
+          for (uint32_t x = 0; x < cnt; ++x) {
+            const double s2 = rl_f64(us, x), e2 = rl_f64(ue, x);
+            rank += (uint32_t)((s2 < ks) | ((s2 == ks) & ((e2 < ke) | ((e2 == ke) & (u0 + x < t)))));
+          }
+        }
+        if (ok) order[rank] = it;
+      }
+      tiled_sorted = order;
+    }
+  }
   __threadfence_block();
   __syncthreads();
   // ---- print_mega_reads: what each printed mega-read needs (overlap_graph.cc:254-299),
@@ -4258,7 +4308,7 @@ __global__ __launch_bounds__(64) void k_mega(GraphDev G, uint32_t n_reads) {
   // name size and unitigs come from its prefix-sum offsets (poff[q + 1] - poff[q] =
   // size + 1), so a path step waits on one load, and the next node's is issued first.
   PROF_T(km4);
-  const int32_t* pr = nt ? tiled : order;
+  const int32_t* pr = nt ? tiled_sorted : order;
   const uint32_t npr = nt ? nt : m;  // print(tiled_mr_.empty() ? sort_tiling_ : tiled_mr_)
   uint32_t done = 0;
   bool host = false;

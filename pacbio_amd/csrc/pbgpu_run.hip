@@ -994,7 +994,7 @@ pbgpu_status pbgpu_host_free(void* p) {
 static uint64_t run_hit_budget() {
   const char* e = getenv("PBGPU_RUN_HIT_BUDGET");
   const uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
-  return v ? v : 256ull << 20;
+  return v ? v : 192ull << 20;
 }
 
 pbgpu_status pbgpu_runner_create(pbgpu_index* const* indexes, size_t n_indexes, const pbgpu_align_params* params,
@@ -1030,6 +1030,9 @@ pbgpu_status pbgpu_runner_create(pbgpu_index* const* indexes, size_t n_indexes, 
       // them for the whole batch with 2x headroom, 63 GB for a cold C2 run).
       // PBGPU_RUN_HIT_BUDGET overrides it.
       a->hit_budget = run_hit_budget();
+      // a batch ends with the read that reaches batch_bases (reads are < 1/8 of a batch here
+      // in practice; a larger one still fits, as an allocation of its own)
+      a->base_cap = R->batch_bases + (R->batch_bases >> 3);
       R->al.push_back(a);
       R->rd.emplace_back(new pbgpu_reads);
       R->views.emplace_back(new RecordsView);

@@ -187,3 +187,19 @@ def test_fit_reciprocal_exact():
     correctly rounded 1.0 / n for every n a strand can reach at C1-C5 scale (< 2^24)."""
     from pacbio_amd import pbgpu
     assert pbgpu.check_reciprocal(0, 1 << 24) == 0
+
+
+@pytest.mark.parametrize("chunk", ["30000", "200000"])
+def test_chunked_resident_batch(small, chunk, monkeypatch):
+    """A resident batch larger than the device holds is aligned in chunks of reads
+    (seeding and sub-batches per chunk, records appended; round 5, so that one
+    pbgpu_align_resident call of C3's 3.6 Gbases no longer runs out of HBM).
+    PBGPU_CHUNK_BASES forces small chunks: the same bytes as the oracle."""
+    monkeypatch.setenv("PBGPU_CHUNK_BASES", chunk)
+    names, seqs = small.sr_names(), small.sr_seqs()
+    pnames, pseqs = small.pb_names(), small.pb_seqs()
+    cfg = dict(forward=True, unitigs_k=31, bases_matching=15.0, max_match=True)
+    exp = _oracle(names, seqs, pnames, pseqs, ul=small.unitig_lengths, **cfg)
+    got, st = _gpu(names, seqs, pnames, pseqs, ul=small.unitig_lengths, budget=50_000, **cfg)
+    assert st["kernel_launches"]["k_seed"] >= 2, st["kernel_launches"]  # one seeding per chunk
+    assert_same_coords(got, exp, f"chunk={chunk}")
