@@ -220,6 +220,28 @@ def _cpu_share():
         return os.cpu_count() or 1
 
 
+def _calibration(value):
+    """SURVEY 8(d)'s calibration of the CPU restatement against the reference on
+    identical inputs (tools/calib_ref.py, committed profile): the reference's own
+    PSA::search and lis_align::indices, compiled from its sources, against the
+    oracle's, one thread each on C2 reads; the reference's whole-path rate is
+    estimated from the oracle's with those two components swapped in."""
+    path = os.path.join(ROOT, "profiles", "r05_calib_ref.json")
+    try:
+        with open(path) as f:
+            c = json.load(f)
+    except (OSError, ValueError):
+        return {}
+    r = c["path"]["ratio_vs_reference"]
+    return {"ratio_vs_reference": r, "reference_estimate_value": value / r,
+            "calibration": {"profile": "profiles/r05_calib_ref.json", "cpu_model": c["cpu_model"],
+                            "threads": c["threads"], "inputs": c["inputs"],
+                            "lookup_reference_over_oracle": c["lookup"]["reference_over_oracle"],
+                            "lis_reference_over_oracle": c["lis"]["reference_over_oracle"],
+                            "note": "ratio_vs_reference = reference time / oracle time on the same reads (> 1: "
+                                    "the oracle is faster); measured in the build container, not on the GPU box"}}
+
+
 def _cmr_runs(cmr, flags, steps):
     """bin/create_mega_reads `steps` + 1 times (the first untimed): the runs' own --timing
     JSON (with PBGPU_DEBUG_STALL=1: any HIP call that blocked > 0.5 s, kept per run)"""
@@ -643,6 +665,7 @@ def main():
         mism = sum(1 for h in set(og) | set(oe) if sorted(rg.get(h, [])) != sorted(re_.get(h, [])))
         cpu = {"value": sbases / sec, "unit": "bases/s", "cores": cthreads, "kind": "port",
                "cpu_model": _cpu_model(),
+               **_calibration(sbases / sec),
                "sample": f"first {nsamp} reads of the rank-0 shard ({sbases} bases, {exp.count(chr(10))} text lines) "
                          f"against the full {args.workload} index; oracle/ C restatement, align + coords text "
                          f"formatting, {cthreads} threads (the job's CPU share of the box), {sec:.2f} s",
