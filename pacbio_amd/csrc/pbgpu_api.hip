@@ -1821,6 +1821,7 @@ static void graph_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   G.ecnt = dead.take(al->g_ecnt, nrec + 1); G.eoff = dead.take(al->g_eoff, nrec + 1);
   G.ovf_list = dead.take(al->g_ovf_list, nrec + 1);
   G.edges = dead.take(al->g_edges, nrec * GRAPH_EBLK);
+  G.bmax = dead.take(al->g_bmax, nrec / 64 + 2);
   G.ovf = al->g_ovf.p;
   uint64_t ovf[2];
   HIPCHK(launch_graph(G, n, nrec, max_n, st, al->g_side, al->g_fork, al->g_join, ovf));
@@ -2015,7 +2016,10 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
       const double fill_small = 0.95 * (double)((1u << hcap_log2) - (1u << hcap_log2) / 4);
       // tests: PBGPU_GROUP_PRED_SCALE=0 routes every read to the smallest table (all overflow paths)
       const double pred_scale = getenv("PBGPU_GROUP_PRED_SCALE") ? atof(getenv("PBGPU_GROUP_PRED_SCALE")) : 1.0;
-      const double fill_big = 0.95 * (double)((1u << kGroupLdsMaxLog2) - (1u << kGroupLdsMaxLog2) / 4);
+#ifndef PBGPU_GROUP_BIG_FILL8
+#define PBGPU_GROUP_BIG_FILL8 6
+#endif
+      const double fill_big = 0.95 * (double)((1u << kGroupLdsMaxLog2) / 8 * PBGPU_GROUP_BIG_FILL8);
       std::vector<uint32_t>& rs = al->h_small;
       std::vector<uint32_t>& rb = al->h_big;
       rs.clear(); rb.clear();

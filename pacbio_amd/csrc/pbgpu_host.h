@@ -386,6 +386,7 @@ struct pbgpu_aligner {
   dbuf<uint64_t> g_poff;
   dbuf<uint32_t> g_pre, g_sizes;
   dbuf<GDesc> g_desc;
+  dbuf<double> g_bmax;
   dbuf<double2> g_imp;
   dbuf<GraphNode> g_out;
   dbuf<uint32_t> g_ecnt;

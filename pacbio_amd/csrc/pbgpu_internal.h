@@ -233,6 +233,10 @@ struct GraphDev {
   uint2* pp;                  // prefix sums along the name: {unitig lengths, info[2u] - info[2u - 1]}
   uint32_t* ounits;           // the name's unitigs in the record's orientation (at poff)
   GDesc* desc;                // per read, in sorted order
+  // per 64 sorted positions of the batch (q >> 6): the largest imp_e of its nodes with
+  // imp_s > 1 (NaN as +inf; -inf if none): k_graph_edges skips a whole block when node i
+  // is past it by more than 31 (every node of it is "not advancing", overlap_graph.cc:20)
+  double* bmax;
   GraphNode* out;
   // the traversal's edges (k_graph_edges): per node in sorted order its count, its
   // first GRAPH_EBLK edges in a block of its own (edges + q * GRAPH_EBLK) and, past

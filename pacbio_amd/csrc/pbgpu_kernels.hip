@@ -549,6 +549,9 @@ constexpr int GROUP_U = PBGPU_GROUP_U, GROUP_U_BIG = PBGPU_GROUP_U_BIG;  // 64-h
 #ifndef PBGPU_GROUP_MINW
 #define PBGPU_GROUP_MINW 1
 #endif
+#ifndef PBGPU_GROUP_BUCKET
+#define PBGPU_GROUP_BUCKET 1  // bucketed LDS-table probing (4 slots a 16-byte read); 0 = slot by slot
+#endif
 template <bool GLOBAL_TABLE, uint32_t B>
 __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_group(IndexView ix, const KRec* __restrict__ krec,
                                                        const uint64_t* __restrict__ roff, const uint32_t* __restrict__ n_kept,
@@ -579,7 +582,10 @@ __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_
   const uint64_t kbase = roff[r];
   const uint32_t nk = n_kept[r], thr = thr_in[r];
   const uint64_t hbase = hit_off[r] - node_base;
-  const uint32_t used_limit = hcap - hcap / 4;
+#ifndef PBGPU_GROUP_BIG_FILL8
+#define PBGPU_GROUP_BIG_FILL8 6  // the LDS tables' fill limit in eighths (the 8192-slot tier's below)
+#endif
+  const uint32_t used_limit = (B == GROUP_BLOCK || GLOBAL_TABLE) ? hcap - hcap / 4 : hcap / 8 * PBGPU_GROUP_BIG_FILL8;
   // Reads touching many super-reads are grouped in P passes over hash partitions
   // of the super-read ids; each partition's lists are placed after the previous
   // ones, so every list is still contiguous and in reference order.
@@ -715,14 +721,81 @@ __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_
           return;
         }
 #endif
+#ifdef PBGPU_PROF
+        const uint64_t gp_t0 = __builtin_amdgcn_s_memtime();
+#endif
+#if PBGPU_GROUP_BUCKET
+        // Bucketed probing (LDS tables): a key lives in the first bucket of 4 slots, from its
+        // home bucket on, that holds it or had room when it was inserted; one 16-byte LDS read
+        // tests 4 slots.  Every window's home bucket is read together; a lane then inserts
+        // into its bucket's first empty slot by compare-and-swap (re-reading the bucket when
+        // another key took that slot) or walks on to the next bucket.  (Round 4's linear
+        // probing walked slot by slot, one LDS round trip each, the wave waiting for its
+        // longest walk; on C4r-shaped reads the table work was ~38 of the 43 ms of pass 0.)
+        uint4 fb_q[GU];
+#pragma unroll
+        for (int u = 0; u < GU; ++u) {
+          fb_q[u] = make_uint4(0u, 0u, 0u, 0u);
+          if (mine_q[u] && !GLOBAL_TABLE) fb_q[u] = *reinterpret_cast<const uint4*>(&tkey[slot_q[u] & ~3u]);
+        }
+        if (!GLOBAL_TABLE) {
+#pragma unroll
+          for (int u = 0; u < GU; ++u) {
+            if (!mine_q[u]) continue;
+            const uint32_t key = sr_q[u] + 1;
+            uint32_t b = slot_q[u] & ~3u, slot = 0;
+            uint4 kk = fb_q[u];
+            bool ok = true;
+            for (uint32_t walk = 0;; ++walk) {
+              const int pos = kk.x == key ? 0 : kk.y == key ? 1 : kk.z == key ? 2 : kk.w == key ? 3 : -1;
+              if (pos >= 0) { slot = b + (uint32_t)pos; break; }
+              if (pass == 1) {  // (present: pass 0 inserted every key of the partition)
+                b = (b + 4) & (hcap - 1);
+                kk = *reinterpret_cast<const uint4*>(&tkey[b]);
+                continue;
+              }
+              const int e = kk.x == 0 ? 0 : kk.y == 0 ? 1 : kk.z == 0 ? 2 : kk.w == 0 ? 3 : -1;
+              if (e < 0) {
+                if (walk >= 8 && (walk >= hcap / 4 || __hip_atomic_load(&s_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) {
+                  s_flag = 1; ok = false; break;
+                }
+                b = (b + 4) & (hcap - 1);
+                kk = *reinterpret_cast<const uint4*>(&tkey[b]);
+                continue;
+              }
+              const uint32_t old = atomicCAS(&tkey[b + (uint32_t)e], 0u, key);
+              if (old == 0) {
+                slot = b + (uint32_t)e;
+                if (atomicAdd(&s_used, 1u) >= used_limit) { s_flag = 1; ok = false; }
+                break;
+              }
+              if (old == key) { slot = b + (uint32_t)e; break; }
+              kk = *reinterpret_cast<const uint4*>(&tkey[b]);  // another key took it: look again
+            }
+            if (pass == 0) { if (ok) atomicAdd(fwdx_q[u] ? &tcf[slot] : &tcb[slot], 1u); }
+            else slot_q[u] = slot;
+          }
+        }
+#endif
 #pragma unroll
         for (int u = 0; u < GU; ++u) {
           first[u] = 0;
-          if (mine_q[u]) first[u] = pass == 0 ? atomicCAS(&tkey[slot_q[u]], 0u, sr_q[u] + 1) : tkey[slot_q[u]];
+          if (mine_q[u] && (GLOBAL_TABLE || !PBGPU_GROUP_BUCKET))
+            first[u] = pass == 0 ? atomicCAS(&tkey[slot_q[u]], 0u, sr_q[u] + 1) : tkey[slot_q[u]];
         }
+#ifdef PBGPU_PROF
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        const uint64_t gp_t1 = __builtin_amdgcn_s_memtime();
+        uint32_t gp_mine = 0, gp_walk = 0;
 #pragma unroll
         for (int u = 0; u < GU; ++u) {
-          if (!mine_q[u]) continue;
+          gp_mine += mine_q[u];
+          gp_walk += __ballot(mine_q[u] && first[u] != sr_q[u] + 1 && !(pass == 0 && first[u] == 0)) != 0;
+        }
+#endif
+#pragma unroll
+        for (int u = 0; u < GU; ++u) {
+          if (!mine_q[u] || (!GLOBAL_TABLE && PBGPU_GROUP_BUCKET)) continue;
           const uint32_t key = sr_q[u] + 1;
           uint32_t slot = slot_q[u], old = first[u];
           if (pass == 0) {
@@ -751,6 +824,17 @@ __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_
             slot_q[u] = slot;
           }
         }
+#ifdef PBGPU_PROF
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        if (B == GROUP_BLOCK_BIG && !GLOBAL_TABLE) {  // slots 41..47: the 8192-slot tier's table work
+          const uint64_t gp_t2 = __builtin_amdgcn_s_memtime();
+          PROF_ADD(41 + 3 * pass, gp_t1 - gp_t0);  // first probes
+          PROF_ADD(42 + 3 * pass, gp_t2 - gp_t1);  // collision walks + count atomics (pass 0)
+          PROF_ADD(43 + 3 * pass, gp_walk);        // windows with a collision walk
+          for (int o = 32; o > 0; o >>= 1) gp_mine += (uint32_t)__shfl_xor((int)gp_mine, o, 64);
+          if (pass == 0) PROF_ADD(47, gp_mine);
+        }
+#endif
         if constexpr (pass == 1) {
           // Scatter: each hit takes the next slot of its (super-read, strand) list.  The
           // waves take their cursors in wave order (one barrier each) and a wave its
@@ -1441,8 +1525,15 @@ __global__ __launch_bounds__(256) void k_order_tiny(const ChainDesc* __restrict_
 }
 
 constexpr int LISW_TINY_N = 255;  // SMAX of the timed tier-0 k_lis_w
+#ifndef PBGPU_LISW_WAVES
+#define PBGPU_LISW_WAVES 0  // experiment: waves per SIMD asked of the compiler (0 = its choice)
+#endif
 template <int SMAX, int WPB>
-__global__ __launch_bounds__(64 * WPB) void k_lis_w(const ChainDesc* __restrict__ chains,
+__global__ __launch_bounds__(64 * WPB)
+#if PBGPU_LISW_WAVES
+__attribute__((amdgpu_waves_per_eu(PBGPU_LISW_WAVES, PBGPU_LISW_WAVES)))
+#endif
+void k_lis_w(const ChainDesc* __restrict__ chains,
                                                     const uint32_t* __restrict__ items, uint32_t n_items,
                                                     const uint32_t* __restrict__ slen, int2* X,
                                                     LNode<uint16_t>* __restrict__ N16, int2* __restrict__ pts,
@@ -3261,6 +3352,26 @@ DEV void name_overlap_reg(const uint32_t (&a)[GRAPH_U], const uint32_t (&bu)[GRA
 #pragma unroll
   for (int u = 0; u < SA; ++u) same &= a[u] == bu[u];
 }
+// G.bmax: a wave per 64 sorted positions.  Positions of reads left to the host hold an
+// earlier batch's descriptors; they are never scanned, and a stale value can only raise
+// a block's maximum (or make it +inf), which skips less, never more.
+__global__ __launch_bounds__(256) void k_graph_bmax(GraphDev G, uint64_t n_recs) {
+  const uint64_t blk = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const uint32_t lane = threadIdx.x & 63;
+  if ((blk << 6) >= n_recs) return;
+  const uint64_t q = (blk << 6) + lane;
+  double v = -INFINITY;
+  if (q < n_recs) {
+    const double is = G.desc[q].imp_s, ie = G.desc[q].imp_e;
+    if (!(is <= 1.0)) v = ie != ie ? INFINITY : ie;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double w = __shfl_xor(v, o, 64);
+    v = w > v ? w : v;
+  }
+  if (lane == 0) G.bmax[blk] = v;
+}
 template <bool OVF>
 __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n_recs, uint64_t n_ovf) {
   __shared__ double s_is[GE_SLOTS], s_ie[GE_SLOTS], s_er[GE_SLOTS];
@@ -3303,6 +3414,9 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
     const uint32_t qe = s_end[ti];
     const double ie_i = s_ie[ti], err_i = s_er[ti];
     uint32_t cnt = 0;
+#ifdef PBGPU_PROF
+    uint64_t ge_seen = 0, ge_far = 0, ge_cand = 0;
+#endif
     if ((q + 1 < qe) & !(ie_i >= s_rl[ti])) {  // (imp_e >= rl: hanging off the 3' end)
       const uint32_t sa = s_meta[ti] >> 16, po_i = s_po[ti];
       const uint32_t sa_u = (uint32_t)__builtin_amdgcn_readfirstlane((int)sa);  // (uniform: the wave's node i)
@@ -3313,10 +3427,29 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
       uint2* const out = OVF ? G.eovf : G.edges;
       const uint64_t ob = OVF ? G.eoff[q] - GRAPH_EBLK : q * GRAPH_EBLK;  // (mod 2^64)
       for (uint64_t j0 = q + 1; j0 < qe; j0 += 64) {
+        // Fast-forward over whole 64-position blocks in which every node is skipped for node i
+        // (imp_s <= 1, or not advancing: imp_e_i > imp_e_j + 31), 64 blocks a test: none of them
+        // can give an edge or the break.  On repeat-rich reads most of a long node's scan is
+        // nodes it contains (C4r: 73% of 252 G scanned positions were skips).
+        {
+          const uint64_t b0 = j0 >> 6, bb = b0 + lane;
+          const bool in = (bb << 6) < qe;
+          const double m = in ? G.bmax[bb] : 0.0;
+          const uint64_t nsk = __ballot(!(in & (ie_i > __dadd_rn(m, 31.0))));
+          if (!(nsk & 1ull)) {  // block b0 (holding j0) is skipped: jump to the first one that is not
+            if (!nsk) { j0 = (b0 + 64) << 6; if (j0 >= qe) break; j0 -= 64; continue; }
+            const uint64_t nb = b0 + (uint64_t)__ffsll((unsigned long long)nsk) - 1;
+            j0 = nb << 6;
+            if (j0 >= qe) break;
+          }
+        }
         const uint64_t j = j0 + lane;
         const bool act = j < qe;
         const uint32_t sj = (uint32_t)((act ? j : q) - q0);
-        // node j: staged, or (a scan past the window) from HBM
+        // node j: staged, or (a scan past the window) from HBM.  Every load is issued before
+        // the tests (measured: loading the name only where the name test runs, after the
+        // skip / break ballot, made the C4r graph stage 240 -> 316 ms: a second round trip
+        // on the critical path costs more than the loads it saves)
         double is_j, ie_j, er_j;
         uint32_t mj, lpa_j, po_j, bu[GRAPH_U];
         if (!OVF && sj < ns) {
@@ -3387,9 +3520,22 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
           out[ob + at] = make_uint2((mj & 0xFFFFu) | ((sb - (uint32_t)nb) << 16), lpa_j - (uint32_t)common);
         }
         cnt += (uint32_t)__builtin_popcountll(em);
+#ifdef PBGPU_PROF
+        {
+          const uint64_t am = __ballot(act & (lane < fb));
+          ge_seen += (uint64_t)__builtin_popcountll(am);
+          ge_far += (uint64_t)__builtin_popcountll(am & __ballot(OVF || sj >= ns));
+          ge_cand += (uint64_t)__builtin_popcountll(__ballot(cand));
+        }
+#endif
         if (bm) break;  // the reference's break
       }
     }
+#ifdef PBGPU_PROF
+    if (!OVF) {  // slots 33..35: positions scanned, of them past the staged window, candidates (name test)
+      PROF_ADD(33, ge_seen); PROF_ADD(34, ge_far); PROF_ADD(35, ge_cand);
+    }
+#endif
     if (!OVF && lane == 0) {
       G.ecnt[q] = cnt;
       if (cnt > GRAPH_EBLK) {  // its region past the block, and listed
@@ -4466,7 +4612,9 @@ hipError_t launch_graph(const GraphDev& G, uint32_t n_reads, uint64_t n_recs, ui
   if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_graph_sort<GRAPH_NM_SMALL>, dim3(n_reads), dim3(GRAPH_SORT_BLOCK), 0, st, G, n_reads);
   if ((e = hipStreamWaitEvent(st, join, 0)) != hipSuccess) return e;
-  // every node's edges (its first GRAPH_EBLK) and the nodes with more
+  // the blocks' largest implied ends (the scans' fast-forward), then every node's edges (its
+  // first GRAPH_EBLK) and the nodes with more
+  hipLaunchKernelGGL(k_graph_bmax, dim3((uint32_t)((n_recs + 255) / 256)), dim3(256), 0, st, G, n_recs);
   const uint32_t eg = (uint32_t)((n_recs + GE_NODES - 1) / GE_NODES);
   hipLaunchKernelGGL(k_graph_edges<false>, dim3(eg), dim3(GE_BLOCK), 0, st, G, n_recs, 0ull);
   if ((e = hipMemcpyAsync(ovf, G.ovf, 16, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;

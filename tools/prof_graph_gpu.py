@@ -53,6 +53,9 @@ def main():
             print(f"k_graph_relax {tier}: blocks {v[7]}, nodes {v[6]}, chunks {v[1]} ({v[1] / nn:.2f} a node); "
                   f"ticks a node: paths wave {v[2] / nn:.0f} (chunk work {v[0] / nn:.0f}), "
                   f"union wave {v[5] / nn:.0f} (finds {v[3] / nn:.0f}, merges {v[4] / nn:.0f})")
+        e = list(buf)[33:36]
+        print(f"k_graph_edges: positions scanned {e[0]} ({e[0] / max(1, st['graph_records']):.1f} a node), past the "
+              f"staged window {e[1]}, name tests {e[2]}")
         w = list(buf)[88:96]
         nw = max(1, w[5])
         print(f"k_mega: waves {w[5]}, candidates {w[7] >> 32}, components {w[7] & 0xffffffff}, "
