@@ -335,3 +335,42 @@ def test_device_graph_long_reads_c4r(tmp_path):
     assert (nrec > 8192).sum() >= 2, np.sort(nrec)[-40:]
     assert not host.any() and al.stats()["graph_host_reads"] == 0
     ds.close()
+
+
+def test_graph_ties_equal_implied_starts(tmp_path):
+    """Ties the device relaxation resolves by rank keys: two super-reads of the
+    same sequence under different names ("1F_2F_3F", "6F_2F_3F") align with identical
+    implied spans, both overlap "2F_3F_4F", which overlaps "3F_4F_5F": node J is reached by
+    two paths of equal length whose start nodes have equal imp_s, so the reference keeps
+    the first (overlap_graph.cc:45, strictly greater).  A third copy ("8F_2F_3F") and a
+    read of the reverse strand add more equal keys.  Device graph == host graph for every
+    tiling, and with -b (path length in bases)."""
+    import random
+    rng = random.Random(11)
+    ulen, step = 400, 370  # unitigs of 400 bases overlapping by k - 1 = 30
+    g = "".join(rng.choice("ACGT") for _ in range(step * 6 + ulen))
+    u = {i: g[(i - 1) * step:(i - 1) * step + ulen] for i in range(1, 7)}
+
+    def sr(ids):
+        s = u[ids[0]]
+        for i in ids[1:]:
+            s += u[i][30:]
+        return s
+    a = sr([1, 2, 3])
+    srs = [("1F_2F_3F", a), ("6F_2F_3F", a), ("2F_3F_4F", sr([2, 3, 4])), ("3F_4F_5F", sr([3, 4, 5])),
+           ("8F_2F_3F", a), ("4F_5F_6F", sr([4, 5, 6]))]
+    (tmp_path / "sr.fa").write_text("".join(f">{n}\n{s}\n" for n, s in srs))
+    read = sr([1, 2, 3, 4, 5, 6])
+    rc = read[::-1].translate(str.maketrans("ACGT", "TGCA"))
+    (tmp_path / "pb.fa").write_text(f">fwd\n{read}\n>rev\n{rc}\n>mid\n{read[200:2000]}\n")
+    (tmp_path / "ul.txt").write_text("".join(f"u{i} {ulen}\n" for i in range(9)))
+    for tiling in ("greedy", "maximal", "weighted", "none"):
+        for extra in ([], ["-b"]):
+            base = ["-s", "1M", "-m", "17", "-k", "31", "-l", str(tmp_path / "ul.txt"), "-T", tiling, "-L", "0",
+                    *extra, "-r", str(tmp_path / "sr.fa"), "-p", str(tmp_path / "pb.fa")]
+            a_out, b_out = str(tmp_path / "dev"), str(tmp_path / "host")
+            _run([*base, "-o", a_out])
+            _run([*base, "--host-graph", "-o", b_out])
+            ta = open(a_out).read()
+            assert ta == open(b_out).read(), (tiling, extra)
+            assert ta.count(">") >= 2, ta
