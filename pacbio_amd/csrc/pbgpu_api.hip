@@ -46,10 +46,9 @@ void launch_seed(int mode, IndexView ix, const uint8_t* seq, const uint64_t* rof
                  KRec* krec, uint32_t* n_kept, uint32_t* thr, uint64_t* nhits, unsigned long long* stats,
                  uint32_t* gcount, uint64_t null_ptr, hipStream_t st);
 void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const uint32_t* n_kept, const uint32_t* thr,
-                  const uint64_t* hit_off, uint64_t node_base, uint32_t r0, const uint32_t* read_list, uint32_t n_list,
+                  const uint64_t* hit_off, uint64_t node_base, uint32_t r0, const uint2* read_list, uint32_t n_list,
                   uint32_t hcap_log2, uint32_t* gtable, GroupOut O, unsigned long long* stats, hipStream_t st);
 uint64_t group_table_words(uint32_t hcap_log2);
-void launch_group_refine(const uint32_t* list, uint32_t n, uint2* prog, hipStream_t st);
 void launch_sr_ul(const uint32_t* ids, uint64_t n, const int32_t* ul, uint64_t n_ul, int32_t* out, hipStream_t st);
 void launch_counts_pack16(bool unpack, const uint32_t* src, uint64_t n, uint32_t* dst, hipStream_t st);
 void launch_occ_sr(const uint64_t* occ, uint64_t n, uint32_t* out, hipStream_t st);
@@ -64,12 +63,15 @@ void launch_chain_order(const uint32_t* lisl, uint32_t n, uint32_t* hist, uint32
                         unsigned long long* sums, hipStream_t st);
 void launch_lis(bool big_nodes, const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen,
                 const int2* X, void* N, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx,
-                unsigned long long* stats, hipStream_t st);
+                unsigned long long* stats, hipStream_t st, const uint32_t* nshift = nullptr);
+void launch_node32_place(const ChainDesc* chains, const uint32_t* items, uint32_t n, const uint32_t* slen,
+                         uint32_t* nshift, unsigned long long* total, hipStream_t st);
+uint32_t node32_chunk();
 void launch_coords(IndexView ix, AlignParamsDev P, const ChainDesc* chains, const uint32_t* list, uint32_t n,
                    const uint64_t* roff, uint32_t emit, ChainOut O, hipStream_t st);
 void launch_discard(const ChainDesc* chains, const uint32_t* list, uint32_t n, const uint32_t* lisl, uint32_t* slen,
-                    int2* X, const void* N16, const void* N32, uint32_t* items_small, uint32_t* n_small,
-                    uint32_t* items_big, uint32_t* n_big, hipStream_t st);
+                    int2* X, const void* N16, const void* N32, const uint32_t* nshift, uint32_t* items_small,
+                    uint32_t* n_small, uint32_t* items_big, uint32_t* n_big, hipStream_t st);
 void launch_lis_wave(int tier, const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen,
                      int2* X, void* N16, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx,
                      unsigned long long* stats, hipStream_t st);
@@ -1253,6 +1255,7 @@ pbgpu_status pbgpu_aligner_create(const pbgpu_index* ix, const pbgpu_align_param
   al->stats.alloc(ST_N + 1);  // + the fine stage's kmers_info capacity counter
   al->info_count.alloc(1);
   al->counters.alloc(128);
+  al->n32total.alloc(1);
   *out = al.release();
   return PBGPU_OK;
   API_CATCH
@@ -1270,7 +1273,8 @@ static void buffer_report(const pbgpu_aligner* al) {
       {"rec_per_read", al->rec_per_read.bytes()},
       {"rec_cursor", al->rec_cursor.bytes()},
       {"order", al->order.bytes()},
-      {"ovf_reads", al->ovf_reads.bytes()},
+      {"ovf_items", al->ovf_items.bytes()},
+      {"rcur", al->rcur.bytes()},
       {"counters", al->counters.bytes()},
       {"sort_scratch", al->sort_scratch.bytes()},
       {"nhits", al->nhits.bytes()},
@@ -1284,6 +1288,7 @@ static void buffer_report(const pbgpu_aligner* al) {
       {"pts", al->pts.bytes()},
       {"nodes", al->nodes.bytes()},
       {"nodes32", al->nodes32.bytes()},
+      {"n32shift", al->n32shift.bytes()},
       {"lisl", al->lisl.bytes()},
       {"hist", al->hist.bytes()},
       {"slen", al->slen.bytes()},
@@ -1299,8 +1304,6 @@ static void buffer_report(const pbgpu_aligner* al) {
       {"info_count", al->info_count.bytes()},
       {"ovf_list", al->ovf_list.bytes()},
       {"read_list", al->read_list.bytes()},
-      {"nparts", al->nparts.bytes()},
-      {"prog", al->prog.bytes()},
       {"gcount", al->gcount.bytes()},
       {"gcount16", al->gcount16.bytes()},
       {"fwin", al->fwin.bytes()},
@@ -1590,13 +1593,26 @@ static uint32_t lis_stage(pbgpu_aligner* al, uint32_t nch, uint64_t Hs, const Li
   HIPCHK(hipMemsetAsync(al->lisl.p, 0, 2ull * nch * 4, st));
   const uint32_t n_strands = order(0, 2 * nch);
   const uint32_t nbig = n_big;
-  if (nbig) al->nodes32.ensure((Hs + 1) * 16);
+  // 32-bit nodes: the strands above LIS_U16_MAX hits only, packed (k_node32_place);
+  // a first reservation at the aligner's first call, so a later batch's long
+  // strand rarely allocates
+  (void)Hs;
+  if (!al->nodes32.n) al->nodes32.ensure_fixed(32ull << 20);
+  al->n32shift.ensure(2ull * nch + 1);
+  if (nbig) {
+    HIPCHK(hipMemsetAsync(al->n32total.p, 0, 8, st));
+    launch_node32_place(al->chains.p, al->perm.p, nbig, al->slen.p, al->n32shift.p, al->n32total.p, st);
+    unsigned long long chunks = 0;
+    HIPCHK(hipMemcpyAsync(&chunks, al->n32total.p, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    al->nodes32.ensure((chunks + 1) * node32_chunk() * 16);
+  }
   // strands longer than k_lis_w's LDS capacity: restore list order in place first.
   // (Running the tiers on separate streams was measured slower: they contend.)
   if (restore) launch_strand_order(al->chains.p, al->perm.p, n_mid, al->slen.p, al->X.p, st);
   if (timed) HIPCHK(hipEventRecord(al->ev[11], st));
   launch_lis(true, al->chains.p, al->perm.p, nbig, al->slen.p, al->X.p, al->nodes32.p, al->pts.p, al->lisl.p, lp,
-             keep_idx, al->stats.p, st);
+             keep_idx, al->stats.p, st, al->n32shift.p);
   // 4095 < n <= 65535: lane-per-strand chunked kernel; n <= 4095: wave-per-strand kernels
   const uint32_t nmid = n_mid, nw2 = n_w2, nw1 = n_w1;
   launch_lis(false, al->chains.p, al->perm.p + nbig, nmid - nbig, al->slen.p, al->X.p, al->nodes.p, al->pts.p,
@@ -1610,6 +1626,8 @@ static uint32_t lis_stage(pbgpu_aligner* al, uint32_t nch, uint64_t Hs, const Li
   launch_lis_lane(al->chains.p, al->perm.p + nw0, n_strands - nw0, al->slen.p, al->X.p, al->nodes.p, al->pts.p,
                   al->lisl.p, lp, keep_idx, al->stats.p, st);
   if (timed) HIPCHK(hipEventRecord(al->ev[10], st));  // the timed k_lis slot: tier-0 k_lis_w alone
+  // tier 0 (9..255 hits).  (A 16-wave tier of its strands of <= 64 hits was measured
+  // no faster: C2 LIS 20.7 vs 20.8 ms, C4r 47.0 vs 48.7, profiles/r05p_lisw.txt.)
   launch_lis_wave(0, al->chains.p, al->perm.p + nw1, nw0 - nw1, al->slen.p, al->X.p, al->nodes.p,
                   al->pts.p, al->lisl.p, lp, keep_idx, al->stats.p, st);
   HIPCHK(hipGetLastError());
@@ -1630,10 +1648,17 @@ struct DeadHits {
   explicit DeadHits(pbgpu_aligner* al)
       : r{{(uint8_t*)al->X.p, al->X.bytes(), 0}, {(uint8_t*)al->pts.p, al->pts.bytes(), 0},
           {(uint8_t*)al->nodes.p, al->nodes.bytes(), 0}} {}
+  // In a ramped batch (pbgpu_run's first batches, tl_grow_scale > 1) a temporary whose
+  // full-batch size would not fit even an empty dead buffer gets its own buffer now,
+  // sized for a full batch (round 5: C4r's edge blocks, 512 B a record, fit the first
+  // batch's dead buffers and were allocated in batch 2, 4-5 GB each)
   template <typename T>
   T* take(dbuf<T>& own, size_t cnt) {
     const size_t bytes = cnt * sizeof(T);
-    if (!getenv("PBGPU_NO_CARVE"))
+    size_t largest = 0;
+    for (auto& x : r) largest = std::max(largest, x.p ? x.n : 0);
+    const bool never = tl_grow_scale > 1.0 && (double)bytes * tl_grow_scale > (double)largest;
+    if (!never && !getenv("PBGPU_NO_CARVE"))
       for (auto& x : r) {
         const size_t a = (x.used + 255) & ~(size_t)255;
         if (x.p && a + bytes <= x.n) { x.used = a + bytes; return reinterpret_cast<T*>(x.p + a); }
@@ -1796,6 +1821,12 @@ static void graph_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   // PBGPU_GRAPH_NMAX (tests): a lower cap on the records of a read traversed on the device
   G.nmax = GRAPH_NMAX_BIG;
   if (const char* e = getenv("PBGPU_GRAPH_NMAX")) G.nmax = (uint32_t)std::min<long>(GRAPH_NMAX_BIG, std::max(0l, atol(e)));
+  // reads of more records relax with their state in HBM (k_graph_relax_big): an LDS
+  // tier's block of 4096-8192 records holds a CU alone, the HBM blocks share CUs (C4r graph
+  // stage 200 -> 160 ms at 2048, C2 unchanged; PBGPU_RELAX_BIG_MIN sets it)
+  G.relax_big_min = 2048;
+  if (const char* e = getenv("PBGPU_RELAX_BIG_MIN"))
+    G.relax_big_min = (uint32_t)std::min<long>(GRAPH_NMAX, std::max(0l, atol(e)));
   // reads past GRAPH_NMAX records keep their sort keys and node state here (6 words a record)
   G.scratch = dead.take(al->sort_scratch, 6ull * nrec + 6);
   al->g_maxn.ensure(1);
@@ -1931,8 +1962,9 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
   al->n_kept.ensure(n); al->thr.ensure(n); al->nhits.ensure(n); al->hit_off.ensure(n + 1);
   std::vector<uint64_t>& hoff = al->h_hoff;
   hoff.resize(n + 1);
-  al->ovf_reads.ensure(n);
+  al->ovf_items.ensure(n);
   al->ovf_list.ensure(n);  // (used only by batches with reads past the first group tier)
+  al->rcur.ensure(n);
   uint64_t rec_done = 0, info_done = 0;
   // records counted per read as they are emitted (ChainOut.per_read), unless --max-match
   // re-emits or a sub-batch is redone after a record overflow: then records_stage counts
@@ -1987,12 +2019,14 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
     O.chain_count = al->counters.p;
     O.chain_cap = (uint32_t)std::min<uint64_t>(al->chains.n, 0xFFFFFFFFu);
     O.n_overflow = al->counters.p + 3;
-    O.overflow_reads = al->ovf_reads.p;
+    O.overflow_items = al->ovf_items.p;
+    O.rcur = al->rcur.p;
     // Reads longest first (hits), so the long-read tail starts early.  The predicted
     // super-read count of a read (hits x chains-per-hit of earlier batches) picks its
     // table: 2048 LDS slots (4 waves), 8192 LDS slots (16 waves), and beyond that the
-    // 8192-slot table over several hash partitions of its super-reads.  A misprediction
-    // only costs time: an overflowing read resumes in the next tier.
+    // 8192-slot table over several hash partitions of its super-reads, a work item (and
+    // block) each.  A misprediction only costs time: an overflowing item goes again in
+    // the next tier or split in two.
     uint32_t n_small = 0, n_bigr = 0;
     {
       const auto th0 = std::chrono::steady_clock::now();
@@ -2008,8 +2042,7 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
       };
       std::vector<uint32_t>& rl = al->h_order;
       std::vector<uint32_t>& cnt = al->h_class;
-      std::vector<uint8_t>& parts = al->h_parts;
-      rl.resize(nr); parts.resize(nr); cnt.assign(NCL + 1, 0);
+      rl.resize(nr); cnt.assign(NCL + 1, 0);
       for (uint32_t r = r0; r < r1; ++r) ++cnt[NCL - 1 - cls(hoff[r + 1] - hoff[r])];
       for (uint32_t c = 0, acc = 0; c <= NCL; ++c) { const uint32_t v = cnt[c]; cnt[c] = acc; acc += v; }
       for (uint32_t r = r0; r < r1; ++r) rl[cnt[NCL - 1 - cls(hoff[r + 1] - hoff[r])]++] = r;
@@ -2020,31 +2053,27 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
 #define PBGPU_GROUP_BIG_FILL8 6
 #endif
       const double fill_big = 0.95 * (double)((1u << kGroupLdsMaxLog2) / 8 * PBGPU_GROUP_BIG_FILL8);
-      std::vector<uint32_t>& rs = al->h_small;
-      std::vector<uint32_t>& rb = al->h_big;
+      std::vector<uint2>& rs = al->h_small;
+      std::vector<uint2>& rb = al->h_big;
       rs.clear(); rb.clear();
       for (uint32_t r : rl) {
         const double pred = (double)(hoff[r + 1] - hoff[r]) * al->chains_per_hit * pred_scale;
-        parts[r - r0] = (uint8_t)std::min(255.0, std::max(1.0, std::ceil(pred / fill_big)));
-        (pred > fill_small ? rb : rs).push_back(r);
+        if (pred <= fill_small) { rs.push_back(group_item(r, 0, 1)); continue; }
+        const uint32_t P = (uint32_t)std::min(4096.0, std::max(1.0, std::ceil(pred / fill_big)));
+        for (uint32_t q = 0; q < P; ++q) rb.push_back(group_item(r, q, P));
       }
       n_small = (uint32_t)rs.size(); n_bigr = (uint32_t)rb.size();
       rs.insert(rs.end(), rb.begin(), rb.end());
       al->acc.ms_host_order += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count();
-      al->read_list.ensure(nr);
-      al->nparts.ensure(n);
-      al->prog.ensure(n);
-      HIPCHK(hipMemcpyAsync(al->read_list.p, rs.data(), (size_t)nr * 4, hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(al->nparts.p + r0, parts.data(), nr, hipMemcpyHostToDevice, st));
+      al->read_list.ensure(rs.size());
+      HIPCHK(hipMemcpyAsync(al->read_list.p, rs.data(), rs.size() * sizeof(uint2), hipMemcpyHostToDevice, st));
     }
-    O.nparts = al->nparts.p;
-    O.prog = al->prog.p;
     for (int attempt = 0;; ++attempt) {
       HIPCHK(hipEventRecord(al->ev[5], st));
       HIPCHK(hipMemsetAsync(al->counters.p, 0, 16 * 4, st));
+      HIPCHK(hipMemsetAsync(al->rcur.p + r0, 0, (size_t)nr * 4, st));
       static_assert(ST_LIS_TESTS == ST_CHAINS + 1, "per-attempt stat slots are adjacent");
       HIPCHK(hipMemsetAsync(al->stats.p + ST_CHAINS, 0, 16, st));  // redone on a retry: counted per attempt
-      O.resume = 0;
       // PBGPU_GROUP_OVERLAP=1 (experiment): the 16-wave tier's reads -- the longest -- on a side
       // stream, started first, beside the 4-wave tier
       static const bool overlap = getenv("PBGPU_GROUP_OVERLAP") && atoi(getenv("PBGPU_GROUP_OVERLAP"));
@@ -2073,7 +2102,6 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
                      al->read_list.p + n_small, n_bigr, kGroupLdsMaxLog2, nullptr, O, al->stats.p, st);
         HIPCHK(hipGetLastError());
       }
-      O.resume = 1;
       uint32_t cnt[4];
       HIPCHK(hipMemcpyAsync(cnt, al->counters.p, 16, hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
@@ -2082,23 +2110,32 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
       uint32_t n_ovf = cnt[3];
       uint32_t lg = hcap_log2;
       while (n_ovf) {
-        std::vector<uint32_t> ovf(n_ovf);
-        HIPCHK(hipMemcpy(ovf.data(), al->ovf_reads.p, n_ovf * 4, hipMemcpyDeviceToHost));
+        std::vector<uint2>& ovf = al->h_items;
+        ovf.resize(n_ovf);
+        HIPCHK(hipMemcpy(ovf.data(), al->ovf_items.p, n_ovf * sizeof(uint2), hipMemcpyDeviceToHost));
         uint64_t mx = 0;
-        for (uint32_t r : ovf) mx = std::max(mx, hoff[r + 1] - hoff[r]);
-        // next tier: the 8192-slot LDS table; a read that overflows it again stays there
-        // with twice its hash partitions (k_group_refine: the placed partitions keep their
-        // lists, the rest split in two), while every read's count fits the u8; past that,
-        // HBM tables x4 each round (results do not depend on the tier).  On C4r reads the
-        // HBM tier took 75 ms a launch (r04h) for what refined LDS passes do in a fraction.
+        for (const uint2& it : ovf) mx = std::max(mx, hoff[it.x + 1] - hoff[it.x]);
+        // next tier: the 8192-slot LDS table; an item that overflows it again stays there
+        // split in two (partition p of P is partitions 2p and 2p + 1 of 2P; the read's
+        // other partitions keep their lists), while every item's P stays <= 4096; past
+        // that, HBM tables x4 each round (results do not depend on the tier).  On C4r reads
+        // the HBM tier took 75 ms a launch (r04h) for what split LDS items do in a fraction.
         const bool refine_off = getenv("PBGPU_GROUP_REFINE") && !atoi(getenv("PBGPU_GROUP_REFINE"));  // (tests)
         bool refine = false;
         if (lg == kGroupLdsMaxLog2 && !refine_off) {
           refine = true;
-          for (uint32_t r : ovf) refine &= al->h_parts[r - r0] <= 127;
+          for (const uint2& it : ovf) refine &= (it.y >> 16) <= 2048;
         }
         if (refine) {
-          for (uint32_t r : ovf) al->h_parts[r - r0] *= 2;
+          std::vector<uint2> two;
+          two.reserve(2 * (size_t)n_ovf);
+          for (const uint2& it : ovf) {
+            const uint32_t p = it.y & 0xFFFFu, P = it.y >> 16;
+            two.push_back(group_item(it.x, 2 * p, 2 * P));
+            two.push_back(group_item(it.x, 2 * p + 1, 2 * P));
+          }
+          ovf.swap(two);
+          n_ovf = (uint32_t)ovf.size();
           ++al->acc.group_refines;
         } else {
           lg = lg < kGroupLdsMaxLog2 ? kGroupLdsMaxLog2 : lg + 2;
@@ -2106,12 +2143,10 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
         if (lg > kGroupLdsMaxLog2 && (1ull << (lg - 2)) > 2 * mx + 256)
           throw std::runtime_error("group table growth did not converge");
         al->ovf_list.ensure(n_ovf);
-        HIPCHK(hipMemcpyAsync(al->ovf_list.p, ovf.data(), n_ovf * 4, hipMemcpyHostToDevice, st));
+        al->ovf_items.ensure(n_ovf);  // (this round's overflow: at most its items)
+        O.overflow_items = al->ovf_items.p;
+        HIPCHK(hipMemcpyAsync(al->ovf_list.p, ovf.data(), n_ovf * sizeof(uint2), hipMemcpyHostToDevice, st));
         HIPCHK(hipMemsetAsync(al->counters.p + 3, 0, 4, st));
-        if (refine) {
-          HIPCHK(hipMemcpyAsync(al->nparts.p + r0, al->h_parts.data(), nr, hipMemcpyHostToDevice, st));
-          launch_group_refine(al->ovf_list.p, n_ovf, al->prog.p, st);
-        }
         if (lg <= kGroupLdsMaxLog2) {
           launch_group(v, krec, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0,
                        al->ovf_list.p, n_ovf, lg, nullptr, O, al->stats.p, st);
@@ -2192,14 +2227,14 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
         uint32_t* small = al->perm.p;            // free after the coords order pass consumed it
         uint32_t* big = al->perm.p + nch;
         HIPCHK(hipMemsetAsync(n_redo, 0, 12, st));
-        launch_discard(al->chains.p, list, nre, al->lisl.p, al->slen.p, al->X.p, al->nodes.p, al->nodes32.p, small,
-                       n_redo + 1, big, n_redo + 2, st);
+        launch_discard(al->chains.p, list, nre, al->lisl.p, al->slen.p, al->X.p, al->nodes.p, al->nodes32.p,
+                       al->n32shift.p, small, n_redo + 1, big, n_redo + 2, st);
         HIPCHK(hipMemcpyAsync(nr3, n_redo, 12, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         launch_lis(false, al->chains.p, small, nr3[1], al->slen.p, al->X.p, al->nodes.p, al->pts.p, al->lisl.p, al->lp,
                    1, al->stats.p, st);
         launch_lis(true, al->chains.p, big, nr3[2], al->slen.p, al->X.p, al->nodes32.p, al->pts.p, al->lisl.p, al->lp,
-                   1, al->stats.p, st);
+                   1, al->stats.p, st, al->n32shift.p);  // strands only shrink: placed by the first pass
         cur ^= 1;
         CO.redo = al->redo[cur].p;
         HIPCHK(hipMemsetAsync(n_redo, 0, 4, st));

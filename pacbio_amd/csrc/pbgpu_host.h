@@ -317,14 +317,18 @@ struct pbgpu_aligner {
   dbuf<int32_t> ul, sr_ul;  // unitig lengths; the same resolved along every super-read name (k_sr_ul)
   // per-batch buffers
   dbuf<KRec> krec;
-  dbuf<uint32_t> n_kept, thr, rec_per_read, rec_cursor, order, ovf_reads, counters;
+  dbuf<uint32_t> n_kept, thr, rec_per_read, rec_cursor, order, counters;
+  dbuf<uint2> ovf_items;
+  dbuf<uint32_t> rcur;
   dbuf<uint64_t> sort_scratch;  // k_rec_sort keys of reads above its LDS capacity: 6 words per record
   dbuf<uint64_t> nhits, hit_off, rec_off, huge_elems;
   dbuf<int2> hits;
   dbuf<ChainDesc> chains;
   dbuf<uint32_t> perm;
   dbuf<int2> X, pts;
-  dbuf<uint8_t> nodes, nodes32;  // LNode<uint16_t> / LNode<uint32_t> per hit
+  dbuf<uint8_t> nodes, nodes32;  // LNode<uint16_t> per hit / LNode<uint32_t> per hit of the long strands
+  dbuf<uint32_t> n32shift;       // per strand item: its first node chunk in nodes32 (k_node32_place)
+  dbuf<unsigned long long> n32total;
   dbuf<uint32_t> lisl, hist, slen;
   dbuf<uint32_t> redo[3];
   dbuf<Rec> recs, recs_sorted;
@@ -349,12 +353,10 @@ struct pbgpu_aligner {
   // pbgpu_run: the most bases a batch holds (0 = unknown): the per-base buffers never grow past it
   uint64_t base_cap = 0;
   double chains_per_hit = 1.0 / 80;  // k_group tier estimate (C2: 1.1 x 1/90), refined after every batch
-  dbuf<uint32_t> ovf_list, read_list;
-  std::vector<uint32_t> h_order, h_class, h_small, h_big;  // host scratch of the group stage's read order
-  std::vector<uint8_t> h_parts;
+  dbuf<uint2> ovf_list, read_list;  // k_group work items (group_item): the overflow round's, the launch's
+  std::vector<uint32_t> h_order, h_class;  // host scratch of the group stage's read order
+  std::vector<uint2> h_small, h_big, h_items;
   std::vector<uint64_t> h_hoff;
-  dbuf<uint8_t> nparts;
-  dbuf<uint2> prog;
   // sharded index: per-base k-mer counts of the current batch (SEED_COUNTS, then summed)
   dbuf<uint32_t> gcount;
   dbuf<uint32_t> gcount16;  // the counts packed two per u32 for the all-reduce (count_pack.h)

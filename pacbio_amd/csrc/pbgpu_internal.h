@@ -85,8 +85,9 @@ struct ChainDesc {
 // the read's hit offset):
 //   X    int2  (pb offset, signed sr offset), written by k_group in list order
 //   N16  8 B   LIS node per hit, LNode<uint16_t> (strands of <= 65535 hits)
-//   N32  16 B  LIS node per hit, LNode<uint32_t> (longer strands; allocated
-//              only when a sub-batch has such strands)
+//   N32  16 B  LIS node per hit of the longer strands, LNode<uint32_t>, packed
+//              (hit index + a per-strand shift, k_node32_place; round 5: it was
+//              per hit of the whole sub-batch)
 //   pts  int2  the strand's LIS points X[lis[0..len)) after k_lis
 // LNode: singly linked list of lis_align::compute_L_P (lis_align.hpp:139-182);
 // nxt doubles as the lis index array after the forward pass (--max-match).
@@ -125,12 +126,14 @@ struct GroupOut {
   ChainDesc* chains;
   uint32_t* chain_count;
   uint32_t chain_cap;
-  uint32_t* overflow_reads;
+  uint2* overflow_items;   // the work items whose table overflowed (group_item)
   uint32_t* n_overflow;
-  const uint8_t* nparts;   // per read: super-read hash partitions grouped one after the other (null = 1)
-  uint2* prog;             // per read: {next partition, hits placed} when its table overflowed
-  int resume;              // continue each read from prog[] (overflow relaunch)
+  uint32_t* rcur;          // per read: hits placed so far by its partitions (P > 1 items)
 };
+// k_group work item {read, partition | partitions << 16}: the read's hits whose super-read
+// falls in hash partition `partition` of `partitions` (floor(h * P / 2^32) of the id's hash,
+// so partition p of P is exactly partitions 2p and 2p + 1 of 2P)
+inline __host__ __device__ uint2 group_item(uint32_t r, uint32_t part, uint32_t nparts) { return make_uint2(r, part | nparts << 16); }
 
 struct LisParams {
   uint32_t W;
@@ -209,11 +212,18 @@ constexpr uint32_t GRAPH_NMAX = 8192;  // records of a read traversed with its n
 // names its node j in 16 bits
 constexpr uint32_t GRAPH_NMAX_BIG = 65535;
 // a record in the per-read sorted order (k_graph's ring of sorted positions)
-struct GDesc {
+// A node's descriptor in sorted order, one 64-byte line: what k_graph_edges tests for
+// a pair, the name's first GRAPH_U units included, so a scan past the staged window
+// reads one line a node (round 4: the descriptor plus a scattered load per unit).  The
+// name's offset (G.poff[read base + idx]) is read only for a pair that overlaps.
+constexpr uint32_t GRAPH_U = 8;  // names of at most this many unitigs are matched in registers
+struct alignas(64) GDesc {
   double imp_s, imp_e, err;
-  uint64_t poff;               // its name's units and prefix sums
-  uint32_t idx, nsz, lp_add, pad;
+  uint16_t idx, nsz;           // its record index in the read (< GRAPH_NMAX_BIG), name unitigs
+  uint32_t lp_add;             // nb_mers or sr_cover
+  uint32_t u[GRAPH_U];         // the name's first units in the record's orientation (0 past nsz)
 };
+static_assert(sizeof(GDesc) == 64, "a descriptor is one 64-byte line");
 struct GraphDev {
   const Rec* recs;            // recs_sorted
   const uint64_t* rec_off;    // per read, into recs
@@ -228,6 +238,7 @@ struct GraphDev {
   uint32_t k;                 // -k
   int bases;                  // -b
   uint32_t nmax;              // reads with more records go to the host (<= GRAPH_NMAX_BIG; tests lower it)
+  uint32_t relax_big_min;     // reads with more records relax with their state in HBM (k_graph_relax_big)
   double2* imp;               // per record: implied start, end
   uint64_t* poff;             // per record: its prefix sums' offset (nsz + 1 each)
   uint2* pp;                  // prefix sums along the name: {unitig lengths, info[2u] - info[2u - 1]}

@@ -29,7 +29,7 @@ namespace pbgpu {
 // Optional phase profiling of k_lis (build with -DPBGPU_PROF; tools/prof_lis.py):
 // per-wave s_memtime deltas summed into g_prof.
 #ifdef PBGPU_PROF
-constexpr int PROF_SLOTS = 112;
+constexpr int PROF_SLOTS = 160;
 __device__ unsigned long long g_prof[PROF_SLOTS];
 #define PROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define PROF_ADD(slot, v) do { if (lane_id() == 0) atomicAdd(&g_prof[slot], (unsigned long long)(v)); } while (0)
@@ -556,7 +556,7 @@ template <bool GLOBAL_TABLE, uint32_t B>
 __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_group(IndexView ix, const KRec* __restrict__ krec,
                                                        const uint64_t* __restrict__ roff, const uint32_t* __restrict__ n_kept,
                                                        const uint32_t* __restrict__ thr_in, const uint64_t* __restrict__ hit_off,
-                                                       uint64_t node_base, uint32_t r0, const uint32_t* __restrict__ read_list,
+                                                       uint64_t node_base, uint32_t r0, const uint2* __restrict__ items,
                                                        uint32_t n_list, uint32_t hcap_log2, uint32_t* gtable, GroupOut O,
                                                        unsigned long long* stats) {
   extern __shared__ uint32_t s_dyn[];
@@ -567,13 +567,15 @@ __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_
   __shared__ uint32_t s_off[B], s_scan[B / 64];
   __shared__ uint2 s_np[B];
   __shared__ ulonglong2 s_ptr[B];
-  __shared__ uint32_t s_flag, s_used, s_cbase;
+  __shared__ uint32_t s_flag, s_used, s_cbase, s_pbase;
   if (blockIdx.x >= n_list) return;
   const uint32_t tid = threadIdx.x;
   const uint32_t wave = tid >> 6;
   constexpr uint32_t NW = B / 64;
   constexpr int GU = B == GROUP_BLOCK ? GROUP_U : GROUP_U_BIG;  // windows per wave and step
-  const uint32_t r = read_list ? read_list[blockIdx.x] : r0 + blockIdx.x;
+  // work item: read r, hash partition `part` of P of its super-reads (group_item)
+  const uint2 item = items ? items[blockIdx.x] : make_uint2(r0 + blockIdx.x, 1u << 16);
+  const uint32_t r = item.x, part = item.y & 0xFFFFu, P = item.y >> 16;
   const uint32_t hcap = 1u << hcap_log2;
   // table: key (sr + 1, 0 = empty), fwd count/cursor, bwd count/cursor
   uint32_t* tkey = GLOBAL_TABLE ? gtable + (uint64_t)blockIdx.x * (3u * hcap) : s_dyn;
@@ -586,13 +588,15 @@ __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_
 #define PBGPU_GROUP_BIG_FILL8 6  // the LDS tables' fill limit in eighths (the 8192-slot tier's below)
 #endif
   const uint32_t used_limit = (B == GROUP_BLOCK || GLOBAL_TABLE) ? hcap - hcap / 4 : hcap / 8 * PBGPU_GROUP_BIG_FILL8;
-  // Reads touching many super-reads are grouped in P passes over hash partitions
-  // of the super-read ids; each partition's lists are placed after the previous
-  // ones, so every list is still contiguous and in reference order.
-  const uint32_t P = O.nparts ? O.nparts[r] : 1u;
-  uint32_t part0 = 0, placed = 0, read_chains = 0;
+  // Reads touching many super-reads are grouped over P hash partitions of the
+  // super-read ids, one block a partition (each scans the read's k-mers and keeps
+  // its partition's super-reads); a partition's lists go to the read's next free
+  // hit range (an atomic cursor per read, O.rcur), so every list is still
+  // contiguous and in reference order.  (Round 4 ran a read's partitions one
+  // after the other in one block: with a sub-batch's few hundred long reads
+  // the longest read's block was the launch.)
+  uint32_t read_chains = 0, part_hits = 0;
   uint32_t p0x = 0;  // PBGPU_EXP_P0_NOTABLE: keeps the loads live
-  if (O.resume) { const uint2 pg = O.prog[r]; part0 = pg.x; placed = pg.y; }
   auto part_of = [&](uint32_t sr) -> uint32_t {
     return P == 1 ? 0u : (uint32_t)(((uint64_t)(sr * 0x85EBCA77u) * P) >> 32);
   };
@@ -600,8 +604,7 @@ __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_
   uint64_t pr_setup[2] = {0, 0}, pr_steps[2] = {0, 0}, pr_compact = 0;
   const uint64_t pr_t0 = __builtin_amdgcn_s_memtime();
 #endif
-  for (uint32_t part = part0; part < P; ++part) {
-  uint32_t part_hits = 0;
+  {
   for (uint32_t i = tid; i < hcap; i += B) { tkey[i] = 0; tcf[i] = 0; tcb[i] = 0; }
   if (tid == 0) { s_flag = 0; s_used = 0; }
   if (GLOBAL_TABLE) __threadfence_block();
@@ -826,13 +829,13 @@ __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_
         }
 #ifdef PBGPU_PROF
         __builtin_amdgcn_s_waitcnt(0xc07f);
-        if (B == GROUP_BLOCK_BIG && !GLOBAL_TABLE) {  // slots 41..47: the 8192-slot tier's table work
+        if (B == GROUP_BLOCK_BIG && !GLOBAL_TABLE) {  // slots 112..118: the 8192-slot tier's table work
           const uint64_t gp_t2 = __builtin_amdgcn_s_memtime();
-          PROF_ADD(41 + 3 * pass, gp_t1 - gp_t0);  // first probes
-          PROF_ADD(42 + 3 * pass, gp_t2 - gp_t1);  // collision walks + count atomics (pass 0)
-          PROF_ADD(43 + 3 * pass, gp_walk);        // windows with a collision walk
+          PROF_ADD(112 + 3 * pass, gp_t1 - gp_t0);  // first probes
+          PROF_ADD(113 + 3 * pass, gp_t2 - gp_t1);  // collision walks + count atomics (pass 0)
+          PROF_ADD(114 + 3 * pass, gp_walk);        // windows with a collision walk
           for (int o = 32; o > 0; o >>= 1) gp_mine += (uint32_t)__shfl_xor((int)gp_mine, o, 64);
-          if (pass == 0) PROF_ADD(47, gp_mine);
+          if (pass == 0) PROF_ADD(118, gp_mine);
         }
 #endif
         if constexpr (pass == 1) {
@@ -902,11 +905,10 @@ __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_
 #ifdef PBGPU_PROF
       const uint64_t pr_c = __builtin_amdgcn_s_memtime();
 #endif
-      if (s_flag) {  // table too full: this read continues from this partition with a larger table
+      if (s_flag) {  // table too full: the item goes again, split in two or with a larger table
         if (tid == 0) {
-          O.prog[r] = make_uint2(part, placed);
           const uint32_t o = atomicAdd(O.n_overflow, 1u);
-          O.overflow_reads[o] = r;
+          O.overflow_items[o] = item;
         }
         return;
       }
@@ -924,10 +926,11 @@ __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_
       read_chains += tn;
       if (tid == 0) {
         s_cbase = atomicAdd(O.chain_count, tn);
+        s_pbase = P == 1 ? 0u : atomicAdd(&O.rcur[r], tsum);
         atomicAdd(&stats[ST_CHAINS], (unsigned long long)tn);
       }
       __syncthreads();
-      uint32_t b0 = placed + esum, ci = s_cbase + enn;
+      uint32_t b0 = s_pbase + esum, ci = s_cbase + enn;
       for (uint32_t j = 0; j < per; ++j) {
         const uint32_t sl = tid * per + j;
         if (!tkey[sl]) continue;
@@ -949,12 +952,11 @@ __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_
 #endif
     }
   }
-  placed += part_hits;
-  }  // partitions
+  }  // the partition
   if (p0x == 0x9E3779B9u) O.sink[0] = make_int2((int)p0x, 0);  // practically never
   if (!GLOBAL_TABLE && B == GROUP_BLOCK && tid == 0) {  // per-launch algorithmic counters (bench roofline)
     atomicAdd(&stats[ST_G0_KEPT], (unsigned long long)nk);
-    atomicAdd(&stats[ST_G0_HITS], (unsigned long long)placed);
+    atomicAdd(&stats[ST_G0_HITS], (unsigned long long)part_hits);
     atomicAdd(&stats[ST_G0_CHAINS], (unsigned long long)read_chains);
   }
 #ifdef PBGPU_PROF
@@ -1208,6 +1210,11 @@ DEV bool linear_ok(double a, double df, double ds) {
   return (df <= __dmul_rn(a, ds)) & (ds <= __dmul_rn(a, df));
 }
 
+// k_lis chunk rows (elements a row) for 16- / 32-bit nodes; k_coords' rows
+#ifndef PBGPU_FIT_CH
+#define PBGPU_FIT_CH 8
+#endif
+constexpr int LIS_CH16 = 8, LIS_CH32 = 8, FIT_CH = PBGPU_FIT_CH;
 // lis_align::compute_L_P (lis_align.hpp:139-182) + indices (:190-204),
 // restated literally, one strand per lane: singly linked list L, first
 // acceptable predecessor in list order, insertion after the first node of
@@ -1222,7 +1229,8 @@ __global__ __launch_bounds__(64) void k_lis(const ChainDesc* __restrict__ chains
                                             uint32_t n_items, const uint32_t* __restrict__ slen,
                                             const int2* __restrict__ X, LNode<I>* __restrict__ N,
                                             int2* __restrict__ pts, uint32_t* __restrict__ lisl, LisParams lp,
-                                            int keep_idx, unsigned long long* stats) {
+                                            int keep_idx, unsigned long long* stats,
+                                            const uint32_t* __restrict__ nshift) {
   constexpr uint32_t NONE = 0xFFFFFFFFu;
   constexpr I INONE = (I)~(I)0;
   __shared__ int2 xs[CH * RS];
@@ -1240,8 +1248,13 @@ __global__ __launch_bounds__(64) void k_lis(const ChainDesc* __restrict__ chains
   }
   ChunkGrid<CH> G;
   G.init(base, n);
+  // nshift (32-bit nodes): the strand's nodes live in a compact array of the long
+  // strands alone, from chunk nshift[item] on (k_node32_place): node index = hit
+  // index + sh, sh a multiple of CH so the node rows stay CH-aligned (unsigned
+  // wrap-around arithmetic)
+  const uint64_t sh = (act && nshift) ? (uint64_t)nshift[item] * CH - (base & ~(uint64_t)(CH - 1)) : 0;
   const int2* Xl = X + base;
-  LNode<I>* Nl = N + base;
+  LNode<I>* Nl = N + (base + sh);
   const uint32_t nch = wave_max_u32(G.chunks());
   auto wide = [](I v) -> uint32_t { return v == INONE ? NONE : (uint32_t)v; };
   uint64_t tests = 0;
@@ -1362,7 +1375,7 @@ __global__ __launch_bounds__(64) void k_lis(const ChainDesc* __restrict__ chains
     }
     lds_fence();
     PROF_T(t3);
-    rows_store<CH>(ns, N, row, lo, hi);
+    rows_store<CH>(ns, N, row + sh, lo, hi);
     lds_fence();  // tile rows read before the next chunk overwrites them
     PROF_T(t4);
 #ifdef PBGPU_PROF
@@ -1388,7 +1401,7 @@ __global__ __launch_bounds__(64) void k_lis(const ChainDesc* __restrict__ chains
   if (j >= 0) {
     sweep_rows(j, lo_n, hi_n);
     px.issue(X, G.row((uint32_t)j), lo_n, hi_n);
-    pn.issue(N, G.row((uint32_t)j), lo_n, hi_n);
+    pn.issue(N, G.row((uint32_t)j) + sh, lo_n, hi_n);
   }
   for (; j >= 0; --j) {
     if (!__ballot(need)) break;
@@ -1403,7 +1416,7 @@ __global__ __launch_bounds__(64) void k_lis(const ChainDesc* __restrict__ chains
       const uint32_t lo1 = later ? G.lo((uint32_t)(j - 1)) : 0, hi1 = later ? G.hi((uint32_t)(j - 1)) : 0;
       (void)r1;
       px.issue(X, r1, lo1, hi1);
-      pn.issue(N, r1, lo1, hi1);
+      pn.issue(N, r1 + sh, lo1, hi1);
     }
     lds_fence();
     if (need && (uint64_t)base + s >= row) {
@@ -1890,7 +1903,7 @@ void k_lis_w(const ChainDesc* __restrict__ chains,
   tests = lane == 0 ? tests : 0;
   tests = wave_sum_u64(tests);
   if (lane == 0 && tests) atomicAdd(&stats[ST_LIS_TESTS], (unsigned long long)tests);
-  if (SMAX == LISW_TINY_N && lane == 0 && my_strands) {  // per-launch work of the timed tier (bench roofline)
+  if (SMAX <= LISW_TINY_N && lane == 0 && my_strands) {  // per-launch work of the timed tier (bench roofline)
     atomicAdd(&stats[ST_L0_HITS], (unsigned long long)my_hits);
     atomicAdd(&stats[ST_L0_STRANDS], (unsigned long long)my_strands);
     atomicAdd(&stats[ST_L0_POINTS], (unsigned long long)my_points);
@@ -2321,7 +2334,8 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
 __global__ void k_discard(const ChainDesc* __restrict__ chains, const uint32_t* __restrict__ list, uint32_t n,
                           const uint32_t* __restrict__ lisl, uint32_t* __restrict__ slen, int2* __restrict__ X,
                           const LNode<uint16_t>* __restrict__ N16, const LNode<uint32_t>* __restrict__ N32,
-                          uint32_t* items_small, uint32_t* n_small, uint32_t* items_big, uint32_t* n_big) {
+                          const uint32_t* __restrict__ nshift, uint32_t* items_small, uint32_t* n_small,
+                          uint32_t* items_big, uint32_t* n_big) {
   for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < n; w += gridDim.x * blockDim.x) {
     const uint32_t c = list[w];
     const ChainDesc d = chains[c];
@@ -2331,7 +2345,9 @@ __global__ void k_discard(const ChainDesc* __restrict__ chains, const uint32_t* 
     const uint64_t base = d.hit_base + (dF ? 0 : d.nf);
     const uint32_t nD = slen[item], lD = dF ? lf : lb;
     int2* XD = X + base;
-    auto lis_at = [&](uint32_t t) -> uint32_t { return nD <= LIS_U16_MAX ? N16[base + t].nxt : N32[base + t].nxt; };
+    // k_node32_place's layout: chunk nshift[item] holds the strand's first CH-aligned row
+    const uint64_t base32 = nD <= LIS_U16_MAX ? 0 : (uint64_t)nshift[item] * LIS_CH32 + (base & (LIS_CH32 - 1));
+    auto lis_at = [&](uint32_t t) -> uint32_t { return nD <= LIS_U16_MAX ? N16[base + t].nxt : N32[base32 + t].nxt; };
     uint32_t wpos = 0, li = 0, next = lD ? lis_at(0) : 0xFFFFFFFFu;
     for (uint32_t rpos = 0; rpos < nD; ++rpos) {
       if (rpos == next) { ++li; next = li < lD ? lis_at(li) : 0xFFFFFFFFu; continue; }
@@ -2344,6 +2360,24 @@ __global__ void k_discard(const ChainDesc* __restrict__ chains, const uint32_t* 
   }
 }
 
+// 32-bit LIS nodes for the strands of more than LIS_U16_MAX hits only: each
+// such strand gets the CH-aligned chunks its hit range spans, at an offset from
+// one atomic counter (placement order is immaterial), so the node array holds
+// those strands' hits, not the sub-batch's (it was 16 B per hit of the whole
+// sub-batch: a multi-GB late allocation on the first batch with a long strand).
+template <int CH>
+__global__ void k_node32_place(const ChainDesc* __restrict__ chains, const uint32_t* __restrict__ items, uint32_t n,
+                               const uint32_t* __restrict__ slen, uint32_t* __restrict__ nshift,
+                               unsigned long long* __restrict__ total_chunks) {
+  for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < n; w += gridDim.x * blockDim.x) {
+    const uint32_t item = items[w];
+    const ChainDesc d = chains[item >> 1];
+    const uint64_t base = d.hit_base + ((item & 1) ? d.nf : 0);
+    const uint64_t a0 = base & ~(uint64_t)(CH - 1);
+    const uint64_t nchunks = (base - a0 + slen[item] + CH - 1) / CH;
+    nshift[item] = (uint32_t)atomicAdd(total_chunks, (unsigned long long)nchunks);
+  }
+}
 __global__ void k_init_slen(const ChainDesc* __restrict__ chains, uint32_t n, uint32_t* slen) {
   for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x) {
     const ChainDesc d = chains[c];
@@ -2696,7 +2730,7 @@ void launch_seed(int mode, IndexView ix, const uint8_t* seq, const uint64_t* rof
 }
 
 void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const uint32_t* n_kept, const uint32_t* thr,
-                  const uint64_t* hit_off, uint64_t node_base, uint32_t r0, const uint32_t* read_list, uint32_t n_list,
+                  const uint64_t* hit_off, uint64_t node_base, uint32_t r0, const uint2* read_list, uint32_t n_list,
                   uint32_t hcap_log2, uint32_t* gtable, GroupOut O, unsigned long long* stats, hipStream_t st) {
   if (!n_list) return;
   if (!gtable) {  // LDS table: hcap_log2 <= 13; the 8192-slot table gets a 16-wave block
@@ -2760,17 +2794,6 @@ void launch_sr_ul(const uint32_t* ids, uint64_t n, const int32_t* ul, uint64_t n
   if (n) hipLaunchKernelGGL(k_sr_ul, dim3(1024), dim3(256), 0, st, ids, n, ul, n_ul, out);
 }
 uint64_t group_table_words(uint32_t hcap_log2) { return (uint64_t)3 << hcap_log2; }
-// A read that overflowed the 8192-slot table in partition p of P resumes with 2P
-// partitions from partition 2p.  part_of() maps a super-read to a hash range
-// floor(h * P / 2^32), so partition p of P is exactly partitions 2p and 2p + 1 of 2P:
-// the partitions already placed keep their lists, and the rest split in two.
-__global__ void k_group_refine(const uint32_t* __restrict__ list, uint32_t n, uint2* prog) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < n) { const uint32_t r = list[t]; prog[r].x *= 2; }
-}
-void launch_group_refine(const uint32_t* list, uint32_t n, uint2* prog, hipStream_t st) {
-  if (n) hipLaunchKernelGGL(k_group_refine, dim3((n + 255) / 256), dim3(256), 0, st, list, n, prog);
-}
 
 static uint32_t grid_for(uint32_t n, uint32_t block, uint32_t cap = 65536) {
   uint64_t g = ((uint64_t)n + block - 1) / block;
@@ -2799,22 +2822,26 @@ void launch_chain_order(const uint32_t* lisl, uint32_t n, uint32_t* hist, uint32
   else hipLaunchKernelGGL((k_len_perm<ChainLisLen>), dim3((n + 256 * LEN_PERM_ITEMS - 1) / (256 * LEN_PERM_ITEMS)), dim3(256), 0,
                           st, f, n, cursor, perm);
 }
-#ifndef PBGPU_FIT_CH
-#define PBGPU_FIT_CH 8
-#endif
-constexpr int LIS_CH16 = 8, LIS_CH32 = 8, FIT_CH = PBGPU_FIT_CH;
 void launch_lis(bool big_nodes, const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen,
                 const int2* X, void* N, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx,
-                unsigned long long* stats, hipStream_t st) {
+                unsigned long long* stats, hipStream_t st, const uint32_t* nshift) {
   if (!n_items) return;
   const dim3 grid((n_items + 63) / 64);
   if (big_nodes)
     hipLaunchKernelGGL((k_lis<uint32_t, LIS_CH32>), grid, dim3(64), 0, st, chains, items, n_items, slen, X,
-                       (LNode<uint32_t>*)N, pts, lisl, lp, keep_idx, stats);
+                       (LNode<uint32_t>*)N, pts, lisl, lp, keep_idx, stats, nshift);
   else
     hipLaunchKernelGGL((k_lis<uint16_t, LIS_CH16>), grid, dim3(64), 0, st, chains, items, n_items, slen, X,
-                       (LNode<uint16_t>*)N, pts, lisl, lp, keep_idx, stats);
+                       (LNode<uint16_t>*)N, pts, lisl, lp, keep_idx, stats, (const uint32_t*)nullptr);
 }
+// returns the chunk count through *total (device); node index = hit index + nshift[item]
+void launch_node32_place(const ChainDesc* chains, const uint32_t* items, uint32_t n, const uint32_t* slen,
+                         uint32_t* nshift, unsigned long long* total, hipStream_t st) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_node32_place<LIS_CH32>, dim3(grid_for(n, 256)), dim3(256), 0, st, chains, items, n, slen,
+                     nshift, total);
+}
+uint32_t node32_chunk() { return LIS_CH32; }
 constexpr uint32_t LISW_TINY = LISW_TINY_N, LISW_SMALL = 511, LISW_LARGE = 4095;
 #ifndef PBGPU_LIS_LANE_MAX
 #define PBGPU_LIS_LANE_MAX 8
@@ -2827,7 +2854,7 @@ void launch_lis_lane(const ChainDesc* chains, const uint32_t* items, uint32_t n_
   if (!lp.ordered)
     hipLaunchKernelGGL((k_order_tiny<PBGPU_LIS_LANE_MAX>), dim3((n_items + 255) / 256), dim3(256), 0, st, chains, items,
                        n_items, slen, X);
-  launch_lis(false, chains, items, n_items, slen, X, N16, pts, lisl, lp, keep_idx, stats, st);
+  launch_lis(false, chains, items, n_items, slen, X, N16, pts, lisl, lp, keep_idx, stats, st, nullptr);
 }
 uint32_t lis_lane_max() { return PBGPU_LIS_LANE_MAX; }
 // CU count of the current device, cached per device (aligners on several
@@ -2880,11 +2907,12 @@ void launch_coords(IndexView ix, AlignParamsDev P, const ChainDesc* chains, cons
   hipLaunchKernelGGL((k_coords<FIT_CH>), dim3((n + 63) / 64), dim3(64), 0, st, ix, P, chains, list, n, roff, emit, O);
 }
 void launch_discard(const ChainDesc* chains, const uint32_t* list, uint32_t n, const uint32_t* lisl, uint32_t* slen,
-                    int2* X, const void* N16, const void* N32, uint32_t* items_small, uint32_t* n_small,
-                    uint32_t* items_big, uint32_t* n_big, hipStream_t st) {
+                    int2* X, const void* N16, const void* N32, const uint32_t* nshift, uint32_t* items_small,
+                    uint32_t* n_small, uint32_t* items_big, uint32_t* n_big, hipStream_t st) {
   if (!n) return;
   hipLaunchKernelGGL(k_discard, dim3(grid_for(n, 256)), dim3(256), 0, st, chains, list, n, lisl, slen, X,
-                     (const LNode<uint16_t>*)N16, (const LNode<uint32_t>*)N32, items_small, n_small, items_big, n_big);
+                     (const LNode<uint16_t>*)N16, (const LNode<uint32_t>*)N32, nshift, items_small, n_small,
+                     items_big, n_big);
 }
 uint32_t len_buckets() { return NLB; }
 void launch_strand_order(const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen, int2* X,
@@ -3177,6 +3205,20 @@ DEV uint32_t graph_unit(const GraphDev& G, uint32_t sr, uint32_t nsz, bool rev, 
   return rev ? G.units[o + nsz - 1 - u] ^ 1u : G.units[o + u];
 }
 DEV uint32_t graph_nsz(const GraphDev& G, uint32_t sr) { return (uint32_t)(G.noff[sr + 1] - G.noff[sr]); }
+// node p of a read (record b + i) as k_graph_edges reads it (k_graph_prep wrote its units)
+DEV void graph_write_desc(const GraphDev& G, uint64_t at, uint64_t b, uint32_t i) {
+  const Rec& R = G.recs[b + i];
+  const double2 m = G.imp[b + i];
+  const uint64_t po = G.poff[b + i];
+  const uint32_t ns = graph_nsz(G, R.sr);
+  GDesc d;
+  d.imp_s = m.x; d.imp_e = m.y; d.err = R.avg_err;
+  d.idx = (uint16_t)i; d.nsz = (uint16_t)ns;
+  d.lp_add = G.bases ? R.sr_cover : (uint32_t)R.nb_mers;
+#pragma unroll
+  for (uint32_t u = 0; u < GRAPH_U; ++u) d.u[u] = u < ns ? G.ounits[po + u] : 0u;
+  G.desc[at] = d;
+}
 constexpr uint32_t GRAPH_PREP_U = 8;  // names of at most this many unitigs: loads batched in registers
 __global__ void k_graph_sizes(GraphDev G, uint64_t n, uint32_t* sizes) {
   for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < n; q += (uint64_t)gridDim.x * blockDim.x)
@@ -3297,11 +3339,7 @@ __global__ __launch_bounds__(GRAPH_SORT_BLOCK) void k_graph_sort(GraphDev G, uin
   __syncthreads();
   bitonic_keys<GRAPH_SORT_BLOCK>(s_hi, s_lo, s_ex, np2);
   for (uint32_t p = threadIdx.x; p < n; p += GRAPH_SORT_BLOCK) {
-    const uint32_t i = s_ex[p];
-    const Rec& R = G.recs[b + i];
-    const double2 m = G.imp[b + i];
-    G.desc[b + p] = GDesc{m.x, m.y, R.avg_err, G.poff[b + i], i, graph_nsz(G, R.sr),
-                          G.bases ? R.sr_cover : (uint32_t)R.nb_mers, 0u};
+    graph_write_desc(G, b + p, b, s_ex[p]);
   }
 }
 // The traversal (overlap_graph.cc:7-59) in two phases.  Everything the reference
@@ -3322,7 +3360,6 @@ __global__ __launch_bounds__(GRAPH_SORT_BLOCK) void k_graph_sort(GraphDev G, uin
 // (ecnt); a node with more (2 in 28k on C2) is listed, with its region past the
 // block.  OVF: a wave per listed node runs its scan again (from HBM) and writes the
 // edges past its block there.
-constexpr uint32_t GRAPH_U = 8;  // names of at most this many unitigs are matched in registers
 constexpr uint32_t GRAPH_NMAX_K = GRAPH_NMAX;  // reads of more records: k_graph_relax_big (state in HBM)
 constexpr uint32_t GRAPH_ROOT_BITS = 13;  // k_graph_relax matches roots by this many bits
 static_assert(GRAPH_NMAX_K <= (1u << GRAPH_ROOT_BITS) && GRAPH_NMAX_K < 0x8000u,
@@ -3376,8 +3413,9 @@ template <bool OVF>
 __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n_recs, uint64_t n_ovf) {
   __shared__ double s_is[GE_SLOTS], s_ie[GE_SLOTS], s_er[GE_SLOTS];
   __shared__ uint32_t s_meta[GE_SLOTS], s_lpa[GE_SLOTS], s_po[GE_SLOTS];
-  __shared__ double s_rl[GE_NODES];    // node i's read length and scan end: the window's
-  __shared__ uint32_t s_end[GE_NODES];  // nodes only (OVF: WAVES <= GE_NODES slots)
+  __shared__ double s_rl[GE_NODES];    // node i's read length, scan end and read base: the
+  __shared__ uint32_t s_end[GE_NODES];  // window's nodes only (OVF: WAVES <= GE_NODES slots)
+  __shared__ uint32_t s_rb[GE_NODES];
   __shared__ uint32_t s_u[GRAPH_U * GE_SLOTS];  // [u * GE_SLOTS + slot]
   constexpr uint32_t WAVES = GE_BLOCK / 64;
   // OVF: slot t holds listed node blockIdx.x * WAVES + t; nothing else is staged
@@ -3394,16 +3432,18 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
     // earlier batch's words there), so nothing of it is read; its slots are never a j of a
     // device read's scan (scans stop at their read's end) and its nodes scan nothing
     const bool dev = graph_on_device(G, n);
-    GDesc d{0.0, 0.0, 0.0, 0u, 0u, 0u, 0u, 0u};
+    GDesc d{};
     if (dev) d = G.desc[q];
     s_is[t] = d.imp_s; s_ie[t] = d.imp_e; s_er[t] = d.err;
-    s_meta[t] = d.idx | (d.nsz << 16); s_lpa[t] = d.lp_add; s_po[t] = (uint32_t)d.poff;  // < 2^32 (host check)
+    s_meta[t] = d.idx | ((uint32_t)d.nsz << 16); s_lpa[t] = d.lp_add;
+    s_po[t] = dev ? (uint32_t)G.poff[e - n + d.idx] : 0u;  // < 2^32 (host check)
     if (t < GE_NODES) {
       s_rl[t] = (double)(G.roff[r + 1] - G.roff[r]);
       s_end[t] = dev ? (uint32_t)e : (uint32_t)(q + 1);  // a read left to the host: no scan
+      s_rb[t] = (uint32_t)(e - n);  // (record indices < 2^32: rec_cap)
     }
 #pragma unroll
-    for (uint32_t u = 0; u < GRAPH_U; ++u) s_u[u * GE_SLOTS + t] = (dev & (u < d.nsz)) ? G.ounits[d.poff + u] : 0u;
+    for (uint32_t u = 0; u < GRAPH_U; ++u) s_u[u * GE_SLOTS + t] = d.u[u];
   }
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
@@ -3413,6 +3453,7 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
     const uint64_t q = OVF ? G.ovf_list[q0 + ti] : q0 + ti;
     const uint32_t qe = s_end[ti];
     const double ie_i = s_ie[ti], err_i = s_er[ti];
+    const uint32_t rb_i = s_rb[ti];  // node i's read base: j's name offset is G.poff[rb_i + idx_j]
     uint32_t cnt = 0;
 #ifdef PBGPU_PROF
     uint64_t ge_seen = 0, ge_far = 0, ge_cand = 0;
@@ -3426,22 +3467,35 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
       auto unit_i = [&](uint32_t t) -> uint32_t { return G.ounits[po_i + t]; };
       uint2* const out = OVF ? G.eovf : G.edges;
       const uint64_t ob = OVF ? G.eoff[q] - GRAPH_EBLK : q * GRAPH_EBLK;  // (mod 2^64)
+      // the skip bits of blocks [ck_b0, ck_b0 + 64) for node i (set: not skippable), kept
+      // across chunks: a test is one bmax load a lane, needed again only past those blocks
+      uint64_t ck_b0 = 0, ck_m = 0;
+      bool ck_set = false;
       for (uint64_t j0 = q + 1; j0 < qe; j0 += 64) {
         // Fast-forward over whole 64-position blocks in which every node is skipped for node i
-        // (imp_s <= 1, or not advancing: imp_e_i > imp_e_j + 31), 64 blocks a test: none of them
-        // can give an edge or the break.  On repeat-rich reads most of a long node's scan is
-        // nodes it contains (C4r: 73% of 252 G scanned positions were skips).
+        // (imp_s <= 1, or not advancing: imp_e_i > imp_e_j + 31): none of them can give an
+        // edge or the break.  On repeat-rich reads most of a long node's scan is nodes it
+        // contains (C4r: 73% of 252 G scanned positions were skips).
         {
-          const uint64_t b0 = j0 >> 6, bb = b0 + lane;
-          const bool in = (bb << 6) < qe;
-          const double m = in ? G.bmax[bb] : 0.0;
-          const uint64_t nsk = __ballot(!(in & (ie_i > __dadd_rn(m, 31.0))));
-          if (!(nsk & 1ull)) {  // block b0 (holding j0) is skipped: jump to the first one that is not
-            if (!nsk) { j0 = (b0 + 64) << 6; if (j0 >= qe) break; j0 -= 64; continue; }
-            const uint64_t nb = b0 + (uint64_t)__ffsll((unsigned long long)nsk) - 1;
-            j0 = nb << 6;
-            if (j0 >= qe) break;
+          uint64_t b0 = j0 >> 6;
+          for (;;) {
+            if (!ck_set || b0 - ck_b0 >= 64) {  // (b0 never decreases)
+              ck_set = true;
+              ck_b0 = b0;
+              const uint64_t bb = b0 + lane;
+              const bool in = (bb << 6) < qe;
+              const double m = in ? G.bmax[bb] : 0.0;
+              ck_m = __ballot(!(in & (ie_i > __dadd_rn(m, 31.0))));
+            }
+            const uint64_t nsk = ck_m >> (b0 - ck_b0);
+            if (nsk & 1ull) break;  // block b0 is scanned
+            if (!nsk) { b0 = ck_b0 + 64; continue; }  // all 64 skipped: test the next 64
+            b0 += (uint64_t)__ffsll((unsigned long long)nsk) - 1;  // the first block that is not
+            j0 = b0 << 6;
+            break;
           }
+          if ((b0 << 6) > j0) j0 = b0 << 6;
+          if (j0 >= qe) break;
         }
         const uint64_t j = j0 + lane;
         const bool act = j < qe;
@@ -3451,17 +3505,17 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
         // skip / break ballot, made the C4r graph stage 240 -> 316 ms: a second round trip
         // on the critical path costs more than the loads it saves)
         double is_j, ie_j, er_j;
-        uint32_t mj, lpa_j, po_j, bu[GRAPH_U];
-        if (!OVF && sj < ns) {
-          is_j = s_is[sj]; ie_j = s_ie[sj]; er_j = s_er[sj]; mj = s_meta[sj]; lpa_j = s_lpa[sj]; po_j = s_po[sj];
+        uint32_t mj, lpa_j, bu[GRAPH_U];
+        const bool staged = !OVF && sj < ns;
+        if (staged) {
+          is_j = s_is[sj]; ie_j = s_ie[sj]; er_j = s_er[sj]; mj = s_meta[sj]; lpa_j = s_lpa[sj];
 #pragma unroll
           for (uint32_t u = 0; u < GRAPH_U; ++u) bu[u] = s_u[u * GE_SLOTS + sj];
         } else {
-          const GDesc dj = G.desc[act ? j : q];
-          is_j = dj.imp_s; ie_j = dj.imp_e; er_j = dj.err; mj = dj.idx | (dj.nsz << 16); lpa_j = dj.lp_add;
-          po_j = (uint32_t)dj.poff;
+          const GDesc dj = G.desc[act ? j : q];  // one 64-byte line
+          is_j = dj.imp_s; ie_j = dj.imp_e; er_j = dj.err; mj = dj.idx | ((uint32_t)dj.nsz << 16); lpa_j = dj.lp_add;
 #pragma unroll
-          for (uint32_t u = 0; u < GRAPH_U; ++u) bu[u] = u < dj.nsz ? G.ounits[dj.poff + u] : 0u;
+          for (uint32_t u = 0; u < GRAPH_U; ++u) bu[u] = dj.u[u];
         }
         const bool skip = (is_j <= 1.0) | (ie_i > __dadd_rn(ie_j, 31.0));  // off the 5' end | not advancing
         const double position_len = __dadd_rn(ie_i, -is_j);
@@ -3473,6 +3527,9 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
         const bool cand = act & !skip & (lane < fb) & (sa >= 2) & (sb >= 2);
         bool edge = false;
         int32_t nb = 0, common = 0;
+        auto po_of_j = [&]() -> uint32_t {
+          return staged ? s_po[sj] : (uint32_t)G.poff[rb_i + (mj & 0xFFFFu)];
+        };
         if (cand) {
           bool same;
           if ((sa <= GRAPH_U) & (sb <= GRAPH_U)) {
@@ -3488,6 +3545,7 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
               default: name_overlap_reg<8>(a, bu, sb, nb, same); break;
             }
           } else {
+            const uint32_t po_j = po_of_j();
             auto unit_j = [&](uint32_t qq) -> uint32_t { return G.ounits[po_j + qq]; };
             const uint32_t u0 = unit_j(0);
             const int t0 = (int)sa - (int)sb + 1;
@@ -3504,7 +3562,7 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
             }
           }
           if (nb && !same) {
-            const uint2 v = G.pp[po_j + (uint32_t)nb];
+            const uint2 v = G.pp[po_of_j() + (uint32_t)nb];
             const int32_t uol = (int32_t)(v.x - (uint32_t)(nb - 1) * km1);
             common = (int32_t)v.y;
             const double duol = (double)uol;
@@ -3532,8 +3590,8 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
       }
     }
 #ifdef PBGPU_PROF
-    if (!OVF) {  // slots 33..35: positions scanned, of them past the staged window, candidates (name test)
-      PROF_ADD(33, ge_seen); PROF_ADD(34, ge_far); PROF_ADD(35, ge_cand);
+    if (!OVF) {  // slots 128..130: positions scanned, of them past the staged window, candidates (name test)
+      PROF_ADD(128, ge_seen); PROF_ADD(129, ge_far); PROF_ADD(130, ge_cand);
     }
 #endif
     if (!OVF && lane == 0) {
@@ -3564,7 +3622,7 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
 // a > b exactly when their keys are), NaN as RANK_NAN, which compares false.
 template <uint32_t NM>
 DEV bool graph_relax_tier(const GraphDev& G, uint32_t n) {
-  if (!graph_on_device(G, n)) return false;
+  if (!graph_on_device(G, n) || n > G.relax_big_min) return false;
   return (n <= NM && n > NM / 2) || (NM == GRAPH_RELAX_MIN && n <= NM);
 }
 template <uint32_t NM>
@@ -3764,6 +3822,9 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
 // record) instead of LDS, one block per such read.
 constexpr uint32_t GRAPH_BIG_BLOCK = 1024;
 DEV bool graph_big(const GraphDev& G, uint32_t n) { return n > GRAPH_NMAX && graph_on_device(G, n); }
+// the relaxation with its state in HBM: the reads past the LDS tiers, and those past
+// G.relax_big_min (their blocks, no LDS, share a CU where an LDS tier's block takes it)
+DEV bool graph_relax_big(const GraphDev& G, uint32_t n) { return n > G.relax_big_min && graph_on_device(G, n); }
 // k_graph_sort for one big read: the bitonic network over np2 <= 2n entries of {hi, lo, ex}
 __global__ __launch_bounds__(GRAPH_BIG_BLOCK) void k_graph_sort_big(GraphDev G, uint32_t n_reads) {
   const uint32_t r = blockIdx.x;
@@ -3787,11 +3848,7 @@ __global__ __launch_bounds__(GRAPH_BIG_BLOCK) void k_graph_sort_big(GraphDev G, 
   __syncthreads();
   bitonic_keys<GRAPH_BIG_BLOCK>(hi, lo, ex, np2);
   for (uint32_t p = threadIdx.x; p < n; p += GRAPH_BIG_BLOCK) {
-    const uint32_t i = (uint32_t)ex[p];
-    const Rec& R = G.recs[b + i];
-    const double2 m = G.imp[b + i];
-    G.desc[b + p] = GDesc{m.x, m.y, R.avg_err, G.poff[b + i], i, graph_nsz(G, R.sr),
-                          G.bases ? R.sr_cover : (uint32_t)R.nb_mers, 0u};
+    graph_write_desc(G, b + p, b, (uint32_t)ex[p]);
   }
 }
 // k_graph_relax for one big read, node state in HBM (8 u32 arrays of n, then the imp_s
@@ -3806,7 +3863,7 @@ __global__ __launch_bounds__(128) void k_graph_relax_big(GraphDev G, uint32_t n_
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint64_t b = G.rec_off[r];
   const uint32_t n = (uint32_t)(G.rec_off[r + 1] - b);
-  if (!graph_big(G, n)) return;
+  if (!graph_relax_big(G, n)) return;
   int32_t* s_lp = reinterpret_cast<int32_t*>(G.scratch + 6 * b);
   int32_t* s_lun = s_lp + n;
   int32_t* s_lst = s_lun + n;
@@ -4635,17 +4692,20 @@ hipError_t launch_graph_relax(const GraphDev& G, uint32_t n_reads, uint64_t n_re
   if (e != hipSuccess) return e;
   // (tiers above the longest read are not launched; the top one also marks the reads
   // left to the host, so it runs whenever a read is past the device cap)
-  if (max_n > GRAPH_NMAX && G.nmax > GRAPH_NMAX)
+  if (max_n > G.relax_big_min && G.nmax > G.relax_big_min)
     hipLaunchKernelGGL(k_graph_relax_big, dim3(n_reads), dim3(128), 0, side, G, n_reads);
-  if (max_n > GRAPH_NMAX / 2 || max_n > G.nmax)
+  // an LDS tier runs when it has reads: some read past NM / 2 records and not past
+  // relax_big_min (an empty launch of a tier's blocks still costs ~1.4 ms per 50k reads)
+  auto tier_has = [&](uint32_t nm) { return max_n > nm / 2 && G.relax_big_min > nm / 2; };
+  if (tier_has(GRAPH_NMAX) || max_n > G.nmax)
     hipLaunchKernelGGL(k_graph_relax<GRAPH_NMAX>, dim3(n_reads), dim3(128), 0, side, G, n_reads);
-  if (max_n > GRAPH_NMAX / 4)
+  if (tier_has(GRAPH_NMAX / 2))
     hipLaunchKernelGGL(k_graph_relax<GRAPH_NMAX / 2>, dim3(n_reads), dim3(128), 0, side, G, n_reads);
-  if (max_n > GRAPH_NMAX / 8)
+  if (tier_has(GRAPH_NMAX / 4))
     hipLaunchKernelGGL(k_graph_relax<GRAPH_NMAX / 4>, dim3(n_reads), dim3(128), 0, side2, G, n_reads);
   if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
   if ((e = hipEventRecord(join2, side2)) != hipSuccess) return e;
-  if (max_n > GRAPH_RELAX_MIN)
+  if (tier_has(GRAPH_NM_SMALL))
     hipLaunchKernelGGL(k_graph_relax<GRAPH_NM_SMALL>, dim3(n_reads), dim3(128), 0, st, G, n_reads);
   hipLaunchKernelGGL(k_graph_relax<GRAPH_RELAX_MIN>, dim3(n_reads), dim3(128), 0, st, G, n_reads);
   if ((e = hipStreamWaitEvent(st, join, 0)) != hipSuccess) return e;

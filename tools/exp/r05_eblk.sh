@@ -1,0 +1,28 @@
+# round 5: edge blocks of 32 vs 64 (graph time, overflow nodes); cmr C4r / C2 late allocations; LIS tests
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+O=gpurun_out/r05s
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread "tests/test_gpu_edge.py::test_long_strands" tests/test_gpu_parity.py > ${O}_tests.log 2>&1 || { tail -30 ${O}_tests.log; exit 1; }
+tail -1 ${O}_tests.log
+for lib in libpbgpu.so libpbgpu_eblk32.so; do
+  for wl in "C2 50000" "C4r 20000"; do
+    set -- $wl
+    echo "== $lib $1" >> ${O}_eblk.txt
+    PBGPU_LIB=pacbio_amd/$lib timeout -k 10 300 python -u tools/prof_graph_gpu.py --workload $1 --reads $2 >> ${O}_eblk.txt 2>&1 || exit 1
+  done
+done
+for w in C2:50000 C4r:20000; do
+  n=${w#*:}; w=${w%:*}; D=/tmp/cmr_$w
+  timeout -k 10 300 python -u -c "
+import sys; sys.path.insert(0, '.')
+from tools.synth import Dataset
+ds = Dataset('$w', seed=42, threads=16, n_pb=$n); ds.write('$D'); ds.close()" || exit 1
+  F="-s 1M -m 17 --psa-min 13 -k 31 -l $D/ul.txt -B 15 --max-count 5000 --stretch-cap 10000 -t 16 -r $D/sr.fa -p $D/pb.fa --timing"
+  CMR=pacbio_amd/bin/create_mega_reads
+  timeout -k 10 120 $CMR $F -o $D/mr > /dev/null 2> /dev/null || exit 1
+  for i in 1 2; do
+    echo "== $w run $i" >> ${O}_cmr.txt
+    PBGPU_DEBUG_STALL=2 PBGPU_DEBUG_BUFFERS=1 timeout -k 10 120 $CMR $F -o $D/mr > /dev/null 2>> ${O}_cmr.txt || exit 1
+  done
+done

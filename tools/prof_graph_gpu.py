@@ -30,10 +30,10 @@ def main():
     al.align_resident(rr)
     L = pbgpu.lib()
     f = getattr(L, "pbgpu_debug_prof", None)
-    buf = (C.c_ulonglong * 112)()
+    buf = (C.c_ulonglong * 160)()
     if f is not None:
         f.argtypes = [C.POINTER(C.c_ulonglong), C.c_int, C.c_int]
-        f(buf, 112, 1)
+        f(buf, 160, 1)
     al.reset_stats()
     t = time.time()
     al.align_resident(rr)
@@ -46,14 +46,14 @@ def main():
           f"{st['graph_host_reads']} left to the host graph (> 8192 records): "
           f"{100.0 * st['graph_host_reads'] / max(1, a.reads):.3f}%")
     if f is not None:
-        f(buf, 112, 1)
+        f(buf, 160, 1)
         for tier, base in (("<= 1024 records", 80), ("> 1024 records", 96)):
             v = list(buf)[base:base + 8]
             nn, nb = max(1, v[6]), max(1, v[7])
             print(f"k_graph_relax {tier}: blocks {v[7]}, nodes {v[6]}, chunks {v[1]} ({v[1] / nn:.2f} a node); "
                   f"ticks a node: paths wave {v[2] / nn:.0f} (chunk work {v[0] / nn:.0f}), "
                   f"union wave {v[5] / nn:.0f} (finds {v[3] / nn:.0f}, merges {v[4] / nn:.0f})")
-        e = list(buf)[33:36]
+        e = list(buf)[128:131]
         print(f"k_graph_edges: positions scanned {e[0]} ({e[0] / max(1, st['graph_records']):.1f} a node), past the "
               f"staged window {e[1]}, name tests {e[2]}")
         w = list(buf)[88:96]

@@ -26,7 +26,7 @@ def main():
     rr = al.upload(blob=blob, offsets=off)
     al.align_resident(rr)
     L = pbgpu.lib()
-    buf = (C.c_ulonglong * 112)()
+    buf = (C.c_ulonglong * 160)()
     f = getattr(L, "pbgpu_debug_prof", None)  # -DPBGPU_PROF builds only
     if f is None:
         al.reset_stats()
@@ -38,11 +38,11 @@ def main():
               f"records {st['ms_records']:.1f}; group refines {st['group_refines']}, HBM-table reads {st['group_hbm_reads']}")
         return
     f.argtypes = [C.POINTER(C.c_ulonglong), C.c_int, C.c_int]
-    f(buf, 112, 1)
+    f(buf, 160, 1)
     al.reset_stats()
     al.align_resident(rr)
     pbgpu.device_synchronize(0)
-    f(buf, 112, 1)
+    f(buf, 160, 1)
     st = al.stats()
     names = ["row_load_issue", "lds_fetch", "element_loop", "row_store", "sweep", "wave_total", "chunks", "waves"]
     v = list(buf)[:8]
@@ -61,9 +61,9 @@ def main():
           f"records {st['ms_records']:.1f}")
     print(f"counters: hits {st['n_hits']}, lis tests {st['n_lis_tests']}, chains {st.get('n_chains')}, "
           f"records {st.get('n_records')}, bases {sum(len(s) for s in ds.pb_seqs()) if a.reads <= 20000 else 'n/a'}")
-    print(f"k_group 8192-slot tier table work (wave ticks): pass 0 first probes {g[41]}, walks+counts {g[42]}, "
-          f"windows walking {g[43]}; pass 1 first probes {g[44]}, walks {g[45]}, windows walking {g[46]}; "
-          f"mine hits (pass 0) {g[47]}")
+    print(f"k_group 8192-slot tier table work (wave ticks): pass 0 first probes {g[112]}, walks+counts {g[113]}, "
+          f"windows walking {g[114]}; pass 1 first probes {g[115]}, walks {g[116]}, windows walking {g[117]}; "
+          f"mine hits (pass 0) {g[118]}")
     for label, sb in (("k_group 2048-slot tier", 8), ("k_group 8192-slot tier", 14)):
         blocks = max(1, g[sb + 5])
         print(f"{label}: blocks={g[sb + 5]} (ms: tier0 {st['kernel_ms']['k_group']:.2f})")
