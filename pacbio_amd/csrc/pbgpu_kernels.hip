@@ -1921,9 +1921,10 @@ void k_lis_w(const ChainDesc* __restrict__ chains,
 typedef __attribute__((address_space(3))) int32_t lds_i32;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
-// kmers_info of names with at most INFO_LDS_UNITIGS unitigs is accumulated in LDS (k_coords)
+// k_coords caches the unitig lengths of names of at most INFO_LDS_UNITIGS unitigs in LDS
 constexpr uint32_t INFO_LDS_UNITIGS = 8, INFO_LDS = 2 * INFO_LDS_UNITIGS - 1;
-template <typename T>
+// CT: the unitig-length cache's element type (lds_i32 in k_coords)
+template <typename T, typename CT = T>
 struct KmersInfo {
   const int32_t* lens;
   uint32_t nsz;
@@ -1932,7 +1933,8 @@ struct KmersInfo {
   T* mers;    // element i at mers[i * stride]
   T* bases;
   uint32_t stride;
-  T* cl;  // optional cache: length of unitig i at cl[i * stride], UL_INVALID if unusable
+  CT* cl;  // optional cache: length of unitig i at cl[i * cstride]
+  uint32_t cstride;
   uint32_t cunitig;
   int32_t cend, prev_pos;
   // Pending increments kept in registers: element 2c (pm, pb: the current
@@ -1945,27 +1947,27 @@ struct KmersInfo {
   static constexpr int32_t UL_INVALID = INT32_MIN;
   DEV int32_t ulen_direct(uint32_t i) const { return i >= nsz ? UL_INVALID : lens[rev ? nsz - 1 - i : i]; }
   DEV int32_t ulen(uint32_t i) const {
-    if (cl) return i < nsz ? cl[i * stride] : UL_INVALID;
+    if (cl) return i < nsz ? cl[i * cstride] : UL_INVALID;
     return ulen_direct(i);
   }
   DEV T& M(uint32_t i) { return mers[i * stride]; }
   DEV T& B(uint32_t i) { return bases[i * stride]; }
-  // x[i] += v; in LDS a no-return atomic add (each lane owns its column): no
-  // read to wait for -- the arrays are read once, after the last point
+  // x[i] += v as a no-return atomic add (each lane owns its elements): no read to
+  // wait for -- the arrays are not read back here
   DEV void acc(T* x, uint32_t i, int32_t v) {
     if constexpr (std::is_same<T, lds_i32>::value) __atomic_fetch_add(x + i * stride, v, __ATOMIC_RELAXED);
-    else x[i * stride] += v;
+    else __hip_atomic_fetch_add(x + i * stride, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   DEV void init(const AlignParamsDev& P, const int32_t* lens_, uint32_t nsz_, bool rev_, T* m, T* b,
-                uint32_t stride_, T* cache = nullptr) {
+                uint32_t stride_, CT* cache = nullptr, uint32_t cstride_ = 0) {
     lens = lens_; nsz = nsz_; rev = rev_; k = (int32_t)P.k; uk = (int32_t)P.unitigs_k;
-    mers = m; bases = b; stride = stride_; cl = nullptr;
+    mers = m; bases = b; stride = stride_; cl = nullptr; cstride = cstride_;
     if (cache) {  // nsz <= INFO_LDS_UNITIGS: independent loads, issued together
       int32_t v[INFO_LDS_UNITIGS];
 #pragma unroll
       for (uint32_t i = 0; i < INFO_LDS_UNITIGS; ++i) v[i] = i < nsz ? ulen_direct(i) : 0;
 #pragma unroll
-      for (uint32_t i = 0; i < INFO_LDS_UNITIGS; ++i) if (i < nsz) cache[i * stride] = v[i];
+      for (uint32_t i = 0; i < INFO_LDS_UNITIGS; ++i) if (i < nsz) cache[i * cstride] = v[i];
       cl = cache;
     }
     const int32_t l0 = ulen(0);
@@ -2217,7 +2219,7 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
   KmersInfo<lds_i32> KI;
   if (info_lds)
     KI.init(P, P.sr_ul + u0, nsz, (R.flags & 2u) != 0, (lds_i32*)(im + lane), (lds_i32*)(ib + lane), 64,
-            (lds_i32*)(iul + lane));
+            (lds_i32*)(iul + lane), 64);
   auto info_pos = [&](int32_t so) -> int32_t {
     const int32_t pos = fwd_align ? so : (int32_t)(R.ql + (uint32_t)so - k + 2u);
     return pos < 0 ? -pos : pos;
@@ -2256,13 +2258,21 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
     a = __ddiv_rn(L.CXY, L.VX); b = __ddiv_rn(L.NB, L.VX);
     R.stretch = a; R.offset = b;
   }
+  R.rs = first.x;
+  R.re = (int32_t)((uint32_t)prev.x + k - 1u);
+  R.qs = first.y; R.qe = prev.y;
+  // the filters read neither the average error nor kmers_info (coords_finish), so they run
+  // before pass 2 and a dropped chain skips it
+  const bool keep = act && nl > 0 && coords_finish(P, rl, R);
   double err = 0;
   // kmers_info (LDS case) rides this pass, not the fit's: the fit's registers are dead
-  // here, and the pass then also runs for single-point chains (-0.6 ms, r04b)
+  // here, and the pass then also runs for single-point chains (-0.6 ms, r04b).  (Round 5
+  // tried the arrays in HBM, allocated before this pass, to free the 7.7 KB of LDS a wave
+  // that limits the kernel's occupancy: 21.0 -> 23.9 ms, the atomics cost more.)
 #ifdef PBGPU_EXP_NO_PASS2
   LS.run(O.pts, 0, ps, [&](const int2 p) {
 #else
-  LS.run(O.pts, (L.n > 1 || info_lds) ? nl : 0, ps, [&](const int2 p) {
+  LS.run(O.pts, (keep && (L.n > 1 || info_lds)) ? nl : 0, ps, [&](const int2 p) {
 #endif
 #ifndef PBGPU_EXP_NO_INFO
     if (info_lds) KI.add(info_pos(p.y));
@@ -2271,10 +2281,6 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
   });
   if (L.n > 1) R.avg_err = __ddiv_rn(err, L.dn);
   PROF_T(kc_t3);
-  R.rs = first.x;
-  R.re = (int32_t)((uint32_t)prev.x + k - 1u);
-  R.qs = first.y; R.qe = prev.y;
-  const bool keep = act && nl > 0 && coords_finish(P, rl, R);
   // info arrays: allocate for kept records, copy the LDS case, or run pass 3 in HBM
   bool info_ok = true, pass3 = false;
   KmersInfo<int32_t> KG;  // pass 3: the arrays in HBM
@@ -3369,6 +3375,7 @@ static_assert(GRAPH_NMAX_BIG <= 0xFFFFu, "an edge holds its node j in 16 bits");
 #define PBGPU_GE_SLOTS 384
 #endif
 constexpr uint32_t GE_NODES = 64, GE_SLOTS = PBGPU_GE_SLOTS, GE_BLOCK = 256;
+
 DEV bool graph_on_device(const GraphDev& G, uint32_t n) { return n > 0 && n <= G.nmax && n <= GRAPH_NMAX_BIG; }
 // super_read_name::overlap (super_read_name.cc:49-72) in registers for a name i of SA
 // unitigs (wave-uniform: the wave's node): the smallest t >= max(SA - sb + 1, 1) with
@@ -3471,39 +3478,42 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
       // across chunks: a test is one bmax load a lane, needed again only past those blocks
       uint64_t ck_b0 = 0, ck_m = 0;
       bool ck_set = false;
-      for (uint64_t j0 = q + 1; j0 < qe; j0 += 64) {
-        // Fast-forward over whole 64-position blocks in which every node is skipped for node i
-        // (imp_s <= 1, or not advancing: imp_e_i > imp_e_j + 31): none of them can give an
-        // edge or the break.  On repeat-rich reads most of a long node's scan is nodes it
-        // contains (C4r: 73% of 252 G scanned positions were skips).
-        {
-          uint64_t b0 = j0 >> 6;
-          for (;;) {
-            if (!ck_set || b0 - ck_b0 >= 64) {  // (b0 never decreases)
-              ck_set = true;
-              ck_b0 = b0;
-              const uint64_t bb = b0 + lane;
-              const bool in = (bb << 6) < qe;
-              const double m = in ? G.bmax[bb] : 0.0;
-              ck_m = __ballot(!(in & (ie_i > __dadd_rn(m, 31.0))));
-            }
-            const uint64_t nsk = ck_m >> (b0 - ck_b0);
-            if (nsk & 1ull) break;  // block b0 is scanned
-            if (!nsk) { b0 = ck_b0 + 64; continue; }  // all 64 skipped: test the next 64
-            b0 += (uint64_t)__ffsll((unsigned long long)nsk) - 1;  // the first block that is not
-            j0 = b0 << 6;
-            break;
+      // Fast-forward over whole 64-position blocks in which every node is skipped for node i
+      // (imp_s <= 1, or not advancing: imp_e_i > imp_e_j + 31): none of them can give an
+      // edge or the break.  On repeat-rich reads most of a long node's scan is nodes it
+      // contains (C4r: 73% of 252 G scanned positions were skips).  Returns the position
+      // the chunk at j0 really starts at (>= qe: the scan is over).
+      auto next_pos = [&](uint64_t j0) -> uint64_t {
+        if (j0 >= qe) return j0;
+        uint64_t b0 = j0 >> 6;
+        for (;;) {
+          if (!ck_set || b0 - ck_b0 >= 64) {  // (b0 never decreases)
+            ck_set = true;
+            ck_b0 = b0;
+            const uint64_t bb = b0 + lane;
+            const bool in = (bb << 6) < qe;
+            const double m = in ? G.bmax[bb] : 0.0;
+            ck_m = __ballot(!(in & (ie_i > __dadd_rn(m, 31.0))));
           }
-          if ((b0 << 6) > j0) j0 = b0 << 6;
-          if (j0 >= qe) break;
+          const uint64_t nsk = ck_m >> (b0 - ck_b0);
+          if (nsk & 1ull) break;  // block b0 is scanned
+          if (!nsk) { b0 = ck_b0 + 64; continue; }  // all 64 skipped: test the next 64
+          b0 += (uint64_t)__ffsll((unsigned long long)nsk) - 1;  // the first block that is not
+          break;
         }
+        return (b0 << 6) > j0 ? b0 << 6 : j0;
+      };
+      // the chunk [j0, j0 + 64) for node i; true at the reference's break
+      auto chunk = [&](uint64_t j0) -> bool {
         const uint64_t j = j0 + lane;
         const bool act = j < qe;
         const uint32_t sj = (uint32_t)((act ? j : q) - q0);
-        // node j: staged, or (a scan past the window) from HBM.  Every load is issued before
-        // the tests (measured: loading the name only where the name test runs, after the
-        // skip / break ballot, made the C4r graph stage 240 -> 316 ms: a second round trip
-        // on the critical path costs more than the loads it saves)
+        // node j: staged, or (a scan past the window) one 64-byte line from HBM.  Every load
+        // is issued before the tests (measured: loading the name only where the name test
+        // runs, after the skip / break ballot, made the C4r graph stage 240 -> 316 ms: a
+        // second round trip on the critical path costs more than the loads it saves; and
+        // loading the next chunk's lines one chunk ahead, two register sets, was slower
+        // too: C4r 159 -> 178 ms, C2 36.5 -> 38.8)
         double is_j, ie_j, er_j;
         uint32_t mj, lpa_j, bu[GRAPH_U];
         const bool staged = !OVF && sj < ns;
@@ -3512,7 +3522,7 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
 #pragma unroll
           for (uint32_t u = 0; u < GRAPH_U; ++u) bu[u] = s_u[u * GE_SLOTS + sj];
         } else {
-          const GDesc dj = G.desc[act ? j : q];  // one 64-byte line
+          const GDesc dj = G.desc[act ? j : q];
           is_j = dj.imp_s; ie_j = dj.imp_e; er_j = dj.err; mj = dj.idx | ((uint32_t)dj.nsz << 16); lpa_j = dj.lp_add;
 #pragma unroll
           for (uint32_t u = 0; u < GRAPH_U; ++u) bu[u] = dj.u[u];
@@ -3586,8 +3596,10 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
           ge_cand += (uint64_t)__builtin_popcountll(__ballot(cand));
         }
 #endif
-        if (bm) break;  // the reference's break
-      }
+        return bm != 0;
+      };
+      for (uint64_t j0 = next_pos(q + 1); j0 < qe; j0 = next_pos(j0 + 64))
+        if (chunk(j0)) break;
     }
 #ifdef PBGPU_PROF
     if (!OVF) {  // slots 128..130: positions scanned, of them past the staged window, candidates (name test)
