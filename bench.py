@@ -601,7 +601,7 @@ def main():
     # production device leg): FETCH_SIZE corrected for the kernel's read shape (random
     # 64-B sectors exact; occurrence runs by the 512-B-run calibration; row streams 2x)
     traffic, traffic_note, summ_name, summ_all = None, None, None, {}
-    for name in ("r04z_rocprof_summary.json", "r04_rocprof_summary.json", "r03m_rocprof_summary.json", "r03k_rocprof_summary.json",
+    for name in ("r05z_rocprof_summary.json", "r04z_rocprof_summary.json", "r04_rocprof_summary.json", "r03m_rocprof_summary.json", "r03k_rocprof_summary.json",
                  "r02e_rocprof_summary.json"):
         summ = os.path.join(ROOT, "profiles", name)
         if os.path.exists(summ):
@@ -615,7 +615,7 @@ def main():
     for kk in per_kernel:
         t = summ_all.get(f"{kk}_traffic_bytes")
         if t:
-            shape = t.get("shape") or ("calibrated_runs" if kk == "k_group" else "guide_2x_fetch_plus_write")
+            shape = t.get("shape") or ("raw_fetch_plus_write" if kk == "k_group" else "guide_2x_fetch_plus_write")
             per_kernel[kk]["traffic_bytes_per_launch"] = t.get(shape)
             per_kernel[kk]["traffic_over_alg"] = round(t.get(shape) / kb[kk], 3) if t.get(shape) else None
             per_kernel[kk]["rocprof_mean_ms"] = (summ_all.get(f"{kk}_device_leg") or {}).get("mean_ms")

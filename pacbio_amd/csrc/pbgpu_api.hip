@@ -1962,7 +1962,7 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
   al->n_kept.ensure(n); al->thr.ensure(n); al->nhits.ensure(n); al->hit_off.ensure(n + 1);
   std::vector<uint64_t>& hoff = al->h_hoff;
   hoff.resize(n + 1);
-  al->ovf_items.ensure(n);
+  al->ovf_items.ensure(n); al->ovf_grow.ensure(n);
   al->ovf_list.ensure(n);  // (used only by batches with reads past the first group tier)
   al->rcur.ensure(n);
   uint64_t rec_done = 0, info_done = 0;
@@ -2019,7 +2019,7 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
     O.chain_count = al->counters.p;
     O.chain_cap = (uint32_t)std::min<uint64_t>(al->chains.n, 0xFFFFFFFFu);
     O.n_overflow = al->counters.p + 3;
-    O.overflow_items = al->ovf_items.p;
+    O.overflow_items = al->ovf_items.p; O.overflow_grow = al->ovf_grow.p;
     O.rcur = al->rcur.p;
     // Reads longest first (hits), so the long-read tail starts early.  The predicted
     // super-read count of a read (hits x chains-per-hit of earlier batches) picks its
@@ -2112,39 +2112,54 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
       while (n_ovf) {
         std::vector<uint2>& ovf = al->h_items;
         ovf.resize(n_ovf);
-        HIPCHK(hipMemcpy(ovf.data(), al->ovf_items.p, n_ovf * sizeof(uint2), hipMemcpyDeviceToHost));
+        std::vector<uint32_t> grow(n_ovf);
+        HIPCHK(hipMemcpyAsync(ovf.data(), al->ovf_items.p, n_ovf * sizeof(uint2), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(grow.data(), al->ovf_grow.p, n_ovf * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
         uint64_t mx = 0;
         for (const uint2& it : ovf) mx = std::max(mx, hoff[it.x + 1] - hoff[it.x]);
-        // next tier: the 8192-slot LDS table; an item that overflows it again stays there
-        // split in two (partition p of P is partitions 2p and 2p + 1 of 2P; the read's
-        // other partitions keep their lists), while every item's P stays <= 4096; past
-        // that, HBM tables x4 each round (results do not depend on the tier).  On C4r reads
-        // the HBM tier took 75 ms a launch (r04h) for what split LDS items do in a fraction.
+        // Next: the 8192-slot LDS table, an overflowing item split into f items (partition p
+        // of P is exactly partitions p f .. p f + f - 1 of P f; the read's other partitions
+        // keep their lists), f the power of two >= its growth estimate (nk / k-mers taken when
+        // the table filled; x 1/4 from the 2048-slot table's fill limit to the 8192-slot
+        // one's), while every item's P stays <= 4096; past that, HBM tables x4 each round
+        // (results do not depend on the tier).  On C4r reads the HBM tier took 75 ms a launch
+        // (r04h) for what split LDS items do in a fraction, and splitting by the estimate
+        // rather than in two saves rounds, each a launch of a few long items.
         const bool refine_off = getenv("PBGPU_GROUP_REFINE") && !atoi(getenv("PBGPU_GROUP_REFINE"));  // (tests)
-        bool refine = false;
-        if (lg == kGroupLdsMaxLog2 && !refine_off) {
-          refine = true;
-          for (const uint2& it : ovf) refine &= (it.y >> 16) <= 2048;
-        }
+        // (each item carries the table it filled: the first round holds both tiers' items)
+        auto split_of = [&](uint32_t i) -> uint32_t {
+          const uint32_t g = grow[i] & 0xFFFFFFu;
+          const bool from_small = (grow[i] >> 24) < kGroupLdsMaxLog2;
+          const uint32_t need = from_small ? (g + 3) / 4 : std::max<uint32_t>(2, g);
+          uint32_t f = 1;
+          while (f < need && f < 64) f <<= 1;
+          return f;
+        };
+        bool refine = !refine_off;
+        if (refine)
+          for (uint32_t i = 0; i < n_ovf; ++i) refine &= (uint64_t)(ovf[i].y >> 16) * split_of(i) <= 4096;
         if (refine) {
-          std::vector<uint2> two;
-          two.reserve(2 * (size_t)n_ovf);
-          for (const uint2& it : ovf) {
-            const uint32_t p = it.y & 0xFFFFu, P = it.y >> 16;
-            two.push_back(group_item(it.x, 2 * p, 2 * P));
-            two.push_back(group_item(it.x, 2 * p + 1, 2 * P));
+          std::vector<uint2> next;
+          next.reserve(2 * (size_t)n_ovf);
+          bool split = false;
+          for (uint32_t i = 0; i < n_ovf; ++i) {
+            const uint32_t p = ovf[i].y & 0xFFFFu, P = ovf[i].y >> 16, f = split_of(i);
+            split |= f > 1;
+            for (uint32_t t = 0; t < f; ++t) next.push_back(group_item(ovf[i].x, p * f + t, P * f));
           }
-          ovf.swap(two);
+          ovf.swap(next);
           n_ovf = (uint32_t)ovf.size();
-          ++al->acc.group_refines;
+          if (split) ++al->acc.group_refines;
+          lg = kGroupLdsMaxLog2;
         } else {
           lg = lg < kGroupLdsMaxLog2 ? kGroupLdsMaxLog2 : lg + 2;
         }
         if (lg > kGroupLdsMaxLog2 && (1ull << (lg - 2)) > 2 * mx + 256)
           throw std::runtime_error("group table growth did not converge");
         al->ovf_list.ensure(n_ovf);
-        al->ovf_items.ensure(n_ovf);  // (this round's overflow: at most its items)
-        O.overflow_items = al->ovf_items.p;
+        al->ovf_items.ensure(n_ovf); al->ovf_grow.ensure(n_ovf);  // (this round's overflow: at most its items)
+        O.overflow_items = al->ovf_items.p; O.overflow_grow = al->ovf_grow.p;
         HIPCHK(hipMemcpyAsync(al->ovf_list.p, ovf.data(), n_ovf * sizeof(uint2), hipMemcpyHostToDevice, st));
         HIPCHK(hipMemsetAsync(al->counters.p + 3, 0, 4, st));
         if (lg <= kGroupLdsMaxLog2) {

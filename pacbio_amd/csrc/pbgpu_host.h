@@ -319,6 +319,7 @@ struct pbgpu_aligner {
   dbuf<KRec> krec;
   dbuf<uint32_t> n_kept, thr, rec_per_read, rec_cursor, order, counters;
   dbuf<uint2> ovf_items;
+  dbuf<uint32_t> ovf_grow;
   dbuf<uint32_t> rcur;
   dbuf<uint64_t> sort_scratch;  // k_rec_sort keys of reads above its LDS capacity: 6 words per record
   dbuf<uint64_t> nhits, hit_off, rec_off, huge_elems;

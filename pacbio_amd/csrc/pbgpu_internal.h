@@ -127,6 +127,7 @@ struct GroupOut {
   uint32_t* chain_count;
   uint32_t chain_cap;
   uint2* overflow_items;   // the work items whose table overflowed (group_item)
+  uint32_t* overflow_grow;  // per overflowing item: ceil(its k-mers / those its pass 0 had taken) | table log2 << 24
   uint32_t* n_overflow;
   uint32_t* rcur;          // per read: hits placed so far by its partitions (P > 1 items)
 };

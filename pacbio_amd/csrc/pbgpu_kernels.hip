@@ -596,6 +596,7 @@ __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_
   // after the other in one block: with a sub-batch's few hundred long reads
   // the longest read's block was the launch.)
   uint32_t read_chains = 0, part_hits = 0;
+  uint32_t g_stop = nk;  // pass 0 over the k-mers [0, g_stop) when the table overflowed
   uint32_t p0x = 0;  // PBGPU_EXP_P0_NOTABLE: keeps the loads live
   auto part_of = [&](uint32_t sr) -> uint32_t {
     return P == 1 ? 0u : (uint32_t)(((uint64_t)(sr * 0x85EBCA77u) * P) >> 32);
@@ -622,7 +623,7 @@ __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_
     auto groups = [&](auto pass_c) {
     constexpr int pass = decltype(pass_c)::value;
     for (uint32_t g0 = 0; g0 < nk; g0 += B) {
-      if (s_flag) break;  // uniform (written before the last barrier)
+      if (s_flag) { g_stop = g0; break; }  // uniform (written before the last barrier)
 #ifdef PBGPU_PROF
       const uint64_t pr_a = __builtin_amdgcn_s_memtime();
 #endif
@@ -905,10 +906,14 @@ __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_
 #ifdef PBGPU_PROF
       const uint64_t pr_c = __builtin_amdgcn_s_memtime();
 #endif
-      if (s_flag) {  // table too full: the item goes again, split in two or with a larger table
+      if (s_flag) {  // table too full: the item goes again, split or with a larger table
         if (tid == 0) {
           const uint32_t o = atomicAdd(O.n_overflow, 1u);
           O.overflow_items[o] = item;
+          // the table filled over the first g_stop k-mers of nk: nk / g_stop estimates how much
+          // larger the item is (the host splits it that many ways; too few only costs a round)
+          const uint32_t grow = g_stop ? (nk + g_stop - 1) / g_stop : nk;
+          O.overflow_grow[o] = (grow < 0xFFFFFFu ? grow : 0xFFFFFFu) | (hcap_log2 << 24);  // | the table it filled
         }
         return;
       }
@@ -3537,9 +3542,10 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
         const bool cand = act & !skip & (lane < fb) & (sa >= 2) & (sb >= 2);
         bool edge = false;
         int32_t nb = 0, common = 0;
-        auto po_of_j = [&]() -> uint32_t {
-          return staged ? s_po[sj] : (uint32_t)G.poff[rb_i + (mj & 0xFFFFu)];
-        };
+        // j's name offset (its prefix sums, and its units past GRAPH_U)
+        // (loaded where needed: issuing it for every candidate before the name test measured
+        // slower, C4r graph stage 154 -> 160 ms)
+        auto po_of_j = [&]() -> uint32_t { return staged ? s_po[sj] : (uint32_t)G.poff[rb_i + (mj & 0xFFFFu)]; };
         if (cand) {
           bool same;
           if ((sa <= GRAPH_U) & (sb <= GRAPH_U)) {
@@ -3863,28 +3869,34 @@ __global__ __launch_bounds__(GRAPH_BIG_BLOCK) void k_graph_sort_big(GraphDev G, 
     graph_write_desc(G, b + p, b, (uint32_t)ex[p]);
   }
 }
-// k_graph_relax for one big read, node state in HBM (8 u32 arrays of n, then the imp_s
-// head bitmap): the same two waves, the same order of updates and unions.  The state is
-// this block's alone and both waves run on one CU, so plain loads and stores with a
-// workgroup fence after each chunk (its stores complete before the next chunk's loads)
-// order it as the LDS kernel's in-order LDS does.
+// k_graph_relax for one big read, node state in HBM (a 16-byte path record per node, the
+// union-find's parent and rank as u32 arrays, then the imp_s head bitmap): the same two
+// waves, the same order of updates and unions.  The state is this block's alone and both
+// waves run on one CU, so plain loads and stores with a workgroup fence after each chunk
+// (its stores complete before the next chunk's loads) order it as the LDS kernel's in-order
+// LDS does.  A node's path fields are one record so that a node j's test and update are one
+// load and one store (round 5: five arrays, two dependent round trips and the flag's
+// read-modify-write a node).
+struct alignas(16) RelaxPath {
+  int32_t lp, lun;       // longest path, its unitigs
+  uint16_t lst, lpv;     // start and previous node (0xFFFF: -1)
+  uint16_t lsk, fl;      // the start's implied-start key (0xFFFF: NaN), flags (1 an edge in, 2 out)
+};
+// (Measured: the union-find's parent and rank in LDS for reads of <= 8192 records, 3 B a
+// node, gained nothing -- C4r graph stage 154.2 vs 154.7 ms -- and <= 16384 lost 10 ms.)
 __global__ __launch_bounds__(128) void k_graph_relax_big(GraphDev G, uint32_t n_reads) {
-  constexpr uint32_t RANK_NAN = 0xFFFFFFFFu, NONE = 0xFFFFFFFFu;
+  constexpr uint32_t RANK_NAN = 0xFFFFu, NONE = 0xFFFFu;
   const uint32_t r = blockIdx.x;
   if (r >= n_reads) return;
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint64_t b = G.rec_off[r];
   const uint32_t n = (uint32_t)(G.rec_off[r + 1] - b);
   if (!graph_relax_big(G, n)) return;
-  int32_t* s_lp = reinterpret_cast<int32_t*>(G.scratch + 6 * b);
-  int32_t* s_lun = s_lp + n;
-  int32_t* s_lst = s_lun + n;
-  int32_t* s_lpv = s_lst + n;
-  uint32_t* s_lsk = reinterpret_cast<uint32_t*>(s_lpv + n);
-  uint32_t* s_par = s_lsk + n;
-  uint32_t* s_rank = s_par + n;
-  uint32_t* s_fl = s_rank + n;                                  // 1 an edge into it, 2 an edge out of it
+  RelaxPath* S = reinterpret_cast<RelaxPath*>(G.scratch + 6 * b);  // 16 n bytes
+  uint32_t* const s_par = reinterpret_cast<uint32_t*>(S + n);      // the union-find: 8 n bytes
+  uint32_t* const s_rank = s_par + n;
   uint64_t* s_head = G.scratch + 6 * b + 4 * (uint64_t)n;     // (n + 63) / 64 words: within 6n
+  static_assert(sizeof(RelaxPath) == 16, "path record");
   for (uint32_t p0 = 0; p0 < n; p0 += 128) {
     const uint32_t p = p0 + tid;
     bool head = false;
@@ -3892,8 +3904,10 @@ __global__ __launch_bounds__(128) void k_graph_relax_big(GraphDev G, uint32_t n_
       const GDesc d = G.desc[b + p];
       const uint32_t it = d.idx;
       head = p == 0 || !(G.desc[b + p - 1].imp_s == d.imp_s);  // (-0 == +0; a NaN heads its own)
-      s_lp[it] = (int32_t)d.lp_add; s_lun[it] = (int32_t)d.nsz; s_lst[it] = -1; s_lpv[it] = -1;
-      s_fl[it] = G.ecnt[b + p] ? 2 : 0;
+      RelaxPath ps;
+      ps.lp = (int32_t)d.lp_add; ps.lun = (int32_t)d.nsz; ps.lst = 0xFFFFu; ps.lpv = 0xFFFFu;
+      ps.lsk = 0; ps.fl = G.ecnt[b + p] ? 2 : 0;
+      S[it] = ps;
       s_par[it] = it; s_rank[it] = 0;
     }
     const uint64_t hm = __ballot(head);
@@ -3905,14 +3919,16 @@ __global__ __launch_bounds__(128) void k_graph_relax_big(GraphDev G, uint32_t n_
     uint32_t w = p >> 6;
     uint64_t m = s_head[w] & (~0ull >> (63 - (p & 63)));
     while (!m) m = s_head[--w];  // position 0 is a head
-    s_lsk[d.idx] = d.imp_s != d.imp_s ? RANK_NAN : w * 64 + 63 - (uint32_t)__builtin_clzll(m);
+    S[d.idx].lsk = (uint16_t)(d.imp_s != d.imp_s ? RANK_NAN : w * 64 + 63 - (uint32_t)__builtin_clzll(m));
   }
   __syncthreads();
   const bool paths = tid < 64;
   auto ldw = [&](uint32_t p) -> uint32_t {
     return p < n ? (G.desc[b + p].idx | (G.ecnt[b + p] << 16)) : 0u;
   };
-  // edge counts past 65535 do not fit the packed word: a node's count comes from ecnt
+  // (a node's edges go to later nodes of its read: at most n - 1 <= 65534, so the count fits
+  // the packed word's 16 bits)
+  static_assert(GRAPH_NMAX_BIG <= 0xFFFFu, "edge counts fit 16 bits");
   uint32_t c0 = 0, cur = ldw(lane), nxt = ldw(64 + lane);
   auto wd = [&](uint32_t x) -> uint32_t {
     const uint32_t o = x - c0;
@@ -3925,21 +3941,22 @@ __global__ __launch_bounds__(128) void k_graph_relax_big(GraphDev G, uint32_t n_
   uint2 pf[GRAPH_RELAX_PF];
 #pragma unroll
   for (uint32_t d = 0; d < GRAPH_RELAX_PF; ++d) pf[d] = ldb(d, wd(d) >> 16);
+  PROF_T(rb_t0);
   for (uint32_t p = 0; p < n; ++p) {
     if (p - c0 == 64) {
       c0 += 64; cur = nxt;
       nxt = ldw(c0 + 64 + lane);
     }
-    const uint32_t w = wd(p), it_i = w & 0xFFFFu;
-    const uint32_t ec = G.ecnt[b + p];  // (wave-uniform load; the packed count is 16 bits)
+    const uint32_t w = wd(p), ec = w >> 16, it_i = w & 0xFFFFu;  // (round 5: ec was a load a node)
     const uint2 blk = pf[0];
 #pragma unroll
     for (uint32_t d = 0; d + 1 < GRAPH_RELAX_PF; ++d) pf[d] = pf[d + 1];
     pf[GRAPH_RELAX_PF - 1] = ldb(p + GRAPH_RELAX_PF, wd(p + GRAPH_RELAX_PF) >> 16);
     if (ec == 0) continue;
-    int32_t lp_i = 0, lun_i = 0, lst_i = 0;
-    uint32_t lsk_i = 0;
-    if (paths) { lp_i = s_lp[it_i]; lun_i = s_lun[it_i]; lst_i = s_lst[it_i]; lsk_i = s_lsk[it_i]; }
+    RelaxPath si{};
+    if (paths) si = S[it_i];
+    const int32_t lp_i = si.lp, lun_i = si.lun;
+    const uint32_t lst_i = si.lst, lsk_i = si.lsk;
     for (uint32_t k0 = 0; k0 < ec; k0 += 64) {
       const bool edge = k0 + lane < ec;
       // the first GRAPH_EBLK edges from the node's block (prefetched), the rest from its region past it
@@ -3948,21 +3965,20 @@ __global__ __launch_bounds__(128) void k_graph_relax_big(GraphDev G, uint32_t n_
       const uint32_t it_j = ce.x & 0xFFFFu;
       if (paths) {
         if (edge) {  // node_info update (overlap_graph.cc:41-56); this lane owns node j
-          s_fl[it_j] |= 1;
+          RelaxPath sj = S[it_j];
+          sj.fl |= 1;  // an edge into j: not a start node
           const int32_t nlpath = (int32_t)((uint32_t)lp_i + ce.y);
-          const int32_t lp_j = s_lp[it_j];
-          bool upd = nlpath > lp_j;
-          if (!upd && nlpath == lp_j) {  // (lstart_imp_s: lsk_i > lsk_j, neither NaN)
-            const uint32_t lsk_j = s_lsk[it_j];
-            upd = s_lst[it_j] == -1 || ((lsk_i != RANK_NAN) & (lsk_j != RANK_NAN) & (lsk_i > lsk_j));
-          }
+          bool upd = nlpath > sj.lp;
+          if (!upd && nlpath == sj.lp)  // (lstart_imp_s: lsk_i > lsk_j, neither NaN)
+            upd = sj.lst == NONE || ((lsk_i != RANK_NAN) & (sj.lsk != RANK_NAN) & (lsk_i > sj.lsk));
           if (upd) {
-            s_lp[it_j] = nlpath;
-            s_lst[it_j] = lst_i == -1 ? (int32_t)it_i : lst_i;
-            s_lsk[it_j] = lsk_i;
-            s_lpv[it_j] = (int32_t)it_i;
-            s_lun[it_j] = lun_i + (int32_t)(ce.x >> 16);
+            sj.lp = nlpath;
+            sj.lst = (uint16_t)(lst_i == NONE ? it_i : lst_i);
+            sj.lsk = (uint16_t)lsk_i;
+            sj.lpv = (uint16_t)it_i;
+            sj.lun = lun_i + (int32_t)(ce.x >> 16);
           }
+          S[it_j] = sj;
         }
       } else {
         // union_sets(it_i, it_j) for this chunk's edges in j order (union_find.cc:13-23)
@@ -4009,12 +4025,18 @@ __global__ __launch_bounds__(128) void k_graph_relax_big(GraphDev G, uint32_t n_
     }
   }
   (void)NONE;
+  PROF_T(rb_t1);
+  // slots 140..: [paths wave] ticks, [union wave] ticks, nodes, blocks
+  PROF_ADD(paths ? 140 : 141, rb_t1 - rb_t0);
+  if (paths) { PROF_ADD(142, n); PROF_ADD(143, 1); }
   __syncthreads();
   for (uint32_t i = tid; i < n; i += 128) {
     uint32_t q = i;
     while (s_par[q] != q) q = s_par[q];
-    const uint32_t fl = (s_fl[i] & 1 ? 0u : GRAPH_START) | (s_fl[i] & 2 ? 0u : GRAPH_END);
-    G.out[b + i] = GraphNode{s_lp[i], s_lst[i], s_lpv[i], s_lun[i], q, fl};
+    const RelaxPath si = S[i];
+    const uint32_t fl = (si.fl & 1 ? 0u : GRAPH_START) | (si.fl & 2 ? 0u : GRAPH_END);
+    G.out[b + i] = GraphNode{si.lp, si.lst == NONE ? -1 : (int32_t)si.lst, si.lpv == NONE ? -1 : (int32_t)si.lpv,
+                             si.lun, q, fl};
   }
 }
 // ====================================================== mega-reads (device)

@@ -120,10 +120,11 @@ def test_dense_group_overflow(dense, cfg):
 @pytest.mark.parametrize("data", ["dense", "small"])
 def test_group_all_overflow(data, refine, dense, small, monkeypatch):
     """Every read predicted to fit the smallest (2048-slot) table: reads touching
-    more super-reads abandon it mid k-mer group and resume in the 8192-slot LDS
-    tier, then either with their hash partitions doubled (the default: the
-    partitions already placed keep their lists) or in HBM tables
-    (PBGPU_GROUP_REFINE=0); a full table must never trap a thread."""
+    more super-reads abandon it mid k-mer group and go again in the 8192-slot
+    LDS tier, split into hash partitions by their growth estimate (the default:
+    an item that overflows again splits again, the partitions already placed
+    keep their lists) or in HBM tables (PBGPU_GROUP_REFINE=0); a full table must
+    never trap a thread."""
     ds = dense if data == "dense" else small
     monkeypatch.setenv("PBGPU_GROUP_PRED_SCALE", "0")
     monkeypatch.setenv("PBGPU_GROUP_REFINE", refine)

@@ -53,6 +53,10 @@ def main():
             print(f"k_graph_relax {tier}: blocks {v[7]}, nodes {v[6]}, chunks {v[1]} ({v[1] / nn:.2f} a node); "
                   f"ticks a node: paths wave {v[2] / nn:.0f} (chunk work {v[0] / nn:.0f}), "
                   f"union wave {v[5] / nn:.0f} (finds {v[3] / nn:.0f}, merges {v[4] / nn:.0f})")
+        rb = list(buf)[140:144]
+        if rb[3]:
+            print(f"k_graph_relax_big: blocks {rb[3]}, nodes {rb[2]}; ticks a node: paths wave {rb[0] / max(1, rb[2]):.0f}, "
+                  f"union wave {rb[1] / max(1, rb[2]):.0f}")
         e = list(buf)[128:131]
         print(f"k_graph_edges: positions scanned {e[0]} ({e[0] / max(1, st['graph_records']):.1f} a node), past the "
               f"staged window {e[1]}, name tests {e[2]}")
