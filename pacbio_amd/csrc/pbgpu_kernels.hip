@@ -3377,7 +3377,7 @@ static_assert(GRAPH_NMAX_K <= (1u << GRAPH_ROOT_BITS) && GRAPH_NMAX_K < 0x8000u,
               "k_graph_relax matches roots by GRAPH_ROOT_BITS and keeps 15-bit indices");
 static_assert(GRAPH_NMAX_BIG <= 0xFFFFu, "an edge holds its node j in 16 bits");
 #ifndef PBGPU_GE_SLOTS
-#define PBGPU_GE_SLOTS 384
+#define PBGPU_GE_SLOTS 192  // (round 5: 384 -> 192 with 8 waves a SIMD, below)
 #endif
 constexpr uint32_t GE_NODES = 64, GE_SLOTS = PBGPU_GE_SLOTS, GE_BLOCK = 256;
 
@@ -3421,7 +3421,17 @@ __global__ __launch_bounds__(256) void k_graph_bmax(GraphDev G, uint64_t n_recs)
   }
   if (lane == 0) G.bmax[blk] = v;
 }
+// Waves per SIMD asked of the compiler (0: its choice).  The scans wait on memory (64% of
+// their wave cycles on C4r), so occupancy pays: 8 waves (64 VGPRs, no spills) with a
+// 192-slot staged window (≈14 KB of LDS a block) against 5 (100 VGPRs, 384 slots): graph
+// stage C4r 155 -> 148 ms, C2 36.1 -> 32.2 (profiles/r05ze_edges_occupancy_ab.txt)
+#ifndef PBGPU_GE_WAVES
+#define PBGPU_GE_WAVES 8
+#endif
 template <bool OVF>
+#if PBGPU_GE_WAVES
+__attribute__((amdgpu_waves_per_eu(PBGPU_GE_WAVES, PBGPU_GE_WAVES)))
+#endif
 __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n_recs, uint64_t n_ovf) {
   __shared__ double s_is[GE_SLOTS], s_ie[GE_SLOTS], s_er[GE_SLOTS];
   __shared__ uint32_t s_meta[GE_SLOTS], s_lpa[GE_SLOTS], s_po[GE_SLOTS];
