@@ -838,9 +838,9 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dom, "rocprof_kernel": ROCPROF_FILE[dom], "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "alg_bytes_per_launch": kb[dom], "avg_launch_ms": avg_ms,
-                         "traffic_source": (f"profiles/{summ_name} (" +
-                                            ("FETCH_SIZE x run-shape calibration" if dom == "k_group" else
-                                             "FETCH_SIZE by read shape") + " + WRITE_SIZE, per device-leg launch)")
+                         "traffic_source": (f"profiles/{summ_name} (FETCH_SIZE as the read shape needs it -- "
+                                            f"{(summ_all.get(dom + '_traffic_bytes') or {}).get('shape', '?')} -- "
+                                            "+ WRITE_SIZE, per device-leg launch, separate passes)")
                          if traffic else None,
                          "traffic_alternatives": traffic_note,
                          "b_rand_gbs": b_rand, "frac_of_b_rand": (achieved / b_rand) if b_rand else None,
