@@ -276,6 +276,9 @@ def main():
     ap.add_argument("--device-streams", type=int, default=1,
                     help="aligners of the device-only leg: 1 = every launch runs alone, so the per-launch event times "
                          "(the roofline) measure the kernel, not two overlapping launches")
+    ap.add_argument("--device-aligners", type=int, default=2,
+                    help="the device leg again with this many aligners per GPU, the product's count (their launches "
+                         "overlap: value_device_aligners, no per-kernel figure); 0 or 1 = skip")
     ap.add_argument("--device-chunk-bases", type=float, default=1.5e9,
                     help="the device leg aligns its resident reads in chunks of at most this many bases (C2's "
                          "617 Mbases are one; C3's 3.6 Gbases in one call need more than 288 GB of working buffers)")
@@ -434,6 +437,27 @@ def main():
         al.free(c)
     al.close()
 
+    # the same leg with the product's aligners per GPU (pbgpu_run / the CLIs run 2): the reads
+    # split between them, their launches overlapping -- throughput only
+    el_dev_al = None
+    if args.device_aligners > 1 and args.device_streams == 1:
+        ala = pbgpu.StreamAligner(index, streams=args.device_aligners, **akw)
+        chunks = upload_chunks(ala)
+        for c in chunks:
+            ala.align_resident(c)
+        pbgpu.device_synchronize(local)
+        comm.barrier()
+        td = time.perf_counter()
+        for _ in range(args.device_steps):
+            for c in chunks:
+                ala.align_resident(c)
+        pbgpu.device_synchronize(local)
+        comm.barrier()
+        el_dev_al = comm.max(time.perf_counter() - td)
+        for c in chunks:
+            ala.free(c)
+        ala.close()
+
     # SURVEY 8(d)'s second flag set: the defaults, without -l / -f (device leg only)
     el_dev2, st2 = None, None
     if not args.skip_default_leg:
@@ -557,6 +581,7 @@ def main():
     total_bases = comm.sum(bases_rank) * args.steps
     value = total_bases / elapsed
     value_device = comm.sum(bases_rank) * args.device_steps / el_dev
+    value_device_al = comm.sum(bases_rank) * args.device_steps / el_dev_al if el_dev_al else None
     # every collective runs on every rank, here, never inside the rank-0 report below
     value_device2 = comm.sum(bases_rank) * args.device_steps / el_dev2 if el_dev2 else None
     value_parts = comm.sum(bases_rank) * args.steps / el_parts if el_parts else None
@@ -769,6 +794,11 @@ def main():
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic (tools/pbsynth.cc, seed 42; SURVEY.md §8d generator), written as FASTA",
+            "value_device_aligners": value_device_al,
+            "value_device_aligners_note": (f"value_device's leg with {args.device_aligners} aligners per GPU (the "
+                                           "CLIs' default), the reads split between them and their launches "
+                                           "overlapping; value_device and the roofline use one aligner"
+                                           if value_device_al else None),
             "value_device": value_device,
             "value_device_note": "reads resident in HBM, device path to sorted records in HBM, no formatting / "
                                  "output (round-1 definition)",

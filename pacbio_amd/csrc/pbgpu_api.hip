@@ -1823,8 +1823,9 @@ static void graph_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   if (const char* e = getenv("PBGPU_GRAPH_NMAX")) G.nmax = (uint32_t)std::min<long>(GRAPH_NMAX_BIG, std::max(0l, atol(e)));
   // reads of more records relax with their state in HBM (k_graph_relax_big): an LDS
   // tier's block of 4096-8192 records holds a CU alone, the HBM blocks share CUs (C4r graph
-  // stage 200 -> 160 ms at 2048, C2 unchanged; PBGPU_RELAX_BIG_MIN sets it)
-  G.relax_big_min = 2048;
+  // stage 200 -> 160 ms at 2048; at 1024 with the path records, C2 32.4 -> 30.2 ms, C4r
+  // +1 ms, profiles/r05zf_graph_ab.txt; PBGPU_RELAX_BIG_MIN sets it)
+  G.relax_big_min = 1024;
   if (const char* e = getenv("PBGPU_RELAX_BIG_MIN"))
     G.relax_big_min = (uint32_t)std::min<long>(GRAPH_NMAX, std::max(0l, atol(e)));
   // reads past GRAPH_NMAX records keep their sort keys and node state here (6 words a record)

@@ -4306,10 +4306,7 @@ __global__ __launch_bounds__(64) void k_mega(GraphDev G, uint32_t n_reads) {
       // containment tests over every lane, the joined right-open interval set kept
       // sorted with strict gaps, so an insert [lo, hi) merges exactly the intervals
       // [s0, e) with s0 = #{y < lo}, e = #{x <= hi}
-#ifndef PBGPU_MEGA_GCAP
-#define PBGPU_MEGA_GCAP 256
-#endif
-      constexpr uint32_t GCAP = PBGPU_MEGA_GCAP;
+      constexpr uint32_t GCAP = 256;  // (128 and 64, for more waves a CU, measured the same)
       __shared__ double2 s_cov[GCAP], s_pl[GCAP], s_tile[GCAP];
       __shared__ int32_t s_it[GCAP];
       const bool in_lds = m <= GCAP;
