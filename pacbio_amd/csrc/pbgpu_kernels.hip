@@ -3528,7 +3528,8 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
         // runs, after the skip / break ballot, made the C4r graph stage 240 -> 316 ms: a
         // second round trip on the critical path costs more than the loads it saves; and
         // loading the next chunk's lines one chunk ahead, two register sets, was slower
-        // too: C4r 159 -> 178 ms, C2 36.5 -> 38.8)
+        // too: C4r 159 -> 178 ms, C2 36.5 -> 38.8 at 5 waves a SIMD; against the 8-wave
+        // kernel, 149 -> 162 / 298 / 562 ms at 5 / 6 / 8 waves, its registers spilling)
         double is_j, ie_j, er_j;
         uint32_t mj, lpa_j, bu[GRAPH_U];
         const bool staged = !OVF && sj < ns;

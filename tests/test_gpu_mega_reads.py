@@ -215,6 +215,14 @@ def test_device_graph_c2_reads(tmp_path):
     _run([*base, "--host-graph", "-o", b], timeout=300)
     ta = open(a).read()
     assert ta.count(">") > 1000 and ta == open(b).read()
+    # many small batches on each of two aligners, with reads past a lowered device cap left to
+    # the host in every batch: their descriptors hold an earlier batch's words, which the edge
+    # scans must never read (round-4 review: stale descriptors of host reads)
+    c = str(tmp_path / "mixed")
+    r = subprocess.run([CMR, *base, "--batch-bases", "2M", "--streams", "2", "-o", c], capture_output=True, text=True,
+                       timeout=300, env=dict(os.environ, PBGPU_GRAPH_NMAX="500"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert open(c).read() == ta
 
 
 def _format_device_mega(name, moff, recs, units, r):
