@@ -1315,7 +1315,7 @@ static void buffer_report(const pbgpu_aligner* al) {
       {"g_poff", al->g_poff.bytes()},
       {"g_pre", al->g_pre.bytes()},
       {"g_sizes", al->g_sizes.bytes()},
-      {"g_desc", al->g_desc.bytes()},
+      {"g_desc", al->g_desc.bytes()}, {"g_spo", al->g_spo.bytes()}, {"g_fd", al->g_fd.bytes()}, {"g_fu0", al->g_fu0.bytes()},
       {"g_imp", al->g_imp.bytes()},
       {"g_out", al->g_out.bytes()},
       {"g_ecnt", al->g_ecnt.bytes()},
@@ -1847,6 +1847,9 @@ static void graph_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   uint32_t* g_pre = dead.take(al->g_pre, 3 * tot + 3);
   G.pp = (uint2*)g_pre; G.ounits = g_pre + 2 * (tot + 1);
   G.imp = dead.take(al->g_imp, nrec + 1); G.desc = dead.take(al->g_desc, nrec + 1);
+  G.spo = dead.take(al->g_spo, nrec + 1);
+  G.fis = dead.take(al->g_fd, 3 * (nrec + 1)); G.fie = G.fis + (nrec + 1); G.fer = G.fie + (nrec + 1);
+  G.fu0 = dead.take(al->g_fu0, nrec + 1);
   if (al->g_mega) G.out = dead.take(al->g_out, nrec + 1);
   else { al->g_out.ensure(nrec + 1); G.out = al->g_out.p; }
   al->g_ovf.ensure(2);

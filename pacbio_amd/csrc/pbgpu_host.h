@@ -389,6 +389,9 @@ struct pbgpu_aligner {
   dbuf<uint64_t> g_poff;
   dbuf<uint32_t> g_pre, g_sizes;
   dbuf<GDesc> g_desc;
+  dbuf<uint32_t> g_spo;
+  dbuf<double> g_fd;
+  dbuf<uint32_t> g_fu0;
   dbuf<double> g_bmax;
   dbuf<double2> g_imp;
   dbuf<GraphNode> g_out;

@@ -245,6 +245,11 @@ struct GraphDev {
   uint2* pp;                  // prefix sums along the name: {unitig lengths, info[2u] - info[2u - 1]}
   uint32_t* ounits;           // the name's unitigs in the record's orientation (at poff)
   GDesc* desc;                // per read, in sorted order
+  uint32_t* spo;              // per sorted position: its record's poff (loaded beside desc)
+  // per sorted position, the fields k_graph_edges' prefilter reads, one array each (a scan
+  // reads them coalesced): implied start, end, error, first unitig of the name
+  double *fis, *fie, *fer;
+  uint32_t* fu0;
   // per 64 sorted positions of the batch (q >> 6): the largest imp_e of its nodes with
   // imp_s > 1 (NaN as +inf; -inf if none): k_graph_edges skips a whole block when node i
   // is past it by more than 31 (every node of it is "not advancing", overlap_graph.cc:20)

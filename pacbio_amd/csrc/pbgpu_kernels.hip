@@ -3229,6 +3229,8 @@ DEV void graph_write_desc(const GraphDev& G, uint64_t at, uint64_t b, uint32_t i
 #pragma unroll
   for (uint32_t u = 0; u < GRAPH_U; ++u) d.u[u] = u < ns ? G.ounits[po + u] : 0u;
   G.desc[at] = d;
+  G.spo[at] = (uint32_t)po;  // (< 2^32: host check)
+  G.fis[at] = m.x; G.fie[at] = m.y; G.fer[at] = R.avg_err; G.fu0[at] = d.u[0];
 }
 constexpr uint32_t GRAPH_PREP_U = 8;  // names of at most this many unitigs: loads batched in registers
 __global__ void k_graph_sizes(GraphDev G, uint64_t n, uint32_t* sizes) {
@@ -3365,7 +3367,8 @@ __global__ __launch_bounds__(GRAPH_SORT_BLOCK) void k_graph_sort(GraphDev G, uin
 // the batch; the window's nodes and the GE_SLOTS - GE_NODES positions after them
 // (implied span, error, name size, first GRAPH_U unitigs, read bounds) are staged
 // in LDS; a wave per node i, lanes j = i + 1 + lane, ... 64 at a time until the
-// reference's break (positions past the staged ones are read from HBM).  Each node
+// reference's break (past the staged positions, a prefilter over per-field arrays in HBM
+// queues the positions that can break or be an edge, tested 64 at a time).  Each node
 // writes its first GRAPH_EBLK edges, in j order, as {j's record index | (unitigs
 // added) << 16, path increment} into a block of its own, and its exact count
 // (ecnt); a node with more (2 in 28k on C2) is listed, with its region past the
@@ -3379,7 +3382,12 @@ static_assert(GRAPH_NMAX_BIG <= 0xFFFFu, "an edge holds its node j in 16 bits");
 #ifndef PBGPU_GE_SLOTS
 #define PBGPU_GE_SLOTS 192  // (round 5: 384 -> 192 with 8 waves a SIMD, below)
 #endif
-constexpr uint32_t GE_NODES = 64, GE_SLOTS = PBGPU_GE_SLOTS, GE_BLOCK = 256;
+#ifndef PBGPU_GE_DIRECT_FAR
+#define PBGPU_GE_DIRECT_FAR 0
+#endif
+// GE_DIRECT_FAR: chunks past the staged window a scan still tests directly before it turns
+// to the prefilter queue (short scans, C2's, end within them)
+constexpr uint32_t GE_NODES = 64, GE_SLOTS = PBGPU_GE_SLOTS, GE_BLOCK = 256, GE_DIRECT_FAR = PBGPU_GE_DIRECT_FAR;
 
 DEV bool graph_on_device(const GraphDev& G, uint32_t n) { return n > 0 && n <= G.nmax && n <= GRAPH_NMAX_BIG; }
 // super_read_name::overlap (super_read_name.cc:49-72) in registers for a name i of SA
@@ -3435,11 +3443,12 @@ __attribute__((amdgpu_waves_per_eu(PBGPU_GE_WAVES, PBGPU_GE_WAVES)))
 __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n_recs, uint64_t n_ovf) {
   __shared__ double s_is[GE_SLOTS], s_ie[GE_SLOTS], s_er[GE_SLOTS];
   __shared__ uint32_t s_meta[GE_SLOTS], s_lpa[GE_SLOTS], s_po[GE_SLOTS];
-  __shared__ double s_rl[GE_NODES];    // node i's read length, scan end and read base: the
+  __shared__ double s_rl[GE_NODES];    // node i's read length and scan end: the
   __shared__ uint32_t s_end[GE_NODES];  // window's nodes only (OVF: WAVES <= GE_NODES slots)
-  __shared__ uint32_t s_rb[GE_NODES];
   __shared__ uint32_t s_u[GRAPH_U * GE_SLOTS];  // [u * GE_SLOTS + slot]
   constexpr uint32_t WAVES = GE_BLOCK / 64;
+  __shared__ uint32_t s_q[WAVES * 128];  // a wave's queue of positions to test in full
+  uint32_t* const sq = s_q + (threadIdx.x >> 6) * 128;
   // OVF: slot t holds listed node blockIdx.x * WAVES + t; nothing else is staged
   const uint64_t q0 = (uint64_t)blockIdx.x * (OVF ? WAVES : GE_NODES);
   if (q0 >= (OVF ? n_ovf : n_recs)) return;
@@ -3458,11 +3467,10 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
     if (dev) d = G.desc[q];
     s_is[t] = d.imp_s; s_ie[t] = d.imp_e; s_er[t] = d.err;
     s_meta[t] = d.idx | ((uint32_t)d.nsz << 16); s_lpa[t] = d.lp_add;
-    s_po[t] = dev ? (uint32_t)G.poff[e - n + d.idx] : 0u;  // < 2^32 (host check)
+    s_po[t] = dev ? G.spo[q] : 0u;
     if (t < GE_NODES) {
       s_rl[t] = (double)(G.roff[r + 1] - G.roff[r]);
       s_end[t] = dev ? (uint32_t)e : (uint32_t)(q + 1);  // a read left to the host: no scan
-      s_rb[t] = (uint32_t)(e - n);  // (record indices < 2^32: rec_cap)
     }
 #pragma unroll
     for (uint32_t u = 0; u < GRAPH_U; ++u) s_u[u * GE_SLOTS + t] = d.u[u];
@@ -3475,7 +3483,6 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
     const uint64_t q = OVF ? G.ovf_list[q0 + ti] : q0 + ti;
     const uint32_t qe = s_end[ti];
     const double ie_i = s_ie[ti], err_i = s_er[ti];
-    const uint32_t rb_i = s_rb[ti];  // node i's read base: j's name offset is G.poff[rb_i + idx_j]
     uint32_t cnt = 0;
 #ifdef PBGPU_PROF
     uint64_t ge_seen = 0, ge_far = 0, ge_cand = 0;
@@ -3518,10 +3525,48 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
         }
         return (b0 << 6) > j0 ? b0 << 6 : j0;
       };
-      // the chunk [j0, j0 + 64) for node i; true at the reference's break
-      auto chunk = [&](uint64_t j0) -> bool {
+      // The prefilter of the chunk [j0, j0 + 64): the positions that can be the reference's
+      // break or an edge of node i, a superset of both -- not skipped, and the break test
+      // itself or j's first unitig among i's unitigs 1 .. sa - 1 (super_read_name::overlap
+      // matches name_j[0] at some t >= 1 of name_i; every position for names longer than
+      // GRAPH_U).  Four fields a position, staged or from the per-field arrays (coalesced);
+      // positions past the first break are dropped.  brk: the chunk holds the break.
+      auto pre = [&](uint64_t j0, bool& brk) -> uint64_t {
         const uint64_t j = j0 + lane;
         const bool act = j < qe;
+        const uint64_t jj = act ? j : q;
+        const uint32_t sj = (uint32_t)(jj - q0);
+        const bool staged = !OVF && sj < ns;
+        double is_j, ie_j, er_j;
+        uint32_t u0;
+        if (staged) {
+          is_j = s_is[sj]; ie_j = s_ie[sj]; er_j = s_er[sj]; u0 = s_u[sj];
+        } else {
+          is_j = G.fis[jj]; ie_j = G.fie[jj]; er_j = G.fer[jj]; u0 = G.fu0[jj];
+        }
+        const bool skip = (is_j <= 1.0) | (ie_i > __dadd_rn(ie_j, 31.0));
+        const double position_len = __dadd_rn(ie_i, -is_j);
+        const double error = __dmul_rn(G.nb_errors, __dadd_rn(err_i, er_j));
+        const bool b = act & !skip & (__dadd_rn(__dmul_rn(position_len, play), error) < kd);
+        bool m = sa_u > GRAPH_U;
+#pragma unroll
+        for (uint32_t t = 1; t < GRAPH_U; ++t) m |= (t < sa_u) & (a[t] == u0);
+        uint64_t pm = __ballot(act & !skip & (b | m));
+        const uint64_t bm = __ballot(b);
+        brk = bm != 0;
+        if (brk) pm &= bm ^ (bm - 1);  // through the first break
+#ifdef PBGPU_PROF
+        ge_seen += (uint64_t)__builtin_popcountll(__ballot(act));
+        ge_far += (uint64_t)__builtin_popcountll(__ballot(act & !staged));
+#endif
+        return pm;
+      };
+      // node i's tests on the chunk [x, x + 64) (direct) or on the queued positions sq[0 .. x),
+      // in j order; true at the reference's break
+      auto chunk = [&](uint64_t x, auto direct_c) -> bool {
+        constexpr bool direct = decltype(direct_c)::value;  // (two instantiations)
+        const bool act = direct ? x + lane < qe : lane < x;
+        const uint64_t j = direct ? x + lane : (act ? (uint64_t)sq[lane] : q);
         const uint32_t sj = (uint32_t)((act ? j : q) - q0);
         // node j: staged, or (a scan past the window) one 64-byte line from HBM.  Every load
         // is issued before the tests (measured: loading the name only where the name test
@@ -3531,14 +3576,15 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
         // too: C4r 159 -> 178 ms, C2 36.5 -> 38.8 at 5 waves a SIMD; against the 8-wave
         // kernel, 149 -> 162 / 298 / 562 ms at 5 / 6 / 8 waves, its registers spilling)
         double is_j, ie_j, er_j;
-        uint32_t mj, lpa_j, bu[GRAPH_U];
+        uint32_t mj, lpa_j, bu[GRAPH_U], po_j;
         const bool staged = !OVF && sj < ns;
         if (staged) {
-          is_j = s_is[sj]; ie_j = s_ie[sj]; er_j = s_er[sj]; mj = s_meta[sj]; lpa_j = s_lpa[sj];
+          is_j = s_is[sj]; ie_j = s_ie[sj]; er_j = s_er[sj]; mj = s_meta[sj]; lpa_j = s_lpa[sj]; po_j = 0;
 #pragma unroll
           for (uint32_t u = 0; u < GRAPH_U; ++u) bu[u] = s_u[u * GE_SLOTS + sj];
         } else {
           const GDesc dj = G.desc[act ? j : q];
+          po_j = G.spo[act ? j : q];  // (coalesced, issued with the node: no second round trip)
           is_j = dj.imp_s; ie_j = dj.imp_e; er_j = dj.err; mj = dj.idx | ((uint32_t)dj.nsz << 16); lpa_j = dj.lp_add;
 #pragma unroll
           for (uint32_t u = 0; u < GRAPH_U; ++u) bu[u] = dj.u[u];
@@ -3553,10 +3599,10 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
         const bool cand = act & !skip & (lane < fb) & (sa >= 2) & (sb >= 2);
         bool edge = false;
         int32_t nb = 0, common = 0;
-        // j's name offset (its prefix sums, and its units past GRAPH_U)
-        // (loaded where needed: issuing it for every candidate before the name test measured
-        // slower, C4r graph stage 154 -> 160 ms)
-        auto po_of_j = [&]() -> uint32_t { return staged ? s_po[sj] : (uint32_t)G.poff[rb_i + (mj & 0xFFFFu)]; };
+        // j's name offset (its prefix sums, and its units past GRAPH_U): staged, or loaded
+        // with the node.  (Round 5: the far nodes' offset came from G.poff by j's record
+        // index, a second dependent round trip; G.spo holds it by sorted position.)
+        auto po_of_j = [&]() -> uint32_t { return staged ? s_po[sj] : po_j; };
         if (cand) {
           bool same;
           if ((sa <= GRAPH_U) & (sb <= GRAPH_U)) {
@@ -3606,17 +3652,55 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
         }
         cnt += (uint32_t)__builtin_popcountll(em);
 #ifdef PBGPU_PROF
-        {
-          const uint64_t am = __ballot(act & (lane < fb));
-          ge_seen += (uint64_t)__builtin_popcountll(am);
-          ge_far += (uint64_t)__builtin_popcountll(am & __ballot(OVF || sj >= ns));
-          ge_cand += (uint64_t)__builtin_popcountll(__ballot(cand));
-        }
+        ge_cand += (uint64_t)__builtin_popcountll(__ballot(cand));
+        if (direct) ge_seen += (uint64_t)__builtin_popcountll(__ballot(act & (lane < fb)));
 #endif
         return bm != 0;
       };
-      for (uint64_t j0 = next_pos(q + 1); j0 < qe; j0 = next_pos(j0 + 64))
-        if (chunk(j0)) break;
+      // Chunks inside the staged window are tested directly (LDS loads are cheap).  Past it,
+      // the prefilter's positions are queued in j order (sq, up to 127) and tested in full
+      // 64 at a time: on repeat-rich reads few of the positions a long scan passes are
+      // candidates (C4r: 23 of 940 a node, 88% of them past the window), and a chunk with
+      // one cost a whole chunk of 64-byte node loads and tests.  A chunk holding the break
+      // ends the scan, the queue tested through it.  (C4r edges 97.5 -> 63.5 ms, C2 9.0 ->
+      // 10.3; the queue for the staged chunks too made C2 11.7 ms, and testing 2 or 5 chunks
+      // past the window directly first was slower on both: profiles/r05zw_*, r05zx_*.)
+      uint32_t qn = 0;
+      bool done = false;
+      uint64_t j0 = next_pos(q + 1);
+      const uint64_t win_end = OVF ? 0 : q0 + ns;
+      for (uint32_t nfar = 0; j0 < qe; j0 = next_pos(j0 + 64)) {
+        const bool far = (j0 + 64 < qe ? j0 + 64 : qe) > win_end;
+        if (far && nfar >= GE_DIRECT_FAR) break;  // a long scan: the queue from here
+        nfar += far ? 1u : 0u;
+        if (chunk(j0, std::true_type{})) { done = true; break; }
+      }
+      for (; j0 < qe && !done; j0 = next_pos(j0 + 64)) {
+        bool brk;
+        const uint64_t pm = pre(j0, brk);
+        if ((pm >> lane) & 1ull)
+          sq[qn + (uint32_t)__builtin_popcountll(pm & ((1ull << lane) - 1))] = (uint32_t)(j0 + lane);
+        qn += (uint32_t)__builtin_popcountll(pm);
+        if (qn >= 64 || brk) {
+          lds_fence();
+          done = chunk(qn < 64 ? qn : 64, std::false_type{});
+          if (qn > 64) {  // the rest to the front
+            const uint32_t v = lane + 64 < qn ? sq[lane + 64] : 0u;
+            lds_fence();
+            sq[lane] = v;
+            lds_fence();
+            qn -= 64;
+            if (!done && brk) done = chunk(qn, std::false_type{});
+          } else {
+            qn = 0;
+          }
+          done |= brk;
+        }
+      }
+      if (!done && qn) {
+        lds_fence();
+        chunk(qn, std::false_type{});
+      }
     }
 #ifdef PBGPU_PROF
     if (!OVF) {  // slots 128..130: positions scanned, of them past the staged window, candidates (name test)
