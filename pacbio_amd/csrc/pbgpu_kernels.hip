@@ -3542,7 +3542,15 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
         if (staged) {
           is_j = s_is[sj]; ie_j = s_ie[sj]; er_j = s_er[sj]; u0 = s_u[sj];
         } else {
+#ifndef PBGPU_GE_FLAT
+          // (global loads spelled out: the compiler made these four flat loads, which also
+          // count against the LDS counter the queue's waits use)
+          typedef const __attribute__((address_space(1))) double gdbl;
+          typedef const __attribute__((address_space(1))) uint32_t gu32;
+          is_j = ((gdbl*)G.fis)[jj]; ie_j = ((gdbl*)G.fie)[jj]; er_j = ((gdbl*)G.fer)[jj]; u0 = ((gu32*)G.fu0)[jj];
+#else
           is_j = G.fis[jj]; ie_j = G.fie[jj]; er_j = G.fer[jj]; u0 = G.fu0[jj];
+#endif
         }
         const bool skip = (is_j <= 1.0) | (ie_i > __dadd_rn(ie_j, 31.0));
         const double position_len = __dadd_rn(ie_i, -is_j);
@@ -3662,8 +3670,8 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
       // 64 at a time: on repeat-rich reads few of the positions a long scan passes are
       // candidates (C4r: 23 of 940 a node, 88% of them past the window), and a chunk with
       // one cost a whole chunk of 64-byte node loads and tests.  A chunk holding the break
-      // ends the scan, the queue tested through it.  (C4r edges 97.5 -> 63.5 ms, C2 9.0 ->
-      // 10.3; the queue for the staged chunks too made C2 11.7 ms, and testing 2 or 5 chunks
+      // ends the scan, the queue tested through it.  (C4r edges 97.5 -> 63.5 ms, 55.1 with the
+      // prefilter's global loads; C2 9.0 -> 10.3; the queue for the staged chunks too made C2 11.7 ms, and testing 2 or 5 chunks
       // past the window directly first was slower on both: profiles/r05zw_*, r05zx_*.)
       uint32_t qn = 0;
       bool done = false;
