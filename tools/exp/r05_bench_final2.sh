@@ -2,5 +2,5 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 900 python -u bench.py > gpurun_out/r05_bench2.json 2> gpurun_out/r05_bench2.err || { tail -30 gpurun_out/r05_bench2.err; exit 1; }
-tail -1 gpurun_out/r05_bench2.json | cut -c1-300
+timeout -k 10 900 python -u bench.py > gpurun_out/r05_bench3.json 2> gpurun_out/r05_bench3.err || { tail -30 gpurun_out/r05_bench3.err; exit 1; }
+tail -1 gpurun_out/r05_bench3.json | cut -c1-300
