@@ -258,6 +258,224 @@ def _cmr_runs(cmr, flags, steps):
     return runs
 
 
+def strong_split(n_total, world, rank):
+    """Rank `rank`'s reads of a strong-scaling run: the contiguous range [lo, hi) of
+    the n_total reads, equal counts (+-1), in rank order -- the reference's
+    split-and-cat of one read set over its jobs (mega_reads_assemble_cluster2.sh:325-354,
+    447: the read file split into batches, one create_mega_reads each, outputs
+    concatenated in batch order).  The generator draws read i from its own seed
+    (tools/pbsynth.cc: stream_seed(seed, 5, i)), so a rank makes exactly its reads."""
+    lo = n_total * rank // world
+    hi = n_total * (rank + 1) // world
+    return lo, hi
+
+
+def _chunk_cuts(off, chunk_bases):
+    """Read cuts of a resident batch into chunks of at most chunk_bases bases"""
+    cuts = [0]
+    for r in range(1, len(off)):
+        if int(off[r]) - int(off[cuts[-1]]) > chunk_bases and r - 1 > cuts[-1]:
+            cuts.append(r - 1)
+    cuts.append(len(off) - 1)
+    return cuts
+
+
+def _device_leg(pbgpu, index, akw, blob, off, chunk_bases, steps, comm, local, streams=1):
+    """The device path over resident reads (uploaded in chunks of <= chunk_bases before
+    the clock): one untimed pass, then `steps` timed passes between barriers and device
+    syncs; returns (max-over-ranks seconds, stats of the timed passes, chunk count)"""
+    cuts = _chunk_cuts(off, chunk_bases)
+    al = pbgpu.StreamAligner(index, streams=streams, **akw)
+    chunks = []
+    for r0, r1 in zip(cuts[:-1], cuts[1:]):
+        if r0 == 0 and r1 == len(off) - 1:
+            chunks.append(al.upload(blob=blob, offsets=off))
+        else:
+            b0, b1 = int(off[r0]), int(off[r1])
+            chunks.append(al.upload(blob=bytes(memoryview(blob)[b0:b1]), offsets=off[r0:r1 + 1] - off[r0]))
+    for c in chunks:
+        al.align_resident(c)
+    al.reset_stats()
+    pbgpu.device_synchronize(local)
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        for c in chunks:
+            al.align_resident(c)
+    pbgpu.device_synchronize(local)
+    comm.barrier()
+    el = comm.max(time.perf_counter() - t0)
+    st = al.stats()
+    for c in chunks:
+        al.free(c)
+    al.close()
+    return el, st, len(cuts) - 1
+
+
+def _per_kernel(st, steps, b_rand=None, b_filt=None, b_table=None, info=None):
+    """Every individually timed kernel's algorithmic bytes per launch, mean HIP-event
+    launch time and fraction of the HBM peak; k_seed also at its access
+    granularity against the mixed roof of gathers measured at the filter's and the
+    table's own sizes (b_filt, b_table)"""
+    kb = _kernel_bytes(st)
+    kms, kn = st["kernel_ms"], st["kernel_launches"]
+    per_kernel = {kk: {"alg_bytes_per_launch": kb[kk], "avg_launch_ms": round(kms[kk] / max(1, kn[kk]), 3),
+                       "achieved_gbs": round(kb[kk] / (kms[kk] / max(1, kn[kk]) * 1e-3) / 1e9, 1),
+                       "frac": round(kb[kk] / (kms[kk] / max(1, kn[kk]) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                       "stage_ms_per_step": round(st["ms_" + STAGE_OF[kk]] / steps, 3)}
+                  for kk in kb if kn.get(kk)}
+    if kn.get("k_seed"):
+        nl = kn["k_seed"]
+        sec = (st["n_bases"] + (st["n_filter"] + st["n_probes"]) * 64 + st["n_kept"] * 16) / nl
+        k_ms = kms["k_seed"] / nl
+        sgbs = sec / (k_ms * 1e-3) / 1e9
+        sv = {"bytes_per_launch": sec, "achieved_gbs": round(sgbs, 1), "frac": round(sgbs / HBM_PEAK_GBS, 4),
+              "frac_of_b_rand": round(sgbs / b_rand, 4) if b_rand else None,
+              "random_accesses_per_launch": (st["n_filter"] + st["n_probes"]) / nl}
+        if b_filt and b_table and info:
+            roof_ms = ((st["n_filter"] / nl) * 64 / (b_filt * 1e9) + (st["n_probes"] / nl) * 64 / (b_table * 1e9) +
+                       ((st["n_bases"] + st["n_kept"] * 16) / nl) / (HBM_PEAK_GBS * 1e9)) * 1e3
+            sv["mixed_roof"] = {"b_filter_gbs": round(b_filt, 1), "filter_bytes": info["filter_bytes"],
+                                "b_table_gbs": round(b_table, 1), "table_bytes": info["table_buckets"] * 64,
+                                "roof_ms": round(roof_ms, 3), "launch_ms": round(k_ms, 3),
+                                "frac": round(roof_ms / k_ms, 4)}
+        per_kernel["k_seed"]["sector_view"] = sv
+    return per_kernel
+
+
+def _path_roofline(st, steps, el):
+    """SURVEY 8(d)'s whole-path algorithmic bytes of a device leg per step"""
+    path_bytes = (0.25 * st["n_bases"] + 64 * st["n_probes"] + 8 * st["n_hits"] + 16 * st["n_hits"] +
+                  16 * st["n_lis_tests"] + 96 * st["n_records"]) / steps
+    gbs = path_bytes / (el / steps) / 1e9
+    return {"bytes_alg_per_step": path_bytes, "achieved": gbs, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+            "formula": "0.25*bases + 64*probes + 8*occurrences + 16*hits + 16*lis_tests + 96*records (SURVEY 8d)"}
+
+
+PROD_KW = dict(forward=True, unitigs_k=31, bases_matching=15.0, max_count=5000, stretch_cap=10000.0)
+
+
+def c4_leg(args, comm, rank, world, local, threads, pbgpu, Dataset, brand=True):
+    """BASELINE configs[3], the configuration north_star targets: the full C4 index (10M
+    super-reads, ~10 Gbp of text over a 250 Mbp genome with 2% 5-50-copy repeats, built on
+    the GPU -- in partitions when its sort does not fit -- from the generator's buffers)
+    and this GPU's share of the 2M reads of 15 kb N50 (--c4-reads, 250k = 2M / 8; weak:
+    every rank its own share, index replicated), production flags, reads resident, one
+    aligner.  Unlike C2's 16 MB presence filter, C4's filter and table are far past the
+    256 MB Infinity Cache, so k_seed is priced with gathers measured at their sizes."""
+    t0 = time.time()
+    ds = Dataset("C4", seed=42, threads=min(threads, 16), n_pb=args.c4_reads, pb_index_base=rank * args.c4_reads)
+    gen_s = time.time() - t0
+    t0 = time.time()
+    ix = pbgpu.Index.from_pointers(*ds.sr_pointers(), k=17, device=local)
+    pbgpu.device_synchronize(local)
+    build_s = time.time() - t0
+    info = ix.info()
+    b_filt = b_table = None
+    if brand:
+        b_filt = pbgpu.measure_gather(local, max(1 << 20, info["filter_bytes"])) if info["filter_bytes"] else None
+        b_table = pbgpu.measure_gather(local, max(1 << 20, info["table_buckets"] * 64))
+    akw = dict(PROD_KW, k=17, unitig_lengths=ds.unitig_lengths)
+    blob, off = ds.pb_blob()
+    bases = int(off[-1])
+    steps = max(1, args.device_steps)
+    el, st, nch = _device_leg(pbgpu, ix, akw, blob, off, args.device_chunk_bases, steps, comm, local)
+    # size-independent properties of the output (the oracle cannot hold this index): the
+    # first reads' records, sorted per read, inside their read and super-read
+    al = pbgpu.Aligner(ix, **akw)
+    ns = min(200, ds.pb.n)
+    rr = al.upload(blob=bytes(memoryview(blob)[:int(off[ns])]), offsets=off[:ns + 1])
+    al.align_resident(rr)
+    co = al.download()
+    rr.close()
+    al.close()
+    import numpy as np
+    r = co.records
+    sr_off = np.ctypeslib.as_array(ds.sr.off, shape=(ds.sr.n + 1,))
+    sr_len = (sr_off[1:] - sr_off[:-1]).astype(np.int64)
+    rl = np.diff(off[:ns + 1].astype(np.int64))
+    rid = np.repeat(np.arange(co.n_reads), np.diff(co.read_offsets.astype(np.int64)))
+    props = bool(len(r) > 0 and np.all(r["ql"].astype(np.int64) == sr_len[r["sr_index"]]) and
+                 np.all((1 <= r["rs"]) & (r["rs"] <= r["re"]) & (r["re"] <= rl[rid])) and
+                 np.all((1 <= r["qs"]) & (r["qs"] <= r["qe"]) & (r["qe"].astype(np.int64) <= r["ql"].astype(np.int64))))
+    key = r["rs"].astype(np.int64) * (1 << 32) + r["re"].astype(np.int64)
+    same = rid[1:] == rid[:-1]
+    props &= bool(np.all(key[1:][same] >= key[:-1][same]))
+    ix.close()
+    ds.close()
+    total = comm.sum(bases)
+    per_kernel = _per_kernel(st, steps, None, b_filt, b_table, info)
+    dom = max(per_kernel, key=lambda kk: per_kernel[kk]["stage_ms_per_step"])
+    return {
+        "workload": ("C4 chr1-scale (BASELINE configs[3]): full index of 10M super-reads over a 250 Mbp genome with "
+                     "2% 5-50-copy repeats, built on this GPU; PacBio reads of 15 kb N50 (lognormal mean 12.5 kb, "
+                     f"sigma 0.6), {args.c4_reads} per GPU (2M / 8 at N = 8), production flags, reads resident"),
+        "scaling": "weak",
+        "bases_per_gpu": bases,
+        "value_device": total * steps / el,
+        "value_device_note": "reads resident in HBM, device path to sorted records in HBM, one aligner per GPU",
+        "ms_per_step": el / steps * 1e3,
+        "chunks": nch,
+        "stage_ms_per_step": {s: round(st["ms_" + s] / steps, 3) for s in ("seed", "group", "lis", "fit", "records")},
+        "counters_per_base": {n: st[n] / max(1, st["n_bases"]) for n in
+                              ("n_kmers", "n_filter", "n_probes", "n_kept", "n_hits", "n_chains", "n_lis_tests",
+                               "n_records")},
+        "kernel_ms_per_launch": {kk: round(st["kernel_ms"][kk] / max(1, st["kernel_launches"][kk]), 3)
+                                 for kk in st["kernel_ms"]},
+        "kernel_launches": dict(st["kernel_launches"]),
+        "group_refines_per_step": st["group_refines"] / steps,
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": per_kernel[dom]["achieved_gbs"],
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": per_kernel[dom]["frac"], "by_kernel": per_kernel},
+        "path_roofline": _path_roofline(st, steps, el),
+        "index": {"n_sr": info["n_sr"], "text_len": info["text_len"], "n_kmers": info["n_kmers"],
+                  "device_bytes": info["device_bytes"], "filter_bytes": info["filter_bytes"],
+                  "table_bytes": info["table_buckets"] * 64, "build_s": round(build_s, 3),
+                  "generate_s": round(gen_s, 3)},
+        "properties_ok": comm.sum(1.0 if props else 0.0) == world,
+        "properties": f"first {ns} reads of each rank: records per read in (rs, re) order, inside their read and "
+                      "super-read, ql = the super-read's length",
+    }
+
+
+def c3_leg(args, comm, rank, world, local, threads, pbgpu, Dataset):
+    """BASELINE configs[2] as a strong-scaling run: the 300k C3 reads (--c3-reads) split over
+    the job's ranks (strong_split), the 1M-super-read k=21 index replicated (every rank
+    builds its own), production flags, reads resident, one aligner per GPU.  `value_device`
+    = all the reads' bases / the max-over-ranks time, so at N ranks it is the whole job's
+    rate on a fixed read set."""
+    lo, hi = strong_split(args.c3_reads, world, rank)
+    t0 = time.time()
+    ds = Dataset("C3", seed=42, threads=min(threads, 16), n_pb=max(1, hi - lo), pb_index_base=lo)
+    gen_s = time.time() - t0
+    t0 = time.time()
+    ix = pbgpu.Index.from_pointers(*ds.sr_pointers(), k=21, device=local)
+    pbgpu.device_synchronize(local)
+    build_s = time.time() - t0
+    akw = dict(PROD_KW, k=21, unitig_lengths=ds.unitig_lengths)
+    blob, off = ds.pb_blob()
+    bases = int(off[-1]) if hi > lo else 0
+    steps = max(1, args.device_steps)
+    el, st, nch = _device_leg(pbgpu, ix, akw, blob, off, args.device_chunk_bases, steps, comm, local)
+    ix.close()
+    ds.close()
+    total = comm.sum(bases)
+    return {
+        "workload": ("C3 yeast-scale (BASELINE configs[2]): 1M super-reads, k=21, index replicated per GPU; "
+                     f"{args.c3_reads} PacBio reads (mean 12 kb) split over the ranks, production flags, reads resident"),
+        "scaling": "strong",
+        "reads_total": args.c3_reads,
+        "reads_this_rank": [lo, hi],
+        "bases_total": total,
+        "value_device": total * steps / el,
+        "value_device_note": "all ranks' bases / max-over-ranks time; one aligner per GPU, records in HBM",
+        "ms_per_step": el / steps * 1e3,
+        "chunks_rank0": nch,
+        "stage_ms_per_step_rank0": {s: round(st["ms_" + s] / steps, 3) for s in ("seed", "group", "lis", "fit", "records")},
+        "index_build_s": round(build_s, 3),
+        "generate_s": round(gen_s, 3),
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -296,6 +514,14 @@ def main():
                          "create_mega_reads and the CPU oracle on the same reads, reported under c4r")
     ap.add_argument("--c4r-cmr-steps", type=int, default=2, help="timed create_mega_reads runs of the C4r leg")
     ap.add_argument("--c4r-cpu-seconds", type=float, default=8.0, help="target C4r CPU-oracle sample duration")
+    ap.add_argument("--c4-reads", type=int, default=250000,
+                    help="reads per GPU of the C4 leg (BASELINE configs[3]: the full 10M-super-read index, 15-kb-N50 "
+                         "reads; 2M / 8 = 250k; 0 = no such leg), reported under c4")
+    ap.add_argument("--c3-reads", type=int, default=300000,
+                    help="reads of the C3 strong-scaling leg (BASELINE configs[2]: 300k reads split over the ranks, "
+                         "index replicated; 0 = no such leg), reported under c3")
+    ap.add_argument("--only", choices=["c4", "c3"], default=None,
+                    help="run only this leg and print its object (profiling runs)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU work: the ranks meet at the barrier and rank 0 prints n_gpus (launch rehearsal)")
     args = ap.parse_args()
@@ -313,6 +539,18 @@ def main():
         return
     from pacbio_amd import pbgpu
     from tools.synth import Dataset, PRESETS
+
+    if args.only:
+        ndev = _device_count()
+        if ndev > 0:
+            local %= ndev
+        if args.only == "c4":
+            leg = c4_leg(args, comm, rank, world, local, _cpu_share(), pbgpu, Dataset, brand=not args.no_brand)
+        else:
+            leg = c3_leg(args, comm, rank, world, local, _cpu_share(), pbgpu, Dataset)
+        if rank == 0:
+            print(json.dumps({"only": args.only, "n_gpus": world, args.only: leg}), flush=True)
+        return
 
     # more ranks than visible GPUs (a rehearsal of the N>1 launch on a 1-GPU box): ranks share
     ndev = _device_count()
@@ -766,6 +1004,16 @@ def main():
         c4["ds"].close()
         shutil.rmtree(c4["wd"], ignore_errors=True)
 
+    # ---- the C3 strong-scaling leg and the C4 leg (BASELINE configs[2] and [3]), after the C2
+    # index is freed: every rank runs them (their collectives too)
+    index_info_c2 = info
+    index.close()
+    index = None
+    c3_out = c3_leg(args, comm, rank, world, local, threads, pbgpu, Dataset) if args.c3_reads > 0 else None
+    c4_full = c4_leg(args, comm, rank, world, local, threads, pbgpu, Dataset, brand=not args.no_brand) \
+        if args.c4_reads > 0 else None
+    info = index_info_c2
+
     # SURVEY 8(d)'s whole-path algorithmic bytes of the device leg: 2-bit read stream,
     # 64-B index probes, occurrences enumerated (8 B), hits grouped (write + read, 16 B),
     # LIS predecessor tests (16 B), records out (96 B)
@@ -878,9 +1126,10 @@ def main():
                          "by_kernel": per_kernel},
             "cpu_baseline": cpu,
             "c4r": c4_out,
+            "c3": c3_out,
+            "c4": c4_full,
         }
         print(json.dumps(out), flush=True)
-    index.close()
     shutil.rmtree(wd, ignore_errors=True)
 
 

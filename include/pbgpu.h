@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PBGPU_ABI_VERSION 7
+#define PBGPU_ABI_VERSION 8
 
 typedef enum pbgpu_status {
   PBGPU_OK = 0,
@@ -63,6 +63,13 @@ pbgpu_status pbgpu_measure_gather(int device, uint64_t buffer_bytes, double* gbp
  * pbgpu_measure_gather) or 512 (random 512-B runs read as 64 consecutive 8-B
  * words, the shape of k_group's occurrence-list reads). */
 pbgpu_status pbgpu_measure_gather_shape(int device, uint64_t buffer_bytes, uint32_t unit_bytes, double* gbps);
+/* Measurement aid: k_group's occurrence-read shape (runs of 52 consecutive 8-B words at
+ * random 8-B-aligned starts): mode 0 reads the 4-B id half of each word (pass 0), mode 1
+ * the 8-B words (pass 1), mode 2 both passes over the same runs, as k_group does.  Per
+ * launch: the 64-B sectors and 128-B lines the runs span and the algorithmic bytes, the
+ * known counts to read FETCH_SIZE against; *gbps = sector bytes per second. */
+pbgpu_status pbgpu_measure_group_shape(int device, uint64_t buffer_bytes, int mode, double* gbps, uint64_t* sectors64,
+                                       uint64_t* lines128, uint64_t* alg_bytes);
 /* Self-check of the fit's reciprocal (least_square_2d.hpp:47-67 divides by the
  * point count n): the device's shortened RN(1/n) against a correctly rounded
  * division for every n in [1, n_max]; *mismatches = the count that differ
@@ -267,6 +274,9 @@ typedef struct {
    * overflowing the 8192-slot table (instead of an HBM table), and reads grouped
    * in HBM tables */
   uint64_t group_refines, group_hbm_reads;
+  /* ABI 8: group-stage work items (a read, or one hash partition of a long read's
+   * super-reads) whose table overflowed, summed over the rounds */
+  uint64_t group_overflow_items;
 } pbgpu_stats;
 pbgpu_status pbgpu_aligner_get_stats(const pbgpu_aligner* al, pbgpu_stats* s);
 pbgpu_status pbgpu_aligner_reset_stats(pbgpu_aligner* al);

@@ -106,8 +106,9 @@ void launch_rec_scatter(const uint32_t* rec_read, uint32_t n, const uint64_t* re
 void launch_rec_place(const uint32_t* rec_read, const uint32_t* rec_slot, uint32_t n, const uint64_t* rec_off,
                       uint32_t* order, hipStream_t st);
 int rec_sort_lcap();
+uint64_t rec_sort_max_tiles(uint64_t nrec);
 void launch_rec_sort(const Rec* recs, const uint64_t* rec_off, const uint32_t* order, uint64_t* gscratch,
-                     uint32_t n_reads, Rec* out, hipStream_t st);
+                     uint32_t n_reads, uint64_t nrec, uint2* tiles, uint32_t* ctr, Rec* out, hipStream_t st);
 }  // namespace pbgpu
 
 using namespace pbgpu;
@@ -725,7 +726,117 @@ __global__ __launch_bounds__(256) void k_gather_runs(const uint2* __restrict__ b
   }
   if ((acc.x & 0xFFFFF) == 0x12345) sink[gid & 1023] = acc;
 }
+// The exact access shape of k_group's occurrence reads (round 6, to calibrate FETCH_SIZE
+// for it): a wave takes RUNS runs of GG_RUN consecutive 8-B words at random 8-B-aligned
+// starts (a k-mer's occurrence list; C2's mean is ~52), lanes 0..GG_RUN-1 one word each.
+// MODE 0: k_group's pass 0 alone -- the 4-B super-read id, the high half of each word
+// (stride 8 B); MODE 1: pass 1 alone -- the whole 8-B word; MODE 2: both, as k_group
+// runs them, all of a wave's runs in pass 0 and then all of them again in pass 1 (a
+// wave's RUNS runs, ~416 KB, stand for one read's lists: with every wave of the chip in
+// flight the second reads find nothing of the first in L2 or the Infinity Cache).
+// The wave counts the 64-B sectors and 128-B lines its runs span (sec[0], sec[1], each
+// pass counted) so FETCH_SIZE can be read against a known byte count.
+constexpr uint32_t GG_RUN = 52, GG_RUNS = 1024, GG_UNR = 8;
+extern "C++" {
+template <int MODE>
+__global__ __launch_bounds__(256) void k_gather_group(const uint2* __restrict__ buf, uint64_t n_words, uint32_t seed,
+                                                      unsigned long long* __restrict__ sec, uint2* __restrict__ sink) {
+  const uint64_t wv = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t lane = threadIdx.x & 63;
+  const bool on = lane < GG_RUN;
+  const uint64_t span = n_words - GG_RUN;
+  auto start = [&](uint32_t r) -> uint64_t {
+    uint64_t h = (wv * GG_RUNS + r) * 0x9E3779B97F4A7C15ull + (uint64_t)seed * 0xBF58476D1CE4E5B9ull;
+    h ^= h >> 31; h *= 0xD6E8FEB86659FD93ull; h ^= h >> 32;
+    return h % span;
+  };
+  const uint32_t* w32 = reinterpret_cast<const uint32_t*>(buf);
+  uint32_t acc = 0;
+  unsigned long long s64 = 0, l128 = 0;
+  for (int pass = (MODE == 1 ? 1 : 0); pass <= (MODE == 0 ? 0 : 1); ++pass) {
+    for (uint32_t r0 = 0; r0 < GG_RUNS; r0 += GG_UNR) {
+      uint32_t v[GG_UNR];
+#pragma unroll
+      for (uint32_t u = 0; u < GG_UNR; ++u) {
+        const uint64_t w = start(r0 + u) + (on ? lane : 0);
+        if (pass == 0) {
+          v[u] = w32[2 * w + 1];
+        } else {
+          const uint2 x = buf[w];
+          v[u] = x.x ^ x.y;
+        }
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < GG_UNR; ++u) acc ^= on ? v[u] : 0u;
+      if (lane == 0) {
+#pragma unroll
+        for (uint32_t u = 0; u < GG_UNR; ++u) {
+          const uint64_t b0 = start(r0 + u) * 8, b1 = b0 + GG_RUN * 8 - 1;
+          s64 += (b1 >> 6) - (b0 >> 6) + 1;
+          l128 += (b1 >> 7) - (b0 >> 7) + 1;
+        }
+      }
+    }
+  }
+  if (lane == 0) { atomicAdd(&sec[0], s64); atomicAdd(&sec[1], l128); }
+  if ((acc & 0xFFFFF) == 0x12345) sink[(wv * 64 + lane) & 1023] = make_uint2(acc, 0);
+}
+}  // extern "C++"
 }  // namespace
+
+pbgpu_status pbgpu_measure_group_shape(int device, uint64_t buffer_bytes, int mode, double* gbps, uint64_t* sectors64,
+                                       uint64_t* lines128, uint64_t* alg_bytes) {
+  if (!gbps || buffer_bytes < (64u << 20) || mode < 0 || mode > 2) return fail(PBGPU_ERR_INVALID, "bad argument");
+  API_TRY
+  HIPCHK(hipSetDevice(device));
+  dbuf<uint2> buf, sink;
+  dbuf<unsigned long long> sec;
+  const uint64_t n_words = buffer_bytes / 8;
+  buf.ensure_fixed(n_words);
+  HIPCHK(hipMemset(buf.p, 0x5A, n_words * 8));
+  sink.ensure_fixed(1024);
+  sec.ensure_fixed(2);
+  hipDeviceProp_t pr;
+  HIPCHK(hipGetDeviceProperties(&pr, device));
+  const uint32_t blocks = (uint32_t)pr.multiProcessorCount * 8;
+  hipStream_t st;
+  HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  hipEvent_t e0, e1;
+  HIPCHK(hipEventCreate(&e0)); HIPCHK(hipEventCreate(&e1));
+  auto launch = [&](uint32_t seed) {
+    if (mode == 0)
+      hipLaunchKernelGGL(k_gather_group<0>, dim3(blocks), dim3(256), 0, st, buf.p, n_words, seed, sec.p, sink.p);
+    else if (mode == 1)
+      hipLaunchKernelGGL(k_gather_group<1>, dim3(blocks), dim3(256), 0, st, buf.p, n_words, seed, sec.p, sink.p);
+    else
+      hipLaunchKernelGGL(k_gather_group<2>, dim3(blocks), dim3(256), 0, st, buf.p, n_words, seed, sec.p, sink.p);
+  };
+  launch(3u);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemsetAsync(sec.p, 0, 16, st));
+  HIPCHK(hipEventRecord(e0, st));
+  const int reps = 3;
+  for (int r = 0; r < reps; ++r) launch(5u + 2u * r);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(e1, st));
+  HIPCHK(hipEventSynchronize(e1));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+  unsigned long long h[2];
+  HIPCHK(hipMemcpy(h, sec.p, 16, hipMemcpyDeviceToHost));
+  const double runs = (double)blocks * 4 * GG_RUNS * (mode == 2 ? 2 : 1);  // run reads per launch
+  const double alg = (double)blocks * 4 * GG_RUNS * GG_RUN * (mode == 0 ? 4.0 : mode == 1 ? 8.0 : 12.0);
+  (void)runs;
+  // per launch: the sectors / lines the runs span, and the algorithmic bytes (4 B a word in
+  // pass 0, 8 B in pass 1); the rate is the 64-B-sector bytes moved per second
+  if (sectors64) *sectors64 = h[0] / reps;
+  if (lines128) *lines128 = h[1] / reps;
+  if (alg_bytes) *alg_bytes = (uint64_t)alg;
+  *gbps = (double)h[0] * 64.0 / (ms * 1e-3) / 1e9;
+  (void)hipEventDestroy(e0); (void)hipEventDestroy(e1); (void)hipStreamDestroy(st);
+  return PBGPU_OK;
+  API_CATCH
+}
 
 pbgpu_status pbgpu_measure_gather(int device, uint64_t buffer_bytes, double* gbps) {
   return pbgpu_measure_gather_shape(device, buffer_bytes, 64, gbps);
@@ -1256,6 +1367,7 @@ pbgpu_status pbgpu_aligner_create(const pbgpu_index* ix, const pbgpu_align_param
   al->info_count.alloc(1);
   al->counters.alloc(128);
   al->n32total.alloc(1);
+  al->rec_tile_ctr.alloc(2);
   *out = al.release();
   return PBGPU_OK;
   API_CATCH
@@ -1687,8 +1799,11 @@ static void records_stage(pbgpu_aligner* al, uint32_t n, uint32_t nrec, bool tim
   al->recs_sorted.ensure(nrec + 1);
   if (counted) launch_rec_place(al->rec_read.p, al->rec_slot.p, nrec, al->rec_off.p, al->order.p, st);
   else launch_rec_scatter(al->rec_read.p, nrec, al->rec_off.p, al->rec_cursor.p, al->order.p, st);
+  uint2* tiles = dead.take(al->rec_tiles, rec_sort_max_tiles(nrec));
+  HIPCHK(hipMemsetAsync(al->rec_tile_ctr.p, 0, 8, st));
   if (timed) HIPCHK(hipEventRecord(al->ev[15], st));
-  launch_rec_sort(al->recs.p, al->rec_off.p, al->order.p, sort_keys, n, al->recs_sorted.p, st);
+  launch_rec_sort(al->recs.p, al->rec_off.p, al->order.p, sort_keys, n, nrec, tiles, al->rec_tile_ctr.p,
+                  al->recs_sorted.p, st);
   HIPCHK(hipGetLastError());
 }
 
@@ -1989,7 +2104,9 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
   // KRec of the chunk's bases: the kernels index it by absolute base offset (roff), so the
   // pointer handed to them is shifted back by the chunk's first base
   al->krec.ensure_capped(h_roff[c1] - cb0 + 1, al->base_cap ? al->base_cap + 1 : ~(size_t)0);
-  KRec* const krec = al->krec.p - cb0;
+  // (as an address computation: the shifted pointer lies below the allocation when cb0 > 0,
+  // and the kernels only index it at offsets >= cb0)
+  KRec* const krec = reinterpret_cast<KRec*>(reinterpret_cast<uintptr_t>(al->krec.p) - (uintptr_t)cb0 * sizeof(KRec));
   HIPCHK(hipEventRecord(al->ev[0], st));
   launch_seed(seed_mode, v, rd->seq.p, rd->off.p + c0, ncr, al->P, krec, al->n_kept.p + c0, al->thr.p + c0,
               al->nhits.p + c0, al->stats.p, gcount, ix->null_ptr, st);
@@ -2060,7 +2177,14 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
       std::vector<uint2>& rs = al->h_small;
       std::vector<uint2>& rb = al->h_big;
       rs.clear(); rb.clear();
+      // tests: PBGPU_GROUP_FIRST_P=P puts every read in the smallest table as P hash-partition
+      // items, so a one-read call can overflow P items at once
+      const uint32_t first_p = getenv("PBGPU_GROUP_FIRST_P") ? (uint32_t)atoi(getenv("PBGPU_GROUP_FIRST_P")) : 0;
       for (uint32_t r : rl) {
+        if (first_p) {
+          for (uint32_t q = 0; q < std::min<uint32_t>(first_p, 4096); ++q) rs.push_back(group_item(r, q, std::min<uint32_t>(first_p, 4096)));
+          continue;
+        }
         const double pred = (double)(hoff[r + 1] - hoff[r]) * al->chains_per_hit * pred_scale;
         if (pred <= fill_small) { rs.push_back(group_item(r, 0, 1)); continue; }
         const uint32_t P = (uint32_t)std::min(4096.0, std::max(1.0, std::ceil(pred / fill_big)));
@@ -2071,6 +2195,11 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
       al->acc.ms_host_order += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count();
       al->read_list.ensure(rs.size());
       HIPCHK(hipMemcpyAsync(al->read_list.p, rs.data(), rs.size() * sizeof(uint2), hipMemcpyHostToDevice, st));
+      // every work item of the first round may overflow (a read split in P items holds P of
+      // them): the overflow list holds one entry per item, not one per read
+      al->ovf_items.ensure(rs.size()); al->ovf_grow.ensure(rs.size());
+      O.overflow_items = al->ovf_items.p; O.overflow_grow = al->ovf_grow.p;
+      O.overflow_cap = (uint32_t)std::min<size_t>(al->ovf_items.n, 0xFFFFFFFFu);
     }
     for (int attempt = 0;; ++attempt) {
       HIPCHK(hipEventRecord(al->ev[5], st));
@@ -2112,6 +2241,8 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
       // reads touching more super-reads than their table holds: the 8192-slot LDS
       // table, then HBM tables growing until they fit
       uint32_t n_ovf = cnt[3];
+      if (n_ovf > O.overflow_cap) throw std::runtime_error("group overflow list past its capacity");
+      al->acc.group_overflow_items += n_ovf;
       uint32_t lg = hcap_log2;
       while (n_ovf) {
         std::vector<uint2>& ovf = al->h_items;
@@ -2164,6 +2295,7 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
         al->ovf_list.ensure(n_ovf);
         al->ovf_items.ensure(n_ovf); al->ovf_grow.ensure(n_ovf);  // (this round's overflow: at most its items)
         O.overflow_items = al->ovf_items.p; O.overflow_grow = al->ovf_grow.p;
+        O.overflow_cap = (uint32_t)std::min<size_t>(al->ovf_items.n, 0xFFFFFFFFu);
         HIPCHK(hipMemcpyAsync(al->ovf_list.p, ovf.data(), n_ovf * sizeof(uint2), hipMemcpyHostToDevice, st));
         HIPCHK(hipMemsetAsync(al->counters.p + 3, 0, 4, st));
         if (lg <= kGroupLdsMaxLog2) {
@@ -2186,6 +2318,8 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
         HIPCHK(hipMemcpyAsync(cnt, al->counters.p, 16, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         n_ovf = cnt[3];
+        if (n_ovf > O.overflow_cap) throw std::runtime_error("group overflow list past its capacity");
+        al->acc.group_overflow_items += n_ovf;
       }
 #ifndef PBGPU_EXP_GROUP_ONLY
       const uint32_t nch = cnt[0];

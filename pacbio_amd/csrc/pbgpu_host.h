@@ -322,6 +322,8 @@ struct pbgpu_aligner {
   dbuf<uint32_t> ovf_grow;
   dbuf<uint32_t> rcur;
   dbuf<uint64_t> sort_scratch;  // k_rec_sort keys of reads above its LDS capacity: 6 words per record
+  dbuf<uint2> rec_tiles;        // (read, tile) work items of those reads (carved from the dead hit buffers)
+  dbuf<uint32_t> rec_tile_ctr;  // their count and the longest such read
   dbuf<uint64_t> nhits, hit_off, rec_off, huge_elems;
   dbuf<int2> hits;
   dbuf<ChainDesc> chains;

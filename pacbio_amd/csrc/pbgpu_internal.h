@@ -129,6 +129,7 @@ struct GroupOut {
   uint2* overflow_items;   // the work items whose table overflowed (group_item)
   uint32_t* overflow_grow;  // per overflowing item: ceil(its k-mers / those its pass 0 had taken) | table log2 << 24
   uint32_t* n_overflow;
+  uint32_t overflow_cap;    // entries of overflow_items / overflow_grow (>= the launch's work items)
   uint32_t* rcur;          // per read: hits placed so far by its partitions (P > 1 items)
 };
 // k_group work item {read, partition | partitions << 16}: the read's hits whose super-read

@@ -909,11 +909,15 @@ __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_
       if (s_flag) {  // table too full: the item goes again, split or with a larger table
         if (tid == 0) {
           const uint32_t o = atomicAdd(O.n_overflow, 1u);
+          // (an item overflows once a launch and the list holds every item of it: the
+          // guard never drops one; the host checks the count against the cap)
+          if (o < O.overflow_cap) {
           O.overflow_items[o] = item;
           // the table filled over the first g_stop k-mers of nk: nk / g_stop estimates how much
           // larger the item is (the host splits it that many ways; too few only costs a round)
           const uint32_t grow = g_stop ? (nk + g_stop - 1) / g_stop : nk;
           O.overflow_grow[o] = (grow < 0xFFFFFFu ? grow : 0xFFFFFFu) | (hcap_log2 << 24);  // | the table it filled
+          }
         }
         return;
       }
@@ -2639,14 +2643,19 @@ DEV void bitonic_keys(uint64_t* hi, uint64_t* lo, EX* ex, uint32_t np2) {
   }
 }
 
-// One block per read: stage the sort keys of the read's records once (LDS, or
-// a global scratch region for reads with more than LCAP records), sort them
-// with a bitonic network, then gather the records in that order.  Padding
-// entries carry all-ones keys and sort last.
+// One block per read of at most LCAP records: stage the sort keys of the read's
+// records in LDS, sort them with a bitonic network, then gather the records in that
+// order (padding entries carry all-ones keys and sort last).  A read of more records
+// is only registered here: its ceil(n / LCAP) tiles go to a list (tiles[], counted in
+// ctr[0], the largest such read in ctr[1]) for k_rec_tile_sort / k_rec_merge /
+// k_rec_gather.  (Round 5 sorted such a read with one block running the bitonic network
+// over HBM scratch padded to a power of two: 136 global passes at 65536 records, 0.04
+// of HBM peak on C4-shaped reads.)
 template <int BLOCK, int LCAP>
 __global__ __launch_bounds__(BLOCK) void k_rec_sort(const Rec* __restrict__ recs, const uint64_t* __restrict__ rec_off,
-                                                    const uint32_t* __restrict__ order_in, uint64_t* gscratch,
-                                                    uint32_t n_reads, Rec* __restrict__ out) {
+                                                    const uint32_t* __restrict__ order_in, uint32_t n_reads,
+                                                    Rec* __restrict__ out, uint2* __restrict__ tiles,
+                                                    uint32_t* __restrict__ ctr) {
   static_assert(LCAP <= 4096, "LDS tie word holds a 12-bit slot");
   __shared__ uint64_t s_hi[LCAP], s_lo[LCAP];
   __shared__ uint32_t s_ex[LCAP];
@@ -2655,37 +2664,166 @@ __global__ __launch_bounds__(BLOCK) void k_rec_sort(const Rec* __restrict__ recs
   const uint64_t b = rec_off[r];
   const uint32_t n = (uint32_t)(rec_off[r + 1] - b);
   if (n == 0) return;
+  if (n > LCAP) {
+    const uint32_t t = (n + LCAP - 1) / LCAP;
+    __shared__ uint32_t s_base;
+    if (threadIdx.x == 0) {
+      s_base = atomicAdd(&ctr[0], t);
+      atomicMax(&ctr[1], n);
+    }
+    __syncthreads();
+    for (uint32_t c = threadIdx.x; c < t; c += BLOCK) tiles[s_base + c] = make_uint2(r, c);
+    return;
+  }
   uint32_t np2 = 1;
   while (np2 < n) np2 <<= 1;
-  if (np2 <= LCAP) {
+  for (uint32_t i = threadIdx.x; i < np2; i += BLOCK) {
+    if (i < n) {
+      const Rec& R = recs[order_in[b + i]];
+      s_hi[i] = rec_key_hi(R); s_lo[i] = rec_key_lo(R); s_ex[i] = (R.emit << 12) | i;
+    } else {
+      s_hi[i] = ~0ull; s_lo[i] = ~0ull; s_ex[i] = ~0u;
+    }
+  }
+  __syncthreads();
+  bitonic_keys<BLOCK>(s_hi, s_lo, s_ex, np2);
+  for (uint32_t i = threadIdx.x; i < n; i += BLOCK) out[b + i] = recs[order_in[b + (s_ex[i] & 0xFFFu)]];
+}
+
+// The keys of a long read in HBM, two buffers of {hi[n], lo[n], ex[n]} per read at its
+// record offset (A: 3 b words on, B: 3 nrec + 3 b on; 6 words a record in all); ex =
+// emit << 32 | the record's read-local index, so keys are unique within a read.
+struct RecKeys {
+  uint64_t *hi, *lo, *ex;
+};
+DEV RecKeys rec_keys(uint64_t* scratch, uint64_t b, uint32_t n, uint64_t buf_off) {
+  uint64_t* h = scratch + buf_off + 3 * b;
+  return RecKeys{h, h + n, h + 2 * (uint64_t)n};
+}
+DEV bool key_lt(uint64_t h0, uint64_t l0, uint64_t e0, uint64_t h1, uint64_t l1, uint64_t e1) {
+  return (h0 < h1) | ((h0 == h1) & ((l0 < l1) | ((l0 == l1) & (e0 < e1))));
+}
+// merge passes a read of n records needs after its tiles are sorted: ceil(log2(tiles))
+DEV uint32_t rec_merge_passes(uint32_t n, uint32_t lcap) {
+  uint32_t p = 0;
+  while (((uint64_t)lcap << p) < n) ++p;
+  return p;
+}
+
+// Tile c of a long read: its <= LCAP keys sorted in LDS, written to buffer A
+template <int BLOCK, int LCAP>
+__global__ __launch_bounds__(BLOCK) void k_rec_tile_sort(const Rec* __restrict__ recs,
+                                                         const uint64_t* __restrict__ rec_off,
+                                                         const uint32_t* __restrict__ order_in,
+                                                         const uint2* __restrict__ tiles, const uint32_t* ctr,
+                                                         uint64_t* scratch) {
+  __shared__ uint64_t s_hi[LCAP], s_lo[LCAP], s_ex[LCAP];
+  const uint32_t n_items = ctr[0];
+  for (uint32_t it = blockIdx.x; it < n_items; it += gridDim.x) {
+    const uint2 tc = tiles[it];
+    const uint64_t b = rec_off[tc.x];
+    const uint32_t n = (uint32_t)(rec_off[tc.x + 1] - b);
+    const uint32_t i0 = tc.y * LCAP, cnt = min((uint32_t)LCAP, n - i0);
+    uint32_t np2 = 1;
+    while (np2 < cnt) np2 <<= 1;
     for (uint32_t i = threadIdx.x; i < np2; i += BLOCK) {
-      if (i < n) {
-        const Rec& R = recs[order_in[b + i]];
-        s_hi[i] = rec_key_hi(R); s_lo[i] = rec_key_lo(R); s_ex[i] = (R.emit << 12) | i;
+      if (i < cnt) {
+        const Rec& R = recs[order_in[b + i0 + i]];
+        s_hi[i] = rec_key_hi(R); s_lo[i] = rec_key_lo(R); s_ex[i] = ((uint64_t)R.emit << 32) | (i0 + i);
       } else {
-        s_hi[i] = ~0ull; s_lo[i] = ~0ull; s_ex[i] = ~0u;
+        s_hi[i] = ~0ull; s_lo[i] = ~0ull; s_ex[i] = ~0ull;
       }
     }
     __syncthreads();
     bitonic_keys<BLOCK>(s_hi, s_lo, s_ex, np2);
-    for (uint32_t i = threadIdx.x; i < n; i += BLOCK) out[b + i] = recs[order_in[b + (s_ex[i] & 0xFFFu)]];
-  } else {
-    // host reserves 6 words per record: np2 <= 2n entries of {hi, lo, ex}
-    uint64_t* hi = gscratch + 6 * b;
-    uint64_t* lo = hi + np2;
-    uint64_t* ex = lo + np2;
-    for (uint32_t i = threadIdx.x; i < np2; i += BLOCK) {
-      if (i < n) {
-        const Rec& R = recs[order_in[b + i]];
-        hi[i] = rec_key_hi(R); lo[i] = rec_key_lo(R); ex[i] = ((uint64_t)R.emit << 32) | i;
-      } else {
-        hi[i] = ~0ull; lo[i] = ~0ull; ex[i] = ~0ull;
-      }
+    const RecKeys A = rec_keys(scratch, b, n, 0);
+    for (uint32_t i = threadIdx.x; i < cnt; i += BLOCK) {
+      A.hi[i0 + i] = s_hi[i]; A.lo[i0 + i] = s_lo[i]; A.ex[i0 + i] = s_ex[i];
     }
-    __threadfence_block();
+    __syncthreads();  // (LDS reused by the next item)
+  }
+}
+
+// Merge pass p of the long reads: sorted runs of w = LCAP << p keys merged pairwise
+// from one buffer into the other.  Work item (read, c) produces the merged outputs
+// [c LCAP, (c + 1) LCAP) of its read: the merge-path split of the chunk's two ends (a
+// binary search each), the two input ranges (<= LCAP keys together) staged in LDS,
+// then each key's output rank = its index + the count of the other range's keys below
+// it (an LDS binary search; keys are unique).  Items of reads already in one run
+// (n <= w) are skipped: their keys stay in the buffer their last pass wrote.
+template <int BLOCK, int LCAP>
+__global__ __launch_bounds__(BLOCK) void k_rec_merge(const uint64_t* __restrict__ rec_off,
+                                                     const uint2* __restrict__ tiles, const uint32_t* ctr,
+                                                     uint64_t* scratch, uint64_t nrec, uint32_t p) {
+  __shared__ uint64_t s_hi[LCAP], s_lo[LCAP], s_ex[LCAP];
+  __shared__ uint32_t s_split[2];
+  const uint64_t w = (uint64_t)LCAP << p;
+  if (w >= ctr[1]) return;  // every long read is one run already
+  const uint32_t n_items = ctr[0];
+  const uint64_t src_off = (p & 1) ? 3 * nrec : 0, dst_off = (p & 1) ? 0 : 3 * nrec;
+  for (uint32_t it = blockIdx.x; it < n_items; it += gridDim.x) {
+    const uint2 tc = tiles[it];
+    const uint64_t b = rec_off[tc.x];
+    const uint32_t n = (uint32_t)(rec_off[tc.x + 1] - b);
+    if (n <= w) continue;  // (uniform over the block)
+    const RecKeys S = rec_keys(scratch, b, n, src_off), D = rec_keys(scratch, b, n, dst_off);
+    const uint64_t o0 = (uint64_t)tc.y * LCAP;
+    const uint64_t s = o0 / (2 * w) * (2 * w);  // the pair's first key
+    const uint32_t la = (uint32_t)min<uint64_t>(w, n - s);
+    const uint32_t lb = (uint32_t)(n - s - la < w ? n - s - la : w);
+    const uint32_t d0 = (uint32_t)(o0 - s), d1 = min(d0 + (uint32_t)LCAP, la + lb);
+    if (threadIdx.x < 2) {
+      // merge path: a = left keys among the first d merged
+      const uint32_t d = threadIdx.x ? d1 : d0;
+      uint32_t lo = d > lb ? d - lb : 0, hi = min(d, la);
+      while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        const uint64_t ia = s + m, ib = s + la + (d - m - 1);
+        if (key_lt(S.hi[ia], S.lo[ia], S.ex[ia], S.hi[ib], S.lo[ib], S.ex[ib])) lo = m + 1;
+        else hi = m;
+      }
+      s_split[threadIdx.x] = lo;
+    }
     __syncthreads();
-    bitonic_keys<BLOCK>(hi, lo, ex, np2);
-    for (uint32_t i = threadIdx.x; i < n; i += BLOCK) out[b + i] = recs[order_in[b + (uint32_t)ex[i]]];
+    const uint32_t a0 = s_split[0], a1 = s_split[1];
+    const uint32_t na = a1 - a0, nb = (d1 - d0) - na, b0 = d0 - a0;
+    for (uint32_t i = threadIdx.x; i < na + nb; i += BLOCK) {
+      const uint64_t g = i < na ? s + a0 + i : s + la + b0 + (i - na);
+      s_hi[i] = S.hi[g]; s_lo[i] = S.lo[g]; s_ex[i] = S.ex[g];
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < na + nb; i += BLOCK) {
+      const uint64_t h = s_hi[i], l = s_lo[i], e = s_ex[i];
+      // the other range: [ob, ob + on) in LDS
+      const uint32_t ob = i < na ? na : 0, on = i < na ? nb : na;
+      uint32_t lo = 0, hi = on;
+      while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (key_lt(s_hi[ob + m], s_lo[ob + m], s_ex[ob + m], h, l, e)) lo = m + 1;
+        else hi = m;
+      }
+      const uint64_t o = s + d0 + (i < na ? i : i - na) + lo;
+      D.hi[o] = h; D.lo[o] = l; D.ex[o] = e;
+    }
+    __syncthreads();  // (LDS reused by the next item)
+  }
+}
+
+// The long reads' records in their sorted order, from the buffer their last pass wrote
+template <int LCAP>
+__global__ void k_rec_gather(const Rec* __restrict__ recs, const uint64_t* __restrict__ rec_off,
+                             const uint32_t* __restrict__ order_in, const uint2* __restrict__ tiles,
+                             const uint32_t* ctr, const uint64_t* __restrict__ scratch, uint64_t nrec,
+                             Rec* __restrict__ out) {
+  const uint32_t n_items = ctr[0];
+  for (uint32_t it = blockIdx.x; it < n_items; it += gridDim.x) {
+    const uint2 tc = tiles[it];
+    const uint64_t b = rec_off[tc.x];
+    const uint32_t n = (uint32_t)(rec_off[tc.x + 1] - b);
+    const uint64_t* ex = scratch + ((rec_merge_passes(n, LCAP) & 1) ? 3 * nrec : 0) + 3 * b + 2 * (uint64_t)n;
+    const uint32_t i0 = tc.y * LCAP, cnt = min((uint32_t)LCAP, n - i0);
+    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x)
+      out[b + i0 + i] = recs[order_in[b + (uint32_t)ex[i0 + i]]];
   }
 }
 
@@ -2965,11 +3103,30 @@ void launch_rec_scatter(const uint32_t* rec_read, uint32_t n, const uint64_t* re
 }
 constexpr int REC_BLOCK = 256, REC_LCAP = 2048;
 int rec_sort_lcap() { return REC_LCAP; }
+// tiles of the reads past REC_LCAP records: a read of n > LCAP records has ceil(n / LCAP) < 2 n / LCAP
+uint64_t rec_sort_max_tiles(uint64_t nrec) { return 2 * nrec / REC_LCAP + 1; }
+// Records sorted per read: the LDS kernel for reads of <= REC_LCAP records; the longer
+// reads' tiles sorted in LDS, then merged pairwise over the scratch's two key buffers
+// (6 words a record, nrec records), then gathered.  ctr: 2 words, zeroed by the caller.
+// max_passes: a bound on the merge passes (the longest read is not known on the host):
+// passes past the longest read's exit at once on the device.
 void launch_rec_sort(const Rec* recs, const uint64_t* rec_off, const uint32_t* order, uint64_t* gscratch,
-                     uint32_t n_reads, Rec* out, hipStream_t st) {
+                     uint32_t n_reads, uint64_t nrec, uint2* tiles, uint32_t* ctr, Rec* out, hipStream_t st) {
   if (!n_reads) return;
   hipLaunchKernelGGL((k_rec_sort<REC_BLOCK, REC_LCAP>), dim3(n_reads), dim3(REC_BLOCK), 0, st, recs, rec_off, order,
-                     gscratch, n_reads, out);
+                     n_reads, out, tiles, ctr);
+  if (nrec <= (uint64_t)REC_LCAP) return;
+  const uint64_t max_tiles = rec_sort_max_tiles(nrec);
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(max_tiles, 8192);
+  hipLaunchKernelGGL((k_rec_tile_sort<REC_BLOCK, REC_LCAP>), dim3(grid), dim3(REC_BLOCK), 0, st, recs, rec_off, order,
+                     tiles, ctr, gscratch);
+  uint32_t passes = 0;
+  while (((uint64_t)REC_LCAP << passes) < nrec) ++passes;
+  for (uint32_t p = 0; p < passes; ++p)
+    hipLaunchKernelGGL((k_rec_merge<REC_BLOCK, REC_LCAP>), dim3(grid), dim3(REC_BLOCK), 0, st, rec_off, tiles, ctr,
+                       gscratch, nrec, p);
+  hipLaunchKernelGGL((k_rec_gather<REC_LCAP>), dim3(grid), dim3(256), 0, st, recs, rec_off, order, tiles, ctr,
+                     gscratch, nrec, out);
 }
 
 // ------------------------------------------------------------ fine launchers

@@ -1005,6 +1005,13 @@ pbgpu_status pbgpu_runner_create(pbgpu_index* const* indexes, size_t n_indexes, 
     if (indexes[i]->n_shards > 1) return fail(PBGPU_ERR_UNSUPPORTED, "the driver needs whole (unsharded) indexes");
   }
   API_TRY
+  // the loops below switch devices: the caller's current device is restored on the way out
+  int caller_dev = 0;
+  HIPCHK(hipGetDevice(&caller_dev));
+  struct RestoreDevice {
+    int d;
+    ~RestoreDevice() { (void)hipSetDevice(d); }
+  } restore_device{caller_dev};
   std::unique_ptr<pbgpu_runner> R(new pbgpu_runner);
   for (size_t i = 0; i < n_indexes; ++i) {  // the devices' use before the aligners (the indexes, other work)
     const int d = indexes[i]->device;

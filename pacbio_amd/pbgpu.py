@@ -26,7 +26,7 @@ STATUS = {0: "OK", 1: "INVALID", 2: "IO", 3: "NOMEM", 4: "DEVICE", 5: "UNSUPPORT
 # every symbol include/pbgpu.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "pbgpu_abi_version", "pbgpu_last_error", "pbgpu_device_count", "pbgpu_device_synchronize",
-    "pbgpu_measure_gather", "pbgpu_measure_gather_shape", "pbgpu_check_reciprocal",
+    "pbgpu_measure_gather", "pbgpu_measure_gather_shape", "pbgpu_measure_group_shape", "pbgpu_check_reciprocal",
     "pbgpu_index_build_fasta", "pbgpu_index_build", "pbgpu_index_free", "pbgpu_index_get_info",
     "pbgpu_index_sr_name", "pbgpu_index_sr_len",
     "pbgpu_align_params_default", "pbgpu_aligner_create", "pbgpu_aligner_free",
@@ -153,7 +153,8 @@ class Stats(C.Structure):
                                                                     ("ms_host_order", C.c_double),
                                                                     ("graph_host_reads", C.c_uint64),
                                                                     ("group_refines", C.c_uint64),
-                                                                    ("group_hbm_reads", C.c_uint64)]
+                                                                    ("group_hbm_reads", C.c_uint64),
+                                                                    ("group_overflow_items", C.c_uint64)]
 
     def as_dict(self):
         d = {n: getattr(self, n) for n, _ in self._fields_ if not n.startswith("kernel_")}
@@ -182,6 +183,8 @@ def lib():
         L.pbgpu_device_synchronize.argtypes = [C.c_int]
         L.pbgpu_measure_gather.argtypes = [C.c_int, C.c_uint64, C.POINTER(C.c_double)]
         L.pbgpu_measure_gather_shape.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.POINTER(C.c_double)]
+        L.pbgpu_measure_group_shape.argtypes = [C.c_int, C.c_uint64, C.c_int, C.POINTER(C.c_double),
+                                                C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         if hasattr(L, "pbgpu_check_reciprocal"):  # (absent from older experiment builds)
             L.pbgpu_check_reciprocal.argtypes = [C.c_int, C.c_uint32, C.POINTER(C.c_uint64)]
         L.pbgpu_index_build_fasta.argtypes = [C.POINTER(C.c_char_p), C.c_size_t, C.POINTER(IndexParams), C.POINTER(vp)]
@@ -262,6 +265,18 @@ def measure_gather(device=0, buffer_bytes=64 << 30, unit_bytes=64):
     g = C.c_double()
     _check(lib().pbgpu_measure_gather_shape(device, buffer_bytes, unit_bytes, C.byref(g)))
     return g.value
+
+
+def measure_group_shape(device=0, buffer_bytes=64 << 30, mode=2):
+    """k_group's occurrence-read shape (pbgpu_measure_group_shape): mode 0 = pass 0's 4-B ids,
+    1 = pass 1's 8-B words, 2 = both passes over the same runs.  Returns a dict: sector-byte
+    rate (GB/s) and, per launch, the 64-B sectors / 128-B lines spanned and the algorithmic
+    bytes (the known counts FETCH_SIZE is read against)."""
+    g, s64, l128, alg = C.c_double(), C.c_uint64(), C.c_uint64(), C.c_uint64()
+    _check(lib().pbgpu_measure_group_shape(device, buffer_bytes, mode, C.byref(g), C.byref(s64), C.byref(l128),
+                                           C.byref(alg)))
+    return {"mode": mode, "sector_gbs": g.value, "sectors64_per_launch": s64.value,
+            "lines128_per_launch": l128.value, "alg_bytes_per_launch": alg.value}
 
 
 def check_reciprocal(device=0, n_max=1 << 24):

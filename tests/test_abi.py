@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert pbgpu.lib().pbgpu_abi_version() == 7
+    assert pbgpu.lib().pbgpu_abi_version() == 8
 
 
 def test_record_layout_matches_header():

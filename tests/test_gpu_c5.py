@@ -31,7 +31,9 @@ import pytest
 from tests._compare import assert_read_order
 from tests.test_gpu_scale import _check_invariants, check_records
 
-pytestmark = pytest.mark.gpu
+# the run takes ~370-400 s on one MI355X (31 shard builds): a per-test limit of its own,
+# above that, so a runner's shorter --timeout does not kill it inside a shard's free
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(1200)]
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 

@@ -140,6 +140,33 @@ def test_group_all_overflow(data, refine, dense, small, monkeypatch):
             assert st["group_refines"] == 0 and st["group_hbm_reads"] > 0, st
 
 
+@pytest.mark.parametrize("first_p", ["2", "4"])
+@pytest.mark.parametrize("data", ["dense", "small"])
+def test_group_first_round_items_overflow(data, first_p, dense, small, monkeypatch):
+    """Every read starts as P hash-partition items in the smallest table
+    (PBGPU_GROUP_FIRST_P): on the dense reads every item overflows, so the first
+    round's overflow list must hold one entry per item -- P per read -- not one per
+    read (the list was sized by reads and k_group wrote past it).  One call
+    per read too, so a one-read batch overflows P items at once."""
+    ds = dense if data == "dense" else small
+    monkeypatch.setenv("PBGPU_GROUP_FIRST_P", first_p)
+    names, seqs = ds.sr_names(), ds.sr_seqs()
+    pnames, pseqs = ds.pb_names(), ds.pb_seqs()
+    exp = _oracle(names, seqs, pnames, pseqs, ul=ds.unitig_lengths, forward=True, unitigs_k=31)
+    got, st = _gpu(names, seqs, pnames, pseqs, ul=ds.unitig_lengths, forward=True, unitigs_k=31)
+    assert_same_coords(got, exp, f"first-round items {data} P={first_p}")
+    if data == "dense":
+        # more items overflowed than there are reads: the case the reads-sized list missed
+        assert st["group_overflow_items"] > len(pseqs), st
+        for i in range(len(pseqs)):
+            one, st1 = _gpu(names, seqs, pnames[i:i + 1], pseqs[i:i + 1], ul=ds.unitig_lengths, forward=True,
+                            unitigs_k=31)
+            e1 = _oracle(names, seqs, pnames[i:i + 1], pseqs[i:i + 1], ul=ds.unitig_lengths, forward=True,
+                         unitigs_k=31)
+            assert_same_coords(one, e1, f"first-round items, read {i} alone, P={first_p}")
+            assert st1["group_overflow_items"] >= 2, st1
+
+
 def test_repeats_threshold():
     from tools.synth import Dataset
     ds = Dataset("small", seed=3, repeat_frac=0.2, n_pb=30)

@@ -382,3 +382,55 @@ def test_graph_ties_equal_implied_starts(tmp_path):
             ta = open(a_out).read()
             assert ta == open(b_out).read(), (tiling, extra)
             assert ta.count(">") >= 2, ta
+
+
+C4R_FLAGS = ["-s", "1M", "-m", "17", "--psa-min", "13", "-k", "31", "-B", "15", "--max-count", "5000",
+             "--stretch-cap", "10000", "-t", "16"]
+
+
+def test_device_graph_full_c4r_equals_host_graph(tmp_path):
+    """All 20k C4r reads (the bench's C4r leg, 25.5 M records, ~2% of the reads past 8192
+    records and none left to the host) through the CLI: the device graph -- the LDS tiers,
+    the HBM sort / relaxation of the long reads, the edge scans' prefilter queue and k_mega --
+    gives the bytes of --host-graph (round 5 checked this only as a profile,
+    profiles/r05zy_cmr_full_device_vs_host.txt; the suite held 300 reads)."""
+    import json
+    from tools.synth import Dataset
+    ds = Dataset("C4r", seed=42, threads=16, n_pb=20000)
+    ds.write(str(tmp_path))
+    ds.close()
+    base = [*C4R_FLAGS, "-l", str(tmp_path / "ul.txt"), "--timing", "-r", str(tmp_path / "sr.fa"),
+            "-p", str(tmp_path / "pb.fa")]
+    dev, host = str(tmp_path / "dev"), str(tmp_path / "host")
+    r = _run([*base, "-o", dev], timeout=600)
+    t = json.loads(r.stderr.strip().splitlines()[-1])
+    assert t["graph_host_reads"] == 0 and t["records"] > 20_000_000, t
+    _run([*base, "--host-graph", "-o", host], timeout=600)
+    td = open(dev).read()
+    assert td.count(">") > 19_000 and td == open(host).read()
+
+
+def test_read_past_8192_records_against_restatement(tmp_path):
+    """A read of more than 8192 records -- C4r read 207 (9191 records: its sort keys and
+    node state in HBM, k_graph_sort_big / k_graph_relax_big) -- checked against the
+    independent Python restatement (oracle/mega_reads.py) on the CPU oracle's records of
+    that read, not only against the product's own host graph (overlap_graph.cc:7-59,
+    mega_reads_per_comp, tile_greedy)."""
+    from tools.synth import Dataset
+    big = Dataset("C4r", seed=42, threads=16, n_pb=1, pb_index_base=207)
+    big.write(str(tmp_path))
+    ul = [int(x) for x in big.unitig_lengths]
+    oix = O.OracleIndex.from_records(big.sr_names(), big.sr_seqs(), 17, threads=16)
+    p = O.params(k=17, forward=True, unitigs_k=31, unitig_lengths=ul, bases_matching=15.0, max_count=5000,
+                 stretch_cap=10000.0)
+    (name,), (seq,) = big.pb_names(), big.pb_seqs()
+    recs = MR.records_of(oix, p, seq)
+    oix.close()
+    big.close()
+    assert len(recs) > 8192, len(recs)
+    out = str(tmp_path / "mr")
+    _run([*C4R_FLAGS, "-l", str(tmp_path / "ul.txt"), "-o", out, "-r", str(tmp_path / "sr.fa"),
+          "-p", str(tmp_path / "pb.fa")], timeout=300)
+    want = _expect([(name.decode(), recs)], ul, 31)
+    assert want.count("\n") > 2
+    assert open(out).read() == want
