@@ -371,6 +371,7 @@ def c4_leg(args, comm, rank, world, local, threads, pbgpu, Dataset, brand=True):
     pbgpu.device_synchronize(local)
     build_s = time.time() - t0
     info = ix.info()
+    print(f"bench c4: index {json.dumps(info)} built in {build_s:.1f} s", file=sys.stderr, flush=True)
     b_filt = b_table = None
     if brand:
         b_filt = pbgpu.measure_gather(local, max(1 << 20, info["filter_bytes"])) if info["filter_bytes"] else None
@@ -379,7 +380,10 @@ def c4_leg(args, comm, rank, world, local, threads, pbgpu, Dataset, brand=True):
     blob, off = ds.pb_blob()
     bases = int(off[-1])
     steps = max(1, args.device_steps)
-    el, st, nch = _device_leg(pbgpu, ix, akw, blob, off, args.device_chunk_bases, steps, comm, local)
+    # resident calls of at most 0.5 Gbases: beside the ~110 GB index, a 1.5-Gbase call's
+    # records and per-hit buffers did not fit the remaining HBM
+    el, st, nch = _device_leg(pbgpu, ix, akw, blob, off, min(args.device_chunk_bases, args.c4_chunk_bases), steps,
+                              comm, local)
     # size-independent properties of the output (the oracle cannot hold this index): the
     # first reads' records, sorted per read, inside their read and super-read
     al = pbgpu.Aligner(ix, **akw)
@@ -517,6 +521,8 @@ def main():
     ap.add_argument("--c4-reads", type=int, default=250000,
                     help="reads per GPU of the C4 leg (BASELINE configs[3]: the full 10M-super-read index, 15-kb-N50 "
                          "reads; 2M / 8 = 250k; 0 = no such leg), reported under c4")
+    ap.add_argument("--c4-chunk-bases", type=float, default=0.5e9,
+                    help="the C4 leg's resident calls hold at most this many bases each")
     ap.add_argument("--c3-reads", type=int, default=300000,
                     help="reads of the C3 strong-scaling leg (BASELINE configs[2]: 300k reads split over the ranks, "
                          "index replicated; 0 = no such leg), reported under c3")
@@ -878,7 +884,9 @@ def main():
     for kk in per_kernel:
         t = summ_all.get(f"{kk}_traffic_bytes")
         if t:
-            shape = t.get("shape") or ("raw_fetch_plus_write" if kk == "k_group" else "guide_2x_fetch_plus_write")
+            # k_group: 2 x FETCH + WRITE, calibrated on its exact access shape (round 6,
+            # profiles/r06c_group_calibration.txt: FETCH_SIZE = 1/2 of the 128-B lines moved)
+            shape = "guide_2x_fetch_plus_write" if kk == "k_group" else (t.get("shape") or "guide_2x_fetch_plus_write")
             per_kernel[kk]["traffic_bytes_per_launch"] = t.get(shape)
             per_kernel[kk]["traffic_over_alg"] = round(t.get(shape) / kb[kk], 3) if t.get(shape) else None
             per_kernel[kk]["rocprof_mean_ms"] = (summ_all.get(f"{kk}_device_leg") or {}).get("mean_ms")

@@ -105,6 +105,9 @@ void launch_rec_scatter(const uint32_t* rec_read, uint32_t n, const uint64_t* re
 // order[rec_off[rec_read[i]] + rec_slot[i]] = i (the slots counted at emission)
 void launch_rec_place(const uint32_t* rec_read, const uint32_t* rec_slot, uint32_t n, const uint64_t* rec_off,
                       uint32_t* order, hipStream_t st);
+#ifdef PBGPU_GRAPH_CHECK
+void graph_check_report();
+#endif
 int rec_sort_lcap();
 uint64_t rec_sort_max_tiles(uint64_t nrec);
 void launch_rec_sort(const Rec* recs, const uint64_t* rec_off, const uint32_t* order, uint64_t* gscratch,
@@ -1330,6 +1333,12 @@ pbgpu_status pbgpu_aligner_create(const pbgpu_index* ix, const pbgpu_align_param
   std::unique_ptr<pbgpu_aligner> al(new pbgpu_aligner);
   al->ix = ix;
   al->device = ix->device;
+  // kmers_info holds 2 u - 1 ints a record (u: the unitigs of its super-read's name,
+  // pb_aligner.cc:84-143): the first estimate is twice the index's mean, grown on overflow
+  {
+    const double mean_u = (double)ix->sr_uids.n / (double)std::max<uint64_t>(1, ix->sr_end - ix->sr_begin);
+    al->info_per_chain = (uint64_t)std::min(32.0, std::max(8.0, std::ceil(2.0 * (2.0 * mean_u - 1.0)) + 4.0));
+  }
   al->prm = *params;
   al->prm.unitig_lengths = nullptr;
   if (params->unitigs_k && params->n_unitigs) {
@@ -1480,6 +1489,9 @@ pbgpu_status pbgpu_aligner_free(pbgpu_aligner* al) {
   if (!al) return PBGPU_OK;
   if (getenv("PBGPU_DEBUG_BUFFERS")) buffer_report(al);
   (void)hipSetDevice(al->device);  // not al->ix: the index may be freed first
+#ifdef PBGPU_GRAPH_CHECK
+  if (al->graph) { (void)hipDeviceSynchronize(); graph_check_report(); }
+#endif
   for (auto& e : al->ev) if (e) (void)hipEventDestroy(e);
   if (al->g_fork) (void)hipEventDestroy(al->g_fork);
   if (al->g_join) (void)hipEventDestroy(al->g_join);
@@ -1961,6 +1973,9 @@ static void graph_stage(pbgpu_aligner* al, const pbgpu_reads* rd) {
   // (with device mega-reads the nodes are temporaries too: only the host reads' come down)
   uint32_t* g_pre = dead.take(al->g_pre, 3 * tot + 3);
   G.pp = (uint2*)g_pre; G.ounits = g_pre + 2 * (tot + 1);
+#ifdef PBGPU_GRAPH_CHECK
+  G.units_total = tot;
+#endif
   G.imp = dead.take(al->g_imp, nrec + 1); G.desc = dead.take(al->g_desc, nrec + 1);
   G.spo = dead.take(al->g_spo, nrec + 1);
   G.fis = dead.take(al->g_fd, 3 * (nrec + 1)); G.fie = G.fis + (nrec + 1); G.fer = G.fie + (nrec + 1);
@@ -2068,7 +2083,14 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
   const uint64_t mem_avail = (uint64_t)mem_free + al->krec.bytes() + al->X.bytes() + al->pts.bytes() + al->nodes.bytes();
   uint64_t chunk_bases = std::max<uint64_t>(1ull << 26, mem_avail / 16 / 8);
   if (const char* e = getenv("PBGPU_CHUNK_BASES")) chunk_bases = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
-  const uint64_t budget = std::max<uint64_t>(1ull << 20, std::min<uint64_t>(al->hit_budget, mem_avail / 24 / 3));
+  // a hit costs 24 B of per-hit buffers (X, pts, nodes) plus, through the chains it makes
+  // (chains_per_hit, learnt), a chain's descriptor and LIS state (~40 B), records (96 + 8 B
+  // each, rec_per_chain of them) and kmers_info (2 x 4 B x info_per_chain): sub-batches of
+  // at most a third of the free memory by that sum
+  const double per_hit = 24.0 + al->chains_per_hit * (40.0 + 104.0 * al->rec_per_chain * (al->P.max_match ? 2.0 : 1.0) +
+                                                      8.0 * (double)al->info_per_chain);
+  const uint64_t budget = std::max<uint64_t>(1ull << 20, std::min<uint64_t>(al->hit_budget,
+                                                                            (uint64_t)((double)mem_avail / per_hit / 3.0)));
   const uint32_t hcap_log2 = 11;
   std::vector<uint64_t> h_roff;  // host copy of the read offsets (the chunk cuts)
   if (rd->h_off.size() == (size_t)n + 1) {
@@ -2336,12 +2358,13 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
       }
       HIPCHK(hipEventRecord(al->ev[6], st));
       const uint32_t n_fit = lis_stage(al, nch, Hs, al->lp, al->P.max_match, true, true);
-      const uint64_t rec_need = rec_done + (uint64_t)nch * (al->P.max_match ? 2 : 1) + 1024 * (attempt + 1);
+      const uint64_t rec_est = (uint64_t)std::ceil((double)nch * std::min(1.0, al->rec_per_chain)) * (al->P.max_match ? 2 : 1);
+      const uint64_t rec_need = rec_done + rec_est + 1024 * (attempt + 1);
       al->recs.grow_keep(std::max<uint64_t>(rec_need, al->rec_hint), rec_done, st);
       al->rec_read.grow_keep(al->recs.n, rec_done, st);
       al->rec_slot.grow_keep(al->recs.n, rec_done, st);
       if (al->P.unitigs_k) {
-        const uint64_t info_need = info_done + (uint64_t)nch * al->info_per_chain + 4096;
+        const uint64_t info_need = info_done + rec_est * al->info_per_chain + 4096;
         al->info_m.grow_keep(info_need, info_done, st);
         al->info_b.grow_keep(info_need, info_done, st);
       } else {
@@ -2414,18 +2437,23 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
       k_n[PBGPU_KERNEL_GROUP]++; k_n[PBGPU_KERNEL_LIS]++; k_n[PBGPU_KERNEL_COORDS]++;
       if (ovf == 0 && nrec <= al->recs.n) {
         if (al->details) capture_details(al, nch, Hs);
+        const uint64_t sub_recs = nrec - rec_done;
         rec_done = nrec; info_done = ninfo;
         n_chains += sub[0]; n_tests += sub[1];
 #ifndef PBGPU_EXP_GROUP_ONLY
         if (Hs) al->chains_per_hit = std::max(1e-4, 1.1 * (double)nch / (double)Hs);
 #endif
+        // (records a chain yields, with a margin; max-match rounds are counted by rec_est's x2)
+        if (nch && !al->P.max_match)
+          al->rec_per_chain = std::min(1.0, std::max(0.02, 1.25 * (double)sub_recs / (double)nch + 0.01));
         break;
       }
       if (attempt > 8) throw std::runtime_error("record buffer growth did not converge");
       counted = false;  // this attempt's emitted records were counted: records_stage recounts
       // grow (keeping the records of earlier sub-batches) and redo this sub-batch from the group pass
       al->rec_hint = std::max<uint64_t>(al->rec_hint, (uint64_t)nrec + 4096);
-      al->info_per_chain = al->info_per_chain * 2 + 16;
+      if (ninfo > info_done + rec_est * al->info_per_chain) al->info_per_chain = al->info_per_chain * 2 + 16;
+      al->rec_per_chain = 1.0;
     }
     r0 = r1;
   }

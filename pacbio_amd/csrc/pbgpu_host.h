@@ -353,6 +353,12 @@ struct pbgpu_aligner {
   hipStream_t grp_side = nullptr;  // the group stage's 16-wave tier (PBGPU_GROUP_OVERLAP)
   hipEvent_t grp_fork = nullptr, grp_join = nullptr;
   uint64_t hit_budget = 4000000000ull, rec_hint = 0, info_per_chain = 32;
+  // records a chain yields (kept by the filters), learnt from the sub-batches so far: the
+  // record buffers of a sub-batch are sized by it instead of one record per chain (C4: 278 M
+  // chains in a sub-batch, 27 GB of records and 71 GB of kmers_info sized by the chains ran
+  // the device out of memory beside its 126-GB index); an overflow redoes the sub-batch and
+  // resets it to 1
+  double rec_per_chain = 1.0;
   // pbgpu_run: the most bases a batch holds (0 = unknown): the per-base buffers never grow past it
   uint64_t base_cap = 0;
   double chains_per_hit = 1.0 / 80;  // k_group tier estimate (C2: 1.1 x 1/90), refined after every batch

@@ -280,6 +280,9 @@ struct GraphDev {
   unsigned long long* units_used;
   uint64_t units_cap;
   uint64_t n_recs;
+#ifdef PBGPU_GRAPH_CHECK
+  uint64_t units_total;       // poff[n_recs]: the batch's name units / prefix sums (bounds-check build)
+#endif
   uint32_t* n_host;           // reads left to the host
   // 6 words per record (the records stage's sort scratch, free by then): reads of more
   // than GRAPH_NMAX records keep their sort keys, then their node state, then k_mega's

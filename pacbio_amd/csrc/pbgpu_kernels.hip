@@ -17,6 +17,7 @@
 #include <atomic>
 #include <stdint.h>
 #include <algorithm>
+#include <cstdio>
 #include <type_traits>
 #include "pbgpu.h"
 #include "pbgpu_internal.h"
@@ -3071,6 +3072,18 @@ void launch_strand_order(const ChainDesc* chains, const uint32_t* items, uint32_
                      slen, X);
 }
 #ifdef PBGPU_PROF
+#ifdef PBGPU_GRAPH_CHECK
+// the check counters so far, printed to stderr by every aligner with a graph at its free
+// (the CLIs run the variant through LD_LIBRARY_PATH and print nothing of their own)
+namespace pbgpu {
+void graph_check_report() {
+  unsigned long long h[5] = {};
+  const hipError_t e = hipMemcpyFromSymbol(h, HIP_SYMBOL(g_graph_check), sizeof(h));
+  fprintf(stderr, "pbgpu graph-check: far_j %llu name_units %llu prefix_sums %llu edge_targets %llu checks %llu%s\n",
+          h[0], h[1], h[2], h[3], h[4], e == hipSuccess ? "" : " (counters unreadable)");
+}
+}  // namespace pbgpu
+#endif
 extern "C" int pbgpu_debug_prof(unsigned long long* out, int n, int reset) {
   if (n > PROF_SLOTS) n = PROF_SLOTS;
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), n * sizeof(unsigned long long)) != hipSuccess) return -1;
@@ -3359,6 +3372,16 @@ void launch_excl_scan(const uint32_t* in32, const uint64_t* in64, uint64_t n, ui
 }
 
 // ========================================================== overlap graph
+#ifdef PBGPU_GRAPH_CHECK
+// Bounds-checking build (tools/r06/graph_check.sh, never the product): every far node k_graph_edges
+// reads, its name offset and prefix-sum index, and every edge target the relaxations read,
+// checked against the batch's arrays; violations counted (and the access redirected to a
+// valid index), reported at process exit.  [0] far j outside (q, qe) / n_recs, [1] name
+// units past the batch's units, [2] prefix sums past them, [3] edge target outside its read,
+// [4] checks made.
+__device__ unsigned long long g_graph_check[5];
+#define GCHECK(ok, slot) do { if (!(ok)) atomicAdd(&g_graph_check[slot], 1ull); } while (0)
+#endif
 // create_mega_reads' per-read overlap graph (overlap_graph.cc:7-59,
 // overlap_graph::traverse, with node_info::reset, overlap_graph.hpp:24-34, and
 // union_find.cc) on the records of recs_sorted: the host then only collects the
@@ -3733,6 +3756,9 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
         const bool act = direct ? x + lane < qe : lane < x;
         const uint64_t j = direct ? x + lane : (act ? (uint64_t)sq[lane] : q);
         const uint32_t sj = (uint32_t)((act ? j : q) - q0);
+#ifdef PBGPU_GRAPH_CHECK
+        if (act) { GCHECK(j > q && j < qe && j < n_recs, 0); GCHECK(true, 4); }
+#endif
         // node j: staged, or (a scan past the window) one 64-byte line from HBM.  Every load
         // is issued before the tests (measured: loading the name only where the name test
         // runs, after the skip / break ballot, made the C4r graph stage 240 -> 316 ms: a
@@ -3750,6 +3776,9 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
         } else {
           const GDesc dj = G.desc[act ? j : q];
           po_j = G.spo[act ? j : q];  // (coalesced, issued with the node: no second round trip)
+#ifdef PBGPU_GRAPH_CHECK
+          if (act) GCHECK((uint64_t)po_j + dj.nsz <= G.units_total, 1);
+#endif
           is_j = dj.imp_s; ie_j = dj.imp_e; er_j = dj.err; mj = dj.idx | ((uint32_t)dj.nsz << 16); lpa_j = dj.lp_add;
 #pragma unroll
           for (uint32_t u = 0; u < GRAPH_U; ++u) bu[u] = dj.u[u];
@@ -3800,6 +3829,9 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
             }
           }
           if (nb && !same) {
+#ifdef PBGPU_GRAPH_CHECK
+            GCHECK((uint64_t)po_of_j() + (uint32_t)nb < G.units_total, 2);
+#endif
             const uint2 v = G.pp[po_of_j() + (uint32_t)nb];
             const int32_t uol = (int32_t)(v.x - (uint32_t)(nb - 1) * km1);
             common = (int32_t)v.y;
@@ -3992,6 +4024,9 @@ __global__ __launch_bounds__(128) void k_graph_relax(GraphDev G, uint32_t n_read
       const uint2 ce = k0 + lane < GRAPH_EBLK ? blk
                                               : (edge ? G.eovf[G.eoff[b + p] + (k0 + lane - GRAPH_EBLK)] : make_uint2(0u, 0u));
       const uint32_t it_j = ce.x & 0xFFFFu;
+#ifdef PBGPU_GRAPH_CHECK
+      if (edge) GCHECK(it_j < n, 3);
+#endif
       PROF_T(pa);
 #ifdef PBGPU_PROF
       ++pr_chunks;
@@ -4223,6 +4258,9 @@ __global__ __launch_bounds__(128) void k_graph_relax_big(GraphDev G, uint32_t n_
       const uint2 ce = k0 + lane < GRAPH_EBLK ? blk
                                               : (edge ? G.eovf[G.eoff[b + p] + (k0 + lane - GRAPH_EBLK)] : make_uint2(0u, 0u));
       const uint32_t it_j = ce.x & 0xFFFFu;
+#ifdef PBGPU_GRAPH_CHECK
+      if (edge) GCHECK(it_j < n, 3);
+#endif
       if (paths) {
         if (edge) {  // node_info update (overlap_graph.cc:41-56); this lane owns node j
           RelaxPath sj = S[it_j];

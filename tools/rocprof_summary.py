@@ -67,11 +67,12 @@ KERNELS = [("k_seed<256, 8, 0>", "k_seed"), ("k_group<false, 256u>", "k_group"),
 # sectors (k_seed's filter words and bucket probes) are counted exactly; k_group's
 # occurrence runs by the 512-B-run calibration; row streams by the guide's 2x
 KT_FIRST, PMC_FIRST = 4, 2  # tools/prof_r03.sh: --device-steps 3 (trace run), 1 (PMC runs)
-# Round 5: k_group's raw FETCH_SIZE equals, to within 1%, the bytes its two passes must read
-# (4 B of super-read id a hit in pass 0, the 8-B occurrence word in pass 1, 32 B a kept
-# k-mer; profiles/r05v_group_hbm.txt): its gathers are 4-8 B a lane, not the 16-B-a-lane
-# streams the x2 correction is for, so its traffic is the raw counters
-SHAPE = {"k_seed": "raw_fetch_plus_write", "k_group": "raw_fetch_plus_write", "k_lis": "guide_2x_fetch_plus_write",
+# Round 6: k_group's exact access shape (runs of 52 8-B occurrence words at random 8-B starts,
+# the 4-B id half in pass 0 and the word in pass 1; tools/calib_group.py,
+# profiles/r06c_group_calibration.txt) reads FETCH_SIZE = exactly 1/2 of the 128-B lines it
+# moves, both passes alike: its traffic is 2 x FETCH + WRITE.  (Round 5 took the raw counter
+# as exact because it matched the algorithmic bytes -- an undercount matched to an undercount.)
+SHAPE = {"k_seed": "raw_fetch_plus_write", "k_group": "guide_2x_fetch_plus_write", "k_lis": "guide_2x_fetch_plus_write",
          "k_coords": "guide_2x_fetch_plus_write", "k_rec_sort": "guide_2x_fetch_plus_write"}
 
 
