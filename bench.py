@@ -870,7 +870,7 @@ def main():
     # production device leg): FETCH_SIZE corrected for the kernel's read shape (random
     # 64-B sectors exact; occurrence runs by the 512-B-run calibration; row streams 2x)
     traffic, traffic_note, summ_name, summ_all = None, None, None, {}
-    for name in ("r05z_rocprof_summary.json", "r04z_rocprof_summary.json", "r04_rocprof_summary.json", "r03m_rocprof_summary.json", "r03k_rocprof_summary.json",
+    for name in ("r06z_rocprof_summary.json", "r05z_rocprof_summary.json", "r04z_rocprof_summary.json", "r04_rocprof_summary.json", "r03m_rocprof_summary.json", "r03k_rocprof_summary.json",
                  "r02e_rocprof_summary.json"):
         summ = os.path.join(ROOT, "profiles", name)
         if os.path.exists(summ):

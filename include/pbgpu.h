@@ -277,6 +277,9 @@ typedef struct {
   /* ABI 8: group-stage work items (a read, or one hash partition of a long read's
    * super-reads) whose table overflowed, summed over the rounds */
   uint64_t group_overflow_items;
+  /* ABI 8: reads grouped from buckets (their hits enumerated once into P >= 2 hash
+   * partitions, each partition's item streaming its bucket) */
+  uint64_t group_bucketed_reads;
 } pbgpu_stats;
 pbgpu_status pbgpu_aligner_get_stats(const pbgpu_aligner* al, pbgpu_stats* s);
 pbgpu_status pbgpu_aligner_reset_stats(pbgpu_aligner* al);

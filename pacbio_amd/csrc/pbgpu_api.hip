@@ -47,7 +47,8 @@ void launch_seed(int mode, IndexView ix, const uint8_t* seq, const uint64_t* rof
                  uint32_t* gcount, uint64_t null_ptr, hipStream_t st);
 void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const uint32_t* n_kept, const uint32_t* thr,
                   const uint64_t* hit_off, uint64_t node_base, uint32_t r0, const uint2* read_list, uint32_t n_list,
-                  uint32_t hcap_log2, uint32_t* gtable, GroupOut O, unsigned long long* stats, hipStream_t st);
+                  uint32_t hcap_log2, uint32_t* gtable, GroupOut O, unsigned long long* stats, hipStream_t st,
+                  int mode = 0);
 uint64_t group_table_words(uint32_t hcap_log2);
 void launch_sr_ul(const uint32_t* ids, uint64_t n, const int32_t* ul, uint64_t n_ul, int32_t* out, hipStream_t st);
 void launch_counts_pack16(bool unpack, const uint32_t* src, uint64_t n, uint32_t* dst, hipStream_t st);
@@ -2084,13 +2085,14 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
   uint64_t chunk_bases = std::max<uint64_t>(1ull << 26, mem_avail / 16 / 8);
   if (const char* e = getenv("PBGPU_CHUNK_BASES")) chunk_bases = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
   // a hit costs 24 B of per-hit buffers (X, pts, nodes) plus, through the chains it makes
-  // (chains_per_hit, learnt), a chain's descriptor and LIS state (~40 B), records (96 + 8 B
-  // each, rec_per_chain of them) and kmers_info (2 x 4 B x info_per_chain): sub-batches of
-  // at most a third of the free memory by that sum
+  // (chains_per_hit), a chain's descriptor and LIS state (~40 B), records (96 + 8 B each,
+  // rec_per_chain of them) and kmers_info (2 x 4 B x info_per_chain): sub-batches of at
+  // most the free memory / 1.25 by that sum once chains_per_hit is learnt from a sub-batch,
+  // a third of it before (the first estimate is C2's 1/80; C4's reads make 1 chain per 9 hits)
   const double per_hit = 24.0 + al->chains_per_hit * (40.0 + 104.0 * al->rec_per_chain * (al->P.max_match ? 2.0 : 1.0) +
                                                       8.0 * (double)al->info_per_chain);
-  const uint64_t budget = std::max<uint64_t>(1ull << 20, std::min<uint64_t>(al->hit_budget,
-                                                                            (uint64_t)((double)mem_avail / per_hit / 3.0)));
+  const uint64_t budget = std::max<uint64_t>(
+      1ull << 20, std::min<uint64_t>(al->hit_budget, (uint64_t)((double)mem_avail / per_hit / (al->cph_learned ? 1.25 : 3.0))));
   const uint32_t hcap_log2 = 11;
   std::vector<uint64_t> h_roff;  // host copy of the read offsets (the chunk cuts)
   if (rd->h_off.size() == (size_t)n + 1) {
@@ -2170,7 +2172,7 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
     // 8192-slot table over several hash partitions of its super-reads, a work item (and
     // block) each.  A misprediction only costs time: an overflowing item goes again in
     // the next tier or split in two.
-    uint32_t n_small = 0, n_bigr = 0;
+    uint32_t n_small = 0, n_bigr = 0, n_bkt = 0, n_split = 0;
     {
       const auto th0 = std::chrono::steady_clock::now();
       // Longest first by a counting sort over hit-count classes (exact below 128 hits, 16
@@ -2198,7 +2200,14 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
       const double fill_big = 0.95 * (double)((1u << kGroupLdsMaxLog2) / 8 * PBGPU_GROUP_BIG_FILL8);
       std::vector<uint2>& rs = al->h_small;
       std::vector<uint2>& rb = al->h_big;
-      rs.clear(); rb.clear();
+      std::vector<uint2>& rbb = al->h_bkt;   // partition items of bucketed reads (MODE 2)
+      std::vector<uint2>& rsp = al->h_split;  // one split item per bucketed read (MODE 1)
+      rs.clear(); rb.clear(); rbb.clear(); rsp.clear();
+      // PBGPU_GROUP_BUCKETS=0 (A/B): every partition item enumerates its read's hits (round 5)
+      const bool buckets_on = !(getenv("PBGPU_GROUP_BUCKETS") && !atoi(getenv("PBGPU_GROUP_BUCKETS")));
+      const double bucket_margin = getenv("PBGPU_GROUP_BUCKET_MARGIN") ? atof(getenv("PBGPU_GROUP_BUCKET_MARGIN")) : 1.5;
+      uint32_t boff_words = 0;
+      al->h_bmeta.assign(nr, make_uint2(0u, 0u));
       // tests: PBGPU_GROUP_FIRST_P=P puts every read in the smallest table as P hash-partition
       // items, so a one-read call can overflow P items at once
       const uint32_t first_p = getenv("PBGPU_GROUP_FIRST_P") ? (uint32_t)atoi(getenv("PBGPU_GROUP_FIRST_P")) : 0;
@@ -2210,10 +2219,32 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
         const double pred = (double)(hoff[r + 1] - hoff[r]) * al->chains_per_hit * pred_scale;
         if (pred <= fill_small) { rs.push_back(group_item(r, 0, 1)); continue; }
         const uint32_t P = (uint32_t)std::min(4096.0, std::max(1.0, std::ceil(pred / fill_big)));
+        if (P >= 2 && buckets_on) {
+          // bucketed: its hits are enumerated once (the split item) into Pb buckets, which
+          // its Pb partition items stream.  An item costs its bucket's entries plus a table
+          // clear and compaction, so more, smaller partitions cost little, while an item
+          // that overflows redoes its bucket in a later round: Pb takes a margin over the
+          // prediction (C4: an overflow round of ~8 ms in a 92-ms sub-batch at 1.0)
+          const uint32_t Pb = (uint32_t)std::min(4096.0, std::ceil(pred * bucket_margin / fill_big));
+          al->h_bmeta[r - r0] = make_uint2(boff_words, Pb);
+          boff_words += Pb + 1;
+          rsp.push_back(group_item(r, 0, Pb));
+          for (uint32_t q = 0; q < Pb; ++q) rbb.push_back(group_item(r, q, Pb));
+          continue;
+        }
         for (uint32_t q = 0; q < P; ++q) rb.push_back(group_item(r, q, P));
       }
       n_small = (uint32_t)rs.size(); n_bigr = (uint32_t)rb.size();
+      n_bkt = (uint32_t)rbb.size(); n_split = (uint32_t)rsp.size();
+      al->acc.group_bucketed_reads += n_split;
       rs.insert(rs.end(), rb.begin(), rb.end());
+      rs.insert(rs.end(), rbb.begin(), rbb.end());
+      rs.insert(rs.end(), rsp.begin(), rsp.end());
+      if (n_split) {
+        al->bmeta.ensure(n);
+        al->boff.ensure(boff_words + 1);
+        HIPCHK(hipMemcpyAsync(al->bmeta.p + r0, al->h_bmeta.data(), (size_t)nr * sizeof(uint2), hipMemcpyHostToDevice, st));
+      }
       al->acc.ms_host_order += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count();
       al->read_list.ensure(rs.size());
       HIPCHK(hipMemcpyAsync(al->read_list.p, rs.data(), rs.size() * sizeof(uint2), hipMemcpyHostToDevice, st));
@@ -2222,6 +2253,9 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
       al->ovf_items.ensure(rs.size()); al->ovf_grow.ensure(rs.size());
       O.overflow_items = al->ovf_items.p; O.overflow_grow = al->ovf_grow.p;
       O.overflow_cap = (uint32_t)std::min<size_t>(al->ovf_items.n, 0xFFFFFFFFu);
+      // the bucketed reads' staging: the sub-batch's LIS buffers, unused until the LIS stage
+      O.stage_x = al->pts.p; O.stage_sr = reinterpret_cast<uint32_t*>(al->nodes.p);
+      O.boff = al->boff.p; O.bmeta = al->bmeta.p;
     }
     for (int attempt = 0;; ++attempt) {
       HIPCHK(hipEventRecord(al->ev[5], st));
@@ -2232,7 +2266,29 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
       // PBGPU_GROUP_OVERLAP=1 (experiment): the 16-wave tier's reads -- the longest -- on a side
       // stream, started first, beside the 4-wave tier
       static const bool overlap = getenv("PBGPU_GROUP_OVERLAP") && atoi(getenv("PBGPU_GROUP_OVERLAP"));
-      if (overlap && n_bigr) {
+      // The split of the bucketed reads (every attempt: a retry after the LIS stage finds the
+      // staging overwritten) on a side stream beside the other tiers, their partition items
+      // after both: alone, a launch of a few long reads' splits held the GPU for its longest
+      // (C2: +1.7 ms of group stage)
+      const bool split_side = n_split && (n_small || n_bigr);
+      if (n_split) {
+        hipStream_t sst = st;
+        if (split_side) {
+          if (!al->grp_side) {
+            HIPCHK(hipStreamCreateWithFlags(&al->grp_side, hipStreamNonBlocking));
+            HIPCHK(hipEventCreateWithFlags(&al->grp_fork, hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&al->grp_join, hipEventDisableTiming));
+          }
+          HIPCHK(hipEventRecord(al->grp_fork, st));
+          HIPCHK(hipStreamWaitEvent(al->grp_side, al->grp_fork, 0));
+          sst = al->grp_side;
+        }
+        launch_group(v, krec, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0,
+                     al->read_list.p + n_small + n_bigr + n_bkt, n_split, 12, nullptr, O, al->stats.p, sst, 1);
+        HIPCHK(hipGetLastError());
+        if (split_side) HIPCHK(hipEventRecord(al->grp_join, al->grp_side));
+      }
+      if (overlap && n_bigr && !n_split) {
         if (!al->grp_side) {
           HIPCHK(hipStreamCreateWithFlags(&al->grp_side, hipStreamNonBlocking));
           HIPCHK(hipEventCreateWithFlags(&al->grp_fork, hipEventDisableTiming));
@@ -2250,13 +2306,17 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
                    hcap_log2, nullptr, O, al->stats.p, st);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(al->ev[9], st));
-      if (overlap && n_bigr) {
+      if (overlap && n_bigr && !n_split) {
         HIPCHK(hipStreamWaitEvent(st, al->grp_join, 0));
       } else {
         launch_group(v, krec, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0,
                      al->read_list.p + n_small, n_bigr, kGroupLdsMaxLog2, nullptr, O, al->stats.p, st);
         HIPCHK(hipGetLastError());
       }
+      if (split_side) HIPCHK(hipStreamWaitEvent(st, al->grp_join, 0));
+      launch_group(v, krec, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0,
+                   al->read_list.p + n_small + n_bigr, n_bkt, kGroupLdsMaxLog2, nullptr, O, al->stats.p, st, 2);
+      HIPCHK(hipGetLastError());
       uint32_t cnt[4];
       HIPCHK(hipMemcpyAsync(cnt, al->counters.p, 16, hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
@@ -2314,27 +2374,35 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
         }
         if (lg > kGroupLdsMaxLog2 && (1ull << (lg - 2)) > 2 * mx + 256)
           throw std::runtime_error("group table growth did not converge");
+        // the items of bucketed reads (they stream their bucket: MODE 2) after the others
+        const uint32_t n_plain = (uint32_t)(std::stable_partition(ovf.begin(), ovf.end(), [&](const uint2& it) {
+                                              return al->h_bmeta[it.x - r0].y == 0;
+                                            }) - ovf.begin());
         al->ovf_list.ensure(n_ovf);
         al->ovf_items.ensure(n_ovf); al->ovf_grow.ensure(n_ovf);  // (this round's overflow: at most its items)
         O.overflow_items = al->ovf_items.p; O.overflow_grow = al->ovf_grow.p;
         O.overflow_cap = (uint32_t)std::min<size_t>(al->ovf_items.n, 0xFFFFFFFFu);
         HIPCHK(hipMemcpyAsync(al->ovf_list.p, ovf.data(), n_ovf * sizeof(uint2), hipMemcpyHostToDevice, st));
         HIPCHK(hipMemsetAsync(al->counters.p + 3, 0, 4, st));
-        if (lg <= kGroupLdsMaxLog2) {
-          launch_group(v, krec, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0,
-                       al->ovf_list.p, n_ovf, lg, nullptr, O, al->stats.p, st);
-          HIPCHK(hipGetLastError());
-        } else {
-          al->acc.group_hbm_reads += n_ovf;
-          const uint64_t words = group_table_words(lg);
-          const uint32_t grp = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_ovf, (1ull << 28) / words));
-          al->gtable.ensure_fixed((uint64_t)grp * words);
-          for (uint32_t s0 = 0; s0 < n_ovf; s0 += grp) {
-            const uint32_t m = std::min(grp, n_ovf - s0);
-            HIPCHK(hipMemsetAsync(al->gtable.p, 0, (size_t)m * words * 4, st));
+        for (int mode = 0; mode <= 2; mode += 2) {
+          const uint32_t i0 = mode ? n_plain : 0, ni = mode ? n_ovf - n_plain : n_plain;
+          if (!ni) continue;
+          if (lg <= kGroupLdsMaxLog2) {
             launch_group(v, krec, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0,
-                         al->ovf_list.p + s0, m, lg, al->gtable.p, O, al->stats.p, st);
+                         al->ovf_list.p + i0, ni, lg, nullptr, O, al->stats.p, st, mode);
             HIPCHK(hipGetLastError());
+          } else {
+            al->acc.group_hbm_reads += ni;
+            const uint64_t words = group_table_words(lg);
+            const uint32_t grp = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ni, (1ull << 28) / words));
+            al->gtable.ensure_fixed((uint64_t)grp * words);
+            for (uint32_t s0 = 0; s0 < ni; s0 += grp) {
+              const uint32_t m = std::min(grp, ni - s0);
+              HIPCHK(hipMemsetAsync(al->gtable.p, 0, (size_t)m * words * 4, st));
+              launch_group(v, krec, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0,
+                           al->ovf_list.p + i0 + s0, m, lg, al->gtable.p, O, al->stats.p, st, mode);
+              HIPCHK(hipGetLastError());
+            }
           }
         }
         HIPCHK(hipMemcpyAsync(cnt, al->counters.p, 16, hipMemcpyDeviceToHost, st));
@@ -2442,6 +2510,7 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
         n_chains += sub[0]; n_tests += sub[1];
 #ifndef PBGPU_EXP_GROUP_ONLY
         if (Hs) al->chains_per_hit = std::max(1e-4, 1.1 * (double)nch / (double)Hs);
+        if (Hs) al->cph_learned = true;
 #endif
         // (records a chain yields, with a margin; max-match rounds are counted by rec_est's x2)
         if (nch && !al->P.max_match)

@@ -323,6 +323,8 @@ struct pbgpu_aligner {
   dbuf<uint32_t> rcur;
   dbuf<uint64_t> sort_scratch;  // k_rec_sort keys of reads above its LDS capacity: 6 words per record
   dbuf<uint2> rec_tiles;        // (read, tile) work items of those reads (carved from the dead hit buffers)
+  dbuf<uint2> bmeta;            // per read of the call: {bucket offsets base, P0} of bucketed reads (GroupOut)
+  dbuf<uint32_t> boff;          // the bucketed reads' bucket offsets (P0 + 1 each)
   dbuf<uint32_t> rec_tile_ctr;  // their count and the longest such read
   dbuf<uint64_t> nhits, hit_off, rec_off, huge_elems;
   dbuf<int2> hits;
@@ -359,12 +361,13 @@ struct pbgpu_aligner {
   // the device out of memory beside its 126-GB index); an overflow redoes the sub-batch and
   // resets it to 1
   double rec_per_chain = 1.0;
+  bool cph_learned = false;  // chains_per_hit measured on a sub-batch (the hit budget's margin)
   // pbgpu_run: the most bases a batch holds (0 = unknown): the per-base buffers never grow past it
   uint64_t base_cap = 0;
   double chains_per_hit = 1.0 / 80;  // k_group tier estimate (C2: 1.1 x 1/90), refined after every batch
   dbuf<uint2> ovf_list, read_list;  // k_group work items (group_item): the overflow round's, the launch's
   std::vector<uint32_t> h_order, h_class;  // host scratch of the group stage's read order
-  std::vector<uint2> h_small, h_big, h_items;
+  std::vector<uint2> h_small, h_big, h_items, h_bkt, h_split, h_bmeta;
   std::vector<uint64_t> h_hoff;
   // sharded index: per-base k-mer counts of the current batch (SEED_COUNTS, then summed)
   dbuf<uint32_t> gcount;

@@ -131,6 +131,17 @@ struct GroupOut {
   uint32_t* n_overflow;
   uint32_t overflow_cap;    // entries of overflow_items / overflow_grow (>= the launch's work items)
   uint32_t* rcur;          // per read: hits placed so far by its partitions (P > 1 items)
+  // Bucketed reads (round 6): a read predicted to need P >= 2 hash partitions has its hits
+  // enumerated once by a split launch (k_group MODE 1), which writes them, stably by
+  // partition, to a staging copy in the sub-batch's LIS buffers (free until the LIS stage):
+  // stage_sr = super-read | bwd << 31, stage_x = {pb offset, 1-based sr offset}, at
+  // the read's hit range; bucket p of the read is [boff[bmeta.x + p], boff[bmeta.x + p + 1]),
+  // read-local, bmeta[r] = {boff base, P0}.  Its partition items (MODE 2) then stream their
+  // bucket instead of re-enumerating every hit of the read (C4: ~4 items a read each did).
+  int2* stage_x;
+  uint32_t* stage_sr;
+  uint32_t* boff;
+  const uint2* bmeta;
 };
 // k_group work item {read, partition | partitions << 16}: the read's hits whose super-read
 // falls in hash partition `partition` of `partitions` (floor(h * P / 2^32) of the id's hash,

@@ -553,7 +553,12 @@ constexpr int GROUP_U = PBGPU_GROUP_U, GROUP_U_BIG = PBGPU_GROUP_U_BIG;  // 64-h
 #ifndef PBGPU_GROUP_BUCKET
 #define PBGPU_GROUP_BUCKET 1  // bucketed LDS-table probing (4 slots a 16-byte read); 0 = slot by slot
 #endif
-template <bool GLOBAL_TABLE, uint32_t B>
+// MODE 0: a work item enumerates its read's hits from the index (k-mer records ->
+// occurrence lists).  MODE 1 (split): one item per bucketed read (P0 partitions) enumerates
+// them once and writes them to the read's P0 buckets (GroupOut::stage_*); no table, no
+// chains.  MODE 2: a partition item of a bucketed read streams its bucket (for a refined
+// item, partition q of Q = P0 f: bucket q / f, its entries filtered by partition).
+template <bool GLOBAL_TABLE, uint32_t B, int MODE>
 __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_group(IndexView ix, const KRec* __restrict__ krec,
                                                        const uint64_t* __restrict__ roff, const uint32_t* __restrict__ n_kept,
                                                        const uint32_t* __restrict__ thr_in, const uint64_t* __restrict__ hit_off,
@@ -583,8 +588,19 @@ __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_
   uint32_t* tcf = tkey + hcap;
   uint32_t* tcb = tcf + hcap;
   const uint64_t kbase = roff[r];
-  const uint32_t nk = n_kept[r], thr = thr_in[r];
   const uint64_t hbase = hit_off[r] - node_base;
+  // MODE 2: the item's bucket [b_lo, b_lo + nk) of the read's staged hits
+  uint32_t b_lo = 0;
+  uint32_t nk = n_kept[r];
+  if constexpr (MODE == 2) {
+    const uint2 bm = O.bmeta[r];
+    const uint32_t p0 = part / (P / bm.y);
+    b_lo = O.boff[bm.x + p0];
+    nk = O.boff[bm.x + p0 + 1] - b_lo;
+  }
+  const uint32_t thr = thr_in[r];
+  // the group loop's step: k-mer records (MODE 0 / 1), or staged hits (MODE 2: 16 windows a wave)
+  constexpr uint32_t GSTEP = MODE == 2 ? B * 16 : B;
 #ifndef PBGPU_GROUP_BIG_FILL8
 #define PBGPU_GROUP_BIG_FILL8 6  // the LDS tables' fill limit in eighths (the 8192-slot tier's below)
 #endif
@@ -623,7 +639,7 @@ __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_
     // flight and waits for all of them
     auto groups = [&](auto pass_c) {
     constexpr int pass = decltype(pass_c)::value;
-    for (uint32_t g0 = 0; g0 < nk; g0 += B) {
+    for (uint32_t g0 = 0; g0 < nk; g0 += GSTEP) {
       if (s_flag) { g_stop = g0; break; }  // uniform (written before the last barrier)
 #ifdef PBGPU_PROF
       const uint64_t pr_a = __builtin_amdgcn_s_memtime();
@@ -631,7 +647,7 @@ __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_
       const uint32_t i = g0 + tid;
       uint32_t nf = 0, nb = 0;
       int32_t pbv = 0;
-      if (i < nk) {
+      if (MODE != 2 && i < nk) {
         const KRec kr = krec[kbase + i];
         if (kr.count <= thr) {
           const uint64_t ptr = kr.occ_ptr & ~(1ull << 63);
@@ -648,10 +664,14 @@ __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_
           pbv = kr.pb_off;
         }
       }
-      s_np[tid] = make_uint2(nf, (uint32_t)pbv);
       uint32_t total;
-      s_off[tid] = block_excl_scan<B>(nf + nb, s_scan, total);
-      __syncthreads();
+      if constexpr (MODE == 2) {
+        total = nk - g0 < GSTEP ? nk - g0 : GSTEP;
+      } else {
+        s_np[tid] = make_uint2(nf, (uint32_t)pbv);
+        s_off[tid] = block_excl_scan<B>(nf + nb, s_scan, total);
+        __syncthreads();
+      }
 #ifdef PBGPU_PROF
       const uint64_t pr_b = __builtin_amdgcn_s_memtime();
       pr_setup[pass] += pr_b - pr_a;
@@ -678,6 +698,23 @@ __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_
 #pragma unroll
         for (int u = 0; u < GU; ++u) {
           const uint32_t h = ((ws + wave * GU + (uint32_t)u) << 6) + lane;
+          if constexpr (MODE == 2) {
+            // a staged hit (the bucket's entries past the group's end reload its first)
+            const bool valid = h < total;
+            const uint64_t at = hbase + b_lo + g0 + (valid ? h : 0u);
+            const uint32_t w = O.stage_sr[at];
+            val_o[u] = valid;
+            fwd_o[u] = (w >> 31) == 0;
+            if constexpr (pass == 0) {
+              e_o[u] = (uint64_t)(w & 0x7FFFFFFFu) << 32;
+              pb_o[u] = 0;
+            } else {
+              const int2 x = O.stage_x[at];
+              e_o[u] = ((uint64_t)(w & 0x7FFFFFFFu) << 32) | (uint32_t)x.y;
+              pb_o[u] = x.x;
+            }
+            continue;
+          }
           // no branch around the load (windows past the group's end load occ[0]): the
           // compiler counts the loads in flight only when every path issues them
           uint32_t lo = 0;  // s_off[0] = 0: fixed depth, branch-free
@@ -713,6 +750,36 @@ __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_
           mine_q[u] = val_q[u] && part_of(sr_q[u]) == part;
           pbx_q[u] = pb_q[u];
           fwdx_q[u] = fwd_q[u];
+        }
+        if constexpr (MODE == 1) {
+          // split: every hit to its partition's bucket -- pass 0 counts (tkey[p]), pass 1
+          // takes the bucket cursor (tcf[p]) in wave turn order, as pass 1 below does
+          if constexpr (pass == 0) {
+#pragma unroll
+            for (int u = 0; u < GU; ++u)
+              if (val_q[u]) atomicAdd(&tkey[part_of(sr_q[u])], 1u);
+          } else {
+            uint32_t pos_q[GU];
+#pragma unroll
+            for (int u = 0; u < GU; ++u) pos_q[u] = 0;
+            for (uint32_t w = 0; w < NW; ++w) {
+              if (wave == w) {
+#pragma unroll
+                for (int u = 0; u < GU; ++u)
+                  if (val_q[u]) pos_q[u] = atomicAdd(&tcf[part_of(sr_q[u])], 1u);
+              }
+              table_barrier();
+            }
+            uint32_t* const sink32 = reinterpret_cast<uint32_t*>(O.sink);
+#pragma unroll
+            for (int u = 0; u < GU; ++u) {
+              (val_q[u] ? O.stage_sr[hbase + pos_q[u]] : sink32[(blockIdx.x + wave) & (GROUP_SINKS - 1)]) =
+                  sr_q[u] | (fwdx_q[u] ? 0u : 0x80000000u);
+              (val_q[u] ? O.stage_x[hbase + pos_q[u]] : O.sink[(blockIdx.x + wave) & (GROUP_SINKS - 1)]) =
+                  make_int2(pbx_q[u], so_q[u]);
+            }
+          }
+          return;
         }
         // The first table probe of every window is issued together (one LDS round trip
         // for the step), then the rare collisions are walked one window at a time.  A
@@ -903,6 +970,31 @@ __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_
     const int pass = pass_rt;
     if (pass == 0) groups(std::integral_constant<int, 0>{});
     else groups(std::integral_constant<int, 1>{});
+    if (MODE == 1 && pass == 0) {
+      // the buckets: an exclusive scan of the P partition counts (<= 4096, hcap), written as
+      // the read's bucket offsets and kept as pass 1's cursors
+      const uint32_t per = (P + B - 1) / B;
+      uint32_t sum = 0;
+      for (uint32_t j = 0; j < per; ++j) {
+        const uint32_t pj = tid * per + j;
+        sum += pj < P ? tkey[pj] : 0u;
+      }
+      uint32_t tot;
+      uint32_t b0 = block_excl_scan<B>(sum, s_scan, tot);
+      const uint32_t ob = O.bmeta[r].x;
+      for (uint32_t j = 0; j < per; ++j) {
+        const uint32_t pj = tid * per + j;
+        if (pj < P) {
+          O.boff[ob + pj] = b0;
+          tcf[pj] = b0;
+          b0 += tkey[pj];
+        }
+      }
+      if (tid == 0) O.boff[ob + P] = tot;
+      __syncthreads();
+      continue;
+    }
+    if (MODE == 1) break;
     if (pass == 0) {
 #ifdef PBGPU_PROF
       const uint64_t pr_c = __builtin_amdgcn_s_memtime();
@@ -964,7 +1056,7 @@ __global__ __launch_bounds__(B, B == GROUP_BLOCK ? PBGPU_GROUP_MINW : 1) void k_
   }
   }  // the partition
   if (p0x == 0x9E3779B9u) O.sink[0] = make_int2((int)p0x, 0);  // practically never
-  if (!GLOBAL_TABLE && B == GROUP_BLOCK && tid == 0) {  // per-launch algorithmic counters (bench roofline)
+  if (MODE == 0 && !GLOBAL_TABLE && B == GROUP_BLOCK && tid == 0) {  // per-launch algorithmic counters (bench roofline)
     atomicAdd(&stats[ST_G0_KEPT], (unsigned long long)nk);
     atomicAdd(&stats[ST_G0_HITS], (unsigned long long)part_hits);
     atomicAdd(&stats[ST_G0_CHAINS], (unsigned long long)read_chains);
@@ -1545,6 +1637,121 @@ __global__ __launch_bounds__(256) void k_order_tiny(const ChainDesc* __restrict_
 #pragma unroll
     for (int j = 0; j < NMAX; ++j) if ((uint32_t)j < n) X[base + j] = v[j];
   }
+}
+
+// Strands of at most NMAX (<= 8) hits, one per lane, entirely in registers: the list order
+// restored by the odd-even network of k_order_tiny (X written back when it moved), then
+// lis_align::compute_L_P (lis_align.hpp:139-182) and indices (:190-204) restated literally
+// -- the singly linked list L walked from its head, the first acceptable predecessor, the
+// insertion after the first node of minimal length seen before it -- with the nodes packed
+// 16 bits each ({nxt, P, len, root} 4 bits apiece, 15 = none) in two 64-bit registers and
+// a node's hit picked from registers by index.  The generic lane-per-strand k_lis staged
+// these strands through LDS rows, stored every node to HBM and read hits and nodes back
+// for the reverse sweep (C4: 1 chain per 9 hits, most strands <= 8 hits: k_lis 13.9 +
+// k_order_tiny 3.2 ms of a 92-ms sub-batch).  Default window only (W = 1, affine
+// step test), no kept lis indices (--max-match takes the generic kernel).
+template <int NMAX>
+__global__ __launch_bounds__(256) void k_lis_tiny(const ChainDesc* __restrict__ chains,
+                                                  const uint32_t* __restrict__ items, uint32_t n_items,
+                                                  const uint32_t* __restrict__ slen, int2* X, int2* __restrict__ pts,
+                                                  uint32_t* __restrict__ lisl, LisParams lp,
+                                                  unsigned long long* stats) {
+  static_assert(NMAX <= 8, "4-bit node fields");
+  constexpr uint32_t NONE = 15;
+  const uint32_t w = blockIdx.x * 256 + threadIdx.x;
+  const bool act = w < n_items;
+  uint32_t item = 0, n = 0;
+  uint64_t base = 0;
+  if (act) {
+    item = items[w];
+    const ChainDesc d = chains[item >> 1];
+    base = d.hit_base + ((item & 1) ? d.nf : 0);
+    n = slen[item];
+  }
+  int2 v[NMAX];
+#pragma unroll
+  for (int j = 0; j < NMAX; ++j) v[j] = (uint32_t)j < n ? X[base + j] : make_int2(0, 0);
+  if (!lp.ordered) {
+    bool moved = false;
+#pragma unroll
+    for (int r = 0; r < NMAX; ++r) {
+#pragma unroll
+      for (int j = r & 1; j + 1 < NMAX; j += 2) {
+        if ((uint32_t)(j + 1) < n && hit_after(v[j], v[j + 1])) {
+          const int2 t = v[j]; v[j] = v[j + 1]; v[j + 1] = t;
+          moved = true;
+        }
+      }
+    }
+    if (moved) {
+#pragma unroll
+      for (int j = 0; j < NMAX; ++j) if ((uint32_t)j < n) X[base + j] = v[j];
+    }
+  }
+  auto xat = [&](uint32_t q) -> int2 {  // v[q], q < NMAX, by selects
+    int2 r = v[0];
+#pragma unroll
+    for (int j = 1; j < NMAX; ++j) r = q == (uint32_t)j ? v[j] : r;
+    return r;
+  };
+  // node q: bits [16 (q & 3), +16) of nd[q >> 2]: nxt | P << 4 | len << 8 | root << 12
+  uint64_t nd0 = 0, nd1 = 0;
+  auto node = [&](uint32_t q) -> uint32_t { return (uint32_t)(((q < 4 ? nd0 : nd1) >> (16 * (q & 3))) & 0xFFFFu); };
+  auto set_node = [&](uint32_t q, uint32_t val) {
+    const uint32_t sh = 16 * (q & 3);
+    const uint64_t m = ~(0xFFFFull << sh), x = (uint64_t)val << sh;
+    if (q < 4) nd0 = (nd0 & m) | x; else nd1 = (nd1 & m) | x;
+  };
+  auto set_nxt = [&](uint32_t q, uint32_t nx) { set_node(q, (node(q) & ~15u) | nx); };
+  uint64_t tests = 0;
+  uint32_t head = NONE, longest = 0, longest_ind = 0;
+  int32_t xmn = INT32_MAX, xmx = INT32_MIN, ymn = INT32_MAX, ymx = INT32_MIN;
+  for (uint32_t i = 0; i < n; ++i) {
+    const int2 xi = xat(i);
+    xmn = min(xmn, xi.x); xmx = max(xmx, xi.x); ymn = min(ymn, xi.y); ymx = max(ymx, xi.y);
+    uint32_t prev = NONE, prev_len = 0, found = NONE, f_len = 0, f_root = 0;
+    for (uint32_t it = head; it != NONE;) {
+      ++tests;
+      const uint32_t nv = node(it), lj = (nv >> 8) & 15u;
+      const int2 xj = xat(it);
+      if ((xi.y > xj.y) && affine_ok(lp.a, lp.b, lp.C, (double)(xi.x - xj.x), (double)(xi.y - xj.y))) {
+        found = it; f_len = lj; f_root = nv >> 12;
+        break;
+      }
+      if (prev == NONE || lj < prev_len) { prev = it; prev_len = lj; }
+      it = nv & 15u;
+    }
+    const uint32_t elen = found != NONE ? f_len + 1 : 1u, eroot = found != NONE ? f_root : i;
+    uint32_t enxt;
+    if (prev == NONE) { enxt = head; head = i; }
+    else { enxt = node(prev) & 15u; set_nxt(prev, i); }
+    set_node(i, enxt | (found << 4) | (elen << 8) | (eroot << 12));
+    if (longest < elen) {
+      const int2 xr = xat(eroot);
+      if (lp.seq_all || linear_ok(lp.a, (double)(xi.x - xr.x), (double)(xi.y - xr.y))) {
+        longest = elen; longest_ind = i;
+      }
+    }
+  }
+  if (act) {
+    // the lis points in ascending order along P (indices, lis_align.hpp:190-204)
+    int2* Pl = pts + base;
+    uint32_t* Pw = (uint32_t*)Pl + 2;
+    const bool cmp = longest >= 2 && (uint32_t)(xmx - xmn) < 65536u && (uint32_t)(ymx - ymn) < 65536u;
+    const int2 last = xat(longest_ind);
+    uint32_t sidx = longest_ind;
+    for (uint32_t t = 0; t < longest; ++t) {
+      const uint32_t o = longest - 1 - t;
+      const int2 p = xat(sidx);
+      if (cmp) Pw[o] = pt_word(last, p);
+      else Pl[o] = p;
+      sidx = (node(sidx) >> 4) & 15u;
+    }
+    if (cmp) { Pw[-2] = (uint32_t)last.x | PT_COMPACT; Pw[-1] = (uint32_t)last.y; }
+    lisl[item] = longest;
+  }
+  tests = wave_sum_u64(tests);
+  if ((threadIdx.x & 63) == 0 && tests) atomicAdd(&stats[ST_LIS_TESTS], (unsigned long long)tests);
 }
 
 constexpr int LISW_TINY_N = 255;  // SMAX of the timed tier-0 k_lis_w
@@ -2879,10 +3086,14 @@ void launch_seed(int mode, IndexView ix, const uint8_t* seq, const uint64_t* rof
                        n_reads, P, krec, n_kept, thr, nhits, stats, gcount, null_ptr);
 }
 
+// mode: k_group's MODE (0: enumerate from the index; 1: split bucketed reads, 16-wave blocks,
+// hcap_log2 12 for the partition counters; 2: partition items of bucketed reads)
 void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const uint32_t* n_kept, const uint32_t* thr,
                   const uint64_t* hit_off, uint64_t node_base, uint32_t r0, const uint2* read_list, uint32_t n_list,
-                  uint32_t hcap_log2, uint32_t* gtable, GroupOut O, unsigned long long* stats, hipStream_t st) {
+                  uint32_t hcap_log2, uint32_t* gtable, GroupOut O, unsigned long long* stats, hipStream_t st,
+                  int mode) {
   if (!n_list) return;
+#define PBGPU_GROUP_ARGS ix, krec, roff, n_kept, thr, hit_off, node_base, r0, read_list, n_list, hcap_log2, gtable, O, stats
   if (!gtable) {  // LDS table: hcap_log2 <= 13; the 8192-slot table gets a 16-wave block
     // PBGPU_GROUP_LDS_PAD (experiment): extra dynamic LDS for the 4-wave tier, so fewer of
     // its blocks share a CU (fewer reads' lists open at once)
@@ -2897,22 +3108,25 @@ void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const ui
     (void)hipGetDevice(&dev);
     const uint64_t bit = 1ull << (dev & 63);
     if (!(attr_done.load(std::memory_order_acquire) & bit)) {
-      (void)hipFuncSetAttribute((const void*)k_group<false, GROUP_BLOCK>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                120 * 1024);
-      (void)hipFuncSetAttribute((const void*)k_group<false, GROUP_BLOCK_BIG>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
+      for (const void* f : {(const void*)k_group<false, GROUP_BLOCK, 0>, (const void*)k_group<false, GROUP_BLOCK_BIG, 0>,
+                            (const void*)k_group<false, GROUP_BLOCK_BIG, 1>, (const void*)k_group<false, GROUP_BLOCK_BIG, 2>})
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
       attr_done.fetch_or(bit, std::memory_order_acq_rel);
     }
-    if (hcap_log2 >= PBGPU_GROUP_BIG_LOG2)
-      hipLaunchKernelGGL((k_group<false, GROUP_BLOCK_BIG>), dim3(n_list), dim3(GROUP_BLOCK_BIG), lds, st, ix, krec, roff,
-                         n_kept, thr, hit_off, node_base, r0, read_list, n_list, hcap_log2, gtable, O, stats);
+    if (mode == 1)
+      hipLaunchKernelGGL((k_group<false, GROUP_BLOCK_BIG, 1>), dim3(n_list), dim3(GROUP_BLOCK_BIG), lds, st, PBGPU_GROUP_ARGS);
+    else if (mode == 2)
+      hipLaunchKernelGGL((k_group<false, GROUP_BLOCK_BIG, 2>), dim3(n_list), dim3(GROUP_BLOCK_BIG), lds, st, PBGPU_GROUP_ARGS);
+    else if (hcap_log2 >= PBGPU_GROUP_BIG_LOG2)
+      hipLaunchKernelGGL((k_group<false, GROUP_BLOCK_BIG, 0>), dim3(n_list), dim3(GROUP_BLOCK_BIG), lds, st, PBGPU_GROUP_ARGS);
     else
-      hipLaunchKernelGGL((k_group<false, GROUP_BLOCK>), dim3(n_list), dim3(GROUP_BLOCK), lds, st, ix, krec, roff, n_kept,
-                         thr, hit_off, node_base, r0, read_list, n_list, hcap_log2, gtable, O, stats);
+      hipLaunchKernelGGL((k_group<false, GROUP_BLOCK, 0>), dim3(n_list), dim3(GROUP_BLOCK), lds, st, PBGPU_GROUP_ARGS);
+  } else if (mode == 2) {
+    hipLaunchKernelGGL((k_group<true, GROUP_BLOCK_BIG, 2>), dim3(n_list), dim3(GROUP_BLOCK_BIG), 0, st, PBGPU_GROUP_ARGS);
   } else {
-    hipLaunchKernelGGL((k_group<true, GROUP_BLOCK_BIG>), dim3(n_list), dim3(GROUP_BLOCK_BIG), 0, st, ix, krec, roff,
-                       n_kept, thr, hit_off, node_base, r0, read_list, n_list, hcap_log2, gtable, O, stats);
+    hipLaunchKernelGGL((k_group<true, GROUP_BLOCK_BIG, 0>), dim3(n_list), dim3(GROUP_BLOCK_BIG), 0, st, PBGPU_GROUP_ARGS);
   }
+#undef PBGPU_GROUP_ARGS
 }
 // IndexView::occ_sr: the high word of every occ word (headers included, unused)
 __global__ void k_occ_sr(const uint64_t* __restrict__ occ, uint64_t n, uint32_t* __restrict__ out) {
@@ -3001,6 +3215,13 @@ void launch_lis_lane(const ChainDesc* chains, const uint32_t* items, uint32_t n_
                      void* N16, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx, unsigned long long* stats,
                      hipStream_t st) {
   if (!n_items) return;
+  // the register kernel: default window, no kept lis indices (PBGPU_LIS_TINY=0: the generic path)
+  static const bool tiny_on = !(getenv("PBGPU_LIS_TINY") && !atoi(getenv("PBGPU_LIS_TINY")));
+  if (tiny_on && !keep_idx && lp.W == 1 && !lp.mer_all) {
+    hipLaunchKernelGGL((k_lis_tiny<PBGPU_LIS_LANE_MAX>), dim3((n_items + 255) / 256), dim3(256), 0, st, chains, items,
+                       n_items, slen, X, pts, lisl, lp, stats);
+    return;
+  }
   if (!lp.ordered)
     hipLaunchKernelGGL((k_order_tiny<PBGPU_LIS_LANE_MAX>), dim3((n_items + 255) / 256), dim3(256), 0, st, chains, items,
                        n_items, slen, X);
@@ -3072,18 +3293,6 @@ void launch_strand_order(const ChainDesc* chains, const uint32_t* items, uint32_
                      slen, X);
 }
 #ifdef PBGPU_PROF
-#ifdef PBGPU_GRAPH_CHECK
-// the check counters so far, printed to stderr by every aligner with a graph at its free
-// (the CLIs run the variant through LD_LIBRARY_PATH and print nothing of their own)
-namespace pbgpu {
-void graph_check_report() {
-  unsigned long long h[5] = {};
-  const hipError_t e = hipMemcpyFromSymbol(h, HIP_SYMBOL(g_graph_check), sizeof(h));
-  fprintf(stderr, "pbgpu graph-check: far_j %llu name_units %llu prefix_sums %llu edge_targets %llu checks %llu%s\n",
-          h[0], h[1], h[2], h[3], h[4], e == hipSuccess ? "" : " (counters unreadable)");
-}
-}  // namespace pbgpu
-#endif
 extern "C" int pbgpu_debug_prof(unsigned long long* out, int n, int reset) {
   if (n > PROF_SLOTS) n = PROF_SLOTS;
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), n * sizeof(unsigned long long)) != hipSuccess) return -1;
@@ -3757,7 +3966,11 @@ __global__ __launch_bounds__(GE_BLOCK) void k_graph_edges(GraphDev G, uint64_t n
         const uint64_t j = direct ? x + lane : (act ? (uint64_t)sq[lane] : q);
         const uint32_t sj = (uint32_t)((act ? j : q) - q0);
 #ifdef PBGPU_GRAPH_CHECK
-        if (act) { GCHECK(j > q && j < qe && j < n_recs, 0); GCHECK(true, 4); }
+        if (act) GCHECK(j > q && j < qe && j < n_recs, 0);
+        {
+          const uint64_t am = __ballot(act);
+          if (lane == 0 && am) atomicAdd(&g_graph_check[4], (unsigned long long)__builtin_popcountll(am));
+        }
 #endif
         // node j: staged, or (a scan past the window) one 64-byte line from HBM.  Every load
         // is issued before the tests (measured: loading the name only where the name test
@@ -5045,3 +5258,16 @@ hipError_t launch_graph_relax(const GraphDev& G, uint32_t n_reads, uint64_t n_re
 }
 
 }  // namespace pbgpu
+
+#ifdef PBGPU_GRAPH_CHECK
+// the check counters so far, printed to stderr by every aligner with a graph at its free
+// (the CLIs run the variant through LD_LIBRARY_PATH and print nothing of their own)
+namespace pbgpu {
+void graph_check_report() {
+  unsigned long long h[5] = {};
+  const hipError_t e = hipMemcpyFromSymbol(h, HIP_SYMBOL(g_graph_check), sizeof(h));
+  fprintf(stderr, "pbgpu graph-check: far_j %llu name_units %llu prefix_sums %llu edge_targets %llu checks %llu%s\n",
+          h[0], h[1], h[2], h[3], h[4], e == hipSuccess ? "" : " (counters unreadable)");
+}
+}  // namespace pbgpu
+#endif

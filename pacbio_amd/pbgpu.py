@@ -154,7 +154,8 @@ class Stats(C.Structure):
                                                                     ("graph_host_reads", C.c_uint64),
                                                                     ("group_refines", C.c_uint64),
                                                                     ("group_hbm_reads", C.c_uint64),
-                                                                    ("group_overflow_items", C.c_uint64)]
+                                                                    ("group_overflow_items", C.c_uint64),
+                                                                    ("group_bucketed_reads", C.c_uint64)]
 
     def as_dict(self):
         d = {n: getattr(self, n) for n, _ in self._fields_ if not n.startswith("kernel_")}

@@ -167,6 +167,27 @@ def test_group_first_round_items_overflow(data, first_p, dense, small, monkeypat
             assert st1["group_overflow_items"] >= 2, st1
 
 
+@pytest.mark.parametrize("data,scale", [("dense", "8"), ("dense", "200"), ("small", "200"), ("small", "2000")])
+def test_group_bucketed_reads(data, scale, dense, small, monkeypatch):
+    """Reads predicted past the 8192-slot table in P >= 2 hash partitions are enumerated
+    once into P buckets (a split item) whose partition items stream them (round 6).
+    PBGPU_GROUP_PRED_SCALE inflates the prediction so that most reads take that path,
+    with P up to hundreds (200): the same bytes as the oracle, and as the round-5 path
+    where every partition item enumerates the read (PBGPU_GROUP_BUCKETS=0)."""
+    ds = dense if data == "dense" else small
+    monkeypatch.setenv("PBGPU_GROUP_PRED_SCALE", scale)
+    names, seqs = ds.sr_names(), ds.sr_seqs()
+    pnames, pseqs = ds.pb_names(), ds.pb_seqs()
+    cfg = dict(ul=ds.unitig_lengths, forward=True, unitigs_k=31)
+    exp = _oracle(names, seqs, pnames, pseqs, **cfg)
+    got, st = _gpu(names, seqs, pnames, pseqs, **cfg)
+    assert st["group_bucketed_reads"] >= len(pseqs) // 2, st
+    assert_same_coords(got, exp, f"bucketed {data} scale={scale}")
+    monkeypatch.setenv("PBGPU_GROUP_BUCKETS", "0")
+    old, st0 = _gpu(names, seqs, pnames, pseqs, **cfg)
+    assert st0["group_bucketed_reads"] == 0 and old == got
+
+
 def test_repeats_threshold():
     from tools.synth import Dataset
     ds = Dataset("small", seed=3, repeat_frac=0.2, n_pb=30)
