@@ -409,7 +409,17 @@ def c4_leg(args, comm, rank, world, local, threads, pbgpu, Dataset, brand=True):
     ds.close()
     total = comm.sum(bases)
     per_kernel = _per_kernel(st, steps, None, b_filt, b_table, info)
-    dom = max(per_kernel, key=lambda kk: per_kernel[kk]["stage_ms_per_step"])
+    # k_group's per-launch figure is its first tier's (the timed launch), which on C4 holds a
+    # few reads: the group stage is priced whole -- every tier, split and bucket launch --
+    # by the algorithmic bytes of all its hits over the stage's time
+    g_alg = (st["n_kept"] * 32 + st["n_hits"] * 16 + st["n_chains"] * 24) / steps
+    g_ms = st["ms_group"] / steps
+    per_kernel["group_stage"] = {"alg_bytes_per_step": g_alg, "stage_ms_per_step": round(g_ms, 3),
+                                 "achieved_gbs": round(g_alg / (g_ms * 1e-3) / 1e9, 1),
+                                 "frac": round(g_alg / (g_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                 "formula": "kept*32 + hits*16 + chains*24 over the group stage (all launches)"}
+    cand = {kk: v for kk, v in per_kernel.items() if kk != "k_group"}
+    dom = max(cand, key=lambda kk: cand[kk]["stage_ms_per_step"])
     return {
         "workload": ("C4 chr1-scale (BASELINE configs[3]): full index of 10M super-reads over a 250 Mbp genome with "
                      "2% 5-50-copy repeats, built on this GPU; PacBio reads of 15 kb N50 (lognormal mean 12.5 kb, "

@@ -2206,6 +2206,16 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
       // PBGPU_GROUP_BUCKETS=0 (A/B): every partition item enumerates its read's hits (round 5)
       const bool buckets_on = !(getenv("PBGPU_GROUP_BUCKETS") && !atoi(getenv("PBGPU_GROUP_BUCKETS")));
       const double bucket_margin = getenv("PBGPU_GROUP_BUCKET_MARGIN") ? atof(getenv("PBGPU_GROUP_BUCKET_MARGIN")) : 1.5;
+      // (from P >= 3: on C2 the few reads of P = 2 grouped slower bucketed, 32.7 against 31.3 ms,
+      // profiles/r06k_bucket_minp.txt)
+      const uint32_t bucket_minp = getenv("PBGPU_GROUP_BUCKET_MINP") ? (uint32_t)atoi(getenv("PBGPU_GROUP_BUCKET_MINP")) : 3;
+      // the bucket items' table: 2^bkt_log2 slots (11: the 2048-slot, 4-wave blocks of the first
+      // tier, five a CU; 13: the 8192-slot 16-wave blocks, one a CU), P sized for its fill limit
+      const uint32_t bkt_log2 = std::min<uint32_t>(kGroupLdsMaxLog2, std::max<uint32_t>(hcap_log2,
+          getenv("PBGPU_GROUP_BUCKET_LOG2") ? (uint32_t)atoi(getenv("PBGPU_GROUP_BUCKET_LOG2")) : 11));
+      al->bkt_log2 = bkt_log2;
+      const double fill_bkt = bkt_log2 >= kGroupLdsMaxLog2 ? fill_big
+                                                           : 0.95 * (double)((1u << bkt_log2) - (1u << bkt_log2) / 4);
       uint32_t boff_words = 0;
       al->h_bmeta.assign(nr, make_uint2(0u, 0u));
       // tests: PBGPU_GROUP_FIRST_P=P puts every read in the smallest table as P hash-partition
@@ -2219,13 +2229,13 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
         const double pred = (double)(hoff[r + 1] - hoff[r]) * al->chains_per_hit * pred_scale;
         if (pred <= fill_small) { rs.push_back(group_item(r, 0, 1)); continue; }
         const uint32_t P = (uint32_t)std::min(4096.0, std::max(1.0, std::ceil(pred / fill_big)));
-        if (P >= 2 && buckets_on) {
+        if (P >= bucket_minp && buckets_on) {
           // bucketed: its hits are enumerated once (the split item) into Pb buckets, which
           // its Pb partition items stream.  An item costs its bucket's entries plus a table
           // clear and compaction, so more, smaller partitions cost little, while an item
           // that overflows redoes its bucket in a later round: Pb takes a margin over the
           // prediction (C4: an overflow round of ~8 ms in a 92-ms sub-batch at 1.0)
-          const uint32_t Pb = (uint32_t)std::min(4096.0, std::ceil(pred * bucket_margin / fill_big));
+          const uint32_t Pb = (uint32_t)std::min(4096.0, std::ceil(pred * bucket_margin / fill_bkt));
           al->h_bmeta[r - r0] = make_uint2(boff_words, Pb);
           boff_words += Pb + 1;
           rsp.push_back(group_item(r, 0, Pb));
@@ -2315,7 +2325,7 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
       }
       if (split_side) HIPCHK(hipStreamWaitEvent(st, al->grp_join, 0));
       launch_group(v, krec, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0,
-                   al->read_list.p + n_small + n_bigr, n_bkt, kGroupLdsMaxLog2, nullptr, O, al->stats.p, st, 2);
+                   al->read_list.p + n_small + n_bigr, n_bkt, al->bkt_log2, nullptr, O, al->stats.p, st, 2);
       HIPCHK(hipGetLastError());
       uint32_t cnt[4];
       HIPCHK(hipMemcpyAsync(cnt, al->counters.p, 16, hipMemcpyDeviceToHost, st));
@@ -2347,8 +2357,9 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
         // (each item carries the table it filled: the first round holds both tiers' items)
         auto split_of = [&](uint32_t i) -> uint32_t {
           const uint32_t g = grow[i] & 0xFFFFFFu;
-          const bool from_small = (grow[i] >> 24) < kGroupLdsMaxLog2;
-          const uint32_t need = from_small ? (g + 3) / 4 : std::max<uint32_t>(2, g);
+          const uint32_t tl = grow[i] >> 24;  // the table it filled: 2^tl slots; the next one is 2^13
+          const uint32_t sh = tl < kGroupLdsMaxLog2 ? kGroupLdsMaxLog2 - tl : 0;
+          const uint32_t need = sh ? (g + (1u << sh) - 1) >> sh : std::max<uint32_t>(2, g);
           uint32_t f = 1;
           while (f < need && f < 64) f <<= 1;
           return f;

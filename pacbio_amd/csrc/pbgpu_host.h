@@ -361,6 +361,7 @@ struct pbgpu_aligner {
   // the device out of memory beside its 126-GB index); an overflow redoes the sub-batch and
   // resets it to 1
   double rec_per_chain = 1.0;
+  uint32_t bkt_log2 = 13;    // the bucket items' table size of the current sub-batch (group stage)
   bool cph_learned = false;  // chains_per_hit measured on a sub-batch (the hit budget's margin)
   // pbgpu_run: the most bases a batch holds (0 = unknown): the per-base buffers never grow past it
   uint64_t base_cap = 0;

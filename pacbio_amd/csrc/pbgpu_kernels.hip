@@ -1639,7 +1639,7 @@ __global__ __launch_bounds__(256) void k_order_tiny(const ChainDesc* __restrict_
   }
 }
 
-// Strands of at most NMAX (<= 8) hits, one per lane, entirely in registers: the list order
+// Strands of at most NMAX (<= 15) hits, one per lane, entirely in registers: the list order
 // restored by the odd-even network of k_order_tiny (X written back when it moved), then
 // lis_align::compute_L_P (lis_align.hpp:139-182) and indices (:190-204) restated literally
 // -- the singly linked list L walked from its head, the first acceptable predecessor, the
@@ -1656,7 +1656,7 @@ __global__ __launch_bounds__(256) void k_lis_tiny(const ChainDesc* __restrict__ 
                                                   const uint32_t* __restrict__ slen, int2* X, int2* __restrict__ pts,
                                                   uint32_t* __restrict__ lisl, LisParams lp,
                                                   unsigned long long* stats) {
-  static_assert(NMAX <= 8, "4-bit node fields");
+  static_assert(NMAX <= 15, "4-bit node fields (15 = none)");
   constexpr uint32_t NONE = 15;
   const uint32_t w = blockIdx.x * 256 + threadIdx.x;
   const bool act = w < n_items;
@@ -1695,12 +1695,22 @@ __global__ __launch_bounds__(256) void k_lis_tiny(const ChainDesc* __restrict__ 
     return r;
   };
   // node q: bits [16 (q & 3), +16) of nd[q >> 2]: nxt | P << 4 | len << 8 | root << 12
-  uint64_t nd0 = 0, nd1 = 0;
-  auto node = [&](uint32_t q) -> uint32_t { return (uint32_t)(((q < 4 ? nd0 : nd1) >> (16 * (q & 3))) & 0xFFFFu); };
+  constexpr int NW = (NMAX + 3) / 4;
+  uint64_t nd[NW];
+#pragma unroll
+  for (int j = 0; j < NW; ++j) nd[j] = 0;
+  auto word = [&](uint32_t q) -> uint64_t {
+    uint64_t r = nd[0];
+#pragma unroll
+    for (int j = 1; j < NW; ++j) r = (q >> 2) == (uint32_t)j ? nd[j] : r;
+    return r;
+  };
+  auto node = [&](uint32_t q) -> uint32_t { return (uint32_t)((word(q) >> (16 * (q & 3))) & 0xFFFFu); };
   auto set_node = [&](uint32_t q, uint32_t val) {
     const uint32_t sh = 16 * (q & 3);
     const uint64_t m = ~(0xFFFFull << sh), x = (uint64_t)val << sh;
-    if (q < 4) nd0 = (nd0 & m) | x; else nd1 = (nd1 & m) | x;
+#pragma unroll
+    for (int j = 0; j < NW; ++j) nd[j] = (q >> 2) == (uint32_t)j ? ((nd[j] & m) | x) : nd[j];
   };
   auto set_nxt = [&](uint32_t q, uint32_t nx) { set_node(q, (node(q) & ~15u) | nx); };
   uint64_t tests = 0;
@@ -3109,14 +3119,17 @@ void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const ui
     const uint64_t bit = 1ull << (dev & 63);
     if (!(attr_done.load(std::memory_order_acquire) & bit)) {
       for (const void* f : {(const void*)k_group<false, GROUP_BLOCK, 0>, (const void*)k_group<false, GROUP_BLOCK_BIG, 0>,
-                            (const void*)k_group<false, GROUP_BLOCK_BIG, 1>, (const void*)k_group<false, GROUP_BLOCK_BIG, 2>})
+                            (const void*)k_group<false, GROUP_BLOCK_BIG, 1>, (const void*)k_group<false, GROUP_BLOCK_BIG, 2>,
+                            (const void*)k_group<false, GROUP_BLOCK, 2>})
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
       attr_done.fetch_or(bit, std::memory_order_acq_rel);
     }
     if (mode == 1)
       hipLaunchKernelGGL((k_group<false, GROUP_BLOCK_BIG, 1>), dim3(n_list), dim3(GROUP_BLOCK_BIG), lds, st, PBGPU_GROUP_ARGS);
-    else if (mode == 2)
+    else if (mode == 2 && hcap_log2 >= PBGPU_GROUP_BIG_LOG2)
       hipLaunchKernelGGL((k_group<false, GROUP_BLOCK_BIG, 2>), dim3(n_list), dim3(GROUP_BLOCK_BIG), lds, st, PBGPU_GROUP_ARGS);
+    else if (mode == 2)
+      hipLaunchKernelGGL((k_group<false, GROUP_BLOCK, 2>), dim3(n_list), dim3(GROUP_BLOCK), lds, st, PBGPU_GROUP_ARGS);
     else if (hcap_log2 >= PBGPU_GROUP_BIG_LOG2)
       hipLaunchKernelGGL((k_group<false, GROUP_BLOCK_BIG, 0>), dim3(n_list), dim3(GROUP_BLOCK_BIG), lds, st, PBGPU_GROUP_ARGS);
     else

@@ -65,6 +65,13 @@ def main():
         print(f"k_group 8192-slot tier table work (wave ticks): pass 0 first probes {g[112]}, walks+counts {g[113]}, "
               f"windows walking {g[114]}; pass 1 first probes {g[115]}, walks {g[116]}, windows walking {g[117]}; "
               f"mine hits (pass 0) {g[118]}")
+        waves = max(1, g[32])
+        tot = max(1, g[33])
+        print(f"k_coords: waves={g[32]} chunks/wave={g[39] / waves:.2f} fit_chains={st['fit_chains']} "
+              f"fit_points={st['fit_points']}")
+        for n, x in zip(["prologue", "pass1 fit+info", "pass2 err", "alloc/finish", "pass3 info", "emit"],
+                        [g[34], g[35], g[36], g[37], g[38], g[42]]):
+            print(f"  {n:16s} {x / waves:10.0f} ticks/wave ({100.0 * x / tot:5.1f}%)")
         for label, sb in (("k_group 2048-slot tier", 8), ("k_group 8192-slot tier", 14)):
             blocks = max(1, g[sb + 5])
             print(f"{label}: blocks={g[sb + 5]}")
