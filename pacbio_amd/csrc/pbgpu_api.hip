@@ -59,7 +59,7 @@ void launch_occ_sr(const uint64_t* occ, uint64_t n, uint32_t* out, hipStream_t s
 constexpr uint32_t kGroupLdsMaxLog2 = PBGPU_GROUP_BIG_LOG2;  // 8192-slot table, 96 KiB of LDS
 void launch_init_slen(const ChainDesc* chains, uint32_t n_chains, uint32_t* slen, hipStream_t st);
 void launch_strand_order(const uint32_t* slen, uint32_t n_items, uint32_t* hist, uint32_t* cursor, uint32_t* perm,
-                         int phase, hipStream_t st);
+                         int phase, hipStream_t st, const ChainDesc* chains = nullptr, uint2* pinfo = nullptr);
 void launch_chain_order(const uint32_t* lisl, uint32_t n, uint32_t* hist, uint32_t* cursor, uint32_t* perm, int phase,
                         unsigned long long* sums, hipStream_t st);
 void launch_lis(bool big_nodes, const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen,
@@ -80,7 +80,7 @@ uint32_t lis_class_bounds(int which);
 uint32_t lis_lane_max();
 void launch_lis_lane(const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen, int2* X,
                      void* N16, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx, unsigned long long* stats,
-                     hipStream_t st);
+                     hipStream_t st, const uint2* pinfo = nullptr);
 uint32_t len_buckets();
 void launch_strand_order(const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen, int2* X,
                          hipStream_t st);
@@ -1684,6 +1684,7 @@ static uint32_t lis_stage(pbgpu_aligner* al, uint32_t nch, uint64_t Hs, const Li
   al->perm.ensure(2ull * nch + 1);
   al->lisl.ensure(2ull * nch + 1);
   al->slen.ensure(2ull * nch + 1);
+  al->pinfo.ensure(2ull * nch + 1);
   uint32_t n_big = 0, n_mid = 0, n_w2 = 0, n_w1 = 0, n_w0 = 0;  // items in classes above LIS_U16_MAX / LISW_LARGE / LISW_SMALL / LISW_TINY
   auto order = [&](int which, uint32_t n_in) -> uint32_t {  // returns the number of items placed
     HIPCHK(hipMemsetAsync(al->hist.p, 0, NB * 4, st));
@@ -1709,7 +1710,8 @@ static uint32_t lis_stage(pbgpu_aligner* al, uint32_t nch, uint64_t Hs, const Li
     }
     cur[0] = acc;
     HIPCHK(hipMemcpyAsync(al->hist.p + NB, cur.data(), NB * 4, hipMemcpyHostToDevice, st));
-    if (which == 0) launch_strand_order(al->slen.p, n_in, nullptr, al->hist.p + NB, al->perm.p, 1, st);
+    if (which == 0) launch_strand_order(al->slen.p, n_in, nullptr, al->hist.p + NB, al->perm.p, 1, st, al->chains.p,
+                                        al->pinfo.p);
     else launch_chain_order(al->lisl.p, n_in, nullptr, al->hist.p + NB, al->perm.p, 1, nullptr, st);
     HIPCHK(hipGetLastError());
     return acc;
@@ -1749,7 +1751,7 @@ static uint32_t lis_stage(pbgpu_aligner* al, uint32_t nch, uint64_t Hs, const Li
   // the shortest strands: lane per strand
   const uint32_t nw0 = std::max(n_w0, nw1);
   launch_lis_lane(al->chains.p, al->perm.p + nw0, n_strands - nw0, al->slen.p, al->X.p, al->nodes.p, al->pts.p,
-                  al->lisl.p, lp, keep_idx, al->stats.p, st);
+                  al->lisl.p, lp, keep_idx, al->stats.p, st, Hs < (1ull << 32) ? al->pinfo.p + nw0 : nullptr);
   if (timed) HIPCHK(hipEventRecord(al->ev[10], st));  // the timed k_lis slot: tier-0 k_lis_w alone
   // tier 0 (9..255 hits).  (A 16-wave tier of its strands of <= 64 hits was measured
   // no faster: C2 LIS 20.7 vs 20.8 ms, C4r 47.0 vs 48.7, profiles/r05p_lisw.txt.)
@@ -2206,9 +2208,9 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
       // PBGPU_GROUP_BUCKETS=0 (A/B): every partition item enumerates its read's hits (round 5)
       const bool buckets_on = !(getenv("PBGPU_GROUP_BUCKETS") && !atoi(getenv("PBGPU_GROUP_BUCKETS")));
       const double bucket_margin = getenv("PBGPU_GROUP_BUCKET_MARGIN") ? atof(getenv("PBGPU_GROUP_BUCKET_MARGIN")) : 1.5;
-      // (from P >= 3: on C2 the few reads of P = 2 grouped slower bucketed, 32.7 against 31.3 ms,
-      // profiles/r06k_bucket_minp.txt)
-      const uint32_t bucket_minp = getenv("PBGPU_GROUP_BUCKET_MINP") ? (uint32_t)atoi(getenv("PBGPU_GROUP_BUCKET_MINP")) : 3;
+      // (from P >= 2: with the 2048-slot bucket items, C4 group 127 -> 103 ms and C4r 43.2 -> 40.0
+      // against P >= 3, C2 31.6 -> 32.2; profiles/r06m_bucket_minp_lg11.txt)
+      const uint32_t bucket_minp = getenv("PBGPU_GROUP_BUCKET_MINP") ? (uint32_t)atoi(getenv("PBGPU_GROUP_BUCKET_MINP")) : 2;
       // the bucket items' table: 2^bkt_log2 slots (11: the 2048-slot, 4-wave blocks of the first
       // tier, five a CU; 13: the 8192-slot 16-wave blocks, one a CU), P sized for its fill limit
       const uint32_t bkt_log2 = std::min<uint32_t>(kGroupLdsMaxLog2, std::max<uint32_t>(hcap_log2,

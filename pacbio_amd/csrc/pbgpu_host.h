@@ -323,6 +323,7 @@ struct pbgpu_aligner {
   dbuf<uint32_t> rcur;
   dbuf<uint64_t> sort_scratch;  // k_rec_sort keys of reads above its LDS capacity: 6 words per record
   dbuf<uint2> rec_tiles;        // (read, tile) work items of those reads (carved from the dead hit buffers)
+  dbuf<uint2> pinfo;            // per permuted strand: {first hit, hits} (lis_stage's strand order)
   dbuf<uint2> bmeta;            // per read of the call: {bucket offsets base, P0} of bucketed reads (GroupOut)
   dbuf<uint32_t> boff;          // the bucketed reads' bucket offsets (P0 + 1 each)
   dbuf<uint32_t> rec_tile_ctr;  // their count and the longest such read

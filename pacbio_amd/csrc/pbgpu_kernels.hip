@@ -1084,12 +1084,20 @@ DEV uint32_t len_bucket(uint32_t n) {
   return 128u + 16u * (l - 7u) + ((n >> (l - 4u)) & 15u);
 }
 struct StrandLen {  // item = chain << 1 | strand (0 fwd, 1 bwd)
+  using Info = uint2;
   const uint32_t* slen;
+  const ChainDesc* chains;  // (info(): the strand's hit range, for the permuted {base, n} array)
   DEV uint32_t operator()(uint32_t i) const { return slen[i]; }
+  DEV uint2 info(uint32_t i, uint32_t n) const {
+    const ChainDesc d = chains[i >> 1];
+    return make_uint2((uint32_t)(d.hit_base + ((i & 1) ? d.nf : 0)), n);
+  }
 };
 struct ChainLisLen {  // item = chain; the longer of its two lis
+  using Info = uint2;
   const uint32_t* lisl;
   DEV uint32_t operator()(uint32_t c) const { const uint32_t a = lisl[2 * c], b = lisl[2 * c + 1]; return a > b ? a : b; }
+  DEV uint2 info(uint32_t, uint32_t) const { return make_uint2(0u, 0u); }
 };
 // sums (optional): [0] += number of non-empty items, [1] += their total length
 // (one atomic pair per block: the work counters of the kernel that consumes them)
@@ -1118,16 +1126,20 @@ __global__ __launch_bounds__(256) void k_len_hist(F f, uint32_t n, uint32_t* his
 // per 4096 items; zero-length items are dropped
 constexpr uint32_t LEN_PERM_ITEMS = 16;
 template <typename F>
-__global__ __launch_bounds__(256) void k_len_perm(F f, uint32_t n, uint32_t* cursor, uint32_t* perm) {
+// pinfo (optional, StrandLen): beside perm, each placed item's {first hit, hits}, so the
+// lane-per-strand LIS reads its strand's range coalesced instead of item -> chain -> range
+__global__ __launch_bounds__(256) void k_len_perm(F f, uint32_t n, uint32_t* cursor, uint32_t* perm,
+                                                  typename F::Info* pinfo) {
   __shared__ uint32_t cnt[NLB], base[NLB];
   for (uint32_t i = threadIdx.x; i < NLB; i += 256) cnt[i] = 0;
   __syncthreads();
   const uint32_t c0 = blockIdx.x * 256 * LEN_PERM_ITEMS + threadIdx.x;
-  uint32_t b[LEN_PERM_ITEMS], loc[LEN_PERM_ITEMS];
+  uint32_t b[LEN_PERM_ITEMS], loc[LEN_PERM_ITEMS], len[LEN_PERM_ITEMS];
 #pragma unroll
   for (uint32_t q = 0; q < LEN_PERM_ITEMS; ++q) {
     const uint32_t c = c0 + q * 256;
-    b[q] = c < n ? len_bucket(f(c)) : 0u;
+    len[q] = c < n ? f(c) : 0u;
+    b[q] = c < n ? len_bucket(len[q]) : 0u;
     loc[q] = b[q] ? atomicAdd(&cnt[b[q]], 1u) : 0u;
   }
   __syncthreads();
@@ -1135,7 +1147,11 @@ __global__ __launch_bounds__(256) void k_len_perm(F f, uint32_t n, uint32_t* cur
   __syncthreads();
 #pragma unroll
   for (uint32_t q = 0; q < LEN_PERM_ITEMS; ++q)
-    if (b[q]) perm[base[b[q]] + loc[q]] = c0 + q * 256;
+    if (b[q]) {
+      const uint32_t at = base[b[q]] + loc[q];
+      perm[at] = c0 + q * 256;
+      if (pinfo) pinfo[at] = f.info(c0 + q * 256, len[q]);
+    }
 }
 
 // ================================================================= lis / fit
@@ -1652,9 +1668,9 @@ __global__ __launch_bounds__(256) void k_order_tiny(const ChainDesc* __restrict_
 // step test), no kept lis indices (--max-match takes the generic kernel).
 template <int NMAX>
 __global__ __launch_bounds__(256) void k_lis_tiny(const ChainDesc* __restrict__ chains,
-                                                  const uint32_t* __restrict__ items, uint32_t n_items,
-                                                  const uint32_t* __restrict__ slen, int2* X, int2* __restrict__ pts,
-                                                  uint32_t* __restrict__ lisl, LisParams lp,
+                                                  const uint32_t* __restrict__ items, const uint2* __restrict__ pinfo,
+                                                  uint32_t n_items, const uint32_t* __restrict__ slen, int2* X,
+                                                  int2* __restrict__ pts, uint32_t* __restrict__ lisl, LisParams lp,
                                                   unsigned long long* stats) {
   static_assert(NMAX <= 15, "4-bit node fields (15 = none)");
   constexpr uint32_t NONE = 15;
@@ -1664,9 +1680,14 @@ __global__ __launch_bounds__(256) void k_lis_tiny(const ChainDesc* __restrict__ 
   uint64_t base = 0;
   if (act) {
     item = items[w];
-    const ChainDesc d = chains[item >> 1];
-    base = d.hit_base + ((item & 1) ? d.nf : 0);
-    n = slen[item];
+    if (pinfo) {  // the strand's range from the permutation pass: no dependent loads
+      const uint2 pi = pinfo[w];
+      base = pi.x; n = pi.y;
+    } else {
+      const ChainDesc d = chains[item >> 1];
+      base = d.hit_base + ((item & 1) ? d.nf : 0);
+      n = slen[item];
+    }
   }
   int2 v[NMAX];
 #pragma unroll
@@ -3181,14 +3202,14 @@ void launch_init_slen(const ChainDesc* chains, uint32_t n_chains, uint32_t* slen
   hipLaunchKernelGGL(k_init_slen, dim3(grid_for(n_chains, 256)), dim3(256), 0, st, chains, n_chains, slen);
 }
 void launch_strand_order(const uint32_t* slen, uint32_t n_items, uint32_t* hist, uint32_t* cursor, uint32_t* perm,
-                         int phase, hipStream_t st) {
+                         int phase, hipStream_t st, const ChainDesc* chains, uint2* pinfo) {
   if (!n_items) return;
-  StrandLen f{slen};
+  StrandLen f{slen, chains};
   if (phase == 0)
     hipLaunchKernelGGL((k_len_hist<StrandLen>), dim3(grid_for(n_items, 256, 2048)), dim3(256), 0, st, f, n_items, hist,
                        (unsigned long long*)nullptr);
   else hipLaunchKernelGGL((k_len_perm<StrandLen>), dim3((n_items + 256 * LEN_PERM_ITEMS - 1) / (256 * LEN_PERM_ITEMS)), dim3(256), 0,
-                          st, f, n_items, cursor, perm);
+                          st, f, n_items, cursor, perm, chains ? pinfo : nullptr);
 }
 void launch_chain_order(const uint32_t* lisl, uint32_t n, uint32_t* hist, uint32_t* cursor, uint32_t* perm, int phase,
                         unsigned long long* sums, hipStream_t st) {
@@ -3197,7 +3218,7 @@ void launch_chain_order(const uint32_t* lisl, uint32_t n, uint32_t* hist, uint32
   if (phase == 0)
     hipLaunchKernelGGL((k_len_hist<ChainLisLen>), dim3(grid_for(n, 256, 2048)), dim3(256), 0, st, f, n, hist, sums);
   else hipLaunchKernelGGL((k_len_perm<ChainLisLen>), dim3((n + 256 * LEN_PERM_ITEMS - 1) / (256 * LEN_PERM_ITEMS)), dim3(256), 0,
-                          st, f, n, cursor, perm);
+                          st, f, n, cursor, perm, (uint2*)nullptr);
 }
 void launch_lis(bool big_nodes, const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen,
                 const int2* X, void* N, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx,
@@ -3226,13 +3247,13 @@ constexpr uint32_t LISW_TINY = LISW_TINY_N, LISW_SMALL = 511, LISW_LARGE = 4095;
 // strands of <= LIS_LANE_MAX hits: order restored lane-per-strand, then k_lis (lane per strand)
 void launch_lis_lane(const ChainDesc* chains, const uint32_t* items, uint32_t n_items, const uint32_t* slen, int2* X,
                      void* N16, int2* pts, uint32_t* lisl, LisParams lp, int keep_idx, unsigned long long* stats,
-                     hipStream_t st) {
+                     hipStream_t st, const uint2* pinfo) {
   if (!n_items) return;
   // the register kernel: default window, no kept lis indices (PBGPU_LIS_TINY=0: the generic path)
   static const bool tiny_on = !(getenv("PBGPU_LIS_TINY") && !atoi(getenv("PBGPU_LIS_TINY")));
   if (tiny_on && !keep_idx && lp.W == 1 && !lp.mer_all) {
     hipLaunchKernelGGL((k_lis_tiny<PBGPU_LIS_LANE_MAX>), dim3((n_items + 255) / 256), dim3(256), 0, st, chains, items,
-                       n_items, slen, X, pts, lisl, lp, stats);
+                       pinfo, n_items, slen, X, pts, lisl, lp, stats);
     return;
   }
   if (!lp.ordered)
