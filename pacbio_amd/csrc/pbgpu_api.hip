@@ -58,6 +58,8 @@ void launch_occ_sr(const uint64_t* occ, uint64_t n, uint32_t* out, hipStream_t s
 #endif
 constexpr uint32_t kGroupLdsMaxLog2 = PBGPU_GROUP_BIG_LOG2;  // 8192-slot table, 96 KiB of LDS
 void launch_init_slen(const ChainDesc* chains, uint32_t n_chains, uint32_t* slen, hipStream_t st);
+void launch_sr_meta(const uint64_t* sr_start, const uint32_t* sr_uoff, uint64_t n_sr, const int32_t* sr_ul, SrMeta* out,
+                    hipStream_t st);
 void launch_strand_order(const uint32_t* slen, uint32_t n_items, uint32_t* hist, uint32_t* cursor, uint32_t* perm,
                          int phase, hipStream_t st, const ChainDesc* chains = nullptr, uint2* pinfo = nullptr);
 void launch_chain_order(const uint32_t* lisl, uint32_t n, uint32_t* hist, uint32_t* cursor, uint32_t* perm, int phase,
@@ -1353,12 +1355,21 @@ pbgpu_status pbgpu_aligner_create(const pbgpu_index* ix, const pbgpu_align_param
   P.mers_factor = params->mers_matching / 100.0; P.bases_factor = params->bases_matching / 100.0;
   P.unitigs_k = params->unitigs_k && params->n_unitigs ? params->unitigs_k : 0;
   P.ul = al->ul.p; P.n_ul = params->unitigs_k ? params->n_unitigs : 0;
-  P.sr_ul = nullptr;
+  P.sr_ul = nullptr; P.sr_meta = nullptr;
   if (P.unitigs_k) {  // lengths along every super-read name, resolved once (k_coords' kmers_info)
     const uint64_t nu = ix->sr_uids.n;
     al->sr_ul.alloc(std::max<uint64_t>(nu, 1));
     launch_sr_ul(ix->sr_uids.p, nu, al->ul.p, P.n_ul, al->sr_ul.p, nullptr);
     HIPCHK(hipGetLastError());
+    // and per super-read its length, name range and first lengths in one line (PBGPU_SR_META=0: off)
+    static const bool meta_on = !(getenv("PBGPU_SR_META") && !atoi(getenv("PBGPU_SR_META")));
+    const uint64_t nloc = ix->sr_end - ix->sr_begin;
+    if (meta_on && nloc) {
+      al->sr_meta.alloc(nloc);
+      launch_sr_meta(ix->d_sr_start.p, ix->sr_uoff.p, nloc, al->sr_ul.p, al->sr_meta.p, nullptr);
+      HIPCHK(hipGetLastError());
+      P.sr_meta = al->sr_meta.p;
+    }
     HIPCHK(hipDeviceSynchronize());
     P.sr_ul = al->sr_ul.p;
   }

@@ -315,6 +315,7 @@ struct pbgpu_aligner {
   LisParams lp{};
   hipStream_t st = nullptr;
   dbuf<int32_t> ul, sr_ul;  // unitig lengths; the same resolved along every super-read name (k_sr_ul)
+  dbuf<SrMeta> sr_meta;     // per super-read of the index: AlignParamsDev::sr_meta (k_sr_meta)
   // per-batch buffers
   dbuf<KRec> krec;
   dbuf<uint32_t> n_kept, thr, rec_per_read, rec_cursor, order, counters;

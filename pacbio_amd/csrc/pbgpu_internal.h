@@ -45,6 +45,14 @@ struct IndexView {
   uint32_t filt_shift;        // word index = filter hash >> filt_shift
 };
 
+// per super-read, what k_coords' prologue reads (one 32-byte line): its length, its name's
+// range in sr_uids / sr_ul, and the name's first SR_META_UL resolved unitig lengths
+constexpr uint32_t SR_META_UL = 5;
+struct SrMeta {
+  uint32_t ql, u0, nsz;
+  int32_t ul[SR_META_UL];
+};
+static_assert(sizeof(SrMeta) == 32, "one 32-byte line");
 struct AlignParamsDev {
   uint32_t k;
   uint32_t window;
@@ -57,6 +65,7 @@ struct AlignParamsDev {
   const int32_t* ul;
   uint64_t n_ul;
   const int32_t* sr_ul;    // unitig length of every name entry (index sr_uids order), INT32_MIN if unusable
+  const SrMeta* sr_meta;   // (with sr_ul) per super-read: SrMeta
   int32_t fine;            // fine_aligner pass: every chain emits a record, no filters (fine_aligner.cc:43-48)
 };
 

@@ -298,6 +298,24 @@ __global__ void k_headers(const uint64_t* keys, const uint64_t* kpos, const uint
 
 // Unitig length of every name entry of the index (sr_uids), for kmers_info:
 // ulen(id) = ul[id], unusable (INT32_MIN) for an invalid id or one past the table
+// SrMeta of every super-read of the index (AlignParamsDev::sr_meta), from its text starts,
+// name offsets and the resolved unitig lengths
+__global__ void k_sr_meta(const uint64_t* sr_start, const uint32_t* sr_uoff, uint64_t n_sr, const int32_t* sr_ul,
+                          SrMeta* out) {
+  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < n_sr; s += (uint64_t)gridDim.x * blockDim.x) {
+    SrMeta m;
+    m.ql = (uint32_t)(sr_start[s + 1] - sr_start[s]);
+    m.u0 = sr_uoff[s];
+    m.nsz = sr_uoff[s + 1] - m.u0;
+#pragma unroll
+    for (uint32_t i = 0; i < SR_META_UL; ++i) m.ul[i] = i < m.nsz ? sr_ul[m.u0 + i] : INT32_MIN;
+    out[s] = m;
+  }
+}
+void launch_sr_meta(const uint64_t* sr_start, const uint32_t* sr_uoff, uint64_t n_sr, const int32_t* sr_ul, SrMeta* out,
+                    hipStream_t st) {
+  if (n_sr) hipLaunchKernelGGL(k_sr_meta, dim3(1024), dim3(256), 0, st, sr_start, sr_uoff, n_sr, sr_ul, out);
+}
 __global__ void k_sr_ul(const uint32_t* ids, uint64_t n, const int32_t* ul, uint64_t n_ul, int32_t* out) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t id = ids[i];
@@ -2218,6 +2236,25 @@ struct KmersInfo {
       for (uint32_t i = 0; i < INFO_LDS_UNITIGS; ++i) if (i < nsz) cache[i * cstride] = v[i];
       cl = cache;
     }
+    start();
+  }
+  // the same with the name's lengths given (fwd order, SrMeta::ul) for nsz <= SR_META_UL:
+  // the cache filled from registers, no loads
+  DEV void init_pre(const AlignParamsDev& P, const int32_t (&f)[SR_META_UL], uint32_t nsz_, bool rev_, T* m, T* b,
+                    uint32_t stride_, CT* cache, uint32_t cstride_) {
+    lens = nullptr; nsz = nsz_; rev = rev_; k = (int32_t)P.k; uk = (int32_t)P.unitigs_k;
+    mers = m; bases = b; stride = stride_; cl = cache; cstride = cstride_;
+#pragma unroll
+    for (uint32_t i = 0; i < SR_META_UL; ++i) {
+      const uint32_t q = rev ? nsz - 1 - i : i;
+      int32_t v = f[0];
+#pragma unroll
+      for (uint32_t j = 1; j < SR_META_UL; ++j) v = q == j ? f[j] : v;
+      if (i < nsz) cache[i * cstride] = v;
+    }
+    start();
+  }
+  DEV void start() {
     const int32_t l0 = ulen(0);
     ok = l0 != UL_INVALID;
     if (!ok) return;
@@ -2453,7 +2490,17 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
   const uint32_t k = P.k;
   Rec R;
   R.nb_mers = (int32_t)nl; R.pb_cons = 0; R.sr_cons = 0; R.pb_cover = k; R.sr_cover = k;
-  R.ql = act ? (uint32_t)(ix.sr_start[d.sr + 1] - ix.sr_start[d.sr]) : 0;
+  // the super-read's length, name range and first unitig lengths: one 32-byte SrMeta line
+  // (kmers_info runs) instead of sr_start, sr_uoff and sr_ul, three random sectors a chain
+  SrMeta sm{};
+  if (act && P.sr_meta) {
+    const uint4* mp = reinterpret_cast<const uint4*>(P.sr_meta + d.sr);
+    const uint4 m0 = mp[0], m1 = mp[1];
+    sm.ql = m0.x; sm.u0 = m0.y; sm.nsz = m0.z;
+    sm.ul[0] = (int32_t)m0.w; sm.ul[1] = (int32_t)m1.x; sm.ul[2] = (int32_t)m1.y; sm.ul[3] = (int32_t)m1.z;
+    sm.ul[4] = (int32_t)m1.w;
+  }
+  R.ql = !act ? 0u : P.sr_meta ? sm.ql : (uint32_t)(ix.sr_start[d.sr + 1] - ix.sr_start[d.sr]);
   // the read length is needed only by the filters at the end: loaded here, with the other
   // descriptor-dependent loads, so it does not stall the wave after the passes
   const uint32_t rl = act ? (uint32_t)(roff[d.read + 1] - roff[d.read]) : 0;
@@ -2462,12 +2509,20 @@ __global__ __launch_bounds__(64) void k_coords(IndexView ix, AlignParamsDev P, c
   R.stretch = 0; R.offset = 0; R.avg_err = 0;
   // kmers_info setup (pb_aligner.cc:62-81): unitig list of the name used for the record
   uint32_t u0 = 0, nsz = 0;
-  if (act && nl && P.unitigs_k) { u0 = ix.sr_uoff[d.sr]; nsz = ix.sr_uoff[d.sr + 1] - u0; }
+  if (act && nl && P.unitigs_k) {
+    if (P.sr_meta) { u0 = sm.u0; nsz = sm.nsz; }
+    else { u0 = ix.sr_uoff[d.sr]; nsz = ix.sr_uoff[d.sr + 1] - u0; }
+  }
   const bool info_lds = nsz && nsz <= INFO_LDS_UNITIGS;
   KmersInfo<lds_i32> KI;
-  if (info_lds)
-    KI.init(P, P.sr_ul + u0, nsz, (R.flags & 2u) != 0, (lds_i32*)(im + lane), (lds_i32*)(ib + lane), 64,
-            (lds_i32*)(iul + lane), 64);
+  if (info_lds) {
+    if (P.sr_meta && nsz <= SR_META_UL)
+      KI.init_pre(P, sm.ul, nsz, (R.flags & 2u) != 0, (lds_i32*)(im + lane), (lds_i32*)(ib + lane), 64,
+                  (lds_i32*)(iul + lane), 64);
+    else
+      KI.init(P, P.sr_ul + u0, nsz, (R.flags & 2u) != 0, (lds_i32*)(im + lane), (lds_i32*)(ib + lane), 64,
+              (lds_i32*)(iul + lane), 64);
+  }
   auto info_pos = [&](int32_t so) -> int32_t {
     const int32_t pos = fwd_align ? so : (int32_t)(R.ql + (uint32_t)so - k + 2u);
     return pos < 0 ? -pos : pos;
