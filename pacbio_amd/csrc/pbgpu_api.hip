@@ -2263,9 +2263,11 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
       rs.insert(rs.end(), rb.begin(), rb.end());
       rs.insert(rs.end(), rbb.begin(), rbb.end());
       rs.insert(rs.end(), rsp.begin(), rsp.end());
+      // sized in every batch, bucketed reads or not: a run's first batches may have none and a
+      // later one some (C2 create_mega_reads: two allocations after the first batch)
+      al->bmeta.ensure(n);
+      al->boff.ensure(std::max<uint32_t>(boff_words + 1, 4096));
       if (n_split) {
-        al->bmeta.ensure(n);
-        al->boff.ensure(boff_words + 1);
         HIPCHK(hipMemcpyAsync(al->bmeta.p + r0, al->h_bmeta.data(), (size_t)nr * sizeof(uint2), hipMemcpyHostToDevice, st));
       }
       al->acc.ms_host_order += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count();

@@ -4480,7 +4480,13 @@ struct alignas(16) RelaxPath {
   uint16_t lsk, fl;      // the start's implied-start key (0xFFFF: NaN), flags (1 an edge in, 2 out)
 };
 // (Measured: the union-find's parent and rank in LDS for reads of <= 8192 records, 3 B a
-// node, gained nothing -- C4r graph stage 154.2 vs 154.7 ms -- and <= 16384 lost 10 ms.)
+// node, gained nothing -- C4r graph stage 154.2 vs 154.7 ms -- and <= 16384 lost 10 ms.
+// Round 6, again with the union-find 2 B a node in LDS (a root's word holding its rank) in
+// tiers of 4096 / 8192 / 16384 / 32768 records on three streams: the union wave 4699 -> 1893
+// cycles a node, the paths wave, 2159-2541, then bounds it; the longest launch 26.5 -> 18.1 ms
+// and the resident graph stage of 20k C4r reads 107.3 -> 106.2 ms, but create_mega_reads on
+// them 0.35 -> 0.38 s: blocks that hold LDS for 10-18 ms take it from the other aligner's
+// k_group tables.  profiles/r06y_relax_uf_lds_tried.txt.)
 __global__ __launch_bounds__(128) void k_graph_relax_big(GraphDev G, uint32_t n_reads) {
   constexpr uint32_t RANK_NAN = 0xFFFFu, NONE = 0xFFFFu;
   const uint32_t r = blockIdx.x;

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--gap-ms", type=float, default=0.3)
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--start", default="k_seed", help="the window opens at this kernel's first launch")
+    ap.add_argument("--last", action="store_true", help="... at its last launch instead")
     a = ap.parse_args()
     rows = []
     with open(a.csv) as f:
@@ -27,7 +28,8 @@ def main():
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]),
                          r.get("Queue_Id"), r.get("Stream_Id")))
     rows.sort()
-    t0 = next((s for s, _, n, _, _ in rows if a.start in n), rows[0][0])
+    starts = [s for s, _, n, _, _ in rows if a.start in n] or [rows[0][0]]
+    t0 = starts[-1] if a.last else starts[0]
     rows = [r for r in rows if r[0] >= t0]
     t1 = max(e for _, e, _, _, _ in rows)
     print(f"window {(t1 - t0) / 1e6:.2f} ms, {len(rows)} kernels (from the first {a.start})")
