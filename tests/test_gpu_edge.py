@@ -188,6 +188,25 @@ def test_group_bucketed_reads(data, scale, dense, small, monkeypatch):
     assert st0["group_bucketed_reads"] == 0 and old == got
 
 
+@pytest.mark.parametrize("extra", [dict(max_match=True, bases_matching=10.0), dict(forward=False, ul=None, unitigs_k=0),
+                                   dict(window_size=3)])
+def test_group_bucketed_reads_modes(extra, dense, monkeypatch):
+    """The bucketed grouping under the modes that read the lists differently downstream:
+    --max-match (discard rounds over the lists), both strands (-f off), a window of 3 (the
+    generic LIS): oracle bytes, and those of the round-5 path (PBGPU_GROUP_BUCKETS=0)."""
+    monkeypatch.setenv("PBGPU_GROUP_PRED_SCALE", "200")
+    names, seqs = dense.sr_names(), dense.sr_seqs()
+    pnames, pseqs = dense.pb_names(), dense.pb_seqs()
+    cfg = dict(dict(ul=dense.unitig_lengths, forward=True, unitigs_k=31), **extra)
+    exp = _oracle(names, seqs, pnames, pseqs, **cfg)
+    got, st = _gpu(names, seqs, pnames, pseqs, **cfg)
+    assert st["group_bucketed_reads"] >= len(pseqs) // 2, st
+    assert_same_coords(got, exp, f"bucketed {extra}")
+    monkeypatch.setenv("PBGPU_GROUP_BUCKETS", "0")
+    old, st0 = _gpu(names, seqs, pnames, pseqs, **cfg)
+    assert st0["group_bucketed_reads"] == 0 and old == got
+
+
 def test_repeats_threshold():
     from tools.synth import Dataset
     ds = Dataset("small", seed=3, repeat_frac=0.2, n_pb=30)
