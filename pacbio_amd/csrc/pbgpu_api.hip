@@ -2185,7 +2185,7 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
     // 8192-slot table over several hash partitions of its super-reads, a work item (and
     // block) each.  A misprediction only costs time: an overflowing item goes again in
     // the next tier or split in two.
-    uint32_t n_small = 0, n_bigr = 0, n_bkt = 0, n_split = 0;
+    uint32_t n_small = 0, n_bigr = 0, n_bkt = 0, n_split = 0, split_pmax = 0;
     {
       const auto th0 = std::chrono::steady_clock::now();
       // Longest first by a counting sort over hit-count classes (exact below 128 hits, 16
@@ -2219,9 +2219,11 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
       // PBGPU_GROUP_BUCKETS=0 (A/B): every partition item enumerates its read's hits (round 5)
       const bool buckets_on = !(getenv("PBGPU_GROUP_BUCKETS") && !atoi(getenv("PBGPU_GROUP_BUCKETS")));
       const double bucket_margin = getenv("PBGPU_GROUP_BUCKET_MARGIN") ? atof(getenv("PBGPU_GROUP_BUCKET_MARGIN")) : 1.5;
-      // (from P >= 2: with the 2048-slot bucket items, C4 group 127 -> 103 ms and C4r 43.2 -> 40.0
-      // against P >= 3, C2 31.6 -> 32.2; profiles/r06m_bucket_minp_lg11.txt)
-      const uint32_t bucket_minp = getenv("PBGPU_GROUP_BUCKET_MINP") ? (uint32_t)atoi(getenv("PBGPU_GROUP_BUCKET_MINP")) : 2;
+      // every read past the 4-wave tier is bucketed (P >= 1).  (From P >= 2 with the 2048-slot
+      // bucket items: C4 group 127 -> 103 ms and C4r 43.2 -> 40.0 against P >= 3, C2 31.6 -> 32.2,
+      // profiles/r06m_bucket_minp_lg11.txt; then P >= 1 with the 8-wave split: C4 94.1 -> 90.5,
+      // C4r and C2 within 0.4 ms, profiles/r06sp_split_block.txt)
+      const uint32_t bucket_minp = getenv("PBGPU_GROUP_BUCKET_MINP") ? (uint32_t)atoi(getenv("PBGPU_GROUP_BUCKET_MINP")) : 1;
       // the bucket items' table: 2^bkt_log2 slots (11: the 2048-slot, 4-wave blocks of the first
       // tier, five a CU; 13: the 8192-slot 16-wave blocks, one a CU), P sized for its fill limit
       const uint32_t bkt_log2 = std::min<uint32_t>(kGroupLdsMaxLog2, std::max<uint32_t>(hcap_log2,
@@ -2230,6 +2232,7 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
       const double fill_bkt = bkt_log2 >= kGroupLdsMaxLog2 ? fill_big
                                                            : 0.95 * (double)((1u << bkt_log2) - (1u << bkt_log2) / 4);
       uint32_t boff_words = 0;
+      split_pmax = 0;
       al->h_bmeta.assign(nr, make_uint2(0u, 0u));
       // tests: PBGPU_GROUP_FIRST_P=P puts every read in the smallest table as P hash-partition
       // items, so a one-read call can overflow P items at once
@@ -2249,6 +2252,7 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
           // that overflows redoes its bucket in a later round: Pb takes a margin over the
           // prediction (C4: an overflow round of ~8 ms in a 92-ms sub-batch at 1.0)
           const uint32_t Pb = (uint32_t)std::min(4096.0, std::ceil(pred * bucket_margin / fill_bkt));
+          split_pmax = std::max(split_pmax, Pb);
           al->h_bmeta[r - r0] = make_uint2(boff_words, Pb);
           boff_words += Pb + 1;
           rsp.push_back(group_item(r, 0, Pb));
@@ -2308,8 +2312,12 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
           HIPCHK(hipStreamWaitEvent(al->grp_side, al->grp_fork, 0));
           sst = al->grp_side;
         }
+        // the split's LDS holds a count and a cursor per partition: sized for the launch's
+        // largest P (its scan and cursors), not the 4096 a read may reach
+        uint32_t split_log2 = 6;
+        while ((1u << split_log2) < split_pmax + 1 && split_log2 < 12) ++split_log2;
         launch_group(v, krec, rd->off.p, al->n_kept.p, al->thr.p, al->hit_off.p, hoff[r0], 0,
-                     al->read_list.p + n_small + n_bigr + n_bkt, n_split, 12, nullptr, O, al->stats.p, sst, 1);
+                     al->read_list.p + n_small + n_bigr + n_bkt, n_split, split_log2, nullptr, O, al->stats.p, sst, 1);
         HIPCHK(hipGetLastError());
         if (split_side) HIPCHK(hipEventRecord(al->grp_join, al->grp_side));
       }

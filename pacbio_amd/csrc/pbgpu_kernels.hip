@@ -3196,11 +3196,29 @@ void launch_group(IndexView ix, const KRec* krec, const uint64_t* roff, const ui
     if (!(attr_done.load(std::memory_order_acquire) & bit)) {
       for (const void* f : {(const void*)k_group<false, GROUP_BLOCK, 0>, (const void*)k_group<false, GROUP_BLOCK_BIG, 0>,
                             (const void*)k_group<false, GROUP_BLOCK_BIG, 1>, (const void*)k_group<false, GROUP_BLOCK_BIG, 2>,
-                            (const void*)k_group<false, GROUP_BLOCK, 2>})
+                            (const void*)k_group<false, GROUP_BLOCK, 2>, (const void*)k_group<false, GROUP_BLOCK, 1>})
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
       attr_done.fetch_or(bit, std::memory_order_acq_rel);
     }
-    if (mode == 1)
+    // the split in 8-wave blocks: per 50k C4 reads its group stage 103.3 -> 93.0 ms against
+    // 16-wave blocks (2 reads a CU at a time), 94.5 with 4 waves, 119 with 2
+    // (profiles/r06sp_split_block.txt; PBGPU_SPLIT_BLOCK 128 / 256 / 512 / 1024)
+    static const int split_b = getenv("PBGPU_SPLIT_BLOCK") ? atoi(getenv("PBGPU_SPLIT_BLOCK")) : 512;
+    if (mode == 1) {
+      static std::atomic<uint64_t> sattr(0);
+      if (!(sattr.load(std::memory_order_acquire) & bit)) {
+        for (const void* f : {(const void*)k_group<false, 128, 1>, (const void*)k_group<false, 512, 1>})
+          (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
+        sattr.fetch_or(bit, std::memory_order_acq_rel);
+      }
+    }
+    if (mode == 1 && split_b == 128)
+      hipLaunchKernelGGL((k_group<false, 128, 1>), dim3(n_list), dim3(128), lds, st, PBGPU_GROUP_ARGS);
+    else if (mode == 1 && split_b == 512)
+      hipLaunchKernelGGL((k_group<false, 512, 1>), dim3(n_list), dim3(512), lds, st, PBGPU_GROUP_ARGS);
+    else if (mode == 1 && split_b == (int)GROUP_BLOCK)
+      hipLaunchKernelGGL((k_group<false, GROUP_BLOCK, 1>), dim3(n_list), dim3(GROUP_BLOCK), lds, st, PBGPU_GROUP_ARGS);
+    else if (mode == 1)
       hipLaunchKernelGGL((k_group<false, GROUP_BLOCK_BIG, 1>), dim3(n_list), dim3(GROUP_BLOCK_BIG), lds, st, PBGPU_GROUP_ARGS);
     else if (mode == 2 && hcap_log2 >= PBGPU_GROUP_BIG_LOG2)
       hipLaunchKernelGGL((k_group<false, GROUP_BLOCK_BIG, 2>), dim3(n_list), dim3(GROUP_BLOCK_BIG), lds, st, PBGPU_GROUP_ARGS);
