@@ -2218,7 +2218,9 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
       rs.clear(); rb.clear(); rbb.clear(); rsp.clear();
       // PBGPU_GROUP_BUCKETS=0 (A/B): every partition item enumerates its read's hits (round 5)
       const bool buckets_on = !(getenv("PBGPU_GROUP_BUCKETS") && !atoi(getenv("PBGPU_GROUP_BUCKETS")));
-      const double bucket_margin = getenv("PBGPU_GROUP_BUCKET_MARGIN") ? atof(getenv("PBGPU_GROUP_BUCKET_MARGIN")) : 1.5;
+      // (1.5 with the 16-wave split; with the 8-wave one 2.0: C4 overflowing items 1514 -> 76 per
+      // 50k reads, group 91.8 -> 89.7 ms, profiles/r06bk_bucket_margin.txt)
+      const double bucket_margin = getenv("PBGPU_GROUP_BUCKET_MARGIN") ? atof(getenv("PBGPU_GROUP_BUCKET_MARGIN")) : 2.0;
       // every read past the 4-wave tier is bucketed (P >= 1).  (From P >= 2 with the 2048-slot
       // bucket items: C4 group 127 -> 103 ms and C4r 43.2 -> 40.0 against P >= 3, C2 31.6 -> 32.2,
       // profiles/r06m_bucket_minp_lg11.txt; then P >= 1 with the 8-wave split: C4 94.1 -> 90.5,
