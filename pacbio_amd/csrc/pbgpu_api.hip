@@ -2301,7 +2301,9 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
       // staging overwritten) on a side stream beside the other tiers, their partition items
       // after both: alone, a launch of a few long reads' splits held the GPU for its longest
       // (C2: +1.7 ms of group stage)
-      const bool split_side = n_split && (n_small || n_bigr);
+      // the split beside the 16-wave tier (both long) on a side stream; beside the 4-wave
+      // tier alone it would stretch that launch (C2 tier 0 21.2 -> 26.2 ms) for little: serial
+      const bool split_side = n_split && n_bigr;
       if (n_split) {
         hipStream_t sst = st;
         if (split_side) {
