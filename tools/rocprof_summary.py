@@ -61,7 +61,7 @@ def counters(d):
 
 # device-leg kernels summarised: (rocprof name, key prefix in the summary) -- the five
 # individually timed kernels of bench.py's roofline.by_kernel
-KERNELS = [("k_seed<256, 8, 0>", "k_seed"), ("k_group<false, 256u>", "k_group"), ("k_lis_w<255, 8>", "k_lis"),
+KERNELS = [("k_seed<256, 8, 0>", "k_seed"), ("k_group<false, 256u, 0>", "k_group"), ("k_lis_w<255, 8>", "k_lis"),
            ("k_coords<8>", "k_coords"), ("k_rec_sort<256, 2048>", "k_rec_sort")]
 # which FETCH_SIZE correction fits each kernel's read shape: random 64-B
 # sectors (k_seed's filter words and bucket probes) are counted exactly; k_group's
