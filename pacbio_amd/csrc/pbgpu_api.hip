@@ -2277,11 +2277,15 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
         HIPCHK(hipMemcpyAsync(al->bmeta.p + r0, al->h_bmeta.data(), (size_t)nr * sizeof(uint2), hipMemcpyHostToDevice, st));
       }
       al->acc.ms_host_order += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count();
-      al->read_list.ensure(rs.size());
+      // the work items of a batch vary with its reads' partitions far more than the reads do
+      // (a bucketed read is 1 + P items): lists of 12 B an item, sized for 16 items a read at
+      // least, so a later batch's count does not allocate (test_no_device_allocation_after_first_batch)
+      const size_t item_room = std::max<size_t>(rs.size(), 16ull * nr + 4096);
+      al->read_list.ensure(item_room);
       HIPCHK(hipMemcpyAsync(al->read_list.p, rs.data(), rs.size() * sizeof(uint2), hipMemcpyHostToDevice, st));
       // every work item of the first round may overflow (a read split in P items holds P of
       // them): the overflow list holds one entry per item, not one per read
-      al->ovf_items.ensure(rs.size()); al->ovf_grow.ensure(rs.size());
+      al->ovf_items.ensure(item_room); al->ovf_grow.ensure(item_room);
       O.overflow_items = al->ovf_items.p; O.overflow_grow = al->ovf_grow.p;
       O.overflow_cap = (uint32_t)std::min<size_t>(al->ovf_items.n, 0xFFFFFFFFu);
       // the bucketed reads' staging: the sub-batch's LIS buffers, unused until the LIS stage
