@@ -2228,8 +2228,10 @@ void aligner_pipeline(pbgpu_aligner* al, const pbgpu_reads* rd, int seed_mode, u
       const uint32_t bucket_minp = getenv("PBGPU_GROUP_BUCKET_MINP") ? (uint32_t)atoi(getenv("PBGPU_GROUP_BUCKET_MINP")) : 1;
       // the bucket items' table: 2^bkt_log2 slots (11: the 2048-slot, 4-wave blocks of the first
       // tier, five a CU; 13: the 8192-slot 16-wave blocks, one a CU), P sized for its fill limit
-      const uint32_t bkt_log2 = std::min<uint32_t>(kGroupLdsMaxLog2, std::max<uint32_t>(hcap_log2,
-          getenv("PBGPU_GROUP_BUCKET_LOG2") ? (uint32_t)atoi(getenv("PBGPU_GROUP_BUCKET_LOG2")) : 11));
+      // (PBGPU_GROUP_BUCKET_LOG2, A/B: 10 .. 13, below the first tier's table too)
+      const uint32_t bkt_log2 = getenv("PBGPU_GROUP_BUCKET_LOG2")
+          ? std::min<uint32_t>(kGroupLdsMaxLog2, std::max<uint32_t>(10, (uint32_t)atoi(getenv("PBGPU_GROUP_BUCKET_LOG2"))))
+          : std::min<uint32_t>(kGroupLdsMaxLog2, std::max<uint32_t>(hcap_log2, 11));
       al->bkt_log2 = bkt_log2;
       const double fill_bkt = bkt_log2 >= kGroupLdsMaxLog2 ? fill_big
                                                            : 0.95 * (double)((1u << bkt_log2) - (1u << bkt_log2) / 4);
